@@ -1,0 +1,146 @@
+"""Host-side sandbox for policy programs (reference-compatible validator).
+
+`SafeExecutor` reproduces the reference's checks
+(`funsearch/safe_execution.py:15-168`) because they decide which LLM
+candidates survive, and therefore what a search run does:
+
+* `validate_code_content` - case-insensitive *substring* blacklist (so
+  ``direction`` is rejected for containing ``dir``);
+* `validate_code_structure` - AST: no imports, no ``__*`` attributes, bare-name
+  calls only to whitelisted builtins / math / operator names;
+* `create_safe_environment` - restricted ``__builtins__`` plus fake ``math`` and
+  ``operator`` namespaces;
+* `execute_policy_function` - one guarded call with a SIGALRM timeout.
+
+This validator is *not* the real isolation boundary of this framework: the
+policy compiler (`policy.compiler`) only lowers a whitelisted grammar to
+bytecode, and the device interpreter enforces an instruction budget, so a
+candidate that passes here but loops forever is stopped on the device rather
+than hanging a worker (the reference has no eval-time timeout).
+"""
+
+from __future__ import annotations
+
+import ast
+import builtins
+import math
+import operator
+import signal
+import threading
+from contextlib import contextmanager
+from typing import Any, Dict
+
+
+class SafeExecutor:
+    ALLOWED_BUILTINS = {
+        "abs", "min", "max", "sum", "len", "range", "enumerate",
+        "int", "float", "bool", "str", "round", "sorted",
+    }
+    ALLOWED_MODULES = {
+        "math": ["sqrt", "log", "exp", "pow", "sin", "cos", "tan"],
+        "operator": ["add", "sub", "mul", "truediv", "mod"],
+    }
+    FORBIDDEN_PATTERNS = [
+        "import", "__", "exec", "eval", "open", "file", "input",
+        "raw_input", "compile", "globals", "locals", "vars",
+        "dir", "hasattr", "getattr", "setattr", "delattr",
+    ]
+
+    def __init__(self, timeout_seconds: int = 10):
+        self.timeout_seconds = timeout_seconds
+
+    # -- static checks -------------------------------------------------------
+    def _is_allowed_function_call(self, func_name: str) -> bool:
+        return any(func_name in names for names in self.ALLOWED_MODULES.values())
+
+    def validate_code_structure(self, code: str) -> bool:
+        try:
+            tree = ast.parse(code)
+        except SyntaxError as exc:
+            raise ValueError(f"Syntax error in generated code: {exc}")
+        for node in ast.walk(tree):
+            if isinstance(node, (ast.Import, ast.ImportFrom)):
+                raise ValueError("Import statements not allowed")
+            if isinstance(node, ast.Attribute) and node.attr.startswith("__"):
+                raise ValueError(f"Access to {node.attr} not allowed")
+            if isinstance(node, ast.Call) and isinstance(node.func, ast.Name):
+                name = node.func.id
+                if name not in self.ALLOWED_BUILTINS and not self._is_allowed_function_call(name):
+                    raise ValueError(f"Function {name} not allowed")
+        return True
+
+    def validate_code_content(self, code: str) -> bool:
+        lowered = code.lower()
+        hit = next((p for p in self.FORBIDDEN_PATTERNS if p in lowered), None)
+        if hit is not None:
+            raise ValueError(f"Forbidden pattern '{hit}' found in code")
+        return True
+
+    def validate(self, code: str) -> bool:
+        """Both checks, content first (the order the reference generator uses)."""
+        return self.validate_code_content(code) and self.validate_code_structure(code)
+
+    # -- execution -----------------------------------------------------------
+    @contextmanager
+    def timeout_handler(self, seconds: int):
+        """SIGALRM-based timeout; a no-op off the main thread (signals are
+        main-thread only), where the device step budget is the guard."""
+        if threading.current_thread() is not threading.main_thread() or seconds <= 0:
+            yield
+            return
+
+        def _expire(signum, frame):
+            raise TimeoutError(f"Code execution timed out after {seconds} seconds")
+
+        previous = signal.signal(signal.SIGALRM, _expire)
+        signal.alarm(int(seconds))
+        try:
+            yield
+        finally:
+            signal.alarm(0)
+            signal.signal(signal.SIGALRM, previous)
+
+    def create_safe_environment(self) -> Dict[str, Any]:
+        safe_builtins = {n: getattr(builtins, n) for n in self.ALLOWED_BUILTINS if hasattr(builtins, n)}
+
+        def namespace(label, module, names):
+            return type(label, (), {n: getattr(module, n) for n in names})()
+
+        return {
+            "__builtins__": safe_builtins,
+            "math": namespace("SafeMath", math, self.ALLOWED_MODULES["math"]),
+            "operator": namespace("SafeOperator", operator, self.ALLOWED_MODULES["operator"]),
+        }
+
+    def execute_policy_function(self, code: str, pod, node) -> float:
+        self.validate_code_content(code)
+        self.validate_code_structure(code)
+        env = self.create_safe_environment()
+        env.update({"pod": pod, "node": node})
+        try:
+            with self.timeout_handler(self.timeout_seconds):
+                exec(code, env)
+                if "priority_function" not in env:
+                    raise ValueError("Generated code must define 'priority_function'")
+                result = env["priority_function"](pod, node)
+                if not isinstance(result, (int, float)):
+                    raise ValueError(f"Priority function must return a number, got {type(result)}")
+                if math.isnan(result) or math.isinf(result):
+                    raise ValueError("Priority function returned NaN or infinite value")
+                return float(result)
+        except TimeoutError:
+            raise ValueError("Code execution timed out")
+        except Exception as exc:
+            raise ValueError(f"Error executing generated code: {exc}")
+
+
+def compile_priority_function(code: str, executor: "SafeExecutor | None" = None):
+    """``exec`` a policy program in the restricted namespace and return its
+    ``priority_function`` (no validation, no timeout: the reference's
+    `FunSearchScheduler._compile_policy` semantics)."""
+    env = (executor or SafeExecutor()).create_safe_environment()
+    exec(code, env)
+    fn = env.get("priority_function")
+    if not fn:
+        raise ValueError("No priority_function found in evolved code")
+    return fn
