@@ -1,0 +1,182 @@
+// pybind11 bindings of the native CPU oracle engine (_fks_cpu).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <atomic>
+#include <thread>
+
+#include "builtin_scorers.hpp"
+#include "engine.hpp"
+#include "vm_cpu.hpp"
+
+namespace py = pybind11;
+using namespace fks;
+
+namespace {
+
+template <class T>
+std::vector<T> vec(const py::dict& d, const char* key) {
+  auto a = py::array_t<T, py::array::c_style | py::array::forcecast>(d[key]);
+  return std::vector<T>(a.data(), a.data() + a.size());
+}
+
+Workload make_workload(const py::dict& d) {
+  Workload w;
+  w.cpu_total = vec<int64_t>(d, "node_cpu_total");
+  w.cpu_left0 = vec<int64_t>(d, "node_cpu_left");
+  w.mem_total = vec<int64_t>(d, "node_mem_total");
+  w.mem_left0 = vec<int64_t>(d, "node_mem_left");
+  w.gpu_left0 = vec<int32_t>(d, "node_gpu_left");
+  w.ngpus = vec<int32_t>(d, "node_ngpus");
+  w.gpu_start = vec<int32_t>(d, "gpu_start");
+  w.gmilli_total = vec<int32_t>(d, "gpu_milli_total");
+  w.gmilli_left0 = vec<int32_t>(d, "gpu_milli_left");
+  w.gmem_total = vec<int64_t>(d, "gpu_mem_total");
+  w.gmem_left0 = vec<int64_t>(d, "gpu_mem_left");
+  w.pcpu = vec<int64_t>(d, "pod_cpu");
+  w.pmem = vec<int64_t>(d, "pod_mem");
+  w.pngpu = vec<int32_t>(d, "pod_ngpu");
+  w.pgmilli = vec<int32_t>(d, "pod_gmilli");
+  w.pctime = vec<int64_t>(d, "pod_ctime");
+  w.pdur = vec<int64_t>(d, "pod_dur");
+  w.prank = vec<int32_t>(d, "pod_rank");
+  w.n_nodes = (int32_t)w.cpu_total.size();
+  w.n_gpus = (int32_t)w.gmilli_total.size();
+  w.n_pods = (int32_t)w.pcpu.size();
+  if ((int)w.gpu_start.size() != w.n_nodes + 1) throw std::invalid_argument("gpu_start must have n_nodes+1 entries");
+  return w;
+}
+
+SimOptions make_options(const py::dict& o) {
+  SimOptions s;
+  if (o.contains("repush")) s.repush = o["repush"].cast<std::string>() == "earliest" ? REPUSH_EARLIEST : REPUSH_FIRST;
+  if (o.contains("gpu_alloc")) s.gpu_alloc = o["gpu_alloc"].cast<std::string>() == "first_fit" ? ALLOC_FIRST_FIT : ALLOC_BEST_FIT;
+  if (o.contains("snapshot_interval")) s.snapshot_interval = o["snapshot_interval"].cast<double>();
+  if (o.contains("truncate")) s.truncate = o["truncate"].cast<bool>();
+  if (o.contains("budget")) s.budget = o["budget"].cast<int64_t>();
+  if (o.contains("record_values")) s.record_values = o["record_values"].cast<bool>();
+  if (o.contains("record_placements")) s.record_placements = o["record_placements"].cast<bool>();
+  return s;
+}
+
+py::dict to_dict(const SimResult& r) {
+  py::dict d;
+  d["exc"] = r.exc; d["score"] = r.score;
+  d["avg_cpu"] = r.avg_cpu; d["avg_mem"] = r.avg_mem;
+  d["avg_gpu_count"] = r.avg_gpu_count; d["avg_gpu_milli"] = r.avg_gpu_milli; d["frag"] = r.frag;
+  d["n_snapshots"] = r.n_snapshots; d["n_frag_events"] = r.n_frag_events; d["n_events"] = r.n_events;
+  d["n_unplaced"] = r.n_unplaced; d["max_nodes"] = r.max_nodes; d["n_repush"] = r.n_repush;
+  d["n_dropped"] = r.n_dropped; d["inexact"] = r.inexact; d["trace_hash"] = r.trace_hash;
+  if (!r.snap_values.empty()) d["snap_values"] = r.snap_values;
+  if (!r.frag_values.empty()) d["frag_values"] = r.frag_values;
+  if (!r.placement.empty()) d["placement"] = r.placement;
+  return d;
+}
+
+// Result table columns for batch calls (float64 [P, 13]).
+constexpr int kCols = 13;
+void fill_row(double* row, const SimResult& r) {
+  row[0] = r.score; row[1] = r.avg_cpu; row[2] = r.avg_mem; row[3] = r.avg_gpu_count;
+  row[4] = r.avg_gpu_milli; row[5] = r.frag; row[6] = (double)r.n_snapshots;
+  row[7] = (double)r.n_frag_events; row[8] = (double)r.n_events; row[9] = (double)r.n_unplaced;
+  row[10] = (double)r.exc; row[11] = r.inexact ? 1.0 : 0.0; row[12] = (double)(r.trace_hash >> 11);
+}
+
+template <class Fn>
+void parallel_for(int64_t n, int threads, Fn fn) {
+  if (threads <= 1 || n <= 1) { for (int64_t i = 0; i < n; ++i) fn(i); return; }
+  std::atomic<int64_t> next{0};
+  std::vector<std::thread> pool;
+  for (int t = 0; t < threads; ++t)
+    pool.emplace_back([&] { for (int64_t i; (i = next.fetch_add(1)) < n;) fn(i); });
+  for (auto& th : pool) th.join();
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_fks_cpu, m) {
+  m.doc() = "Native CPU oracle engine of funsearch_kubernetes_simulator_amd";
+  py::class_<Workload>(m, "Workload")
+      .def(py::init(&make_workload))
+      .def_readonly("n_nodes", &Workload::n_nodes)
+      .def_readonly("n_gpus", &Workload::n_gpus)
+      .def_readonly("n_pods", &Workload::n_pods);
+
+  m.def("simulate_builtin", [](const Workload& w, int family, std::vector<double> weights, py::dict opts) {
+    BuiltinScorer sc; sc.family = family;
+    for (size_t i = 0; i < weights.size() && i < 16; ++i) sc.w[i] = weights[i];
+    SimOptions o = make_options(opts);
+    SimResult r;
+    { py::gil_scoped_release rel; r = simulate(w, sc, o); }
+    return to_dict(r);
+  }, py::arg("workload"), py::arg("family"), py::arg("weights") = std::vector<double>{}, py::arg("options") = py::dict());
+
+  m.def("simulate_builtin_batch", [](const Workload& w, int family,
+                                     py::array_t<double, py::array::c_style | py::array::forcecast> weights,
+                                     py::dict opts, int threads) {
+    const int64_t P = weights.shape(0), K = weights.ndim() > 1 ? weights.shape(1) : 0;
+    SimOptions o = make_options(opts);
+    py::array_t<double> out({P, (int64_t)kCols});
+    double* op = out.mutable_data();
+    const double* wp = weights.data();
+    {
+      py::gil_scoped_release rel;
+      parallel_for(P, threads, [&](int64_t i) {
+        BuiltinScorer sc; sc.family = family;
+        for (int64_t k = 0; k < K && k < 16; ++k) sc.w[k] = wp[i * K + k];
+        SimResult r = simulate(w, sc, o);
+        fill_row(op + i * kCols, r);
+      });
+    }
+    return out;
+  }, py::arg("workload"), py::arg("family"), py::arg("weights"), py::arg("options") = py::dict(), py::arg("threads") = 1);
+
+  m.def("simulate_program", [](const Workload& w, py::bytes code, std::vector<double> fconst,
+                               std::vector<int64_t> iconst, std::vector<uint8_t> ctag, py::dict opts) {
+    Program prog = make_program(code, fconst, iconst, ctag);
+    SimOptions o = make_options(opts);
+    SimResult r;
+    { py::gil_scoped_release rel; VmScorer sc(prog, o.budget); r = simulate(w, sc, o); if (r.exc == EXC_NONE && sc.exc) r.exc = sc.exc; }
+    return to_dict(r);
+  }, py::arg("workload"), py::arg("code"), py::arg("fconst"), py::arg("iconst"), py::arg("ctag"), py::arg("options") = py::dict());
+
+  m.def("simulate_program_batch", [](const Workload& w, std::vector<py::bytes> codes,
+                                     std::vector<std::vector<double>> fconsts,
+                                     std::vector<std::vector<int64_t>> iconsts,
+                                     std::vector<std::vector<uint8_t>> ctags, py::dict opts, int threads) {
+    const int64_t P = (int64_t)codes.size();
+    std::vector<Program> progs;
+    for (int64_t i = 0; i < P; ++i) progs.push_back(make_program(codes[i], fconsts[i], iconsts[i], ctags[i]));
+    SimOptions o = make_options(opts);
+    py::array_t<double> out({P, (int64_t)kCols});
+    double* op = out.mutable_data();
+    {
+      py::gil_scoped_release rel;
+      parallel_for(P, threads, [&](int64_t i) {
+        VmScorer sc(progs[i], o.budget);
+        SimResult r = simulate(w, sc, o);
+        if (r.exc == EXC_NONE && sc.exc) r.exc = sc.exc;
+        fill_row(op + i * kCols, r);
+      });
+    }
+    return out;
+  }, py::arg("workload"), py::arg("codes"), py::arg("fconsts"), py::arg("iconsts"), py::arg("ctags"),
+     py::arg("options") = py::dict(), py::arg("threads") = 1);
+
+  m.def("score_program_once", [](py::bytes code, std::vector<double> fconst, std::vector<int64_t> iconst,
+                                 std::vector<uint8_t> ctag, py::dict pod, py::dict node, std::vector<int64_t> gpu_left,
+                                 std::vector<int64_t> gpu_total, std::vector<int64_t> gpu_mem) {
+    // Single (pod, node) evaluation of a program; used by compiler unit tests.
+    Program prog = make_program(code, fconst, iconst, ctag);
+    return vm_score_once(prog, pod, node, gpu_left, gpu_total, gpu_mem);
+  });
+
+  m.def("exact_mean", [](std::vector<double> xs) {
+    FixedAcc a; for (double x : xs) a.add(x);
+    return py::make_tuple(fixed_mean(a), a.inexact);
+  });
+  m.attr("RESULT_COLUMNS") = py::make_tuple("score", "avg_cpu", "avg_mem", "avg_gpu_count", "avg_gpu_milli",
+                                            "frag", "n_snapshots", "n_frag_events", "n_events", "n_unplaced",
+                                            "exc", "inexact", "trace_hash_hi");
+}

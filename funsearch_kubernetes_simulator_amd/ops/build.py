@@ -1,0 +1,89 @@
+"""In-tree build of the native extensions.
+
+* ``_fks_cpu``  - C++17 oracle engine + bytecode VM (g++, pybind11);
+* ``_fks_hip``  - MI355X replay kernels (hipcc ``--offload-arch=gfx950``,
+  pybind11 host side).  It links ``libamdhip64.so.7`` by SONAME so that, once
+  ``torch`` is imported, the process shares torch's HIP runtime.
+
+Both land next to this file so they travel with the repository snapshot to
+the GPU box.  ``python -m funsearch_kubernetes_simulator_amd.ops.build``
+rebuilds whatever is stale (sources newer than the .so).
+"""
+
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+from typing import List
+
+from .._paths import CSRC_DIR, NATIVE_DIR
+
+ARCH = os.environ.get("FKS_OFFLOAD_ARCH", "gfx950")
+
+
+def _py_includes() -> List[str]:
+    import pybind11
+    return [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+
+
+def _ext_suffix() -> str:
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def _stale(target: Path, sources: List[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(s.stat().st_mtime > t for s in sources)
+
+
+def _run(cmd: List[str]) -> None:
+    print("[fks build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def _deps(*globs: str) -> List[Path]:
+    out: List[Path] = []
+    for g in globs:
+        out.extend(sorted(CSRC_DIR.glob(g)))
+    return out
+
+
+def build_cpu(force: bool = False) -> Path:
+    target = NATIVE_DIR / f"_fks_cpu{_ext_suffix()}"
+    srcs = _deps("cpu/*.cpp", "cpu/*.hpp", "include/fks/*.hpp")
+    if force or _stale(target, srcs):
+        cxx = os.environ.get("CXX", "g++")
+        cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
+               "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
+               *_py_includes(), f"-I{CSRC_DIR / 'include'}", str(CSRC_DIR / "cpu" / "module.cpp"),
+               "-o", str(target), "-lpthread"]
+        _run(cmd)
+    return target
+
+
+def build_hip(force: bool = False) -> Path:
+    target = NATIVE_DIR / f"_fks_hip{_ext_suffix()}"
+    srcs = _deps("hip/*.hip", "hip/*.h", "hip/*.cpp", "include/fks/*.hpp")
+    if force or _stale(target, srcs):
+        hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
+               "-fvisibility=hidden", "-ffp-contract=off", "-fno-fast-math",
+               "-munsafe-fp-atomics", "-Wno-unused-result",
+               *_py_includes(), f"-I{CSRC_DIR / 'include'}", f"-I{CSRC_DIR / 'hip'}",
+               str(CSRC_DIR / "hip" / "module.hip"), "-o", str(target)]
+        _run(cmd)
+    return target
+
+
+def build_all(force: bool = False) -> None:
+    build_cpu(force)
+    if (CSRC_DIR / "hip" / "module.hip").exists():
+        build_hip(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)
