@@ -215,7 +215,7 @@ SimResult simulate(const Workload& w, Scorer& scorer, const SimOptions& opt) {
         st.gmilli_left[w.gpu_start[n] + assigned_gpus[k]] += w.pgmilli[p];
         used_gmilli -= w.pgmilli[p];
       }
-      hsh = mix_event(hsh, ((uint64_t)p << 2) | 1, (uint64_t)ev.time);
+      hsh = mix_event(hsh, ((uint64_t)(uint32_t)w.prank[p] << 2) | 1, (uint64_t)ev.time);
     } else {
       // ---- creation: argmax over nodes in cluster order
       ScoreCtx ctx{w, st, p, ev.time};
@@ -275,7 +275,7 @@ SimResult simulate(const Workload& w, Scorer& scorer, const SimOptions& opt) {
         } else {
           ++res.n_dropped;
         }
-        hsh = mix_event(hsh, ((uint64_t)p << 2) | 2, (uint64_t)ev.time);
+        hsh = mix_event(hsh, ((uint64_t)(uint32_t)w.prank[p] << 2) | 2, (uint64_t)ev.time);
       } else {
         // ---- commit
         const int n = best_node;
@@ -308,7 +308,7 @@ SimResult simulate(const Workload& w, Scorer& scorer, const SimOptions& opt) {
           }
         }
         heap_push(heap, HeapItem{ev.time + w.pdur[p], w.prank[p], p, 1});
-        hsh = mix_event(hsh, ((uint64_t)p << 2), ((uint64_t)ev.time << 8) ^ (uint64_t)n);
+        hsh = mix_event(hsh, ((uint64_t)(uint32_t)w.prank[p] << 2), ((uint64_t)ev.time << 8) ^ (uint64_t)n);
       }
     }
     // ---- evaluator hook

@@ -1,0 +1,419 @@
+// k_replay: batched exact replay of the OpenB event trace on MI355X.
+//
+// One workgroup = one wave64 = one candidate policy.  Per policy:
+//   * the event heap lives in LDS as packed u64 keys
+//       key = time << (RB+LB) | rank << LB | gpu_mask << (2+NB) | node << 2 | kind
+//     compared on (key >> LB) = (time, pod rank): exactly the reference's
+//     (time, pod_id) tuple order (simulator/event_simulator.py:16-17), and
+//     manipulated with CPython's heapq algorithms so the array layout -- which
+//     the repush rule observes -- is bit-identical to the reference's;
+//   * lanes = nodes (64 x NPASS nodes); each lane keeps its node's cpu / mem /
+//     GPU-count / per-GPU-milli state in VGPRs, so scoring, the placement
+//     argmax (wave max + ballot/ffs for the first-node tie-break), best-fit GPU
+//     selection, fragmentation sums and active-node counts are register-only;
+//   * the waiting-pod multiset needed by the fragmentation metric is a
+//     per-lane histogram over the distinct gpu_milli classes, its minimum a
+//     ballot; membership is carried by the heap entry itself (kind 1 =
+//     re-queued creation = the pod is waiting);
+//   * the evaluator's utilisation / fragmentation means are accumulated in
+//     exact 128-bit fixed point and finished by k_eval_reduce.
+// The scorer (built-in families, or the bytecode VM) is a template argument.
+#pragma once
+
+#include "device_common.h"
+
+namespace fksd {
+
+constexpr int kGmax = 8;        // GPUs per node held in registers
+constexpr int kKinds = 2;       // kind field bits
+constexpr int kFresh = 0, kRetry = 1, kDelete = 2;
+
+enum ExcCode : int32_t {
+  EXC_NONE = 0, EXC_ZERO_DIVISION = 1, EXC_VALUE = 2, EXC_OVERFLOW = 3, EXC_TYPE = 4,
+  EXC_INDEX = 5, EXC_ALLOC = 6, EXC_NAME = 7, EXC_UNSUPPORTED = 100, EXC_BUDGET = 101,
+};
+
+struct DevWorkload {
+  int32_t n_nodes, n_pods, n_classes, pad0;
+  const int32_t* cpu_total;   // [64*NPASS]
+  const int32_t* cpu_left0;
+  const int32_t* mem_total;
+  const int32_t* mem_left0;
+  const int32_t* gpu_left0;
+  const int32_t* ngpus;
+  const int32_t* gml_total;   // [node][kGmax]
+  const int32_t* gml_left0;   // [node][kGmax]
+  const int64_t* gmem_total;  // [node][kGmax] (GPU memory MiB, read-only field)
+  const int4* pod;            // by rank: {cpu, mem, dur, gmilli | ngpu<<16 | cls<<24}
+  const int32_t* pod_ctime;   // by rank: original creation time (pod.creation_time of fresh events)
+  const uint64_t* heap0;      // initial heapified keys
+  const int32_t* class_value; // ascending distinct gpu_milli of GPU pods
+  int64_t tot_cpu, tot_mem, tot_gcnt, tot_gmilli;
+  int64_t used_cpu0, used_mem0, used_gcnt0, used_gmilli0;
+  int32_t rank_bits, node_bits, low_bits, time_bits;
+  double snapshot_interval;
+  int32_t repush_earliest, first_fit_alloc, truncate, pad1;
+};
+
+struct DevResult {
+  int64_t n_events, n_snap, n_frag, n_unplaced, n_repush, max_nodes;
+  uint64_t hash;
+  int32_t exc, inexact;
+  uint64_t acc_lo[5];
+  uint64_t acc_hi[5];
+};
+
+// Per-lane view of node state handed to a scorer.
+template <int NPASS>
+struct NodeRegs {
+  int32_t cpu_left[NPASS], mem_left[NPASS], gpu_left[NPASS];
+  int32_t cpu_total[NPASS], mem_total[NPASS], ngpus[NPASS];
+  int32_t gml[NPASS][kGmax], gmt[NPASS][kGmax];
+};
+
+struct PodView {
+  int32_t cpu, mem, dur, gmilli, ngpu, cls;
+  int64_t ctime;  // current creation time (event time)
+  int32_t rank;
+};
+
+// Scorer contract:  score(pass, node_regs, pod, valid) -> int64 priority after
+// int(max(0, s)) truncation, exceptions reported through `exc`.
+
+// ----------------------------------------------------------------------------
+// LDS heap, CPython heapq algorithms.  Every lane executes the same uniform
+// operations (broadcast LDS reads, same-address writes).
+__device__ __forceinline__ uint64_t hkey(uint64_t k, int lb) { return k >> lb; }
+
+__device__ __forceinline__ void heap_siftdown(uint64_t* h, int startpos, int pos, uint64_t item, int lb) {
+  const uint64_t ik = hkey(item, lb);
+  while (pos > startpos) {
+    int parent = (pos - 1) >> 1;
+    uint64_t p = h[parent];
+    if (ik < hkey(p, lb)) { h[pos] = p; pos = parent; continue; }
+    break;
+  }
+  h[pos] = item;
+}
+
+// _siftup(heap, 0) with heap[0] := item, heap size n
+__device__ __forceinline__ void heap_siftup_root(uint64_t* h, int n, uint64_t item, int lb) {
+  int pos = 0;
+  int child = 1;
+  while (child < n) {
+    int right = child + 1;
+    uint64_t c = h[child];
+    if (right < n) {
+      uint64_t r = h[right];
+      if (!(hkey(c, lb) < hkey(r, lb))) { child = right; c = r; }
+    }
+    h[pos] = c;
+    pos = child;
+    child = 2 * pos + 1;
+  }
+  heap_siftdown(h, 0, pos, item, lb);
+}
+
+// ----------------------------------------------------------------------------
+template <int NPASS, class Scorer>
+__device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* heap, DevResult* out) {
+  const int lane = lane_id();
+  const int lb = W.low_bits, nb = W.node_bits;
+  const int rb = W.rank_bits;
+  const int tshift = rb + lb;
+  const uint64_t time_max = (W.time_bits >= 63) ? ~0ull : ((1ull << W.time_bits) - 1);
+  const int N = W.n_pods;
+
+  for (int i = lane; i < N; i += kWave) heap[i] = W.heap0[i];
+
+  NodeRegs<NPASS> nr;
+#pragma unroll
+  for (int ps = 0; ps < NPASS; ++ps) {
+    const int node = ps * kWave + lane;
+    nr.cpu_left[ps] = W.cpu_left0[node];
+    nr.mem_left[ps] = W.mem_left0[node];
+    nr.gpu_left[ps] = W.gpu_left0[node];
+    nr.cpu_total[ps] = W.cpu_total[node];
+    nr.mem_total[ps] = W.mem_total[node];
+    nr.ngpus[ps] = W.ngpus[node];
+#pragma unroll
+    for (int j = 0; j < kGmax; ++j) {
+      nr.gml[ps][j] = W.gml_left0[node * kGmax + j];
+      nr.gmt[ps][j] = W.gml_total[node * kGmax + j];
+    }
+  }
+  // waiting histogram over gpu_milli classes: class k -> lane k%64, slot k/64
+  constexpr int KP = 4;  // up to 256 classes
+  int32_t wcnt[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) wcnt[k] = 0;
+
+  int64_t used_cpu = W.used_cpu0, used_mem = W.used_mem0, used_gcnt = W.used_gcnt0, used_gml = W.used_gmilli0;
+  FixedAccD acc[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) acc[k].init();
+  int64_t processed = 0, n_repush = 0, n_dropped = 0, max_nodes = 0;
+  double thr = W.snapshot_interval;
+  uint64_t hsh = 0xcbf29ce484222325ull;
+  int32_t exc = EXC_NONE;
+  int n = N;
+  __syncthreads();
+
+  while (n > 0) {
+    // ---------------- pop
+    const uint64_t top = uniu64(heap[0]);
+    const uint64_t last = uniu64(heap[n - 1]);
+    --n;
+    if (n > 0) heap_siftup_root(heap, n, last, lb);
+
+    const int kind = (int)(top & 3);
+    const int rank = (int)((top >> lb) & ((1ull << rb) - 1));
+    const int64_t t = (int64_t)(top >> tshift);
+    const int4 prec = W.pod[rank];
+    PodView pod;
+    pod.cpu = prec.x; pod.mem = prec.y; pod.dur = prec.z;
+    pod.gmilli = prec.w & 0xFFFF; pod.ngpu = (prec.w >> 16) & 0xFF; pod.cls = (prec.w >> 24) & 0xFF;
+    pod.ctime = t; pod.rank = rank;
+
+    if (kind == kDelete) {
+      const int node = (int)((top >> 2) & ((1u << nb) - 1));
+      const int mask = (int)((top >> (2 + nb)) & 0xFF);
+#pragma unroll
+      for (int ps = 0; ps < NPASS; ++ps) {
+        if (ps * kWave + lane == node) {
+          nr.cpu_left[ps] += pod.cpu;
+          nr.mem_left[ps] += pod.mem;
+          nr.gpu_left[ps] += pod.ngpu;
+#pragma unroll
+          for (int j = 0; j < kGmax; ++j)
+            if ((mask >> j) & 1) nr.gml[ps][j] += pod.gmilli;
+        }
+      }
+      used_cpu -= pod.cpu; used_mem -= pod.mem; used_gcnt -= pod.ngpu;
+      used_gml -= (int64_t)pod.gmilli * __builtin_popcount(mask);
+      hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 1, (uint64_t)t);
+    } else {
+      // ---------------- creation: score all nodes, argmax (first node wins ties)
+      int64_t best = 0;
+      int best_node = -1;
+#pragma unroll
+      for (int ps = 0; ps < NPASS; ++ps) {
+        const bool valid = (ps * kWave + lane) < W.n_nodes;
+        int lexc = EXC_NONE;
+        int64_t s = valid ? scorer.template score<NPASS>(ps, nr, pod, lexc) : 0;
+        if (!valid) lexc = EXC_NONE;
+        const uint64_t bad = ballot(lexc != EXC_NONE);
+        if (bad) { exc = readlane(lexc, first_lane(bad)); break; }
+        const int64_t m = wave_max64(s);
+        if (m > best) {
+          best = m;
+          best_node = ps * kWave + first_lane(ballot(s == m));
+        }
+      }
+      if (exc != EXC_NONE) break;
+
+      if (best_node < 0) {
+        // ---------------- failed placement
+        if (kind == kFresh && pod.ngpu > 0) {
+#pragma unroll
+          for (int k = 0; k < KP; ++k)
+            if (k * kWave + lane == pod.cls) wcnt[k] += 1;
+        }
+        // fragmentation: min gpu_milli over waiting GPU pods, stranded milli below it
+        double frag = 0.0;
+        int mcls = -1;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+          const uint64_t b = ballot(wcnt[k] > 0);
+          if (mcls < 0 && b) mcls = k * kWave + first_lane(b);
+        }
+        if (mcls >= 0) {
+          const int m = W.class_value[mcls];
+          int64_t stranded = 0;
+#pragma unroll
+          for (int ps = 0; ps < NPASS; ++ps)
+#pragma unroll
+            for (int j = 0; j < kGmax; ++j) {
+              const int l = nr.gml[ps][j];
+              if (j < nr.ngpus[ps] && 0 < l && l < m) stranded += l;
+            }
+          stranded = uni64(wave_sum64(stranded));
+          frag = W.tot_gmilli > 0 ? (double)stranded / (double)W.tot_gmilli : 0.0;
+        }
+        acc[4].add(frag);
+        // repush: first DELETION in heap-array order (or the earliest one)
+        int64_t anchor = -1;
+        if (!W.repush_earliest) {
+          for (int base = 0; base < n; base += kWave) {
+            const int i = base + lane;
+            const bool del = i < n && (heap[i] & 3) == kDelete;
+            const uint64_t b = ballot(del);
+            if (b) {
+              const int f = base + first_lane(b);
+              anchor = (int64_t)(uniu64(heap[f]) >> tshift);
+              break;
+            }
+          }
+        } else {
+          int64_t mn = INT64_MAX;
+          for (int base = 0; base < n; base += kWave) {
+            const int i = base + lane;
+            int64_t tv = INT64_MAX;
+            if (i < n) { uint64_t k = heap[i]; if ((k & 3) == kDelete) tv = (int64_t)(k >> tshift); }
+            tv = -wave_max64(-tv);
+            mn = tv < mn ? tv : mn;
+          }
+          anchor = mn == INT64_MAX ? -1 : mn;
+        }
+        if (anchor >= 0) {
+          const uint64_t nt = (uint64_t)(anchor + 1);
+          if (nt > time_max) { exc = EXC_UNSUPPORTED; break; }
+          const uint64_t key = (nt << tshift) | ((uint64_t)rank << lb) | kRetry;
+          heap_siftdown(heap, 0, n, key, lb);
+          ++n;
+          ++n_repush;
+        } else {
+          ++n_dropped;
+        }
+        hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 2, (uint64_t)t);
+      } else {
+        // ---------------- commit on best_node
+        const int bp = best_node / kWave, bl = best_node % kWave;
+        int gmask = 0;
+        int ok = 1;
+        if (pod.ngpu > 0) {
+          // every lane selects for its own node; lane bl of pass bp is used
+          int mymask = 0, myok = 1;
+#pragma unroll
+          for (int ps = 0; ps < NPASS; ++ps) {
+            if (ps != bp) continue;
+            int cnt = 0;
+#pragma unroll
+            for (int j = 0; j < kGmax; ++j) cnt += (j < nr.ngpus[ps] && nr.gml[ps][j] >= pod.gmilli);
+            myok = cnt >= pod.ngpu;
+#pragma unroll
+            for (int j = 0; j < kGmax; ++j) {
+              const bool vj = j < nr.ngpus[ps] && nr.gml[ps][j] >= pod.gmilli;
+              int r = 0;
+              if (W.first_fit_alloc) {
+#pragma unroll
+                for (int i = 0; i < kGmax; ++i)
+                  r += (i < j && i < nr.ngpus[ps] && nr.gml[ps][i] >= pod.gmilli);
+              } else {
+#pragma unroll
+                for (int i = 0; i < kGmax; ++i) {
+                  const bool vi = i < nr.ngpus[ps] && nr.gml[ps][i] >= pod.gmilli;
+                  r += vi && (nr.gml[ps][i] < nr.gml[ps][j] || (nr.gml[ps][i] == nr.gml[ps][j] && i < j));
+                }
+              }
+              if (vj && r < pod.ngpu) mymask |= 1 << j;
+            }
+          }
+          gmask = readlane(mymask, bl);
+          ok = readlane(myok, bl);
+        }
+        if (!ok) { exc = EXC_ALLOC; break; }
+#pragma unroll
+        for (int ps = 0; ps < NPASS; ++ps) {
+          if (ps == bp && lane == bl) {
+            nr.cpu_left[ps] -= pod.cpu;
+            nr.mem_left[ps] -= pod.mem;
+            nr.gpu_left[ps] -= pod.ngpu;
+#pragma unroll
+            for (int j = 0; j < kGmax; ++j)
+              if ((gmask >> j) & 1) nr.gml[ps][j] -= pod.gmilli;
+          }
+        }
+        used_cpu += pod.cpu; used_mem += pod.mem; used_gcnt += pod.ngpu;
+        used_gml += (int64_t)pod.gmilli * __builtin_popcount(gmask);
+        if (kind == kRetry && pod.ngpu > 0) {
+#pragma unroll
+          for (int k = 0; k < KP; ++k)
+            if (k * kWave + lane == pod.cls) wcnt[k] -= 1;
+        }
+        const uint64_t dt = (uint64_t)(t + pod.dur);
+        if (t + pod.dur < 0 || dt > time_max) { exc = EXC_UNSUPPORTED; break; }
+        const uint64_t key = (dt << tshift) | ((uint64_t)rank << lb) |
+                             ((uint64_t)gmask << (2 + nb)) | ((uint64_t)best_node << 2) | kDelete;
+        heap_siftdown(heap, 0, n, key, lb);
+        ++n;
+        hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2), ((uint64_t)t << 8) ^ (uint64_t)best_node);
+      }
+    }
+
+    // ---------------- evaluator hook
+    ++processed;
+    const double progress = (double)processed / (double)N;
+    if (progress >= thr) {
+      const double r0 = W.tot_cpu > 0 ? (double)used_cpu / (double)W.tot_cpu : 0.0;
+      const double r1 = W.tot_mem > 0 ? (double)used_mem / (double)W.tot_mem : 0.0;
+      const double r2 = W.tot_gcnt > 0 ? (double)used_gcnt / (double)W.tot_gcnt : 0.0;
+      const double r3 = W.tot_gmilli > 0 ? (double)used_gml / (double)W.tot_gmilli : 0.0;
+      acc[0].add(r0); acc[1].add(r1); acc[2].add(r2); acc[3].add(r3);
+      thr += W.snapshot_interval;
+    }
+    // active nodes (max_nodes; informational)
+    int active = 0;
+#pragma unroll
+    for (int ps = 0; ps < NPASS; ++ps) {
+      const bool valid = (ps * kWave + lane) < W.n_nodes;
+      const bool a = valid && (nr.cpu_left[ps] < nr.cpu_total[ps] || nr.mem_left[ps] < nr.mem_total[ps] ||
+                               nr.gpu_left[ps] < nr.ngpus[ps]);
+      active += __popcll(ballot(a));
+    }
+    max_nodes = active > max_nodes ? active : max_nodes;
+  }
+
+  if (lane == 0) {
+    out->n_events = processed;
+    out->n_snap = acc[0].count;
+    out->n_frag = acc[4].count;
+    out->n_unplaced = n_dropped;
+    out->n_repush = n_repush;
+    out->max_nodes = max_nodes;
+    out->hash = hsh;
+    out->exc = exc;
+    int inexact = 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      inexact |= acc[k].inexact;
+      out->acc_lo[k] = (uint64_t)(u128)acc[k].sum;
+      out->acc_hi[k] = (uint64_t)((u128)acc[k].sum >> 64);
+    }
+    out->inexact = inexact;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// k_eval_reduce: exact means -> EvaluationResults + policy score, one lane per
+// policy (reference simulator/evaluator.py:77-127).
+// out columns: score, avg_cpu, avg_mem, avg_gcnt, avg_gmilli, frag, n_snap, n_frag,
+//              n_events, n_unplaced, exc, inexact, hash_hi
+__global__ void k_eval_reduce(const DevResult* __restrict__ res, double* __restrict__ table, int P) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const DevResult r = res[p];
+  double* row = table + (size_t)p * 13;
+  double avg[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const i128 s = (i128)(((u128)r.acc_hi[k] << 64) | r.acc_lo[k]);
+    const int64_t c = k < 4 ? r.n_snap : r.n_frag;
+    avg[k] = c > 0 ? fixed_div_round_dev(s, (uint64_t)c) : 0.0;
+  }
+  double score = 0.0;
+  if (r.exc == EXC_NONE && r.n_snap > 0 && r.n_unplaced == 0) {
+    const double overall = (avg[0] + avg[1] + avg[2] + avg[3]) / 4.0;
+    const double pen = avg[4] < 0.1 ? avg[4] : 0.1;
+    double s = overall - pen;
+    s = s < 1.0 ? s : 1.0;
+    score = s > 0.0 ? s : 0.0;
+  }
+  row[0] = score;
+  row[1] = avg[0]; row[2] = avg[1]; row[3] = avg[2]; row[4] = avg[3]; row[5] = avg[4];
+  row[6] = (double)r.n_snap; row[7] = (double)r.n_frag; row[8] = (double)r.n_events;
+  row[9] = (double)r.n_unplaced; row[10] = (double)r.exc; row[11] = (double)r.inexact;
+  row[12] = (double)(r.hash >> 11);
+}
+
+}  // namespace fksd

@@ -1,0 +1,118 @@
+// Built-in policy families on the device (twins of csrc/cpu/builtin_scorers.hpp,
+// op-for-op, so the replays are bit-identical; compiled with
+// -ffp-contract=off: Python never fuses a multiply into an add).
+#pragma once
+
+#include "replay.hip.h"
+
+namespace fksd {
+
+enum BuiltinFamily : int32_t { FAM_FIRST_FIT = 0, FAM_BEST_FIT = 1, FAM_RANDOM_LINEAR = 2, FAM_FEATURE_LINEAR = 3 };
+constexpr int kFeatureCount = 12;
+constexpr int kWeights = 16;
+
+// int(max(0, s)) of a float score produced by `max(1, int(score))`-style code
+__device__ __forceinline__ int64_t trunc_score(double s, int& exc) {
+  if (isnan(s)) { exc = EXC_VALUE; return 0; }
+  if (isinf(s)) { exc = EXC_OVERFLOW; return 0; }
+  if (fabs(s) >= 9.2233720368547758e18) { exc = EXC_UNSUPPORTED; return 0; }
+  const int64_t v = (int64_t)s;
+  return v > 1 ? v : 1;
+}
+
+template <int NPASS>
+__device__ __forceinline__ bool feasible(int ps, const NodeRegs<NPASS>& nr, const PodView& pod) {
+  if (pod.cpu > nr.cpu_left[ps] || pod.mem > nr.mem_left[ps] || pod.ngpu > nr.gpu_left[ps]) return false;
+  if (pod.ngpu > 0) {
+    int avail = 0;
+#pragma unroll
+    for (int j = 0; j < kGmax; ++j) avail += (j < nr.ngpus[ps] && nr.gml[ps][j] >= pod.gmilli);
+    if (avail < pod.ngpu) return false;
+  }
+  return true;
+}
+
+struct BuiltinScorerDev {
+  int32_t family;
+  double w[kWeights];
+
+  template <int NPASS>
+  __device__ int64_t score(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, int& exc) const {
+    if (!feasible<NPASS>(ps, nr, pod)) return 0;
+    switch (family) {
+      case FAM_FIRST_FIT:
+        return 1000;
+      case FAM_BEST_FIT: {
+        const int64_t rc = (int64_t)nr.cpu_left[ps] - pod.cpu;
+        const int64_t rm = (int64_t)nr.mem_left[ps] - pod.mem;
+        const int64_t rg = (int64_t)nr.gpu_left[ps] - pod.ngpu;
+        if (nr.cpu_total[ps] == 0 || nr.mem_total[ps] == 0) { exc = EXC_ZERO_DIVISION; return 0; }
+        const double nc = (double)rc / (double)nr.cpu_total[ps];
+        const double nm = (double)rm / (double)nr.mem_total[ps];
+        const int gd = nr.ngpus[ps] > 1 ? nr.ngpus[ps] : 1;
+        const double ng = (double)rg / (double)gd;
+        const double t = nc * 0.33 + nm * 0.33;
+        const double nrm = t + ng * 0.34;
+        const double x = (1.0 - nrm) * 10000.0;
+        return trunc_score(x, exc);
+      }
+      case FAM_RANDOM_LINEAR: {
+        double s = w[0] + (double)nr.cpu_left[ps] * w[1];
+        s = s + (double)nr.mem_left[ps] * w[2];
+        if (pod.ngpu > 0 && nr.gpu_left[ps] > 0) s = s + (double)nr.gpu_left[ps] * w[3];
+        return trunc_score(s, exc);
+      }
+      case FAM_FEATURE_LINEAR: {
+        double f[kFeatureCount];
+        features<NPASS>(ps, nr, pod, f);
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < kFeatureCount; ++k)
+          if (w[k] != 0.0) s = s + w[k] * f[k];
+        return trunc_score(s, exc);
+      }
+    }
+    exc = EXC_UNSUPPORTED;
+    return 0;
+  }
+
+  template <int NPASS>
+  __device__ static void features(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, double* f) {
+    const int ng = nr.ngpus[ps];
+    const int64_t cpu_tot = nr.cpu_total[ps] > 1 ? nr.cpu_total[ps] : 1;
+    const int64_t mem_tot = nr.mem_total[ps] > 1 ? nr.mem_total[ps] : 1;
+    const int ngd = ng > 1 ? ng : 1;
+    f[0] = 1.0;
+    const double rc = (double)((int64_t)nr.cpu_left[ps] - pod.cpu) / (double)cpu_tot;
+    const double rm = (double)((int64_t)nr.mem_left[ps] - pod.mem) / (double)mem_tot;
+    f[1] = rc;
+    f[2] = rm;
+    f[3] = (double)((int64_t)nr.gpu_left[ps] - pod.ngpu) / (double)ngd;
+    f[4] = fabs(rc - rm);
+    int64_t free_m = 0, idle = 0, part = 0, best = -1;
+#pragma unroll
+    for (int j = 0; j < kGmax; ++j) {
+      if (j < ng) {
+        const int32_t l = nr.gml[ps][j];
+        free_m += l;
+        idle += (l == nr.gmt[ps][j]);
+        part += (0 < l && l < nr.gmt[ps][j]);
+        if (pod.ngpu > 0 && l >= pod.gmilli && (best < 0 || l - pod.gmilli < best)) best = l - pod.gmilli;
+      }
+    }
+    f[5] = (double)free_m / 1000.0;
+    {
+      const int64_t d = pod.gmilli > 1 ? pod.gmilli : 1;
+      int64_t m = free_m % d;
+      if (m != 0 && ((m < 0) != (d < 0))) m += d;
+      f[6] = (double)m / 1000.0;
+    }
+    f[7] = (double)idle / (double)ngd;
+    f[8] = (double)part / (double)ngd;
+    f[9] = (pod.ngpu == 0 && ng > 0) ? 1.0 : 0.0;
+    f[10] = best < 0 ? 0.0 : (double)best / 1000.0;
+    f[11] = (double)nr.cpu_total[ps] / 100000.0;
+  }
+};
+
+}  // namespace fksd

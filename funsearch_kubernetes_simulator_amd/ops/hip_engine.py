@@ -1,0 +1,208 @@
+"""Python front-end of the MI355X replay engine (``_fks_hip``).
+
+`DeviceEvaluator` turns a `Workload` into the device layout (pods relabelled
+by id rank, node / GPU state padded to 64-lane passes, the initial event heap
+heapified once on the host with CPython's own ``heapq``), uploads it to HBM
+once, and evaluates batches of policies -- built-in families (weights as
+data) or compiled bytecode programs -- with one k_replay workgroup per
+policy.
+
+On a GPU box the extension must load: there is no silent CPU fallback here
+(callers that want one use `engine.evaluate`, which routes explicitly).
+"""
+
+from __future__ import annotations
+
+import heapq
+import math
+import os
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ..core.arrays import Workload
+from ..policy.compiler import CompiledPolicy
+from .cpu_engine import FAMILY, RESULT_COLUMNS  # noqa: F401  (same table layout)
+
+GMAX = 8
+WEIGHTS_PER_POLICY = 16
+LDS_BYTES_PER_CU = 160 * 1024
+VREG_BYTES = 64 * 8  # one VM register: 64 lanes x 8 B
+
+_mod = None
+
+
+def native():
+    """Load ``_fks_hip`` (torch first, so the process shares torch's HIP runtime)."""
+    global _mod
+    if _mod is None:
+        try:
+            import torch  # noqa: F401
+        except Exception:
+            pass
+        if os.environ.get("FKS_NO_AUTOBUILD") != "1":
+            from .build import build_hip
+            build_hip()
+        from . import _fks_hip  # noqa: F401
+        _mod = _fks_hip
+    return _mod
+
+
+def device_available() -> bool:
+    try:
+        return native().device_count() > 0
+    except Exception:
+        return False
+
+
+class UnsupportedWorkload(ValueError):
+    """The workload exceeds a device-layout limit (the CPU engine handles it)."""
+
+
+def _bits(n: int) -> int:
+    return max(1, int(math.ceil(math.log2(max(2, n)))))
+
+
+def prepare_device_workload(w: Workload) -> Dict[str, object]:
+    c, p = w.cluster, w.pods
+    N, P = c.n_nodes, p.n_pods
+    if N == 0 or P == 0:
+        raise UnsupportedWorkload("empty workload")
+    if N > 256:
+        raise UnsupportedWorkload("more than 256 nodes")
+    if c.max_gpus_per_node > GMAX:
+        raise UnsupportedWorkload(f"more than {GMAX} GPUs on a node")
+    if len(np.unique(p.pod_rank)) != P:
+        raise UnsupportedWorkload("duplicate pod ids")
+    if P * 8 > LDS_BYTES_PER_CU - 4096:
+        raise UnsupportedWorkload("trace longer than the LDS-resident heap")
+    for name, arr in (("cpu", c.node_cpu_total), ("mem", c.node_mem_total), ("pcpu", p.pod_cpu),
+                      ("pmem", p.pod_mem), ("dur", p.pod_dur), ("ctime", p.pod_ctime)):
+        if arr.size and (arr.max() >= 2 ** 31 or arr.min() < -(2 ** 31)):
+            raise UnsupportedWorkload(f"{name} outside int32")
+    if p.pod_ctime.min() < 0 or p.pod_dur.min() < 0:
+        raise UnsupportedWorkload("negative times")
+    if p.pod_gmilli.max(initial=0) >= 2 ** 16 or p.pod_gmilli.min(initial=0) < 0 \
+            or p.pod_ngpu.max(initial=0) >= 2 ** 8 or p.pod_ngpu.min(initial=0) < 0:
+        raise UnsupportedWorkload("gpu request outside the packed pod record")
+    npass = 1 if N <= 64 else (2 if N <= 128 else 4)
+    NP = 64 * npass
+
+    def pad(a, dtype):
+        out = np.zeros(NP, dtype=dtype)
+        out[:N] = a
+        return out
+
+    gml_total = np.zeros((NP, GMAX), dtype=np.int32)
+    gml_left = np.zeros((NP, GMAX), dtype=np.int32)
+    gmem_total = np.zeros((NP, GMAX), dtype=np.int64)
+    for i in range(N):
+        a, b = int(c.gpu_start[i]), int(c.gpu_start[i + 1])
+        gml_total[i, :b - a] = c.gpu_milli_total[a:b]
+        gml_left[i, :b - a] = c.gpu_milli_left[a:b]
+        gmem_total[i, :b - a] = c.gpu_mem_total[a:b]
+
+    gpu_pods = p.pod_ngpu > 0
+    classes = np.unique(p.pod_gmilli[gpu_pods]).astype(np.int32)
+    if classes.size > 256:
+        raise UnsupportedWorkload("more than 256 distinct gpu_milli requests")
+    if classes.size == 0:
+        classes = np.zeros(1, dtype=np.int32)
+    cls = np.searchsorted(classes, p.pod_gmilli).astype(np.int64)
+    cls[~gpu_pods] = 0
+
+    order = np.argsort(p.pod_rank, kind="stable")           # by rank
+    rec = np.zeros((P, 4), dtype=np.int32)
+    rec[:, 0] = p.pod_cpu[order]
+    rec[:, 1] = p.pod_mem[order]
+    rec[:, 2] = p.pod_dur[order]
+    rec[:, 3] = (p.pod_gmilli[order].astype(np.int64) | (p.pod_ngpu[order].astype(np.int64) << 16)
+                 | (cls[order] << 24)).astype(np.int64).astype(np.uint32).view(np.int32)
+
+    rank_bits, node_bits = _bits(P), _bits(N)
+    low_bits = 2 + node_bits + GMAX
+    time_bits = 64 - rank_bits - low_bits
+    if int(p.pod_ctime.max()) + int(p.pod_dur.max()) >= 2 ** min(time_bits, 62):
+        raise UnsupportedWorkload("times exceed the packed key")
+    items = [(int(t), int(r)) for t, r in zip(p.pod_ctime, p.pod_rank)]
+    heapq.heapify(items)   # CPython's heapify on (time, rank): the reference's initial layout
+    heap0 = np.array([(t << (rank_bits + low_bits)) | (r << low_bits) for t, r in items], dtype=np.uint64)
+
+    used = dict(
+        used_cpu=int((c.node_cpu_total - c.node_cpu_left).sum()),
+        used_mem=int((c.node_mem_total - c.node_mem_left).sum()),
+        used_gcnt=int((c.node_ngpus.astype(np.int64) - c.node_gpu_left).sum()),
+        used_gmilli=int((c.gpu_milli_total.astype(np.int64) - c.gpu_milli_left).sum()),
+    )
+    return dict(
+        n_nodes=N, n_pods=P, n_classes=int(classes.size), npass=npass,
+        cpu_total=pad(c.node_cpu_total, np.int32), cpu_left=pad(c.node_cpu_left, np.int32),
+        mem_total=pad(c.node_mem_total, np.int32), mem_left=pad(c.node_mem_left, np.int32),
+        gpu_left=pad(c.node_gpu_left, np.int32), ngpus=pad(c.node_ngpus, np.int32),
+        gml_total=gml_total, gml_left=gml_left, gmem_total=gmem_total,
+        pod=rec, pod_ctime=p.pod_ctime[order].astype(np.int32), heap0=heap0, class_value=classes,
+        tot_cpu=int(c.node_cpu_total.sum()), tot_mem=int(c.node_mem_total.sum()),
+        tot_gcnt=int(c.node_ngpus.sum()), tot_gmilli=int(c.gpu_milli_total.astype(np.int64).sum()),
+        rank_bits=rank_bits, node_bits=node_bits, low_bits=low_bits, time_bits=time_bits, **used,
+    )
+
+
+def pack_programs(progs: Sequence[CompiledPolicy]):
+    """Concatenate bytecode + constant pools for one device launch."""
+    codes, offsets, lengths, kpay, koff, ktag = [], [], [], [], [], []
+    pos = kpos = 0
+    for prg in progs:
+        offsets.append(pos)
+        lengths.append(prg.n_insns)
+        koff.append(kpos)
+        codes.append(prg.code)
+        pos += prg.n_insns
+        for f, i, t in zip(prg.fconst, prg.iconst, prg.ctag):
+            kpay.append(int(np.array(f, dtype=np.float64).view(np.int64)) if t == 1 else int(i))
+            ktag.append(t)
+        kpos += len(prg.ctag)
+    return (b"".join(codes), np.array(offsets, np.int32), np.array(lengths, np.int32),
+            np.array(kpay or [0], np.int64), np.array(koff, np.int32), np.array(ktag or [0], np.uint8))
+
+
+class DeviceEvaluator:
+    """A workload resident on one MI355X, evaluating policy batches."""
+
+    def __init__(self, workload: Workload, device: int = 0, options: Optional[dict] = None):
+        self.workload = workload
+        self.device = device
+        self.layout = prepare_device_workload(workload)
+        self._eng = native().DeviceEngine(self.layout, device)
+        if options:
+            self._eng.set_options(dict(options))
+
+    def info(self) -> dict:
+        return dict(self._eng.info())
+
+    def set_options(self, **opts) -> None:
+        self._eng.set_options(opts)
+
+    def evaluate_builtin(self, family: "str | Sequence[str]", weights: Optional[np.ndarray] = None,
+                         n: Optional[int] = None) -> np.ndarray:
+        if isinstance(family, str):
+            count = n if n is not None else (len(weights) if weights is not None else 1)
+            fam = np.full(count, FAMILY[family], dtype=np.int32)
+        else:
+            fam = np.array([FAMILY[f] for f in family], dtype=np.int32)
+        W = np.zeros((len(fam), WEIGHTS_PER_POLICY), dtype=np.float64)
+        if weights is not None:
+            weights = np.asarray(weights, dtype=np.float64).reshape(len(fam), -1)
+            W[:, :weights.shape[1]] = weights
+        return self._eng.evaluate_builtin(fam, W)
+
+    def evaluate_programs(self, progs: Sequence[CompiledPolicy]) -> np.ndarray:
+        if not progs:
+            return np.zeros((0, len(RESULT_COLUMNS)))
+        nregs = max(p.nregs for p in progs)
+        return self._eng.evaluate_programs(*pack_programs(progs), nregs)
+
+    def launch_builtin_async(self, n: int) -> None:
+        self._eng.launch_builtin_async(n)
+
+    def synchronize(self) -> None:
+        self._eng.synchronize()
