@@ -23,7 +23,7 @@ cpu = ce.simulate_builtin_batch(w, "random_linear", wts[:64])
 print(json.dumps({"cpu_gpu_equal_64": bool(np.array_equal(cpu, tab[:64]))}), flush=True)
 names = list(reference_policies()); progs = [compile_policy(reference_policies()[n]) for n in names]
 t = time.time(); tv = dev.evaluate_programs(progs); dt = time.time() - t
-print(json.dumps({"vm": {n: [tv[i, 0], tv[i, 0] == reference_scores()[n], int(tv[i, 10])] for i, n in enumerate(names)}, "vm_s": dt}), flush=True)
+print(json.dumps({"vm": {n: [float(tv[i, 0]), bool(tv[i, 0] == reference_scores()[n]), int(tv[i, 10])] for i, n in enumerate(names)}, "vm_s": dt}), flush=True)
 progs256 = [progs[i % 5] for i in range(1024)]
 dev.evaluate_programs(progs256[:8])
 t = time.time(); tv = dev.evaluate_programs(progs256); dt = time.time() - t
