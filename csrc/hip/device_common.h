@@ -45,6 +45,48 @@ __device__ __forceinline__ int64_t wave_sum64(int64_t v) {
   for (int m = 32; m >= 1; m >>= 1) v += shfl_xor64(v, m);
   return v;
 }
+// ---- DPP (register-crossbar) reductions: no LDS round trip --------------------
+// Classic GFX9 wave64 reduction ladder: row_shr 1/2/3, row_shr 4 (bank mask),
+// row_shr 8 (bank mask), row_bcast 15, row_bcast 31; the full result lands in
+// lane 63.  Lanes without a DPP source keep `old` = the identity.
+template <int CTRL, int ROW_MASK, int BANK_MASK>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v, uint64_t ident) {
+  const int lo = __builtin_amdgcn_update_dpp((int)(uint32_t)ident, (int)(uint32_t)v, CTRL, ROW_MASK, BANK_MASK, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(uint32_t)(ident >> 32), (int)(uint32_t)(v >> 32), CTRL, ROW_MASK,
+                                             BANK_MASK, false);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+struct OpMaxU64 {
+  static constexpr uint64_t ident = 0;
+  __device__ static uint64_t f(uint64_t a, uint64_t b) { return a > b ? a : b; }
+};
+struct OpSumU64 {
+  static constexpr uint64_t ident = 0;
+  __device__ static uint64_t f(uint64_t a, uint64_t b) { return a + b; }
+};
+template <class Op>
+__device__ __forceinline__ uint64_t wave_reduce_dpp(uint64_t v) {
+  const uint64_t x = v;                                // first three read the ORIGINAL values
+  v = Op::f(v, dpp64<0x111, 0xF, 0xF>(x, Op::ident));  // row_shr:1
+  v = Op::f(v, dpp64<0x112, 0xF, 0xF>(x, Op::ident));  // row_shr:2
+  v = Op::f(v, dpp64<0x113, 0xF, 0xF>(x, Op::ident));  // row_shr:3
+  v = Op::f(v, dpp64<0x114, 0xF, 0xE>(v, Op::ident));  // row_shr:4 bank_mask 0xe
+  v = Op::f(v, dpp64<0x118, 0xF, 0xC>(v, Op::ident));  // row_shr:8 bank_mask 0xc
+  v = Op::f(v, dpp64<0x142, 0xA, 0xF>(v, Op::ident));  // row_bcast:15 row_mask 0xa
+  v = Op::f(v, dpp64<0x143, 0xC, 0xF>(v, Op::ident));  // row_bcast:31 row_mask 0xc
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) { return wave_reduce_dpp<OpMaxU64>(v); }
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) { return (int64_t)wave_reduce_dpp<OpSumU64>((uint64_t)v); }
+// swap adjacent lane pairs (quad_perm [1,0,3,2])
+__device__ __forceinline__ uint64_t swap_pairs64(uint64_t v) {
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)v, 0xB1, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), 0xB1, 0xF, 0xF, false);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ int first_lane(uint64_t m) { return __ffsll((unsigned long long)m) - 1; }
 

@@ -1,0 +1,126 @@
+// Wave-parallel CPython heapq on an LDS-resident u64 key array.
+//
+// CPython's heappop/_siftup walks root->leaf always taking the smaller child
+// (the right one when !(left < right)), moves each chosen child up one
+// level, drops the last element at the leaf and bubbles it up (_siftdown).
+// The chosen path depends only on the ORIGINAL array, so the wave gathers
+// whole 5-level subtrees below the current path end (62 lanes, one
+// ds_read_b64), decides every left/right choice of the subtree at once
+// (sibling exchange by DPP + one ballot) and follows the path with a few
+// scalar bit operations; the final bubble-up position is a ballot over the
+// path values and all writes land in one parallel store.  heappush's bubble-up
+// likewise gathers all ancestors at once: their values are sorted along the
+// path, so the insertion depth is a popcount.
+//
+// The resulting array is bit-identical to CPython's after every operation
+// (the repush rule observes the layout), verified against the serial code
+// and the CPU oracle.  A parallel bitmap marks the slots holding DELETION
+// events so "first deletion in array order" is a ballot over 64-word chunks.
+#pragma once
+
+#include "device_common.h"
+
+namespace fksd {
+
+constexpr int kDelKind = 2;
+
+__device__ __forceinline__ bool key_lt(uint64_t a, uint64_t b, int lb) { return (a >> lb) < (b >> lb); }
+
+struct WaveHeap {
+  uint64_t* h;        // keys
+  uint32_t* delmap;   // bit p set <=> h[p] is a deletion
+  int lb;             // low (payload) bits below the (time, rank) compare key
+
+  __device__ __forceinline__ void mark(int pos, uint64_t v) const {
+    const uint32_t bit = 1u << (pos & 31);
+    if ((v & 3) == kDelKind) atomicOr(&delmap[pos >> 5], bit);
+    else atomicAnd(&delmap[pos >> 5], ~bit);
+  }
+
+  // Removes the root of a heap that holds n+1 items; `last` (= old h[n]) is
+  // re-inserted (CPython: heap.pop(); heap[0] = last; _siftup(heap, 0)).
+  // n = new size (>= 1).
+  __device__ void pop_reinsert(int n, uint64_t last) const {
+    const int lane = lane_id();
+    // lane l in [0, 62): subtree level r (1..5), index i within the level
+    const int r = lane < 2 ? 1 : lane < 6 ? 2 : lane < 14 ? 3 : lane < 30 ? 4 : 5;
+    const int i = lane - ((1 << r) - 2);
+    int pos = 0;        // current path end (uniform)
+    int k = 0;          // path length (uniform)
+    int my_pos = 0;     // lane l (1..k): position p_l of path entry l
+    uint64_t my_val = 0;  //               and its original value v_l
+    for (;;) {
+      if (2 * pos + 1 >= n) break;
+      const int idx = ((pos + 1) << r) - 1 + i;
+      const bool valid = lane < 62 && idx < n;
+      const uint64_t v = valid ? h[idx] : ~0ull;
+      const uint64_t sib = swap_pairs64(v);
+      // even lanes hold left children: go right iff right exists and !(L < R)
+      const bool go_right = ((lane & 1) == 0) && valid && (idx + 1 < n) && !key_lt(v, sib, lb);
+      const uint64_t right_mask = ballot(go_right);
+      int cur = 0;   // index at the previous relative level
+      bool leaf = false;
+#pragma unroll
+      for (int lv = 1; lv <= 5; ++lv) {
+        const int left_idx = ((pos + 1) << lv) - 1 + 2 * cur;
+        if (left_idx >= n) { leaf = true; break; }
+        const int left_lane = (1 << lv) - 2 + 2 * cur;
+        const int choose = (int)((right_mask >> left_lane) & 1);
+        cur = 2 * cur + choose;
+        const int take_lane = left_lane + choose;
+        const uint64_t val = (uint64_t)readlane64((int64_t)v, take_lane);
+        ++k;
+        if (lane == k) { my_pos = left_idx + choose; my_val = val; }
+      }
+      pos = readlane(my_pos, k);
+      if (leaf) break;
+    }
+    // bubble `last` up: first path index m >= 1 with last < v_m; target j = m-1
+    const bool gt = lane >= 1 && lane <= k && key_lt(last, my_val, lb);
+    const uint64_t g = ballot(gt);
+    const int j = g ? first_lane(g) - 1 : k;
+    // moves: v_l -> p_{l-1} for 1 <= l <= j ; last -> p_j
+    int prev_pos = __builtin_amdgcn_update_dpp(0, my_pos, 0x111, 0xF, 0xF, false);  // row_shr:1 (lanes 1..15)
+    if (lane == 1) prev_pos = 0;
+    if (lane >= 1 && lane <= j) { h[prev_pos] = my_val; mark(prev_pos, my_val); }
+    const int pj = j == 0 ? 0 : readlane(my_pos, j);
+    if (lane == 0) { h[pj] = last; mark(pj, last); }
+  }
+
+  // CPython heappush on a heap of n items (item lands at index <= n).
+  __device__ void push(int n, uint64_t item) const {
+    const int lane = lane_id();
+    // ancestors a_l = ((n+1) >> l) - 1, l >= 1, exist while (n+1) >> l >= 1
+    const int l = lane + 1;
+    const int anc = lane < 30 ? ((n + 1) >> l) - 1 : -1;
+    const bool valid = anc >= 0 && n > 0;
+    const uint64_t v = valid ? h[anc] : 0;
+    const bool gt = valid && key_lt(item, v, lb);
+    const int J = __popcll(ballot(gt));        // sorted path: a prefix from the bottom
+    // moves: v_l -> a_{l-1} (a_0 = n) for l <= J ; item -> a_J
+    const int dst = lane < 30 ? ((n + 1) >> (l - 1)) - 1 : 0;
+    if (gt) { h[dst] = v; mark(dst, v); }
+    const int aJ = J == 0 ? n : ((n + 1) >> J) - 1;
+    if (lane == 0) { h[aJ] = item; mark(aJ, item); }
+  }
+
+  // index of the first DELETION in h[0, n), or -1
+  __device__ int first_deletion(int n) const {
+    const int lane = lane_id();
+    const int words = (n + 31) >> 5;
+    for (int base = 0; base < words; base += kWave) {
+      const int wi = base + lane;
+      uint32_t w = wi < words ? delmap[wi] : 0u;
+      if (wi == words - 1 && (n & 31)) w &= (1u << (n & 31)) - 1;   // stale bits past the end
+      const uint64_t b = ballot(w != 0);
+      if (b) {
+        const int fl = first_lane(b);
+        const uint32_t fw = (uint32_t)readlane((int)w, fl);
+        return ((base + fl) << 5) + (__ffs(fw) - 1);
+      }
+    }
+    return -1;
+  }
+};
+
+}  // namespace fksd

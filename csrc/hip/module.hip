@@ -56,6 +56,74 @@ __global__ __launch_bounds__(64) void k_replay_vm(DevWorkload W, DevProgramTable
   replay_one<NPASS>(W, sc, heap, out + p);
 }
 
+// Phase-profiled variants (s_memtime per phase; diagnostics only, NPASS = 1).
+__global__ __launch_bounds__(64) void k_replay_builtin_prof(DevWorkload W, const int32_t* __restrict__ fam,
+                                                            const double* __restrict__ weights, DevResult* out,
+                                                            uint64_t* prof) {
+  extern __shared__ uint64_t heap[];
+  const int p = blockIdx.x;
+  BuiltinScorerDev sc;
+  sc.family = fam[p];
+#pragma unroll
+  for (int k = 0; k < kWeights; ++k) sc.w[k] = weights[(size_t)p * kWeights + k];
+  replay_one<1, BuiltinScorerDev, PhaseProf>(W, sc, heap, out + p, prof + (size_t)p * 8);
+}
+
+__global__ __launch_bounds__(64) void k_replay_vm_prof(DevWorkload W, DevProgramTable T, DevResult* out,
+                                                       int64_t budget, uint64_t* prof) {
+  extern __shared__ uint64_t heap[];
+  const int p = blockIdx.x;
+  VmScorerDev sc;
+  sc.init(T, p, W, budget);
+  replay_one<1, VmScorerDev, PhaseProf>(W, sc, heap, out + p, prof + (size_t)p * 8);
+}
+
+// ---- primitive self-tests (one wave) ----------------------------------------------
+// out[0] = wave max, out[1] = wave sum, out[2..65] = pair-swapped values,
+// out[66..129] = row_shr:1 of the low 32 bits
+__global__ __launch_bounds__(64) void k_test_wave_ops(const uint64_t* in, uint64_t* out) {
+  const int lane = lane_id();
+  const uint64_t v = in[lane];
+  const uint64_t m = wave_max_u64(v);
+  const int64_t s = wave_sum_i64((int64_t)v);
+  const uint64_t sw = swap_pairs64(v);
+  const int sh = __builtin_amdgcn_update_dpp(-1, (int)(uint32_t)v, 0x111, 0xF, 0xF, false);
+  if (lane == 0) { out[0] = m; out[1] = (uint64_t)s; }
+  out[2 + lane] = sw;
+  out[66 + lane] = (uint64_t)(int64_t)sh;
+}
+
+// Run a sequence of heap operations (op >= 0: push key op; op < 0: pop) on the
+// wave-parallel LDS heap; returns the final array (size in out_n).
+__global__ __launch_bounds__(64) void k_test_heap(const uint64_t* init, int n0, const int64_t* ops, int nops,
+                                                   int lb, uint64_t* out, int* out_n, uint64_t* popped) {
+  extern __shared__ uint64_t lds[];
+  const int lane = lane_id();
+  WaveHeap hp;
+  hp.h = lds;
+  hp.delmap = reinterpret_cast<uint32_t*>(lds + 4096);
+  hp.lb = lb;
+  for (int i = lane; i < n0; i += 64) lds[i] = init[i];
+  for (int i = lane; i < 256; i += 64) hp.delmap[i] = 0;
+  __syncthreads();
+  int n = n0, np = 0;
+  for (int k = 0; k < nops; ++k) {
+    const int64_t op = ops[k];
+    if (op >= 0) { hp.push(n, (uint64_t)op); ++n; }
+    else if (n > 0) {
+      const uint64_t top = uniu64(lds[0]);
+      const uint64_t last = uniu64(lds[n - 1]);
+      --n;
+      if (n > 0) hp.pop_reinsert(n, last);
+      if (lane == 0) popped[np] = top;
+      ++np;
+    }
+  }
+  __syncthreads();
+  for (int i = lane; i < n; i += 64) out[i] = lds[i];
+  if (lane == 0) *out_n = n;
+}
+
 template <class T>
 T* dev_upload(const py::array& a, hipStream_t s, std::vector<void*>& owned) {
   py::buffer_info bi = a.request();
@@ -93,6 +161,9 @@ class DeviceEngine {
     W_.pod_ctime = dev_upload<int32_t>(arr("pod_ctime"), stream_, owned_);
     W_.heap0 = dev_upload<uint64_t>(arr("heap0"), stream_, owned_);
     W_.class_value = dev_upload<int32_t>(arr("class_value"), stream_, owned_);
+    W_.snap_fire = dev_upload<int64_t>(arr("snap_fire"), stream_, owned_);
+    W_.n_fire = (int32_t)arr("snap_fire").size();
+    W_.thr_after_fire = d["thr_after_fire"].cast<double>();
     W_.tot_cpu = geti("tot_cpu"); W_.tot_mem = geti("tot_mem");
     W_.tot_gcnt = geti("tot_gcnt"); W_.tot_gmilli = geti("tot_gmilli");
     W_.used_cpu0 = geti("used_cpu"); W_.used_mem0 = geti("used_mem");
@@ -101,7 +172,7 @@ class DeviceEngine {
     W_.low_bits = (int32_t)geti("low_bits"); W_.time_bits = (int32_t)geti("time_bits");
     W_.snapshot_interval = 0.05;
     HIP_OK(hipStreamSynchronize(stream_));
-    lds_bytes_ = (size_t)W_.n_pods * sizeof(uint64_t);
+    lds_bytes_ = (size_t)lds_heap_entries(W_.n_pods) * sizeof(uint64_t) + (size_t)lds_delmap_words(W_.n_pods) * 4;
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, device_));
     num_cus_ = prop.multiProcessorCount;
@@ -113,7 +184,7 @@ class DeviceEngine {
     set_lds_attr(reinterpret_cast<const void*>(&k_replay_builtin<2>), lds_bytes_);
     set_lds_attr(reinterpret_cast<const void*>(&k_replay_builtin<4>), lds_bytes_);
     // VM launches add the virtual register file behind the (64-aligned) heap
-    heap_pad_bytes_ = (size_t)((W_.n_pods + 63) & ~63) * sizeof(uint64_t);
+    heap_pad_bytes_ = (size_t)lds_vreg_offset(W_.n_pods) * sizeof(uint64_t);
     const size_t vm_max = (size_t)160 * 1024;
     set_lds_attr(reinterpret_cast<const void*>(&k_replay_vm<1>), vm_max);
     set_lds_attr(reinterpret_cast<const void*>(&k_replay_vm<2>), vm_max);
@@ -167,6 +238,48 @@ class DeviceEngine {
       launch_vm(P, lds);
     }
     return collect(P);
+  }
+
+  // Per-policy phase cycle counts (s_memtime) of a builtin or program batch.
+  py::tuple profile(py::object fam_or_none, py::object weights_or_none, py::object programs_or_none) {
+    if (npass_ != 1) throw std::invalid_argument("profiling supports <= 64 nodes");
+    HIP_OK(hipSetDevice(device_));
+    int P;
+    uint64_t* d_prof = nullptr;
+    if (!programs_or_none.is_none()) {
+      py::tuple t = programs_or_none.cast<py::tuple>();
+      auto offsets = t[1].cast<py::array_t<int32_t>>();
+      P = (int)offsets.size();
+      int nregs = t[6].cast<int>();
+      ensure_batch(P);
+      std::string code = t[0].cast<py::bytes>();
+      upload_programs(code, offsets, t[2].cast<py::array_t<int32_t>>(), t[3].cast<py::array_t<int64_t>>(),
+                      t[4].cast<py::array_t<int32_t>>(), t[5].cast<py::array_t<uint8_t>>());
+      HIP_OK(hipMalloc(&d_prof, (size_t)P * 8 * 8));
+      DevProgramTable T{reinterpret_cast<const uint64_t*>(d_code_), reinterpret_cast<const int32_t*>(d_poff_),
+                        reinterpret_cast<const int64_t*>(d_kpay_), reinterpret_cast<const uint8_t*>(d_ktag_)};
+      const size_t lds = heap_pad_bytes_ + (size_t)nregs * 64 * 8;
+      set_lds_attr(reinterpret_cast<const void*>(&k_replay_vm_prof), (size_t)160 * 1024);
+      hipLaunchKernelGGL(k_replay_vm_prof, dim3(P), dim3(64), lds, stream_, W_, T, d_res_, budget_, d_prof);
+    } else {
+      auto fam = fam_or_none.cast<py::array_t<int32_t, py::array::c_style | py::array::forcecast>>();
+      auto weights = weights_or_none.cast<py::array_t<double, py::array::c_style | py::array::forcecast>>();
+      P = (int)fam.size();
+      ensure_batch(P);
+      HIP_OK(hipMemcpyAsync(d_fam_, fam.data(), (size_t)P * 4, hipMemcpyHostToDevice, stream_));
+      HIP_OK(hipMemcpyAsync(d_w_, weights.data(), (size_t)P * kWeights * 8, hipMemcpyHostToDevice, stream_));
+      HIP_OK(hipMalloc(&d_prof, (size_t)P * 8 * 8));
+      set_lds_attr(reinterpret_cast<const void*>(&k_replay_builtin_prof), lds_bytes_);
+      hipLaunchKernelGGL(k_replay_builtin_prof, dim3(P), dim3(64), lds_bytes_, stream_, W_, d_fam_, d_w_, d_res_,
+                         d_prof);
+    }
+    HIP_OK(hipGetLastError());
+    hipLaunchKernelGGL(k_eval_reduce, dim3((P + 63) / 64), dim3(64), 0, stream_, d_res_, d_tab_, P);
+    py::array_t<uint64_t> prof({(py::ssize_t)P, (py::ssize_t)8});
+    HIP_OK(hipMemcpyAsync(prof.mutable_data(), d_prof, (size_t)P * 64, hipMemcpyDeviceToHost, stream_));
+    py::array_t<double> tab = collect(P);
+    HIP_OK(hipFree(d_prof));
+    return py::make_tuple(tab, prof);
   }
 
   // Launch only (no host sync / copy-back): for timing loops and graph capture.
@@ -293,6 +406,49 @@ class DeviceEngine {
   void* d_ktag_ = nullptr; size_t ktag_cap_ = 0;
 };
 
+py::array_t<uint64_t> test_wave_ops(py::array_t<uint64_t, py::array::c_style | py::array::forcecast> vals) {
+  if (vals.size() != 64) throw std::invalid_argument("need 64 values");
+  uint64_t *din = nullptr, *dout = nullptr;
+  HIP_OK(hipMalloc(&din, 64 * 8));
+  HIP_OK(hipMalloc(&dout, 130 * 8));
+  HIP_OK(hipMemcpy(din, vals.data(), 64 * 8, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_test_wave_ops, dim3(1), dim3(64), 0, 0, din, dout);
+  HIP_OK(hipGetLastError());
+  py::array_t<uint64_t> out(130);
+  HIP_OK(hipMemcpy(out.mutable_data(), dout, 130 * 8, hipMemcpyDeviceToHost));
+  (void)hipFree(din);
+  (void)hipFree(dout);
+  return out;
+}
+
+py::tuple test_heap(py::array_t<uint64_t, py::array::c_style | py::array::forcecast> init,
+                    py::array_t<int64_t, py::array::c_style | py::array::forcecast> ops, int lb) {
+  const int n0 = (int)init.size(), nops = (int)ops.size();
+  if (n0 + nops > 4096) throw std::invalid_argument("test heap too large");
+  uint64_t *di, *dout, *dpop;
+  int64_t* dops;
+  int* dn;
+  HIP_OK(hipMalloc(&di, (n0 + 1) * 8));
+  HIP_OK(hipMalloc(&dops, (nops + 1) * 8));
+  HIP_OK(hipMalloc(&dout, 4096 * 8));
+  HIP_OK(hipMalloc(&dpop, (nops + 1) * 8));
+  HIP_OK(hipMalloc(&dn, 4));
+  if (n0) HIP_OK(hipMemcpy(di, init.data(), n0 * 8, hipMemcpyHostToDevice));
+  if (nops) HIP_OK(hipMemcpy(dops, ops.data(), nops * 8, hipMemcpyHostToDevice));
+  const size_t lds = 4096 * 8 + 1024;
+  HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_test_heap), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)lds));
+  hipLaunchKernelGGL(k_test_heap, dim3(1), dim3(64), lds, 0, di, n0, dops, nops, lb, dout, dn, dpop);
+  HIP_OK(hipGetLastError());
+  int n = 0;
+  HIP_OK(hipMemcpy(&n, dn, 4, hipMemcpyDeviceToHost));
+  py::array_t<uint64_t> out(n), popped(nops);
+  if (n) HIP_OK(hipMemcpy(out.mutable_data(), dout, (size_t)n * 8, hipMemcpyDeviceToHost));
+  if (nops) HIP_OK(hipMemcpy(popped.mutable_data(), dpop, (size_t)nops * 8, hipMemcpyDeviceToHost));
+  for (void* p : {(void*)di, (void*)dops, (void*)dout, (void*)dpop, (void*)dn}) (void)hipFree(p);
+  return py::make_tuple(out, popped);
+}
+
 int device_count() {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -304,11 +460,14 @@ int device_count() {
 PYBIND11_MODULE(_fks_hip, m) {
   m.doc() = "MI355X replay kernels of funsearch_kubernetes_simulator_amd";
   m.def("device_count", &device_count);
+  m.def("test_wave_ops", &test_wave_ops);
+  m.def("test_heap", &test_heap);
   py::class_<DeviceEngine>(m, "DeviceEngine")
       .def(py::init<py::dict, int>(), py::arg("workload"), py::arg("device") = 0)
       .def("set_options", &DeviceEngine::set_options)
       .def("evaluate_builtin", &DeviceEngine::evaluate_builtin)
       .def("evaluate_programs", &DeviceEngine::evaluate_programs)
+      .def("profile", &DeviceEngine::profile)
       .def("launch_builtin_async", &DeviceEngine::launch_builtin_async)
       .def("synchronize", &DeviceEngine::synchronize)
       .def("info", &DeviceEngine::info);

@@ -5,27 +5,32 @@
 //       key = time << (RB+LB) | rank << LB | gpu_mask << (2+NB) | node << 2 | kind
 //     compared on (key >> LB) = (time, pod rank): exactly the reference's
 //     (time, pod_id) tuple order (simulator/event_simulator.py:16-17), and
-//     manipulated with CPython's heapq algorithms so the array layout -- which
-//     the repush rule observes -- is bit-identical to the reference's;
+//     manipulated with CPython's heapq algorithms -- wave-parallel, see
+//     heap_wave.h -- so the array layout, which the repush rule observes, is
+//     bit-identical to the reference's;
 //   * lanes = nodes (64 x NPASS nodes); each lane keeps its node's cpu / mem /
 //     GPU-count / per-GPU-milli state in VGPRs, so scoring, the placement
-//     argmax (wave max + ballot/ffs for the first-node tie-break), best-fit GPU
-//     selection, fragmentation sums and active-node counts are register-only;
+//     argmax (DPP wave max + ballot/ffs for the first-node tie-break),
+//     best-fit GPU selection, fragmentation sums and active-node counts are
+//     register-only;
 //   * the waiting-pod multiset needed by the fragmentation metric is a
 //     per-lane histogram over the distinct gpu_milli classes, its minimum a
 //     ballot; membership is carried by the heap entry itself (kind 1 =
 //     re-queued creation = the pod is waiting);
-//   * the evaluator's utilisation / fragmentation means are accumulated in
-//     exact 128-bit fixed point and finished by k_eval_reduce.
+//   * snapshot triggers come from a host-precomputed schedule (the same IEEE
+//     `processed / total >= threshold`, `threshold += 0.05` sequence), and the
+//     evaluator's means are accumulated in exact 128-bit fixed point and
+//     finished by k_eval_reduce.
+// LDS per policy: heap (N padded to 64) | deletion bitmap | [VM registers].
 // The scorer (built-in families, or the bytecode VM) is a template argument.
 #pragma once
 
 #include "device_common.h"
+#include "heap_wave.h"
 
 namespace fksd {
 
 constexpr int kGmax = 8;        // GPUs per node held in registers
-constexpr int kKinds = 2;       // kind field bits
 constexpr int kFresh = 0, kRetry = 1, kDelete = 2;
 
 enum ExcCode : int32_t {
@@ -34,7 +39,7 @@ enum ExcCode : int32_t {
 };
 
 struct DevWorkload {
-  int32_t n_nodes, n_pods, n_classes, pad0;
+  int32_t n_nodes, n_pods, n_classes, n_fire;
   const int32_t* cpu_total;   // [64*NPASS]
   const int32_t* cpu_left0;
   const int32_t* mem_total;
@@ -45,13 +50,15 @@ struct DevWorkload {
   const int32_t* gml_left0;   // [node][kGmax]
   const int64_t* gmem_total;  // [node][kGmax] (GPU memory MiB, read-only field)
   const int4* pod;            // by rank: {cpu, mem, dur, gmilli | ngpu<<16 | cls<<24}
-  const int32_t* pod_ctime;   // by rank: original creation time (pod.creation_time of fresh events)
+  const int32_t* pod_ctime;   // by rank: original creation time
   const uint64_t* heap0;      // initial heapified keys
   const int32_t* class_value; // ascending distinct gpu_milli of GPU pods
+  const int64_t* snap_fire;   // processed-event counts that trigger snapshots 0..n_fire-1
   int64_t tot_cpu, tot_mem, tot_gcnt, tot_gmilli;
   int64_t used_cpu0, used_mem0, used_gcnt0, used_gmilli0;
   int32_t rank_bits, node_bits, low_bits, time_bits;
   double snapshot_interval;
+  double thr_after_fire;      // threshold value after the last precomputed snapshot
   int32_t repush_earliest, first_fit_alloc, truncate, pad1;
 };
 
@@ -62,6 +69,13 @@ struct DevResult {
   uint64_t acc_lo[5];
   uint64_t acc_hi[5];
 };
+
+// LDS layout helpers (in u64 units)
+__host__ __device__ inline int lds_heap_entries(int n_pods) { return (n_pods + 63) & ~63; }
+__host__ __device__ inline int lds_delmap_words(int n_pods) { return (((n_pods + 31) >> 5) + 63) & ~63; }
+__host__ __device__ inline int lds_vreg_offset(int n_pods) {
+  return lds_heap_entries(n_pods) + lds_delmap_words(n_pods) / 2;
+}
 
 // Per-lane view of node state handed to a scorer.
 template <int NPASS>
@@ -77,46 +91,78 @@ struct PodView {
   int32_t rank;
 };
 
-// Scorer contract:  score(pass, node_regs, pod, valid) -> int64 priority after
-// int(max(0, s)) truncation, exceptions reported through `exc`.
+// Scorer contract:  score<NPASS>(pass, node_regs, pod, exc) -> int64 priority
+// after int(max(0, s)) truncation (>= 0), exceptions reported through `exc`.
 
 // ----------------------------------------------------------------------------
-// LDS heap, CPython heapq algorithms.  Every lane executes the same uniform
-// operations (broadcast LDS reads, same-address writes).
-__device__ __forceinline__ uint64_t hkey(uint64_t k, int lb) { return k >> lb; }
-
-__device__ __forceinline__ void heap_siftdown(uint64_t* h, int startpos, int pos, uint64_t item, int lb) {
-  const uint64_t ik = hkey(item, lb);
-  while (pos > startpos) {
-    int parent = (pos - 1) >> 1;
-    uint64_t p = h[parent];
-    if (ik < hkey(p, lb)) { h[pos] = p; pos = parent; continue; }
-    break;
+// Phase profiler (s_memtime deltas; compiled out with NoProf).
+struct NoProf {
+  __device__ void start() {}
+  __device__ void mark(int) {}
+  __device__ void flush(uint64_t*) {}
+};
+struct PhaseProf {
+  uint64_t acc[8];
+  uint64_t last;
+  __device__ void start() {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0;
+    last = __builtin_amdgcn_s_memtime();
   }
-  h[pos] = item;
-}
+  __device__ void mark(int ph) {
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    acc[ph] += now - last;
+    last = now;
+  }
+  __device__ void flush(uint64_t* o) {
+    if (lane_id() == 0)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = acc[k];
+  }
+};
+enum Phase { PH_POP = 0, PH_DELETE = 1, PH_SCORE = 2, PH_FAIL = 3, PH_COMMIT = 4, PH_EVAL = 5 };
 
-// _siftup(heap, 0) with heap[0] := item, heap size n
-__device__ __forceinline__ void heap_siftup_root(uint64_t* h, int n, uint64_t item, int lb) {
-  int pos = 0;
-  int child = 1;
-  while (child < n) {
-    int right = child + 1;
-    uint64_t c = h[child];
-    if (right < n) {
-      uint64_t r = h[right];
-      if (!(hkey(c, lb) < hkey(r, lb))) { child = right; c = r; }
+// GPU pick on one node (lane-local): mask of the `need` tightest-fitting
+// eligible GPUs (stable: ties by index) or the first `need` eligible GPUs.
+template <int NPASS>
+__device__ __forceinline__ int pick_gpus(const NodeRegs<NPASS>& nr, int ps, int gm, int need, bool first_fit,
+                                         int& ok) {
+  const int ng = nr.ngpus[ps];
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < kGmax; ++j) cnt += (j < ng && nr.gml[ps][j] >= gm);
+  ok = cnt >= need;
+  int mask = 0;
+  if (need == 1 && !first_fit) {
+    int best = -1, bv = 0;
+#pragma unroll
+    for (int j = 0; j < kGmax; ++j) {
+      const int l = nr.gml[ps][j];
+      if (j < ng && l >= gm && (best < 0 || l < bv)) { best = j; bv = l; }
     }
-    h[pos] = c;
-    pos = child;
-    child = 2 * pos + 1;
+    mask = best >= 0 ? (1 << best) : 0;
+    return mask;
   }
-  heap_siftdown(h, 0, pos, item, lb);
+#pragma unroll
+  for (int j = 0; j < kGmax; ++j) {
+    const bool vj = j < ng && nr.gml[ps][j] >= gm;
+    int r = 0;
+#pragma unroll
+    for (int i = 0; i < kGmax; ++i) {
+      const bool vi = i < ng && nr.gml[ps][i] >= gm;
+      r += first_fit ? (vi && i < j)
+                     : (vi && (nr.gml[ps][i] < nr.gml[ps][j] || (nr.gml[ps][i] == nr.gml[ps][j] && i < j)));
+    }
+    if (vj && r < need) mask |= 1 << j;
+  }
+  return mask;
 }
 
 // ----------------------------------------------------------------------------
-template <int NPASS, class Scorer>
-__device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* heap, DevResult* out) {
+template <int NPASS, class Scorer, class Prof = NoProf>
+__device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* lds, DevResult* out,
+                           uint64_t* prof_out = nullptr) {
+  Prof prof;
   const int lane = lane_id();
   const int lb = W.low_bits, nb = W.node_bits;
   const int rb = W.rank_bits;
@@ -124,7 +170,12 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* heap,
   const uint64_t time_max = (W.time_bits >= 63) ? ~0ull : ((1ull << W.time_bits) - 1);
   const int N = W.n_pods;
 
-  for (int i = lane; i < N; i += kWave) heap[i] = W.heap0[i];
+  WaveHeap heap;
+  heap.h = lds;
+  heap.delmap = reinterpret_cast<uint32_t*>(lds + lds_heap_entries(N));
+  heap.lb = lb;
+  for (int i = lane; i < N; i += kWave) lds[i] = W.heap0[i];
+  for (int i = lane; i < lds_delmap_words(N); i += kWave) heap.delmap[i] = 0u;
 
   NodeRegs<NPASS> nr;
 #pragma unroll
@@ -153,27 +204,31 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* heap,
 #pragma unroll
   for (int k = 0; k < 5; ++k) acc[k].init();
   int64_t processed = 0, n_repush = 0, n_dropped = 0, max_nodes = 0;
-  double thr = W.snapshot_interval;
+  int ksnap = 0;
+  int64_t next_fire = W.n_fire > 0 ? W.snap_fire[0] : INT64_MAX;
+  double thr = W.thr_after_fire;   // used once the precomputed schedule is exhausted
   uint64_t hsh = 0xcbf29ce484222325ull;
   int32_t exc = EXC_NONE;
   int n = N;
   __syncthreads();
+  prof.start();
 
   while (n > 0) {
-    // ---------------- pop
-    const uint64_t top = uniu64(heap[0]);
-    const uint64_t last = uniu64(heap[n - 1]);
+    // ---------------- pop (pod record load issued first, consumed after the sift)
+    const uint64_t top = uniu64(lds[0]);
+    const int rank = (int)((top >> lb) & ((1ull << rb) - 1));
+    const int4 prec = W.pod[rank];
+    const uint64_t last = uniu64(lds[n - 1]);
     --n;
-    if (n > 0) heap_siftup_root(heap, n, last, lb);
+    if (n > 0) heap.pop_reinsert(n, last);
 
     const int kind = (int)(top & 3);
-    const int rank = (int)((top >> lb) & ((1ull << rb) - 1));
     const int64_t t = (int64_t)(top >> tshift);
-    const int4 prec = W.pod[rank];
     PodView pod;
     pod.cpu = prec.x; pod.mem = prec.y; pod.dur = prec.z;
     pod.gmilli = prec.w & 0xFFFF; pod.ngpu = (prec.w >> 16) & 0xFF; pod.cls = (prec.w >> 24) & 0xFF;
     pod.ctime = t; pod.rank = rank;
+    prof.mark(PH_POP);
 
     if (kind == kDelete) {
       const int node = (int)((top >> 2) & ((1u << nb) - 1));
@@ -192,6 +247,7 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* heap,
       used_cpu -= pod.cpu; used_mem -= pod.mem; used_gcnt -= pod.ngpu;
       used_gml -= (int64_t)pod.gmilli * __builtin_popcount(mask);
       hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 1, (uint64_t)t);
+      prof.mark(PH_DELETE);
     } else {
       // ---------------- creation: score all nodes, argmax (first node wins ties)
       int64_t best = 0;
@@ -204,13 +260,14 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* heap,
         if (!valid) lexc = EXC_NONE;
         const uint64_t bad = ballot(lexc != EXC_NONE);
         if (bad) { exc = readlane(lexc, first_lane(bad)); break; }
-        const int64_t m = wave_max64(s);
+        const int64_t m = (int64_t)wave_max_u64((uint64_t)s);   // scores are >= 0
         if (m > best) {
           best = m;
           best_node = ps * kWave + first_lane(ballot(s == m));
         }
       }
       if (exc != EXC_NONE) break;
+      prof.mark(PH_SCORE);
 
       if (best_node < 0) {
         // ---------------- failed placement
@@ -237,78 +294,47 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* heap,
               const int l = nr.gml[ps][j];
               if (j < nr.ngpus[ps] && 0 < l && l < m) stranded += l;
             }
-          stranded = uni64(wave_sum64(stranded));
+          stranded = wave_sum_i64(stranded);
           frag = W.tot_gmilli > 0 ? (double)stranded / (double)W.tot_gmilli : 0.0;
         }
         acc[4].add(frag);
         // repush: first DELETION in heap-array order (or the earliest one)
         int64_t anchor = -1;
         if (!W.repush_earliest) {
-          for (int base = 0; base < n; base += kWave) {
-            const int i = base + lane;
-            const bool del = i < n && (heap[i] & 3) == kDelete;
-            const uint64_t b = ballot(del);
-            if (b) {
-              const int f = base + first_lane(b);
-              anchor = (int64_t)(uniu64(heap[f]) >> tshift);
-              break;
-            }
-          }
+          const int f = heap.first_deletion(n);
+          if (f >= 0) anchor = (int64_t)(uniu64(lds[f]) >> tshift);
         } else {
-          int64_t mn = INT64_MAX;
+          uint64_t mn = ~0ull;
           for (int base = 0; base < n; base += kWave) {
             const int i = base + lane;
-            int64_t tv = INT64_MAX;
-            if (i < n) { uint64_t k = heap[i]; if ((k & 3) == kDelete) tv = (int64_t)(k >> tshift); }
-            tv = -wave_max64(-tv);
+            uint64_t tv = ~0ull;
+            if (i < n) { const uint64_t k = lds[i]; if ((k & 3) == kDelete) tv = k >> tshift; }
+            tv = ~wave_max_u64(~tv);
             mn = tv < mn ? tv : mn;
           }
-          anchor = mn == INT64_MAX ? -1 : mn;
+          anchor = mn == ~0ull ? -1 : (int64_t)mn;
         }
         if (anchor >= 0) {
           const uint64_t nt = (uint64_t)(anchor + 1);
           if (nt > time_max) { exc = EXC_UNSUPPORTED; break; }
-          const uint64_t key = (nt << tshift) | ((uint64_t)rank << lb) | kRetry;
-          heap_siftdown(heap, 0, n, key, lb);
+          heap.push(n, (nt << tshift) | ((uint64_t)rank << lb) | kRetry);
           ++n;
           ++n_repush;
         } else {
           ++n_dropped;
         }
         hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 2, (uint64_t)t);
+        prof.mark(PH_FAIL);
       } else {
         // ---------------- commit on best_node
         const int bp = best_node / kWave, bl = best_node % kWave;
         int gmask = 0;
         int ok = 1;
         if (pod.ngpu > 0) {
-          // every lane selects for its own node; lane bl of pass bp is used
           int mymask = 0, myok = 1;
 #pragma unroll
-          for (int ps = 0; ps < NPASS; ++ps) {
-            if (ps != bp) continue;
-            int cnt = 0;
-#pragma unroll
-            for (int j = 0; j < kGmax; ++j) cnt += (j < nr.ngpus[ps] && nr.gml[ps][j] >= pod.gmilli);
-            myok = cnt >= pod.ngpu;
-#pragma unroll
-            for (int j = 0; j < kGmax; ++j) {
-              const bool vj = j < nr.ngpus[ps] && nr.gml[ps][j] >= pod.gmilli;
-              int r = 0;
-              if (W.first_fit_alloc) {
-#pragma unroll
-                for (int i = 0; i < kGmax; ++i)
-                  r += (i < j && i < nr.ngpus[ps] && nr.gml[ps][i] >= pod.gmilli);
-              } else {
-#pragma unroll
-                for (int i = 0; i < kGmax; ++i) {
-                  const bool vi = i < nr.ngpus[ps] && nr.gml[ps][i] >= pod.gmilli;
-                  r += vi && (nr.gml[ps][i] < nr.gml[ps][j] || (nr.gml[ps][i] == nr.gml[ps][j] && i < j));
-                }
-              }
-              if (vj && r < pod.ngpu) mymask |= 1 << j;
-            }
-          }
+          for (int ps = 0; ps < NPASS; ++ps)
+            if (ps == bp) mymask = pick_gpus<NPASS>(nr, ps, pod.gmilli, pod.ngpu, W.first_fit_alloc != 0, myok);
           gmask = readlane(mymask, bl);
           ok = readlane(myok, bl);
         }
@@ -333,24 +359,28 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* heap,
         }
         const uint64_t dt = (uint64_t)(t + pod.dur);
         if (t + pod.dur < 0 || dt > time_max) { exc = EXC_UNSUPPORTED; break; }
-        const uint64_t key = (dt << tshift) | ((uint64_t)rank << lb) |
-                             ((uint64_t)gmask << (2 + nb)) | ((uint64_t)best_node << 2) | kDelete;
-        heap_siftdown(heap, 0, n, key, lb);
+        heap.push(n, (dt << tshift) | ((uint64_t)rank << lb) | ((uint64_t)gmask << (2 + nb)) |
+                         ((uint64_t)best_node << 2) | kDelete);
         ++n;
         hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2), ((uint64_t)t << 8) ^ (uint64_t)best_node);
+        prof.mark(PH_COMMIT);
       }
     }
 
-    // ---------------- evaluator hook
+    // ---------------- evaluator hook (snapshot schedule precomputed on the host)
     ++processed;
-    const double progress = (double)processed / (double)N;
-    if (progress >= thr) {
+    bool fire;
+    if (ksnap < W.n_fire) fire = processed >= next_fire;
+    else fire = (double)processed / (double)N >= thr;
+    if (fire) {
       const double r0 = W.tot_cpu > 0 ? (double)used_cpu / (double)W.tot_cpu : 0.0;
       const double r1 = W.tot_mem > 0 ? (double)used_mem / (double)W.tot_mem : 0.0;
       const double r2 = W.tot_gcnt > 0 ? (double)used_gcnt / (double)W.tot_gcnt : 0.0;
       const double r3 = W.tot_gmilli > 0 ? (double)used_gml / (double)W.tot_gmilli : 0.0;
       acc[0].add(r0); acc[1].add(r1); acc[2].add(r2); acc[3].add(r3);
-      thr += W.snapshot_interval;
+      if (ksnap >= W.n_fire) thr += W.snapshot_interval;
+      ++ksnap;
+      next_fire = ksnap < W.n_fire ? W.snap_fire[ksnap] : INT64_MAX;
     }
     // active nodes (max_nodes; informational)
     int active = 0;
@@ -362,7 +392,9 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* heap,
       active += __popcll(ballot(a));
     }
     max_nodes = active > max_nodes ? active : max_nodes;
+    prof.mark(PH_EVAL);
   }
+  if (prof_out) prof.flush(prof_out);
 
   if (lane == 0) {
     out->n_events = processed;

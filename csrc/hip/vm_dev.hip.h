@@ -332,7 +332,7 @@ struct VmScorerDev {
     budget = bud;
     limited = bud > 0;
     extern __shared__ uint64_t lds_all[];
-    vregs = lds_all + ((W.n_pods + 63) & ~63);
+    vregs = lds_all + lds_vreg_offset(W.n_pods);
   }
 
   template <int NPASS>

@@ -63,7 +63,28 @@ def _bits(n: int) -> int:
     return max(1, int(math.ceil(math.log2(max(2, n)))))
 
 
-def prepare_device_workload(w: Workload) -> Dict[str, object]:
+def snapshot_schedule(total_events: int, interval: float = 0.05, count: int = 4096):
+    """Processed-event counts at which the reference evaluator snapshots.
+
+    Replays `evaluator.py:55-67` exactly: snapshot k fires at the first event
+    count c after the previous snapshot with ``c / total >= thr_k`` (IEEE
+    division, the same as Python's int/int), and ``thr`` advances by repeated
+    ``+= interval``.  Returns (fire counts, threshold after the last one)."""
+    fire = np.zeros(count, dtype=np.int64)
+    thr, prev = interval, 0
+    for k in range(count):
+        c = max(prev + 1, int(thr * total_events) - 2)
+        while c - 1 > prev and (c - 1) / total_events >= thr:
+            c -= 1
+        while c / total_events < thr:
+            c += 1
+        fire[k] = c
+        prev = c
+        thr += interval
+    return fire, thr
+
+
+def prepare_device_workload(w: Workload, snapshot_interval: float = 0.05) -> Dict[str, object]:
     c, p = w.cluster, w.pods
     N, P = c.n_nodes, p.n_pods
     if N == 0 or P == 0:
@@ -134,7 +155,9 @@ def prepare_device_workload(w: Workload) -> Dict[str, object]:
         used_gcnt=int((c.node_ngpus.astype(np.int64) - c.node_gpu_left).sum()),
         used_gmilli=int((c.gpu_milli_total.astype(np.int64) - c.gpu_milli_left).sum()),
     )
+    fire, thr_after = snapshot_schedule(P, snapshot_interval)
     return dict(
+        snap_fire=fire, thr_after_fire=float(thr_after),
         n_nodes=N, n_pods=P, n_classes=int(classes.size), npass=npass,
         cpu_total=pad(c.node_cpu_total, np.int32), cpu_left=pad(c.node_cpu_left, np.int32),
         mem_total=pad(c.node_mem_total, np.int32), mem_left=pad(c.node_mem_left, np.int32),
@@ -171,15 +194,21 @@ class DeviceEvaluator:
     def __init__(self, workload: Workload, device: int = 0, options: Optional[dict] = None):
         self.workload = workload
         self.device = device
-        self.layout = prepare_device_workload(workload)
+        options = dict(options or {})
+        interval = float(options.get("snapshot_interval", 0.05))
+        self.layout = prepare_device_workload(workload, interval)
         self._eng = native().DeviceEngine(self.layout, device)
-        if options:
-            self._eng.set_options(dict(options))
+        options["snapshot_interval"] = interval
+        self._eng.set_options(options)
+        self.options = options
 
     def info(self) -> dict:
         return dict(self._eng.info())
 
     def set_options(self, **opts) -> None:
+        if "snapshot_interval" in opts and opts["snapshot_interval"] != self.options["snapshot_interval"]:
+            raise ValueError("snapshot_interval is baked into the device schedule; build a new DeviceEvaluator")
+        self.options.update(opts)
         self._eng.set_options(opts)
 
     def evaluate_builtin(self, family: "str | Sequence[str]", weights: Optional[np.ndarray] = None,
@@ -200,6 +229,19 @@ class DeviceEvaluator:
             return np.zeros((0, len(RESULT_COLUMNS)))
         nregs = max(p.nregs for p in progs)
         return self._eng.evaluate_programs(*pack_programs(progs), nregs)
+
+    PHASES = ("pop", "delete", "score", "fail", "commit", "eval")
+
+    def profile_builtin(self, family: str, weights: np.ndarray):
+        """(result table, per-policy cycle counts [P, 8] by PHASES)."""
+        fam = np.full(len(weights), FAMILY[family], dtype=np.int32)
+        W = np.zeros((len(fam), WEIGHTS_PER_POLICY), dtype=np.float64)
+        W[:, :np.asarray(weights).shape[1]] = weights
+        return self._eng.profile(fam, W, None)
+
+    def profile_programs(self, progs: Sequence[CompiledPolicy]):
+        packed = pack_programs(progs) + (max(p.nregs for p in progs),)
+        return self._eng.profile(None, None, packed)
 
     def launch_builtin_async(self, n: int) -> None:
         self._eng.launch_builtin_async(n)
