@@ -87,6 +87,18 @@ __device__ __forceinline__ uint64_t swap_pairs64(uint64_t v) {
   return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
+// Vector load whose address the compiler must treat as divergent: the result
+// stays in VGPRs and is waited for (vmcnt) only where it is first used, so a
+// uniform load can be issued early and overlap LDS work instead of being
+// hoisted into SGPRs with an immediate wait.
+__device__ __forceinline__ int4 load_vgpr(const int4* p) {
+  const uint64_t a = (uint64_t)p;
+  uint32_t lo = (uint32_t)a;
+  asm volatile("v_mov_b32 %0, %0" : "+v"(lo));
+  const int4* q = reinterpret_cast<const int4*>((a & 0xFFFFFFFF00000000ull) | lo);
+  return *q;
+}
+
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ int first_lane(uint64_t m) { return __ffsll((unsigned long long)m) - 1; }
 

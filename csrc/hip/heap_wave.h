@@ -45,46 +45,76 @@ struct WaveHeap {
     // lane l in [0, 62): subtree level r (1..5), index i within the level
     const int r = lane < 2 ? 1 : lane < 6 ? 2 : lane < 14 ? 3 : lane < 30 ? 4 : 5;
     const int i = lane - ((1 << r) - 2);
-    int pos = 0;        // current path end (uniform)
-    int k = 0;          // path length (uniform)
-    int my_pos = 0;     // lane l (1..k): position p_l of path entry l
-    uint64_t my_val = 0;  //               and its original value v_l
-    for (;;) {
-      if (2 * pos + 1 >= n) break;
+    // Up to 4 rounds of 5 levels (depth <= 20, n < 2^20): each round keeps its
+    // gathered values; a lane is ON the path when its subtree index equals the
+    // path choice at its level (computed with scalar bit ops from one ballot).
+    constexpr int kRounds = 4;
+    uint64_t val[kRounds];
+    int posv[kRounds];
+    bool on[kRounds];
+    int start[kRounds + 1];  // path-end position entering each round
+    int lev[kRounds];        // levels taken in each round
+    int pos = 0, rounds = 0;
+#pragma unroll
+    for (int rd = 0; rd < kRounds; ++rd) {
+      start[rd] = pos;
+      val[rd] = 0; posv[rd] = 0; on[rd] = false; lev[rd] = 0;
+      if (rd > 0 && (lev[rd - 1] < 5 || rounds < rd)) continue;   // previous round hit a leaf
+      if (2 * pos + 1 >= n) continue;
+      rounds = rd + 1;
       const int idx = ((pos + 1) << r) - 1 + i;
       const bool valid = lane < 62 && idx < n;
       const uint64_t v = valid ? h[idx] : ~0ull;
       const uint64_t sib = swap_pairs64(v);
-      // even lanes hold left children: go right iff right exists and !(L < R)
       const bool go_right = ((lane & 1) == 0) && valid && (idx + 1 < n) && !key_lt(v, sib, lb);
       const uint64_t right_mask = ballot(go_right);
-      int cur = 0;   // index at the previous relative level
-      bool leaf = false;
+      // scalar walk: path index per level, bit-packed (cur at level lv in bits)
+      int cur = 0, taken = 0;
+      uint32_t path_code = 0;  // 5 bits per level: index within level
 #pragma unroll
       for (int lv = 1; lv <= 5; ++lv) {
         const int left_idx = ((pos + 1) << lv) - 1 + 2 * cur;
-        if (left_idx >= n) { leaf = true; break; }
-        const int left_lane = (1 << lv) - 2 + 2 * cur;
-        const int choose = (int)((right_mask >> left_lane) & 1);
-        cur = 2 * cur + choose;
-        const int take_lane = left_lane + choose;
-        const uint64_t val = (uint64_t)readlane64((int64_t)v, take_lane);
-        ++k;
-        if (lane == k) { my_pos = left_idx + choose; my_val = val; }
+        if (taken == lv - 1 && left_idx < n) {
+          const int left_lane = (1 << lv) - 2 + 2 * cur;
+          cur = 2 * cur + (int)((right_mask >> left_lane) & 1);
+          path_code |= (uint32_t)cur << (5 * (lv - 1));
+          taken = lv;
+        }
       }
-      pos = readlane(my_pos, k);
-      if (leaf) break;
+      lev[rd] = taken;
+      const int my_cur = (int)((path_code >> (5 * (r - 1))) & 31);
+      on[rd] = lane < 62 && r <= taken && i == my_cur;
+      val[rd] = v;
+      posv[rd] = idx;
+      pos = ((pos + 1) << taken) - 1 + cur;   // new path end
     }
-    // bubble `last` up: first path index m >= 1 with last < v_m; target j = m-1
-    const bool gt = lane >= 1 && lane <= k && key_lt(last, my_val, lb);
-    const uint64_t g = ballot(gt);
-    const int j = g ? first_lane(g) - 1 : k;
-    // moves: v_l -> p_{l-1} for 1 <= l <= j ; last -> p_j
-    int prev_pos = __builtin_amdgcn_update_dpp(0, my_pos, 0x111, 0xF, 0xF, false);  // row_shr:1 (lanes 1..15)
-    if (lane == 1) prev_pos = 0;
-    if (lane >= 1 && lane <= j) { h[prev_pos] = my_val; mark(prev_pos, my_val); }
-    const int pj = j == 0 ? 0 : readlane(my_pos, j);
-    if (lane == 0) { h[pj] = last; mark(pj, last); }
+    // bubble `last` up: first path entry (in path order) with last < v; it
+    // and everything below keep their values, `last` lands on its parent slot
+    int jr = -1, jl = 0;   // round / lane of the first such entry
+#pragma unroll
+    for (int rd = 0; rd < kRounds; ++rd) {
+      const uint64_t g = ballot(on[rd] && key_lt(last, val[rd], lb));
+      if (jr < 0 && g) { jr = rd; jl = first_lane(g); }
+    }
+    // moves: every path entry ABOVE the first greater one moves to its parent
+    int target;  // slot receiving `last`
+    if (jr < 0) {
+      target = pos;  // last path entry (leaf) -- all entries moved up
+    } else {
+      const int lvl = jl < 2 ? 1 : jl < 6 ? 2 : jl < 14 ? 3 : jl < 30 ? 4 : 5;
+      const int idx_j = ((start[jr] + 1) << lvl) - 1 + (jl - ((1 << lvl) - 2));
+      target = (idx_j - 1) >> 1;   // its parent: path entry j-1 (or the root)
+    }
+#pragma unroll
+    for (int rd = 0; rd < kRounds; ++rd) {
+      const bool above = jr < 0 || rd < jr || (rd == jr && lane < jl);
+      if (on[rd] && above) {
+        const int parent = (posv[rd] - 1) >> 1;
+        h[parent] = val[rd];
+        mark(parent, val[rd]);
+      }
+    }
+    if (lane == 0) { h[target] = last; mark(target, last); }
   }
 
   // CPython heappush on a heap of n items (item lands at index <= n).

@@ -160,8 +160,10 @@ __device__ __forceinline__ int pick_gpus(const NodeRegs<NPASS>& nr, int ps, int 
 
 // ----------------------------------------------------------------------------
 template <int NPASS, class Scorer, class Prof = NoProf>
-__device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* lds, DevResult* out,
+__device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* hbuf, uint32_t* delmap, DevResult* out,
                            uint64_t* prof_out = nullptr) {
+  // hbuf: the policy's heap array -- LDS (fast, 2 policies/CU on the 8k trace)
+  // or its private slice of an HBM buffer (any trace length, 12+ policies/CU)
   Prof prof;
   const int lane = lane_id();
   const int lb = W.low_bits, nb = W.node_bits;
@@ -171,10 +173,10 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* lds, 
   const int N = W.n_pods;
 
   WaveHeap heap;
-  heap.h = lds;
-  heap.delmap = reinterpret_cast<uint32_t*>(lds + lds_heap_entries(N));
+  heap.h = hbuf;
+  heap.delmap = delmap;
   heap.lb = lb;
-  for (int i = lane; i < N; i += kWave) lds[i] = W.heap0[i];
+  for (int i = lane; i < N; i += kWave) hbuf[i] = W.heap0[i];
   for (int i = lane; i < lds_delmap_words(N); i += kWave) heap.delmap[i] = 0u;
 
   NodeRegs<NPASS> nr;
@@ -215,18 +217,19 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* lds, 
 
   while (n > 0) {
     // ---------------- pop (pod record load issued first, consumed after the sift)
-    const uint64_t top = uniu64(lds[0]);
+    const uint64_t top = uniu64(hbuf[0]);
     const int rank = (int)((top >> lb) & ((1ull << rb) - 1));
-    const int4 prec = W.pod[rank];
-    const uint64_t last = uniu64(lds[n - 1]);
+    const int4 precv = load_vgpr(&W.pod[rank]);
+    const uint64_t last = uniu64(hbuf[n - 1]);
     --n;
     if (n > 0) heap.pop_reinsert(n, last);
 
     const int kind = (int)(top & 3);
     const int64_t t = (int64_t)(top >> tshift);
     PodView pod;
-    pod.cpu = prec.x; pod.mem = prec.y; pod.dur = prec.z;
-    pod.gmilli = prec.w & 0xFFFF; pod.ngpu = (prec.w >> 16) & 0xFF; pod.cls = (prec.w >> 24) & 0xFF;
+    const int pw = uni(precv.w);
+    pod.cpu = uni(precv.x); pod.mem = uni(precv.y); pod.dur = uni(precv.z);
+    pod.gmilli = pw & 0xFFFF; pod.ngpu = (pw >> 16) & 0xFF; pod.cls = (pw >> 24) & 0xFF;
     pod.ctime = t; pod.rank = rank;
     prof.mark(PH_POP);
 
@@ -302,13 +305,13 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* lds, 
         int64_t anchor = -1;
         if (!W.repush_earliest) {
           const int f = heap.first_deletion(n);
-          if (f >= 0) anchor = (int64_t)(uniu64(lds[f]) >> tshift);
+          if (f >= 0) anchor = (int64_t)(uniu64(hbuf[f]) >> tshift);
         } else {
           uint64_t mn = ~0ull;
           for (int base = 0; base < n; base += kWave) {
             const int i = base + lane;
             uint64_t tv = ~0ull;
-            if (i < n) { const uint64_t k = lds[i]; if ((k & 3) == kDelete) tv = k >> tshift; }
+            if (i < n) { const uint64_t k = hbuf[i]; if ((k & 3) == kDelete) tv = k >> tshift; }
             tv = ~wave_max_u64(~tv);
             mn = tv < mn ? tv : mn;
           }

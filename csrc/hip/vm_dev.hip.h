@@ -322,7 +322,7 @@ struct VmScorerDev {
   bool limited;
   uint64_t* vregs;     // LDS: [reg][64]
 
-  __device__ void init(const DevProgramTable& T, int p, const DevWorkload& W, int64_t bud) {
+  __device__ void init(const DevProgramTable& T, int p, const DevWorkload& W, int64_t bud, uint64_t* vreg_base) {
     const int off = T.meta[3 * p], koff = T.meta[3 * p + 2];
     code = T.code + off;
     kpay = T.kpay + koff;
@@ -331,8 +331,7 @@ struct VmScorerDev {
     n_nodes = W.n_nodes;
     budget = bud;
     limited = bud > 0;
-    extern __shared__ uint64_t lds_all[];
-    vregs = lds_all + lds_vreg_offset(W.n_pods);
+    vregs = vreg_base;
   }
 
   template <int NPASS>

@@ -1,0 +1,241 @@
+"""`evaluate()`: score policy programs on the fastest exact engine available.
+
+Routing per program (every path yields the reference's score bit-for-bit):
+
+1. compile to bytecode (`policy.compiler`); programs outside the native
+   subset go straight to the object engine (CPython ``exec``, step 4);
+2. MI355X (`ops.hip_engine`): one k_replay wave per program, all programs of
+   a call in one launch;
+3. native CPU VM (`ops.cpu_engine`): for no-GPU hosts, for programs the device
+   reports as EXC_UNSUPPORTED (bigint / complex / trig / near-tie math), and
+   for results whose exact-mean accumulator flagged `inexact`;
+4. object engine (`simulator.KubernetesSimulator` + ``exec``), which *is* the
+   reference semantics, for whatever the native engines cannot express.
+
+Scores follow `evaluate_policy_standalone` (`funsearch/funsearch_integration.py:30-64`):
+any exception during the replay gives score 0.  `EvalResult.exc` tells which
+exception class it was; `EvalResult.engine` which engine produced it.
+"""
+
+from __future__ import annotations
+
+import copy
+import os
+from concurrent.futures import ProcessPoolExecutor
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from .core.arrays import Workload
+from .core.traces import load_default_workload
+from .policy.bytecode import Exc
+from .policy.compiler import CompiledPolicy, try_compile
+from .simulator.metrics import EvaluationResults
+
+COLS = {name: i for i, name in enumerate(
+    ("score", "avg_cpu", "avg_mem", "avg_gpu_count", "avg_gpu_milli", "frag", "n_snapshots",
+     "n_frag_events", "n_events", "n_unplaced", "exc", "inexact", "trace_hash_hi"))}
+
+
+@dataclass
+class EvalResult:
+    score: float
+    exc: int = 0
+    engine: str = ""
+    results: Optional[EvaluationResults] = None
+    n_events: int = 0
+    detail: Dict[str, float] = field(default_factory=dict)
+
+    @property
+    def ok(self) -> bool:
+        return self.exc == 0
+
+
+def _row_to_result(row: np.ndarray, engine: str) -> EvalResult:
+    exc = int(row[COLS["exc"]])
+    if exc:
+        return EvalResult(0.0 if exc not in (Exc.UNSUPPORTED, Exc.BUDGET) else 0.0, exc, engine,
+                          n_events=int(row[COLS["n_events"]]))
+    res = EvaluationResults(
+        avg_cpu_utilization=float(row[COLS["avg_cpu"]]),
+        avg_memory_utilization=float(row[COLS["avg_mem"]]),
+        avg_gpu_count_utilization=float(row[COLS["avg_gpu_count"]]),
+        avg_gpu_memory_utilization=float(row[COLS["avg_gpu_milli"]]),
+        gpu_fragmentation_score=float(row[COLS["frag"]]),
+        num_snapshots=int(row[COLS["n_snapshots"]]),
+        num_fragmentation_events=int(row[COLS["n_frag_events"]]))
+    return EvalResult(float(row[COLS["score"]]), 0, engine, res, int(row[COLS["n_events"]]),
+                      {"n_unplaced": float(row[COLS["n_unplaced"]]), "trace_hash_hi": float(row[COLS["trace_hash_hi"]])})
+
+
+# ---------------------------------------------------------------------------- object engine
+def object_engine_eval(code: str, workload: Workload, budget_s: float = 0.0) -> EvalResult:
+    """Reference-semantics replay with CPython ``exec`` (the exact fallback)."""
+    from .funsearch.scheduler import FunSearchScheduler
+    from .simulator import DiscreteEventSimulator, KubernetesSimulator, SchedulingEvaluator
+    try:
+        sched = FunSearchScheduler(code)
+        cluster, pods = workload.to_objects()
+        ev = SchedulingEvaluator(cluster, enabled=True)
+        sim = KubernetesSimulator(cluster, pods, DiscreteEventSimulator(pods), sched, evaluator=ev)
+        sim.run_schedule()
+        res = ev.get_evaluation_results()
+        return EvalResult(float(ev.get_policy_score(pods)), 0, "object", res, sim.events_processed)
+    except Exception as exc:  # any exception aborts the replay -> score 0
+        return EvalResult(0.0, _exc_code(exc), "object")
+
+
+def _exc_code(exc: BaseException) -> int:
+    if isinstance(exc, ZeroDivisionError):
+        return int(Exc.ZERO_DIVISION)
+    if isinstance(exc, OverflowError):
+        return int(Exc.OVERFLOW)
+    if isinstance(exc, IndexError):
+        return int(Exc.INDEX)
+    if isinstance(exc, NameError):
+        return int(Exc.NAME)
+    if isinstance(exc, TypeError):
+        return int(Exc.TYPE)
+    return int(Exc.VALUE)
+
+
+def _object_worker(args):
+    code, workload = args
+    return object_engine_eval(code, workload)
+
+
+# ---------------------------------------------------------------------------- evaluator
+class Evaluator:
+    """Batched exact evaluator bound to one workload.
+
+    ``device``: ``"auto"`` (MI355X if visible, else CPU), ``"gpu"``/``int``
+    (HIP device index; fails loudly if unavailable), or ``"cpu"``.
+    """
+
+    def __init__(self, workload: Optional[Workload] = None, device="auto", options: Optional[dict] = None,
+                 cpu_threads: int = 0, object_workers: int = 0):
+        self.workload = workload or load_default_workload()
+        self.options = dict(options or {})
+        self.cpu_threads = cpu_threads or os.cpu_count() or 1
+        self.object_workers = object_workers or min(8, os.cpu_count() or 1)
+        self.device = None
+        want_gpu = device not in ("cpu", None)
+        if want_gpu:
+            from .ops import hip_engine
+            idx = device if isinstance(device, int) else int(os.environ.get("LOCAL_RANK", 0))
+            available = hip_engine.device_available()
+            if not available and device != "auto":
+                raise RuntimeError("HIP device requested but none is visible")
+            if available:
+                try:
+                    self.device = hip_engine.DeviceEvaluator(self.workload, idx, self.options)
+                except hip_engine.UnsupportedWorkload:
+                    if device != "auto":
+                        raise
+        self.stats = {"device": 0, "cpu_vm": 0, "object": 0, "compile_errors": 0}
+
+    @property
+    def backend(self) -> str:
+        return "hip" if self.device is not None else "cpu"
+
+    # -- built-in parametric families -------------------------------------------
+    def evaluate_family(self, family: str, weights: np.ndarray) -> np.ndarray:
+        """[P, 13] result table for P members of a built-in family."""
+        if self.device is not None:
+            return self.device.evaluate_builtin(family, weights)
+        from .ops import cpu_engine
+        return cpu_engine.simulate_builtin_batch(self.workload, family, weights,
+                                                 cpu_engine.SimOptions(**self._cpu_opts()), self.cpu_threads)
+
+    def _cpu_opts(self) -> dict:
+        keep = ("repush", "gpu_alloc", "snapshot_interval", "budget")
+        return {k: v for k, v in self.options.items() if k in keep}
+
+    # -- programs ---------------------------------------------------------------------
+    def evaluate_programs(self, codes: Sequence[str]) -> List[EvalResult]:
+        n = len(codes)
+        out: List[Optional[EvalResult]] = [None] * n
+        compiled: List[Optional[CompiledPolicy]] = []
+        for c in codes:
+            prog, err = try_compile(c)
+            if prog is None:
+                self.stats["compile_errors"] += 1
+            compiled.append(prog)
+        # 1) device
+        pending = [i for i, p in enumerate(compiled) if p is not None]
+        if self.device is not None:
+            dev_idx = [i for i in pending if compiled[i].device_ok]
+            if dev_idx:
+                tab = self.device.evaluate_programs([compiled[i] for i in dev_idx])
+                for row, i in zip(tab, dev_idx):
+                    if int(row[COLS["exc"]]) == Exc.UNSUPPORTED or row[COLS["inexact"]]:
+                        continue
+                    out[i] = _row_to_result(row, "hip")
+                    self.stats["device"] += 1
+        # 2) native CPU VM
+        cpu_idx = [i for i in pending if out[i] is None]
+        if cpu_idx:
+            from .ops import cpu_engine
+            tab = cpu_engine.simulate_program_batch(self.workload, [compiled[i] for i in cpu_idx],
+                                                    cpu_engine.SimOptions(**self._cpu_opts()), self.cpu_threads)
+            for row, i in zip(tab, cpu_idx):
+                if int(row[COLS["exc"]]) == Exc.UNSUPPORTED or row[COLS["inexact"]]:
+                    continue
+                out[i] = _row_to_result(row, "cpu")
+                self.stats["cpu_vm"] += 1
+        # 3) object engine (exact by construction)
+        rest = [i for i in range(n) if out[i] is None]
+        if rest:
+            if self._object_engine_ok():
+                jobs = [(codes[i], self.workload) for i in rest]
+                if len(rest) > 1 and self.object_workers > 1:
+                    with ProcessPoolExecutor(max_workers=min(self.object_workers, len(rest))) as ex:
+                        results = list(ex.map(_object_worker, jobs))
+                else:
+                    results = [_object_worker(j) for j in jobs]
+            else:
+                results = [EvalResult(0.0, int(Exc.UNSUPPORTED), "none") for _ in rest]
+            for i, r in zip(rest, results):
+                out[i] = r
+                self.stats["object"] += 1
+        return out  # type: ignore[return-value]
+
+    def _object_engine_ok(self) -> bool:
+        # the object engine implements only the reference's semantics
+        return (self.options.get("repush", "first") == "first"
+                and self.options.get("gpu_alloc", "best_fit") == "best_fit"
+                and float(self.options.get("snapshot_interval", 0.05)) == 0.05)
+
+    def scores(self, codes: Sequence[str]) -> List[float]:
+        return [r.score for r in self.evaluate_programs(codes)]
+
+
+_default: Dict[str, Evaluator] = {}
+
+
+def evaluate(codes, device="auto", workload: Optional[Workload] = None, **options) -> List[float]:
+    """Scores of policy programs (one program text or a list of them).
+
+    Compatible with the reference's fitness: identical to running
+    `evaluate_policy_standalone` on each program (exception -> 0)."""
+    single = isinstance(codes, str)
+    codes = [codes] if single else list(codes)
+    if workload is None and not options:
+        key = str(device)
+        ev = _default.get(key)
+        if ev is None:
+            ev = _default[key] = Evaluator(None, device)
+    else:
+        ev = Evaluator(workload, device, options)
+    scores = ev.scores(codes)
+    return scores[0] if single else scores
+
+
+def evaluate_detailed(codes: Sequence[str], device="auto", workload: Optional[Workload] = None,
+                      **options) -> List[EvalResult]:
+    return Evaluator(workload, device, options).evaluate_programs(list(codes))
+
+
+def copy_workload(w: Workload) -> Workload:
+    return copy.deepcopy(w)

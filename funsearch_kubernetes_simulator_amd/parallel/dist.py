@@ -1,0 +1,155 @@
+"""One process per GPU, collectives over RCCL (torch.distributed "nccl").
+
+The island model needs only small collectives: an all-gather of fixed-size
+elite records every K generations (migration) and a max all-reduce (global
+best / early stop / max-over-ranks timing).  On MI355X these run over RCCL on
+the xGMI links; at these message sizes (a few KB to ~200 KB) they are
+latency-bound, so we send one padded tensor per migration rather than many
+small ones.  Without GPUs (tests, CPU hosts) the same API runs on gloo.
+"""
+
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+    device: Optional[object] = None   # torch.device used for collective buffers
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+
+_ctx: Optional[DistContext] = None
+
+
+def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = None) -> DistContext:
+    """Initialise from torchrun-style env vars (RANK/WORLD_SIZE/LOCAL_RANK,
+    MASTER_ADDR defaults to 127.0.0.1).  Single-process runs need nothing."""
+    global _ctx
+    if _ctx is not None:
+        return _ctx
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world <= 1:
+        _ctx = DistContext(rank=0, world_size=1, local_rank=local, backend="none")
+        return _ctx
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29511")
+    if use_gpu is None:
+        use_gpu = torch.cuda.is_available()
+    if backend is None:
+        backend = "nccl" if use_gpu else "gloo"
+    device = torch.device("cpu")
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    if not dist.is_initialized():
+        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+    _ctx = DistContext(rank=rank, world_size=world, local_rank=local, backend=backend, device=device)
+    return _ctx
+
+
+def context() -> DistContext:
+    return _ctx or init_distributed()
+
+
+def barrier() -> None:
+    ctx = context()
+    if ctx.distributed:
+        import torch.distributed as dist
+        if ctx.backend == "nccl":
+            import torch
+            dist.barrier(device_ids=[ctx.local_rank])
+            torch.cuda.synchronize()
+        else:
+            dist.barrier()
+
+
+def all_gather_array(x: np.ndarray) -> np.ndarray:
+    """[world, *x.shape]: every rank's array (same shape/dtype on all ranks)."""
+    ctx = context()
+    if not ctx.distributed:
+        return x[None].copy()
+    import torch
+    import torch.distributed as dist
+    t = torch.from_numpy(np.ascontiguousarray(x)).to(ctx.device)
+    out = [torch.empty_like(t) for _ in range(ctx.world_size)]
+    dist.all_gather(out, t)
+    return np.stack([o.cpu().numpy() for o in out])
+
+
+def all_reduce_max(v: float) -> float:
+    ctx = context()
+    if not ctx.distributed:
+        return float(v)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(v)], dtype=torch.float64, device=ctx.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def all_reduce_sum(v: float) -> float:
+    ctx = context()
+    if not ctx.distributed:
+        return float(v)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(v)], dtype=torch.float64, device=ctx.device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def shutdown() -> None:
+    global _ctx
+    if _ctx is not None and _ctx.distributed:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
+    _ctx = None
+
+
+# -------------------------------------------------------------------- program records
+RECORD_BYTES = 4096   # max packed program text per migrant (longer programs are not migrated)
+
+
+def pack_programs(codes, scores, width: int = RECORD_BYTES) -> np.ndarray:
+    """Fixed-size byte records [E, 16 + width]: score (f64), length (i64), utf-8 text."""
+    out = np.zeros((len(codes), 16 + width), dtype=np.uint8)
+    for i, (c, s) in enumerate(zip(codes, scores)):
+        b = c.encode("utf-8")
+        if len(b) > width:
+            b = b""   # too long: sent as an empty slot
+        out[i, :8] = np.frombuffer(np.float64(s).tobytes(), dtype=np.uint8)
+        out[i, 8:16] = np.frombuffer(np.int64(len(b)).tobytes(), dtype=np.uint8)
+        out[i, 16:16 + len(b)] = np.frombuffer(b, dtype=np.uint8)
+    return out
+
+
+def unpack_programs(rec: np.ndarray):
+    res = []
+    for row in rec.reshape(-1, rec.shape[-1]):
+        n = int(np.frombuffer(row[8:16].tobytes(), dtype=np.int64)[0])
+        if n <= 0:
+            continue
+        score = float(np.frombuffer(row[:8].tobytes(), dtype=np.float64)[0])
+        res.append((bytes(row[16:16 + n]).decode("utf-8"), score))
+    return res

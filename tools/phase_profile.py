@@ -10,17 +10,15 @@ from funsearch_kubernetes_simulator_amd.policy.compiler import compile_policy
 w = load_default_workload()
 dev = DeviceEvaluator(w)
 rng = np.random.default_rng(0)
-P = 512
-wts = np.stack([rng.uniform(1000, 5000, P), rng.uniform(1e-4, 1e-2, P), rng.uniform(1e-5, 1e-3, P), rng.uniform(10, 1000, P)], 1)
 def report(tag, tab, prof):
     ev = tab[:, 8]
-    tot = prof.sum(1)
-    out = {"tag": tag, "cycles_per_event": float((tot / ev).mean()),
-           "phase_cycles_per_event": {ph: float((prof[:, i] / ev).mean()) for i, ph in enumerate(DeviceEvaluator.PHASES)},
-           "events": float(ev.mean())}
+    out = {"tag": tag, "cycles_per_event": round(float((prof.sum(1) / ev).mean()), 1),
+           "phases": {ph: round(float((prof[:, i] / ev).mean()), 1) for i, ph in enumerate(DeviceEvaluator.PHASES)}}
     print(json.dumps(out), flush=True)
-tab, prof = dev.profile_builtin("random_linear", wts); report("random_linear", tab, prof)
-for fam in ("first_fit", "best_fit"):
-    tab, prof = dev.profile_builtin(fam, np.zeros((64, 4))); report(fam, tab, prof)
+for mode, P in (("lds", 512), ("hbm", 512), ("hbm", 3072)):
+    dev.set_options(heap_mode=mode)
+    wts = np.stack([rng.uniform(1000, 5000, P), rng.uniform(1e-4, 1e-2, P), rng.uniform(1e-5, 1e-3, P), rng.uniform(10, 1000, P)], 1)
+    tab, prof = dev.profile_builtin("random_linear", wts); report(f"random_linear/{mode}/P{P}", tab, prof)
+dev.set_options(heap_mode="lds")
 progs = [compile_policy(c) for c in reference_policies().values()]
-tab, prof = dev.profile_programs(progs * 8); report("vm_reference", tab, prof)
+tab, prof = dev.profile_programs(progs * 8); report("vm_reference/lds", tab, prof)
