@@ -1,0 +1,210 @@
+"""Multi-island FunSearch over program text: `run_funsearch`.
+
+Layout: one process per GPU (`parallel.dist`), ``islands.per_rank``
+populations per process.  Each generation:
+
+1. every island asks the LLM backend for children of two random elites
+   (one shared thread pool -> concurrent LLM requests across islands);
+2. all children of all islands are evaluated in ONE batched engine call
+   (one k_replay wave per program on the MI355X);
+3. each island merges its own children with the reference's rules
+   (similarity filter, elites + children, truncate);
+4. every ``migrate_every`` generations the best ``migrants`` programs of every
+   island are all-gathered across ranks (fixed-size byte records over RCCL)
+   and injected into the next island of a global ring;
+5. global best / early stop via an all-reduce max.
+
+With ``islands.per_rank = 1`` on one process this is exactly `SimpleFunSearch`.
+Checkpoints (``checkpoint.dir``) hold every island's population so a run can
+`resume` after a crash, which the reference cannot.
+"""
+
+from __future__ import annotations
+
+import concurrent.futures
+import json
+import os
+import time
+from typing import List, Optional, Tuple
+
+from ..engine import Evaluator
+from ..parallel import dist
+from ..utils.metrics import MetricsLog
+from .llm import make_client
+from .search import FEEDBACK, SimpleFunSearch, load_config
+
+
+class IslandFunSearch:
+    def __init__(self, config, evaluator: Optional[Evaluator] = None, verbose: bool = False):
+        self.config = load_config(config)
+        self.ctx = dist.init_distributed(use_gpu=(self.config.get("device") or {}).get("kind", "auto") != "cpu")
+        isl = self.config.get("islands") or {}
+        self.n_islands = int(isl.get("per_rank", 1))
+        self.migrate_every = int(isl.get("migrate_every", 50))
+        self.n_migrants = int(isl.get("migrants", 2))
+        dev = (self.config.get("device") or {}).get("kind", "auto")
+        if dev == "auto" and self.ctx.backend == "nccl":
+            dev = self.ctx.local_rank
+        self.evaluator = evaluator or Evaluator(device=dev)
+        llm_cfg = dict(self.config.get("llm") or {})
+        base_seed = int(llm_cfg.get("seed", 0)) + 1000003 * self.ctx.rank
+        self.islands: List[SimpleFunSearch] = []
+        for i in range(self.n_islands):
+            cfg = json.loads(json.dumps(self.config))
+            cfg.setdefault("llm", dict(llm_cfg))
+            if cfg["llm"].get("backend") in ("mutation", "offline"):
+                cfg["llm"]["seed"] = base_seed + 7919 * i
+            cfg["checkpoint"] = {}
+            self.islands.append(SimpleFunSearch(cfg, evaluator=self.evaluator, seed=base_seed + i,
+                                                llm_client=None if cfg.get("llm") else make_client(cfg["llm"]),
+                                                verbose=verbose))
+        self.generation = 0
+        self.evaluations = 0
+        self.verbose = verbose
+        log_path = self.config.get("log_path")
+        if log_path and self.ctx.world_size > 1:
+            root, ext = os.path.splitext(log_path)
+            log_path = f"{root}.rank{self.ctx.rank}{ext}"
+        self.log = MetricsLog(log_path)
+        ck = self.config.get("checkpoint") or {}
+        self.ck_dir = ck.get("dir")
+        self.ck_every = int(ck.get("every", 0))
+
+    # -- helpers --------------------------------------------------------------------------
+    @property
+    def best(self) -> Tuple[Optional[str], float]:
+        b = max(self.islands, key=lambda s: s.best_score)
+        return b.best_policy, b.best_score
+
+    def initialize(self) -> None:
+        first = self.islands[0]
+        if not first.population:
+            first.initialize_population()
+        for s in self.islands[1:]:
+            if not s.population:
+                s.population = list(first.population)
+                s.best_policy, s.best_score = first.best_policy, first.best_score
+
+    def evolve(self) -> dict:
+        t0 = time.time()
+        self.generation += 1
+        plans = []
+        for s in self.islands:
+            s.generation += 1
+            s.population.sort(key=lambda x: x[1], reverse=True)
+            elites = s.population[:s.elite_size]
+            n_new = min(s.policies_per_generation, s.population_size - len(elites))
+            plans.append((s, elites, max(0, n_new)))
+        jobs = [(k, i) for k, (s, el, n) in enumerate(plans) if el for i in range(n)]
+        workers = max(1, min(64, sum(s.max_workers for s in self.islands)))
+        with concurrent.futures.ThreadPoolExecutor(max_workers=workers) as ex:
+            outs = list(ex.map(lambda ki: (ki[0],) + plans[ki[0]][0]._generate_single_policy(
+                ki[1], plans[ki[0]][1], FEEDBACK), jobs))
+        children = [(k, code) for k, _, code in outs if code]
+        t_gen = time.time()
+        results = self.evaluator.evaluate_programs([c for _, c in children]) if children else []
+        t_eval = time.time()
+        self.evaluations += len(children)
+        for k, (s, elites, _) in enumerate(plans):
+            new = []
+            for (kk, code), res in zip(children, results):
+                if kk != k or s._is_too_similar(code, res.score):
+                    continue
+                new.append((code, res.score))
+                if res.score > s.best_score:
+                    s.best_score, s.best_policy = res.score, code
+            s.population = sorted(elites + new, key=lambda x: x[1], reverse=True)[:s.population_size]
+        if self.migrate_every and self.generation % self.migrate_every == 0:
+            self.migrate()
+        best_local = self.best[1]
+        best_global = dist.all_reduce_max(best_local)
+        rec = dict(kind="generation", rank=self.ctx.rank, generation=self.generation, best=best_local,
+                   best_global=best_global, children=len(children),
+                   islands=[round(s.best_score, 6) for s in self.islands],
+                   llm_s=round(t_gen - t0, 4), eval_s=round(t_eval - t_gen, 4),
+                   evals_per_s=round(len(children) / max(1e-9, t_eval - t_gen), 2))
+        self.log.write(**rec)
+        if self.ck_dir and self.ck_every and self.generation % self.ck_every == 0:
+            self.save_checkpoint()
+        return rec
+
+    def migrate(self) -> None:
+        """Ring migration of each island's best programs across all ranks."""
+        k = self.n_migrants
+        recs = []
+        for s in self.islands:
+            top = sorted(s.population, key=lambda x: x[1], reverse=True)[:k]
+            top += [("", float("-inf"))] * (k - len(top))
+            recs.append(dist.pack_programs([c for c, _ in top], [sc for _, sc in top]))
+        import numpy as np
+        local = np.stack(recs)                                  # [I, k, bytes]
+        glob = dist.all_gather_array(local)                     # [W, I, k, bytes]
+        W, I = glob.shape[0], glob.shape[1]
+        flat = glob.reshape(W * I, k, -1)
+        for li, s in enumerate(self.islands):
+            g = self.ctx.rank * I + li
+            src = flat[(g - 1) % (W * I)]
+            incoming = dist.unpack_programs(src)
+            known = {c for c, _ in s.population}
+            for code, score in incoming:
+                if code not in known:
+                    s.population.append((code, score))
+                    if score > s.best_score:
+                        s.best_score, s.best_policy = score, code
+            s.population = sorted(s.population, key=lambda x: x[1], reverse=True)[:s.population_size]
+
+    def run(self, generations: Optional[int] = None, resume: bool = False) -> Tuple[Optional[str], float]:
+        if resume and self.ck_dir:
+            path = os.path.join(self.ck_dir, f"islands_rank{self.ctx.rank}.json")
+            if os.path.exists(path):
+                self.load_checkpoint(path)
+        self.initialize()
+        generations = generations or self.islands[0].max_generations
+        threshold = self.islands[0].early_stop_threshold
+        start = self.generation
+        while self.generation - start < generations:
+            rec = self.evolve()
+            if self.verbose and self.ctx.is_main:
+                print(json.dumps(rec), flush=True)
+            if rec["best_global"] >= threshold:
+                break
+        return self.global_best()
+
+    def global_best(self) -> Tuple[Optional[str], float]:
+        code, score = self.best
+        if not self.ctx.distributed:
+            return code, score
+        rec = dist.pack_programs([code or ""], [score])
+        allr = dist.all_gather_array(rec)
+        best = max(dist.unpack_programs(allr), key=lambda cs: cs[1], default=(code, score))
+        return best
+
+    # -- checkpoint ----------------------------------------------------------------------
+    def save_checkpoint(self) -> str:
+        os.makedirs(self.ck_dir, exist_ok=True)
+        path = os.path.join(self.ck_dir, f"islands_rank{self.ctx.rank}.json")
+        state = {"format": "fks-islands-checkpoint-v1", "generation": self.generation,
+                 "evaluations": self.evaluations, "islands": [s.state_dict() for s in self.islands]}
+        tmp = path + ".tmp"
+        with open(tmp, "w") as fh:
+            json.dump(state, fh)
+        os.replace(tmp, path)
+        return path
+
+    def load_checkpoint(self, path: str) -> None:
+        with open(path) as fh:
+            st = json.load(fh)
+        if st.get("format") != "fks-islands-checkpoint-v1":
+            raise ValueError(f"not an island checkpoint: {path}")
+        self.generation = int(st["generation"])
+        self.evaluations = int(st.get("evaluations", 0))
+        for s, ss in zip(self.islands, st["islands"]):
+            s.generation = int(ss["generation"])
+            s.population = [(p["code"], float(p["score"])) for p in ss["population"]]
+            s.best_policy, s.best_score = ss["best_policy"], float(ss["best_score"])
+
+
+def run_funsearch(config="configs/offline_islands.json", generations: Optional[int] = None, resume: bool = False,
+                  evaluator: Optional[Evaluator] = None, verbose: bool = False) -> Tuple[Optional[str], float]:
+    """Run the (multi-island, multi-GPU) FunSearch loop; returns (best_code, best_score)."""
+    return IslandFunSearch(config, evaluator=evaluator, verbose=verbose).run(generations, resume)

@@ -731,7 +731,9 @@ class Compiler:
             return self.load_const(self.globals[name])
         if name in ("True", "False"):
             return self.load_const(1 if name == "True" else 0)
-        raise CompileError(f"unsupported name {name}")
+        # never assigned anywhere: NameError when (and only when) reached
+        self.raise_(Exc.NAME)
+        return self.load_const(0)
 
     def expr(self, e) -> Val:
         m = getattr(self, "e_" + type(e).__name__, None)
