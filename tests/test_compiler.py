@@ -1,0 +1,169 @@
+"""Policy compiler + native VM vs CPython ``exec`` (value AND type AND exception parity)."""
+import math
+import re
+
+import numpy as np
+import pytest
+
+from funsearch_kubernetes_simulator_amd.core.model import GPU, Node, Pod
+from funsearch_kubernetes_simulator_amd.engine import _exc_code
+from funsearch_kubernetes_simulator_amd.models.library import reference_policies, seed_policies
+from funsearch_kubernetes_simulator_amd.ops import cpu_engine
+from funsearch_kubernetes_simulator_amd.policy.bytecode import Exc, Op
+from funsearch_kubernetes_simulator_amd.policy.compiler import CompileError, compile_policy
+from funsearch_kubernetes_simulator_amd.policy.sandbox import compile_priority_function
+
+
+def test_opcode_table_matches_header():
+    import pathlib
+    hdr = (pathlib.Path(__file__).parents[1] / "csrc/include/fks/bytecode.hpp").read_text()
+    found = dict(re.findall(r"OP_([A-Z0-9_]+) = (\d+)", hdr))
+    assert found, "no opcodes parsed"
+    for name, val in found.items():
+        assert Op[name] == int(val), name
+    assert len(found) == len(Op)
+
+
+def run_vm(code, pod, node):
+    prog = compile_policy(code)
+    gl = [g.gpu_milli_left for g in node.gpus]
+    gt = [g.gpu_milli_total for g in node.gpus]
+    gm = [g.memory_mib_total for g in node.gpus]
+    pd = dict(cpu_milli=pod.cpu_milli, memory_mib=pod.memory_mib, num_gpu=pod.num_gpu, gpu_milli=pod.gpu_milli,
+              creation_time=pod.creation_time, duration_time=pod.duration_time)
+    nd = dict(cpu_milli_left=node.cpu_milli_left, cpu_milli_total=node.cpu_milli_total,
+              memory_mib_left=node.memory_mib_left, memory_mib_total=node.memory_mib_total, gpu_left=node.gpu_left)
+    kind, val = cpu_engine.native().score_program_once(prog.code, prog.fconst, prog.iconst, prog.ctag, pd, nd,
+                                                        gl, gt, gm)
+    return kind, val
+
+
+def run_py(code, pod, node):
+    fn = compile_priority_function(code)
+    try:
+        v = fn(pod, node)
+    except Exception as exc:
+        return "exc", _exc_code(exc)
+    if isinstance(v, bool):
+        return "int", int(v)
+    if isinstance(v, int):
+        return "int", v
+    if isinstance(v, float):
+        return "float", v
+    # None / lists / objects: the scheduler's int(max(0, v)) raises TypeError
+    return "exc", int(Exc.TYPE)
+
+
+def same(a, b):
+    if a[0] == "none":
+        a = ("exc", int(Exc.TYPE))
+    if b[0] == "none":
+        b = ("exc", int(Exc.TYPE))
+    if a[0] != b[0]:
+        return False
+    if a[0] == "float":
+        return (math.isnan(a[1]) and math.isnan(b[1])) or (a[1] == b[1] and math.copysign(1, a[1]) == math.copysign(1, b[1]))
+    return a[1] == b[1]
+
+
+def random_state(rng):
+    ng = int(rng.integers(0, 9))
+    total = int(rng.choice([1000, 1000, 500]))
+    gpus = [GPU(16000, 16000, int(rng.integers(-50, total + 1)), total) for _ in range(ng)]
+    cpu_t = int(rng.choice([0, 32000, 64000, 96000, 128000])) if rng.random() < 0.05 else int(rng.choice([32000, 64000, 96000]))
+    mem_t = int(rng.choice([131072, 262144, 786432]))
+    node = Node("n", int(rng.integers(-1000, cpu_t + 1)), cpu_t, int(rng.integers(-100, mem_t + 1)), mem_t,
+                int(rng.integers(-1, ng + 2)), gpus)
+    pod = Pod("p", int(rng.integers(0, 20000)), int(rng.integers(0, 40000)), int(rng.choice([0, 0, 1, 1, 2, 4, 8])),
+              int(rng.choice([0, 100, 250, 460, 500, 1000])), "", int(rng.integers(0, 10 ** 7)),
+              int(rng.integers(0, 10 ** 6)))
+    return pod, node
+
+
+ALL_PROGRAMS = {**{f"ref:{k}": v for k, v in reference_policies().items()},
+                **{f"seed:{k}": v for k, v in seed_policies().items()}}
+
+
+@pytest.mark.parametrize("name", sorted(ALL_PROGRAMS))
+def test_shipped_programs_match_cpython(name):
+    code = ALL_PROGRAMS[name]
+    rng = np.random.default_rng(abs(hash(name)) % 2 ** 32)
+    for _ in range(400):
+        pod, node = random_state(rng)
+        a, b = run_vm(code, pod, node), run_py(code, pod, node)
+        assert same(a, b), (name, a, b, pod, node)
+
+
+SNIPPETS = [
+    # arithmetic and typing
+    "return 7 // 2 + 7 % 3 + (-7) // 2 + (-7) % 3",
+    "return 7.5 // 2 + (-7.5) % 2 + 7 / 2",
+    "return 2 ** 10 + 2 ** -1 + (-2) ** 3",
+    "return (node.cpu_milli_left + 0.5) ** 0.5",
+    "return (node.cpu_milli_left - 1000) ** 0.5",
+    "return 10 / (node.gpu_left - node.gpu_left)",
+    "return 10.0 % (pod.num_gpu * 0.0)",
+    "return int(node.cpu_milli_left / 7) + round(node.memory_mib_left / 3) + round(2.5) + round(3.5) + round(-2.5)",
+    "return abs(-node.cpu_milli_left) + abs(-1.5) + float(3) + int(-3.7) + bool(node.gpus)",
+    "return max(pod.cpu_milli, node.cpu_milli_left, 5) - min(3, 1.0, 1)",
+    "return math.sqrt(abs(node.cpu_milli_left)) + math.log(pod.cpu_milli + 1) + math.exp(-pod.num_gpu)",
+    "return math.log(pod.cpu_milli + 1, 2) + math.pow(2, pod.num_gpu) + math.sqrt(-1 if pod.num_gpu > 100 else 4)",
+    "return math.log(node.cpu_milli_left)",
+    "return operator.add(1, 2) * operator.mul(3, 4) - operator.sub(pod.num_gpu, 1) + operator.truediv(1, 4) + operator.mod(7, 3)",
+    "return math.sin(pod.cpu_milli) + math.cos(1) + math.tan(0.5)",
+    "return -(2 ** 62) * 4",
+    "return 1e308 * 10 > 0",
+    "return int(float('nan') if False else 1e300 * 1e300)",
+    # control flow, short circuit, comparisons
+    "return (len(node.gpus) > 0 and node.gpus[0].gpu_milli_left) or 42",
+    "return node.gpus[0].gpu_milli_left if len(node.gpus) > 0 else -1",
+    "return node.gpus[0].gpu_milli_left",
+    "return node.gpus[-1].gpu_milli_left + node.gpus[len(node.gpus) - 1].gpu_milli_total",
+    "x = 0\n    if pod.cpu_milli > 100:\n        x = 1\n    elif pod.cpu_milli > 50:\n        x = 2\n    else:\n        x = 3\n    return x",
+    "return 1 < pod.num_gpu < 4 <= node.gpu_left",
+    "return not node.gpus and pod.num_gpu == 0",
+    "if pod.num_gpu > 0:\n        y = 5\n    return y",
+    "return undefined_thing + 1",
+    "s = 0\n    for g in node.gpus:\n        if g.gpu_milli_left < 500:\n            continue\n        s += g.gpu_milli_left\n        if s > 1500:\n            break\n    return s",
+    "s = 0\n    for i in range(len(node.gpus)):\n        s += node.gpus[i].gpu_milli_left * i\n    for i in range(10, 0, -3):\n        s -= i\n    return s",
+    "s = 0\n    for i, g in enumerate(node.gpus):\n        s += i * g.gpu_milli_left\n    return s",
+    "i = 0\n    while i < node.gpu_left:\n        i += 1\n    return i",
+    "w = [0.3, 0.3, 0.4]\n    t = 0.0\n    for x in w:\n        t += x\n    return t * 1000 + w[0] + w[-1] + len(w) + sum(w) + max(w)",
+    # comprehensions / reductions / sorting
+    "return sum(g.gpu_milli_left for g in node.gpus if g.gpu_milli_left >= pod.gpu_milli)",
+    "return max(g.gpu_milli_left for g in node.gpus) - min(g.gpu_milli_left for g in node.gpus)",
+    "return max((g.gpu_milli_left for g in node.gpus if g.gpu_milli_left > 2000), default=-5)",
+    "e = [g for g in node.gpus if g.gpu_milli_left >= pod.gpu_milli][:pod.num_gpu]\n    return len(e) * 1000 + sum(g.gpu_milli_left for g in e)",
+    "v = sorted([g for g in node.gpus], key=lambda g: g.gpu_milli_left)\n    return sum((i + 1) * g.gpu_milli_left for i, g in enumerate(v)) if False else sum(g.gpu_milli_left * 3 for g in v[:2])",
+    "v = sorted(node.gpus, key=lambda g: -g.gpu_milli_left, reverse=True)\n    return v[0].gpu_milli_left if v else 0",
+    "return len([g for g in node.gpus if g.gpu_milli_left == g.gpu_milli_total]) + len(node.gpus[1:3]) + len(node.gpus[:-1])",
+    "return sum(x * x for x in range(pod.num_gpu)) + sum([i for i in range(3)] if False else [1, 2])",
+    "a, b = pod.cpu_milli, node.cpu_milli_left\n    a, b = b, a\n    return a - b",
+    "return pod.creation_time % 1000 + pod.duration_time // 7",
+    "return sorted(node.gpus)[0].gpu_milli_left if len(node.gpus) == 1 else 3",
+    "return sorted(node.gpus)",
+]
+
+
+@pytest.mark.parametrize("snippet", SNIPPETS)
+def test_snippets_match_cpython(snippet):
+    code = f"def priority_function(pod, node):\n    {snippet}\n"
+    try:
+        compile_policy(code)
+    except CompileError:
+        pytest.skip("outside the native subset (object-engine path)")
+    rng = np.random.default_rng(len(snippet))
+    for _ in range(200):
+        pod, node = random_state(rng)
+        a, b = run_vm(code, pod, node), run_py(code, pod, node)
+        if a == ("exc", int(Exc.UNSUPPORTED)):
+            continue   # native engines defer these to the exact object engine
+        assert same(a, b), (snippet, a, b, pod, node)
+
+
+def test_unsupported_constructs_raise_compile_error():
+    for body in ("return str(pod.cpu_milli)", "import os\n    return 1", "global x\n    return 1",
+                 "node.cpu_milli_left = 5\n    return 1", "return [1, 2][pod.num_gpu]",
+                 "return {1: 2}[1]", "return pod.gpu_spec"):
+        with pytest.raises(CompileError):
+            compile_policy(f"def priority_function(pod, node):\n    {body}\n")

@@ -1,0 +1,54 @@
+"""Device bytecode VM vs CPU VM: full replays of many programs on sub-traces."""
+import numpy as np
+import pytest
+
+from funsearch_kubernetes_simulator_amd.core.arrays import Workload
+from funsearch_kubernetes_simulator_amd.models import families as fam
+from funsearch_kubernetes_simulator_amd.models.library import reference_policies, seed_policies
+from funsearch_kubernetes_simulator_amd.ops import cpu_engine as ce
+from funsearch_kubernetes_simulator_amd.policy.bytecode import Exc
+from funsearch_kubernetes_simulator_amd.policy.compiler import CompileError, compile_policy
+
+from test_compiler import SNIPPETS
+
+pytestmark = pytest.mark.gpu
+
+
+def _programs():
+    codes = list(reference_policies().values()) + list(seed_policies().values())
+    rng = np.random.default_rng(9)
+    codes += [fam.to_program("feature_linear", w) for w in fam.sample_feature_linear(6, rng)]
+    codes += [fam.to_program("random_linear", w) for w in fam.sample_random_linear(4, rng)]
+    for s in SNIPPETS:
+        body = s if "return" in s else s + "\n    return 1"
+        codes.append("def priority_function(pod, node):\n    if (pod.cpu_milli > node.cpu_milli_left or "
+                     "pod.memory_mib > node.memory_mib_left or pod.num_gpu > node.gpu_left):\n        return 0\n"
+                     "    if pod.num_gpu > 0 and sum(1 for g in node.gpus if g.gpu_milli_left >= pod.gpu_milli) "
+                     "< pod.num_gpu:\n        return 0\n    " + body + "\n")
+    progs = []
+    for c in codes:
+        try:
+            progs.append(compile_policy(c))
+        except CompileError:
+            pass
+    return progs
+
+
+@pytest.mark.parametrize("mode", ["lds", "hbm"])
+def test_device_vm_equals_cpu_vm(default_workload, mode):
+    from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
+    if not he.device_available():
+        pytest.fail("GPU test collected but no HIP device is visible")
+    w = default_workload
+    sub = Workload(w.cluster, w.pods.subset(np.arange(1000, 1600)))
+    dev = he.DeviceEvaluator(sub, options={"heap_mode": mode})
+    progs = _programs()
+    gpu = dev.evaluate_programs(progs)
+    cpu = ce.simulate_program_batch(sub, progs, threads=8)
+    compared = 0
+    for i, p in enumerate(progs):
+        if int(gpu[i, 10]) == Exc.UNSUPPORTED:
+            continue   # deferred to the host by design (trig, near-tie math, bigint)
+        assert np.array_equal(gpu[i], cpu[i]), (i, p.source[-300:], gpu[i], cpu[i])
+        compared += 1
+    assert compared >= len(progs) - 6

@@ -1,0 +1,106 @@
+"""Trace ingestion quirks, synthetic generator, and multi-process (gloo) collectives."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from funsearch_kubernetes_simulator_amd.core import TraceParser, synthetic_workload
+from funsearch_kubernetes_simulator_amd.core.arrays import Workload, dense_rank
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_parser_defaults_and_files():
+    p = TraceParser()
+    cluster, pods = p.parse_workload()
+    assert len(cluster.nodes_dict) == 16 and len(pods) == 8152
+    assert cluster.num_gpus == 64
+    assert "openb_pod_list_default.csv" in p.get_available_pod_files()
+    assert p.get_available_node_files() == ["openb_node_list_all_node.csv", "openb_node_list_gpu_node.csv"]
+    assert pods[1].duration_time == 12902960 - 427061
+
+
+def test_multigpu_traces_raise_like_reference():
+    with pytest.raises(KeyError):
+        TraceParser().parse_pods("openb_pod_list_multigpu20.csv")
+
+
+def test_all_node_csv_has_cpu_only_nodes():
+    nodes = TraceParser().parse_nodes("openb_node_list_all_node.csv")
+    assert len(nodes) == 1523
+    assert sum(1 for n in nodes.values() if not n.gpus) == 310
+
+
+def test_k8s_yaml_matches_csv():
+    p = TraceParser()
+    y = p.parse_node_yaml()
+    c = p.parse_cluster("openb_node_list_gpu_node.csv")
+    assert len(y) == len(c) == 1213
+    for nid, n in list(c.nodes_dict.items())[:50]:
+        m = y.nodes_dict[nid]
+        assert (m.cpu_milli_total, m.memory_mib_total, m.gpu_left, len(m.gpus)) == \
+               (n.cpu_milli_total, n.memory_mib_total, n.gpu_left, len(n.gpus))
+
+
+def test_dense_rank_ties():
+    assert list(dense_rank(["b", "a", "b", "c"])) == [1, 0, 1, 2]
+
+
+def test_synthetic_workload_shape():
+    w = synthetic_workload(n_nodes=64, n_pods=4000, seed=1)
+    assert w.cluster.n_nodes == 64 and w.pods.n_pods == 4000
+    assert np.all(np.diff(w.pods.pod_ctime) >= 0)
+    c, p = w.to_objects()
+    w2 = Workload.from_objects(c, p)
+    assert w2.fingerprint() == w.fingerprint()
+
+
+def _run_torchrun(script: str, nproc: int = 2, timeout: int = 600):
+    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(29000 + os.getpid() % 1000), script]
+    return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+def test_gloo_collectives_and_migration(tmp_path):
+    script = tmp_path / "w.py"
+    script.write_text(
+        "import json, numpy as np\n"
+        "from funsearch_kubernetes_simulator_amd.parallel import dist\n"
+        "from funsearch_kubernetes_simulator_amd.funsearch.param_islands import make_islands, migrate\n"
+        "ctx = dist.init_distributed(use_gpu=False)\n"
+        "x = np.full((2, 3), ctx.rank, dtype=np.float64)\n"
+        "g = dist.all_gather_array(x)\n"
+        "assert g.shape == (2, 2, 3) and g[1].max() == 1\n"
+        "assert dist.all_reduce_max(ctx.rank * 10.0) == 10.0\n"
+        "isl = make_islands(2, 'random_linear', 4, 3, seed=ctx.rank)\n"
+        "for i in isl:\n"
+        "    w = i.propose(); i.update(w, np.arange(len(w)) + 100.0 * ctx.rank)\n"
+        "migrate(isl, 2, dist.all_gather_array)\n"
+        "rec = dist.pack_programs(['abc' * ctx.rank, 'x'], [1.0, 2.0])\n"
+        "allr = dist.all_gather_array(rec)\n"
+        "progs = dist.unpack_programs(allr)\n"
+        "assert ('x', 2.0) in progs\n"
+        "if ctx.rank == 0: print(json.dumps({'ok': True, 'best_island0': float(isl[0].elite_scores.max())}))\n"
+        "dist.shutdown()\n")
+    r = _run_torchrun(str(script))
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    # island 0 of rank 0 received rank 1's migrants (scores >= 100)
+    assert out["ok"] and out["best_island0"] >= 100
+
+
+def test_bench_two_ranks_cpu():
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(30000 + os.getpid() % 1000),
+                        os.path.join(REPO, "bench.py"), "--gpus", "2", "--device", "cpu", "--steps", "2",
+                        "--warmup", "1", "--islands", "1", "--candidates", "4", "--migrate-every", "1"],
+                       env=dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1"), capture_output=True, text=True,
+                       timeout=900)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0 and line["scaling"] == "weak"
+    assert line["config"]["global_batch"] == 8
