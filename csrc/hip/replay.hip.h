@@ -429,6 +429,12 @@ __global__ void k_eval_reduce(const DevResult* __restrict__ res, double* __restr
   if (p >= P) return;
   const DevResult r = res[p];
   double* row = table + (size_t)p * 13;
+  if (r.exc != EXC_NONE) {   // an aborted replay reports only its exception class
+#pragma unroll
+    for (int k = 0; k < 13; ++k) row[k] = 0.0;
+    row[10] = (double)r.exc;
+    return;
+  }
   double avg[5];
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
