@@ -15,9 +15,11 @@ enum BuiltinFamily : int32_t {
   FAM_BEST_FIT = 1,    // reference _create_best_fit_policy
   FAM_RANDOM_LINEAR = 2,  // reference _create_random_policy (base, cpu, mem, gpu factors)
   FAM_FEATURE_LINEAR = 3, // generalised linear feature family (models/families.py)
+  FAM_COMPOSITE_LINEAR = 4, // champion-containing 16-term basis (models/families.py)
 };
 
 constexpr int kFeatureCount = 12;
+constexpr int kCompositeCount = 16;
 
 struct BuiltinScorer {
   int32_t family = FAM_FIRST_FIT;
@@ -74,9 +76,72 @@ struct BuiltinScorer {
         o.v = Num::I(std::max<int64_t>(1, (int64_t)s));
         return o;
       }
+      case FAM_COMPOSITE_LINEAR: {
+        double f[kCompositeCount];
+        composite_vector(c, n, f);
+        double s = 0.0;
+        for (int k = 0; k < kCompositeCount; ++k)
+          if (w[k] != 0.0) s = s + w[k] * f[k];
+        if (std::isnan(s)) { o.exc = EXC_VALUE; return o; }
+        if (std::isinf(s)) { o.exc = EXC_OVERFLOW; return o; }
+        if (std::fabs(s) >= 9.2233720368547758e18) { o.exc = EXC_UNSUPPORTED; return o; }
+        o.v = Num::I(std::max<int64_t>(1, (int64_t)s));
+        return o;
+      }
     }
     o.exc = EXC_UNSUPPORTED;
     return o;
+  }
+
+  // Composite family (models/families.py COMPOSITE_FEATURES), Python
+  // int/float rules, feasible (pod, node) only.
+  static void composite_vector(const ScoreCtx& c, int n, double* f) {
+    const Workload& W = c.w;
+    const ClusterState& S = c.s;
+    const int p = c.pod;
+    const int g0 = W.gpu_start[n], ng = W.ngpus[n];
+    const bool gpod = W.pngpu[p] > 0;
+    const double cpu_u = (double)(W.cpu_total[n] - S.cpu_left[n]) / (double)std::max<int64_t>(1, W.cpu_total[n]);
+    const double mem_u = (double)(W.mem_total[n] - S.mem_left[n]) / (double)std::max<int64_t>(1, W.mem_total[n]);
+    int64_t free_m = 0, idle = 0, gmax = 0, gmin = 0, best = -1;
+    for (int j = 0; j < ng; ++j) {
+      const int64_t l = S.gmilli_left[g0 + j];
+      free_m += l;
+      idle += (l == W.gmilli_total[g0 + j]);
+      gmax = j == 0 ? l : std::max(gmax, l);
+      gmin = j == 0 ? l : std::min(gmin, l);
+      if (gpod && l >= W.pgmilli[p] && (best < 0 || l - W.pgmilli[p] < best)) best = l - W.pgmilli[p];
+    }
+    double gpu_u = 0.0;
+    if (gpod) {
+      const int64_t cap = (int64_t)S.gpu_left[n] * W.gmilli_total[g0];
+      gpu_u = (double)(cap - free_m) / (double)std::max<int64_t>(1, cap);
+    }
+    f[0] = 1.0;
+    f[1] = cpu_u < 0.7 ? 1.0 - cpu_u : 0.0;
+    f[2] = cpu_u >= 0.7 ? 1.0 - cpu_u : 0.0;
+    f[3] = mem_u < 0.7 ? 1.0 - mem_u : 0.0;
+    f[4] = mem_u >= 0.7 ? 1.0 - mem_u : 0.0;
+    f[5] = gpod ? (gpu_u < 0.7 ? 1.0 - gpu_u : 0.0) : 0.0;
+    f[6] = gpod ? (gpu_u >= 0.7 ? 1.0 - gpu_u : 0.0) : 0.0;
+    if (gpod) {
+      const int64_t d = std::max<int64_t>(1, W.pgmilli[p]);
+      int64_t m = free_m % d;
+      if (m != 0 && ((m < 0) != (d < 0))) m += d;
+      f[7] = (double)m;
+    } else {
+      f[7] = 0.0;
+    }
+    const double a = (double)S.cpu_left[n] / (double)std::max<int64_t>(1, S.mem_left[n]);
+    const double b = (double)W.pcpu[p] / (double)std::max<int64_t>(1, W.pmem[p]);
+    f[8] = std::fabs(a - b);
+    f[9] = (S.cpu_left[n] > W.pcpu[p] * 2 && S.mem_left[n] > W.pmem[p] * 2) ? 1.0 : 0.0;
+    f[10] = gpod ? (double)(gmax - gmin) : 0.0;
+    f[11] = (W.cpu_total[n] > 10000 && W.mem_total[n] > 64) ? 1.0 : 0.0;
+    f[12] = (cpu_u > 0.9 || mem_u > 0.9) ? 1.0 : 0.0;
+    f[13] = best < 0 ? 0.0 : (double)best / 1000.0;
+    f[14] = (double)idle / (double)std::max(1, ng);
+    f[15] = (W.pngpu[p] == 0 && ng > 0) ? 1.0 : 0.0;
   }
 
   // Feature vector of the generalised linear family.  Each entry is the

@@ -62,12 +62,6 @@ struct DevBuf {
   T* as() const { return reinterpret_cast<T*>(p); }
 };
 
-template <class KBuiltin, class KVm>
-struct KernelSet {
-  KBuiltin builtin[3];  // NPASS 1, 2, 4
-  KVm vm[3];
-};
-
 class DeviceEngine {
  public:
   DeviceEngine(py::dict d, int device) : device_(device) {
@@ -166,6 +160,9 @@ class DeviceEngine {
       throw std::invalid_argument("weights must be [P, 16] float64");
     HIP_OK(hipSetDevice(device_));
     ensure_batch(P);
+    fam_spec_ = P > 0 ? fam.at(0) : -1;
+    for (int i = 1; i < P && fam_spec_ >= 0; ++i)
+      if (fam.at(i) != fam_spec_) fam_spec_ = -1;
     HIP_OK(hipMemcpyAsync(fam_.p, fam.data(), (size_t)P * 4, hipMemcpyHostToDevice, stream_));
     HIP_OK(hipMemcpyAsync(w_.p, weights.data(), (size_t)P * kWeights * 8, hipMemcpyHostToDevice, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
@@ -198,14 +195,13 @@ class DeviceEngine {
     const size_t lds = lds_bytes(g, is_vm ? nregs : 0);
     uint64_t* gh = g ? gheap_for(P) : nullptr;
     if (is_vm) {
-      DevProgramTable T = table();
-      if (g) hipLaunchKernelGGL(k_replay_vm_prof<true>, dim3(P), dim3(64), lds, stream_, W_, T, res_.as<DevResult>(), budget_, gh, prof_.as<uint64_t>());
-      else hipLaunchKernelGGL(k_replay_vm_prof<false>, dim3(P), dim3(64), lds, stream_, W_, T, res_.as<DevResult>(), budget_, gh, prof_.as<uint64_t>());
+      const fksk::VmArgs a{W_, table(), res_.as<DevResult>(), budget_, gh, prof_.as<uint64_t>()};
+      HIP_OK(fksk::launch_vm_prof(g, P, lds, stream_, a));
     } else {
-      if (g) hipLaunchKernelGGL(k_replay_builtin_prof<true>, dim3(P), dim3(64), lds, stream_, W_, fam_.as<int32_t>(), w_.as<double>(), res_.as<DevResult>(), gh, prof_.as<uint64_t>());
-      else hipLaunchKernelGGL(k_replay_builtin_prof<false>, dim3(P), dim3(64), lds, stream_, W_, fam_.as<int32_t>(), w_.as<double>(), res_.as<DevResult>(), gh, prof_.as<uint64_t>());
+      const fksk::BuiltinArgs a{W_, fam_.as<int32_t>(), w_.as<double>(), res_.as<DevResult>(), gh,
+                                prof_.as<uint64_t>()};
+      HIP_OK(fksk::launch_builtin_prof(g, P, lds, stream_, a));
     }
-    HIP_OK(hipGetLastError());
     reduce(P);
     py::array_t<uint64_t> prof({(py::ssize_t)P, (py::ssize_t)8});
     HIP_OK(hipMemcpyAsync(prof.mutable_data(), prof_.p, (size_t)P * 64, hipMemcpyDeviceToHost, stream_));
@@ -230,14 +226,10 @@ class DeviceEngine {
 
   void set_attrs() {
     const int mx = (int)kMaxLds;
-#define FKS_ATTR(f) HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(&f), hipFuncAttributeMaxDynamicSharedMemorySize, mx))
-    FKS_ATTR((k_replay_builtin<1, false>)); FKS_ATTR((k_replay_builtin<2, false>)); FKS_ATTR((k_replay_builtin<4, false>));
-    FKS_ATTR((k_replay_builtin<1, true>)); FKS_ATTR((k_replay_builtin<2, true>)); FKS_ATTR((k_replay_builtin<4, true>));
-    FKS_ATTR((k_replay_vm<1, false>)); FKS_ATTR((k_replay_vm<2, false>)); FKS_ATTR((k_replay_vm<4, false>));
-    FKS_ATTR((k_replay_vm<1, true>)); FKS_ATTR((k_replay_vm<2, true>)); FKS_ATTR((k_replay_vm<4, true>));
-    FKS_ATTR((k_replay_builtin_prof<false>)); FKS_ATTR((k_replay_builtin_prof<true>));
-    FKS_ATTR((k_replay_vm_prof<false>)); FKS_ATTR((k_replay_vm_prof<true>));
-#undef FKS_ATTR
+    HIP_OK(fksk::set_builtin_attrs_np1(mx)); HIP_OK(fksk::set_builtin_attrs_np2(mx));
+    HIP_OK(fksk::set_builtin_attrs_np4(mx));
+    HIP_OK(fksk::set_vm_attrs_np1(mx)); HIP_OK(fksk::set_vm_attrs_np2(mx)); HIP_OK(fksk::set_vm_attrs_np4(mx));
+    HIP_OK(fksk::set_prof_attrs(mx));
   }
 
   bool use_gheap(int P) const {
@@ -299,15 +291,10 @@ class DeviceEngine {
     const bool g = use_gheap(P);
     const size_t lds = lds_bytes(g, 0);
     uint64_t* gh = g ? gheap_for(P) : nullptr;
-    const dim3 grid(P), block(64);
-    const int32_t* f = fam_.as<int32_t>();
-    const double* w = w_.as<double>();
-    DevResult* r = res_.as<DevResult>();
-#define FKS_LB(NP, G) hipLaunchKernelGGL((k_replay_builtin<NP, G>), grid, block, lds, stream_, W_, f, w, r, gh)
-    if (g) { if (npass_ == 1) FKS_LB(1, true); else if (npass_ == 2) FKS_LB(2, true); else FKS_LB(4, true); }
-    else { if (npass_ == 1) FKS_LB(1, false); else if (npass_ == 2) FKS_LB(2, false); else FKS_LB(4, false); }
-#undef FKS_LB
-    HIP_OK(hipGetLastError());
+    const fksk::BuiltinArgs a{W_, fam_.as<int32_t>(), w_.as<double>(), res_.as<DevResult>(), gh, nullptr};
+    if (npass_ == 1) HIP_OK(fksk::launch_builtin_np1(g, fam_spec_, P, lds, stream_, a));
+    else if (npass_ == 2) HIP_OK(fksk::launch_builtin_np2(g, fam_spec_, P, lds, stream_, a));
+    else HIP_OK(fksk::launch_builtin_np4(g, fam_spec_, P, lds, stream_, a));
     reduce(P);
   }
 
@@ -316,14 +303,10 @@ class DeviceEngine {
     const size_t lds = lds_bytes(g, nregs);
     if (lds > kMaxLds) throw std::invalid_argument("heap + VM registers exceed the 160 KiB LDS");
     uint64_t* gh = g ? gheap_for(P) : nullptr;
-    const dim3 grid(P), block(64);
-    DevProgramTable T = table();
-    DevResult* r = res_.as<DevResult>();
-#define FKS_LV(NP, G) hipLaunchKernelGGL((k_replay_vm<NP, G>), grid, block, lds, stream_, W_, T, r, budget_, gh)
-    if (g) { if (npass_ == 1) FKS_LV(1, true); else if (npass_ == 2) FKS_LV(2, true); else FKS_LV(4, true); }
-    else { if (npass_ == 1) FKS_LV(1, false); else if (npass_ == 2) FKS_LV(2, false); else FKS_LV(4, false); }
-#undef FKS_LV
-    HIP_OK(hipGetLastError());
+    const fksk::VmArgs a{W_, table(), res_.as<DevResult>(), budget_, gh, nullptr};
+    if (npass_ == 1) HIP_OK(fksk::launch_vm_np1(g, P, lds, stream_, a));
+    else if (npass_ == 2) HIP_OK(fksk::launch_vm_np2(g, P, lds, stream_, a));
+    else HIP_OK(fksk::launch_vm_np4(g, P, lds, stream_, a));
     reduce(P);
   }
 
@@ -348,6 +331,7 @@ class DeviceEngine {
   hipStream_t stream_ = nullptr;
   DevWorkload W_;
   int npass_ = 1;
+  int fam_spec_ = -1;   // family shared by the whole staged batch, or -1
   size_t heap_bytes_ = 0, delmap_bytes_ = 0;
   bool lds_heap_ok_ = true;
   int num_cus_ = 0;

@@ -1,0 +1,56 @@
+// Host-side launch API of the replay kernels.
+//
+// The kernels are compiled in separate translation units (one per NPASS and
+// kind, see replay_kernels.hip and ops/build.py) so the many template
+// instances build in parallel; module.hip only sees these launchers.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "replay.hip.h"
+#include "vm_dev.hip.h"
+
+namespace fksk {
+
+using fksd::DevProgramTable;
+using fksd::DevResult;
+using fksd::DevWorkload;
+
+struct BuiltinArgs {
+  DevWorkload W;
+  const int32_t* fam;     // [P] family id per policy
+  const double* weights;  // [P, kWeights]
+  DevResult* out;
+  uint64_t* gheap;        // HBM heap slices (GHEAP) or nullptr
+  uint64_t* prof;         // [P, 8] phase cycles (profiling launches only)
+};
+
+struct VmArgs {
+  DevWorkload W;
+  DevProgramTable T;
+  DevResult* out;
+  int64_t budget;
+  uint64_t* gheap;
+  uint64_t* prof;
+};
+
+// One set of launchers per NPASS (1, 2, 4), named *_np<NPASS>.
+// fam_spec >= 0: every policy of the batch has that family (specialised
+// kernel); -1: mixed batch.
+#define FKS_DECLARE_NPASS(N)                                                                          \
+  hipError_t launch_builtin_np##N(bool gheap, int fam_spec, int P, size_t lds, hipStream_t s,         \
+                                  const BuiltinArgs& a);                                              \
+  hipError_t launch_vm_np##N(bool gheap, int P, size_t lds, hipStream_t s, const VmArgs& a);          \
+  hipError_t set_builtin_attrs_np##N(int max_lds);                                                    \
+  hipError_t set_vm_attrs_np##N(int max_lds);
+FKS_DECLARE_NPASS(1)
+FKS_DECLARE_NPASS(2)
+FKS_DECLARE_NPASS(4)
+#undef FKS_DECLARE_NPASS
+
+// phase-profiled variants (NPASS = 1)
+hipError_t launch_builtin_prof(bool gheap, int P, size_t lds, hipStream_t s, const BuiltinArgs& a);
+hipError_t launch_vm_prof(bool gheap, int P, size_t lds, hipStream_t s, const VmArgs& a);
+hipError_t set_prof_attrs(int max_lds);
+
+}  // namespace fksk

@@ -3,9 +3,10 @@
 // DeviceEngine uploads one workload (SoA, already relabelled by pod rank and
 // with the initial heap pre-heapified on the host) to HBM once, then
 // evaluates batches of candidate policies: one k_replay workgroup per policy
-// (LDS-resident heap), followed by k_eval_reduce, on the engine's own HIP
-// stream.  Results come back as a float64 [P, 13] table with the same
-// columns as the CPU oracle's batch API.
+// (replay_kernels.hip, separate translation units), followed by
+// k_eval_reduce (here), on the engine's own HIP stream.  Results come back
+// as a float64 [P, 13] table with the same columns as the CPU oracle's batch
+// API.
 #include <hip/hip_runtime.h>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
@@ -16,6 +17,7 @@
 #include <string>
 #include <vector>
 
+#include "launch.h"
 #include "replay.hip.h"
 #include "scorers.hip.h"
 #include "vm_dev.hip.h"
@@ -26,81 +28,44 @@ using namespace fksd;
 
 namespace {
 
-// Where a policy's heap, deletion bitmap and VM registers live.
-//   GHEAP = false: heap | bitmap | vregs all in LDS (2 policies/CU on the 8k trace)
-//   GHEAP = true : heap in its HBM slice, bitmap | vregs in LDS (12-16 policies/CU)
-struct Slot {
-  uint64_t* h;
-  uint32_t* delmap;
-  uint64_t* vregs;
-};
-template <bool GHEAP>
-__device__ __forceinline__ Slot policy_slot(const DevWorkload& W, uint64_t* gheap, int p) {
-  extern __shared__ uint64_t lds[];
-  const int N = W.n_pods;
-  Slot s;
-  if (GHEAP) {
-    s.h = gheap + (size_t)p * lds_heap_entries(N);
-    s.delmap = reinterpret_cast<uint32_t*>(lds);
-    s.vregs = lds + lds_delmap_words(N) / 2;
-  } else {
-    s.h = lds;
-    s.delmap = reinterpret_cast<uint32_t*>(lds + lds_heap_entries(N));
-    s.vregs = lds + lds_vreg_offset(N);
+// ----------------------------------------------------------------------------
+// k_eval_reduce: exact means -> EvaluationResults + policy score, one lane per
+// policy (reference simulator/evaluator.py:77-127).
+// out columns: score, avg_cpu, avg_mem, avg_gcnt, avg_gmilli, frag, n_snap, n_frag,
+//              n_events, n_unplaced, exc, inexact, hash_hi
+__global__ __launch_bounds__(64) void k_eval_reduce(const DevResult* __restrict__ res, double* __restrict__ table, int P) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const DevResult r = res[p];
+  double* row = table + (size_t)p * 13;
+  if (r.exc != EXC_NONE) {   // an aborted replay reports only its exception class
+#pragma unroll
+    for (int k = 0; k < 13; ++k) row[k] = 0.0;
+    row[10] = (double)r.exc;
+    return;
   }
-  return s;
-}
-
-// Waves per SIMD the kernel is compiled for: the LDS-heap variant is LDS-bound at
-// 2 waves/CU anyway; the HBM-heap variant trades registers for occupancy.
-#define FKS_BOUNDS(G) __launch_bounds__(64, (G) ? 4 : 1)
-
-template <int NPASS, bool GHEAP>
-__global__ FKS_BOUNDS(GHEAP) void k_replay_builtin(DevWorkload W, const int32_t* __restrict__ fam,
-                                                   const double* __restrict__ weights, DevResult* out,
-                                                   uint64_t* gheap) {
-  const int p = blockIdx.x;
-  const Slot s = policy_slot<GHEAP>(W, gheap, p);
-  BuiltinScorerDev sc;
-  sc.family = fam[p];
+  double avg[5];
 #pragma unroll
-  for (int k = 0; k < kWeights; ++k) sc.w[k] = weights[(size_t)p * kWeights + k];
-  replay_one<NPASS>(W, sc, s.h, s.delmap, out + p);
+  for (int k = 0; k < 5; ++k) {
+    const i128 s = (i128)(((u128)r.acc_hi[k] << 64) | r.acc_lo[k]);
+    const int64_t c = k < 4 ? r.n_snap : r.n_frag;
+    avg[k] = c > 0 ? fixed_div_round_dev(s, (uint64_t)c) : 0.0;
+  }
+  double score = 0.0;
+  if (r.exc == EXC_NONE && r.n_snap > 0 && r.n_unplaced == 0) {
+    const double overall = (avg[0] + avg[1] + avg[2] + avg[3]) / 4.0;
+    const double pen = avg[4] < 0.1 ? avg[4] : 0.1;
+    double s = overall - pen;
+    s = s < 1.0 ? s : 1.0;
+    score = s > 0.0 ? s : 0.0;
+  }
+  row[0] = score;
+  row[1] = avg[0]; row[2] = avg[1]; row[3] = avg[2]; row[4] = avg[3]; row[5] = avg[4];
+  row[6] = (double)r.n_snap; row[7] = (double)r.n_frag; row[8] = (double)r.n_events;
+  row[9] = (double)r.n_unplaced; row[10] = (double)r.exc; row[11] = (double)r.inexact;
+  row[12] = (double)(r.hash >> 11);
 }
 
-template <int NPASS, bool GHEAP>
-__global__ FKS_BOUNDS(GHEAP) void k_replay_vm(DevWorkload W, DevProgramTable T, DevResult* out, int64_t budget,
-                                              uint64_t* gheap) {
-  const int p = blockIdx.x;
-  const Slot s = policy_slot<GHEAP>(W, gheap, p);
-  VmScorerDev sc;
-  sc.init(T, p, W, budget, s.vregs);
-  replay_one<NPASS>(W, sc, s.h, s.delmap, out + p);
-}
-
-// Phase-profiled variants (s_memtime per phase; diagnostics only, NPASS = 1).
-template <bool GHEAP>
-__global__ FKS_BOUNDS(GHEAP) void k_replay_builtin_prof(DevWorkload W, const int32_t* __restrict__ fam,
-                                                        const double* __restrict__ weights, DevResult* out,
-                                                        uint64_t* gheap, uint64_t* prof) {
-  const int p = blockIdx.x;
-  const Slot s = policy_slot<GHEAP>(W, gheap, p);
-  BuiltinScorerDev sc;
-  sc.family = fam[p];
-#pragma unroll
-  for (int k = 0; k < kWeights; ++k) sc.w[k] = weights[(size_t)p * kWeights + k];
-  replay_one<1, BuiltinScorerDev, PhaseProf>(W, sc, s.h, s.delmap, out + p, prof + (size_t)p * 8);
-}
-
-template <bool GHEAP>
-__global__ FKS_BOUNDS(GHEAP) void k_replay_vm_prof(DevWorkload W, DevProgramTable T, DevResult* out, int64_t budget,
-                                                   uint64_t* gheap, uint64_t* prof) {
-  const int p = blockIdx.x;
-  const Slot s = policy_slot<GHEAP>(W, gheap, p);
-  VmScorerDev sc;
-  sc.init(T, p, W, budget, s.vregs);
-  replay_one<1, VmScorerDev, PhaseProf>(W, sc, s.h, s.delmap, out + p, prof + (size_t)p * 8);
-}
 
 // ---- primitive self-tests (one wave) ----------------------------------------------
 // out[0] = wave max, out[1] = wave sum, out[2..65] = pair-swapped values,

@@ -419,42 +419,4 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* hbuf,
   }
 }
 
-// ----------------------------------------------------------------------------
-// k_eval_reduce: exact means -> EvaluationResults + policy score, one lane per
-// policy (reference simulator/evaluator.py:77-127).
-// out columns: score, avg_cpu, avg_mem, avg_gcnt, avg_gmilli, frag, n_snap, n_frag,
-//              n_events, n_unplaced, exc, inexact, hash_hi
-__global__ void k_eval_reduce(const DevResult* __restrict__ res, double* __restrict__ table, int P) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P) return;
-  const DevResult r = res[p];
-  double* row = table + (size_t)p * 13;
-  if (r.exc != EXC_NONE) {   // an aborted replay reports only its exception class
-#pragma unroll
-    for (int k = 0; k < 13; ++k) row[k] = 0.0;
-    row[10] = (double)r.exc;
-    return;
-  }
-  double avg[5];
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    const i128 s = (i128)(((u128)r.acc_hi[k] << 64) | r.acc_lo[k]);
-    const int64_t c = k < 4 ? r.n_snap : r.n_frag;
-    avg[k] = c > 0 ? fixed_div_round_dev(s, (uint64_t)c) : 0.0;
-  }
-  double score = 0.0;
-  if (r.exc == EXC_NONE && r.n_snap > 0 && r.n_unplaced == 0) {
-    const double overall = (avg[0] + avg[1] + avg[2] + avg[3]) / 4.0;
-    const double pen = avg[4] < 0.1 ? avg[4] : 0.1;
-    double s = overall - pen;
-    s = s < 1.0 ? s : 1.0;
-    score = s > 0.0 ? s : 0.0;
-  }
-  row[0] = score;
-  row[1] = avg[0]; row[2] = avg[1]; row[3] = avg[2]; row[4] = avg[3]; row[5] = avg[4];
-  row[6] = (double)r.n_snap; row[7] = (double)r.n_frag; row[8] = (double)r.n_events;
-  row[9] = (double)r.n_unplaced; row[10] = (double)r.exc; row[11] = (double)r.inexact;
-  row[12] = (double)(r.hash >> 11);
-}
-
 }  // namespace fksd

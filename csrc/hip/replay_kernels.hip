@@ -1,0 +1,180 @@
+// Replay kernels: one wave64 workgroup per candidate policy.
+//
+// Compiled once per (FKS_KIND, FKS_NPASS) by ops/build.py:
+//   FKS_KIND 0 -> built-in family kernels for FKS_NPASS (one instance per family + a mixed one)
+//   FKS_KIND 1 -> bytecode-VM kernels for FKS_NPASS
+//   FKS_KIND 2 -> phase-profiled diagnostics kernels (NPASS = 1)
+// Each unit defines the matching launchers of launch.h.
+#include <hip/hip_runtime.h>
+
+#include "launch.h"
+#include "replay.hip.h"
+#include "scorers.hip.h"
+#include "vm_dev.hip.h"
+
+#ifndef FKS_KIND
+#define FKS_KIND 0
+#endif
+#ifndef FKS_NPASS
+#define FKS_NPASS 1
+#endif
+
+using namespace fksd;
+
+namespace {
+
+// Where a policy's heap, deletion bitmap and VM registers live.
+//   GHEAP = false: heap | bitmap | vregs all in LDS (2 policies/CU on the 8k trace)
+//   GHEAP = true : heap in its HBM slice, bitmap | vregs in LDS (12-16 policies/CU)
+struct Slot {
+  uint64_t* h;
+  uint32_t* delmap;
+  uint64_t* vregs;
+};
+template <bool GHEAP>
+__device__ __forceinline__ Slot policy_slot(const DevWorkload& W, uint64_t* gheap, int p) {
+  extern __shared__ uint64_t lds[];
+  const int N = W.n_pods;
+  Slot s;
+  if (GHEAP) {
+    s.h = gheap + (size_t)p * lds_heap_entries(N);
+    s.delmap = reinterpret_cast<uint32_t*>(lds);
+    s.vregs = lds + lds_delmap_words(N) / 2;
+  } else {
+    s.h = lds;
+    s.delmap = reinterpret_cast<uint32_t*>(lds + lds_heap_entries(N));
+    s.vregs = lds + lds_vreg_offset(N);
+  }
+  return s;
+}
+
+// Waves per SIMD the kernel is compiled for: the LDS-heap variant is LDS-bound at
+// 2 waves/CU anyway; the HBM-heap variant trades registers for occupancy.
+#define FKS_BOUNDS(G) __launch_bounds__(64, (G) ? 4 : 1)
+
+template <class T>
+hipError_t raise_lds(T* f, int max_lds) {
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize, max_lds);
+}
+
+#if FKS_KIND == 0
+template <int NPASS, bool GHEAP, int FAM>
+__global__ FKS_BOUNDS(GHEAP) void k_replay_builtin(fksk::BuiltinArgs a) {
+  const int p = blockIdx.x;
+  const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
+  BuiltinScorerDev<FAM> sc;
+  sc.load(a.fam[p], a.weights + (size_t)p * kWeights);
+  replay_one<NPASS>(a.W, sc, s.h, s.delmap, a.out + p);
+}
+
+template <int NPASS, bool GHEAP>
+hipError_t launch_g(int fam, int P, size_t lds, hipStream_t st, const fksk::BuiltinArgs& a) {
+#define FKS_CASE(F) \
+  case F: hipLaunchKernelGGL((k_replay_builtin<NPASS, GHEAP, F>), dim3(P), dim3(64), lds, st, a); break;
+  switch (fam) {
+    FKS_CASE(FAM_FIRST_FIT)
+    FKS_CASE(FAM_BEST_FIT)
+    FKS_CASE(FAM_RANDOM_LINEAR)
+    FKS_CASE(FAM_FEATURE_LINEAR)
+    FKS_CASE(FAM_COMPOSITE_LINEAR)
+    default: hipLaunchKernelGGL((k_replay_builtin<NPASS, GHEAP, -1>), dim3(P), dim3(64), lds, st, a);
+  }
+#undef FKS_CASE
+  return hipGetLastError();
+}
+
+template <int NPASS, bool GHEAP>
+hipError_t attrs_g(int mx) {
+  hipError_t e = hipSuccess;
+  for (hipError_t r : {raise_lds(&k_replay_builtin<NPASS, GHEAP, -1>, mx),
+                       raise_lds(&k_replay_builtin<NPASS, GHEAP, FAM_FIRST_FIT>, mx),
+                       raise_lds(&k_replay_builtin<NPASS, GHEAP, FAM_BEST_FIT>, mx),
+                       raise_lds(&k_replay_builtin<NPASS, GHEAP, FAM_RANDOM_LINEAR>, mx),
+                       raise_lds(&k_replay_builtin<NPASS, GHEAP, FAM_FEATURE_LINEAR>, mx),
+                       raise_lds(&k_replay_builtin<NPASS, GHEAP, FAM_COMPOSITE_LINEAR>, mx)})
+    if (r != hipSuccess) e = r;
+  return e;
+}
+#endif
+
+#if FKS_KIND == 1
+template <int NPASS, bool GHEAP>
+__global__ FKS_BOUNDS(GHEAP) void k_replay_vm(fksk::VmArgs a) {
+  const int p = blockIdx.x;
+  const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
+  VmScorerDev sc;
+  sc.init(a.T, p, a.W, a.budget, s.vregs);
+  replay_one<NPASS>(a.W, sc, s.h, s.delmap, a.out + p);
+}
+#endif
+
+#if FKS_KIND == 2
+template <bool GHEAP>
+__global__ FKS_BOUNDS(GHEAP) void k_replay_builtin_prof(fksk::BuiltinArgs a) {
+  const int p = blockIdx.x;
+  const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
+  BuiltinScorerDev<-1> sc;
+  sc.load(a.fam[p], a.weights + (size_t)p * kWeights);
+  replay_one<1, BuiltinScorerDev<-1>, PhaseProf>(a.W, sc, s.h, s.delmap, a.out + p, a.prof + (size_t)p * 8);
+}
+
+template <bool GHEAP>
+__global__ FKS_BOUNDS(GHEAP) void k_replay_vm_prof(fksk::VmArgs a) {
+  const int p = blockIdx.x;
+  const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
+  VmScorerDev sc;
+  sc.init(a.T, p, a.W, a.budget, s.vregs);
+  replay_one<1, VmScorerDev, PhaseProf>(a.W, sc, s.h, s.delmap, a.out + p, a.prof + (size_t)p * 8);
+}
+#endif
+
+}  // namespace
+
+namespace fksk {
+
+#define FKS_CAT2(a, b) a##b
+#define FKS_CAT(a, b) FKS_CAT2(a, b)
+
+#if FKS_KIND == 0
+hipError_t FKS_CAT(launch_builtin_np, FKS_NPASS)(bool gheap, int fam, int P, size_t lds, hipStream_t s, const BuiltinArgs& a) {
+  return gheap ? launch_g<FKS_NPASS, true>(fam, P, lds, s, a) : launch_g<FKS_NPASS, false>(fam, P, lds, s, a);
+}
+hipError_t FKS_CAT(set_builtin_attrs_np, FKS_NPASS)(int mx) {
+  const hipError_t e = attrs_g<FKS_NPASS, true>(mx);
+  return e != hipSuccess ? e : attrs_g<FKS_NPASS, false>(mx);
+}
+#endif
+
+#if FKS_KIND == 1
+hipError_t FKS_CAT(launch_vm_np, FKS_NPASS)(bool gheap, int P, size_t lds, hipStream_t s, const VmArgs& a) {
+  if (gheap) hipLaunchKernelGGL((k_replay_vm<FKS_NPASS, true>), dim3(P), dim3(64), lds, s, a);
+  else hipLaunchKernelGGL((k_replay_vm<FKS_NPASS, false>), dim3(P), dim3(64), lds, s, a);
+  return hipGetLastError();
+}
+hipError_t FKS_CAT(set_vm_attrs_np, FKS_NPASS)(int mx) {
+  const hipError_t e = raise_lds(&k_replay_vm<FKS_NPASS, true>, mx);
+  return e != hipSuccess ? e : raise_lds(&k_replay_vm<FKS_NPASS, false>, mx);
+}
+#endif
+
+#if FKS_KIND == 2
+hipError_t launch_builtin_prof(bool gheap, int P, size_t lds, hipStream_t s, const BuiltinArgs& a) {
+  if (gheap) hipLaunchKernelGGL(k_replay_builtin_prof<true>, dim3(P), dim3(64), lds, s, a);
+  else hipLaunchKernelGGL(k_replay_builtin_prof<false>, dim3(P), dim3(64), lds, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_vm_prof(bool gheap, int P, size_t lds, hipStream_t s, const VmArgs& a) {
+  if (gheap) hipLaunchKernelGGL(k_replay_vm_prof<true>, dim3(P), dim3(64), lds, s, a);
+  else hipLaunchKernelGGL(k_replay_vm_prof<false>, dim3(P), dim3(64), lds, s, a);
+  return hipGetLastError();
+}
+hipError_t set_prof_attrs(int mx) {
+  hipError_t e = hipSuccess;
+  for (hipError_t r : {raise_lds(&k_replay_builtin_prof<true>, mx), raise_lds(&k_replay_builtin_prof<false>, mx),
+                       raise_lds(&k_replay_vm_prof<true>, mx), raise_lds(&k_replay_vm_prof<false>, mx)})
+    if (r != hipSuccess) e = r;
+  return e;
+}
+#endif
+
+}  // namespace fksk

@@ -7,8 +7,11 @@
 
 namespace fksd {
 
-enum BuiltinFamily : int32_t { FAM_FIRST_FIT = 0, FAM_BEST_FIT = 1, FAM_RANDOM_LINEAR = 2, FAM_FEATURE_LINEAR = 3 };
+enum BuiltinFamily : int32_t {
+  FAM_FIRST_FIT = 0, FAM_BEST_FIT = 1, FAM_RANDOM_LINEAR = 2, FAM_FEATURE_LINEAR = 3, FAM_COMPOSITE_LINEAR = 4
+};
 constexpr int kFeatureCount = 12;
+constexpr int kCompositeCount = 16;
 constexpr int kWeights = 16;
 
 // int(max(0, s)) of a float score produced by `max(1, int(score))`-style code
@@ -32,14 +35,30 @@ __device__ __forceinline__ bool feasible(int ps, const NodeRegs<NPASS>& nr, cons
   return true;
 }
 
+// Number of weights a family reads (the rest are never loaded).
+__host__ __device__ constexpr int family_weights(int fam) {
+  return fam == FAM_RANDOM_LINEAR ? 4 : fam == FAM_FEATURE_LINEAR ? kFeatureCount
+       : fam == FAM_COMPOSITE_LINEAR ? kCompositeCount : fam < 0 ? kWeights : 0;
+}
+
+// FAM >= 0: the family is a compile-time constant (one kernel instance per
+// family, so a launch only carries the registers of its own scorer);
+// FAM = -1: mixed-family batches dispatch on the per-policy id.
+template <int FAM = -1>
 struct BuiltinScorerDev {
   int32_t family;
   double w[kWeights];
 
+  __device__ void load(int32_t fam_id, const double* __restrict__ wp) {
+    family = FAM >= 0 ? FAM : fam_id;
+#pragma unroll
+    for (int k = 0; k < kWeights; ++k) w[k] = k < family_weights(FAM) ? wp[k] : 0.0;
+  }
+
   template <int NPASS>
   __device__ int64_t score(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, int& exc) const {
     if (!feasible<NPASS>(ps, nr, pod)) return 0;
-    switch (family) {
+    switch (FAM >= 0 ? FAM : family) {
       case FAM_FIRST_FIT:
         return 1000;
       case FAM_BEST_FIT: {
@@ -71,9 +90,68 @@ struct BuiltinScorerDev {
           if (w[k] != 0.0) s = s + w[k] * f[k];
         return trunc_score(s, exc);
       }
+      case FAM_COMPOSITE_LINEAR:
+        return trunc_score(composite<NPASS>(ps, nr, pod), exc);
     }
     exc = EXC_UNSUPPORTED;
     return 0;
+  }
+
+  // twin of fks::BuiltinScorer::composite_vector (csrc/cpu/builtin_scorers.hpp):
+  // the weighted terms are accumulated as they are produced (same order and
+  // rounding as `score += w_k * (f_k)`), so no 16-double feature vector is
+  // held live across the node loop.
+  template <int NPASS>
+  __device__ double composite(int ps, const NodeRegs<NPASS>& nr, const PodView& pod) const {
+    const int ng = nr.ngpus[ps];
+    const bool gpod = pod.ngpu > 0;
+    const int64_t ct = nr.cpu_total[ps], mt = nr.mem_total[ps];
+    const int64_t cl = nr.cpu_left[ps], ml = nr.mem_left[ps];
+    const double cpu_u = (double)(ct - cl) / (double)(ct > 1 ? ct : 1);
+    const double mem_u = (double)(mt - ml) / (double)(mt > 1 ? mt : 1);
+    int64_t free_m = 0, idle = 0, gmax = 0, gmin = 0, best = -1;
+#pragma unroll
+    for (int j = 0; j < kGmax; ++j) {
+      if (j < ng) {
+        const int64_t l = nr.gml[ps][j];
+        free_m += l;
+        idle += (l == nr.gmt[ps][j]);
+        gmax = (j == 0 || l > gmax) ? l : gmax;
+        gmin = (j == 0 || l < gmin) ? l : gmin;
+        if (gpod && l >= pod.gmilli && (best < 0 || l - pod.gmilli < best)) best = l - pod.gmilli;
+      }
+    }
+    double gpu_u = 0.0;
+    if (gpod) {
+      const int64_t cap = (int64_t)nr.gpu_left[ps] * nr.gmt[ps][0];
+      gpu_u = (double)(cap - free_m) / (double)(cap > 1 ? cap : 1);
+    }
+    double s = 0.0;
+    auto acc = [&](int k, double f) { if (w[k] != 0.0) s = s + w[k] * f; };
+    acc(0, 1.0);
+    acc(1, cpu_u < 0.7 ? 1.0 - cpu_u : 0.0);
+    acc(2, cpu_u >= 0.7 ? 1.0 - cpu_u : 0.0);
+    acc(3, mem_u < 0.7 ? 1.0 - mem_u : 0.0);
+    acc(4, mem_u >= 0.7 ? 1.0 - mem_u : 0.0);
+    acc(5, gpod ? (gpu_u < 0.7 ? 1.0 - gpu_u : 0.0) : 0.0);
+    acc(6, gpod ? (gpu_u >= 0.7 ? 1.0 - gpu_u : 0.0) : 0.0);
+    {
+      const int64_t d = pod.gmilli > 1 ? pod.gmilli : 1;
+      int64_t m = free_m % d;
+      if (m != 0 && ((m < 0) != (d < 0))) m += d;
+      acc(7, gpod ? (double)m : 0.0);
+    }
+    const double a = (double)cl / (double)(ml > 1 ? ml : 1);
+    const double b = (double)pod.cpu / (double)(pod.mem > 1 ? pod.mem : 1);
+    acc(8, fabs(a - b));
+    acc(9, (cl > (int64_t)pod.cpu * 2 && ml > (int64_t)pod.mem * 2) ? 1.0 : 0.0);
+    acc(10, gpod ? (double)(gmax - gmin) : 0.0);
+    acc(11, (ct > 10000 && mt > 64) ? 1.0 : 0.0);
+    acc(12, (cpu_u > 0.9 || mem_u > 0.9) ? 1.0 : 0.0);
+    acc(13, best < 0 ? 0.0 : (double)best / 1000.0);
+    acc(14, (double)idle / (double)(ng > 1 ? ng : 1));
+    acc(15, (!gpod && ng > 0) ? 1.0 : 0.0);
+    return s;
   }
 
   template <int NPASS>

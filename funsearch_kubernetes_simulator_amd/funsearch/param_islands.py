@@ -102,7 +102,7 @@ class ParamIsland:
 
 
 def make_islands(n: int, family: str, n_candidates: int, elite_size: int, seed: int) -> List[ParamIsland]:
-    sampler = fam.sample_random_linear if family == "random_linear" else fam.sample_feature_linear
+    sampler = fam.SAMPLERS[family]
     return [ParamIsland(family, n_candidates, elite_size, np.random.default_rng(seed + 7919 * i), sampler)
             for i in range(n)]
 

@@ -15,6 +15,10 @@ engine or handed to the LLM loop with a bit-identical score.
 * ``feature_linear`` -- a 12-feature linear score (remaining-capacity
   fractions, balance, GPU fragmentation / slack / idle-GPU terms, node size)
   used by the evolutionary search.
+* ``composite_linear`` -- a 16-term basis that contains the reference
+  champion's scoring terms (piecewise utilisation, GPU-milli remainder,
+  ratio balance, bonuses/penalties), so search starts next to 0.4901 and
+  explores around it.
 """
 
 from __future__ import annotations
@@ -92,11 +96,83 @@ def sample_feature_linear(n: int, rng: np.random.Generator, scale: float = 1000.
     return w
 
 
+# ---------------------------------------------------------------- composite_linear
+#: Shared sub-expressions of the composite family (evaluated once per call,
+#: never raise: every divisor is clamped with max(1, .)).
+COMPOSITE_PREAMBLE = (
+    "    cpu_u = (node.cpu_milli_total - node.cpu_milli_left) / max(1, node.cpu_milli_total)\n"
+    "    mem_u = (node.memory_mib_total - node.memory_mib_left) / max(1, node.memory_mib_total)\n"
+    "    gpu_u = ((node.gpu_left * node.gpus[0].gpu_milli_total - sum(g.gpu_milli_left for g in node.gpus))"
+    " / max(1, node.gpu_left * node.gpus[0].gpu_milli_total)) if pod.num_gpu > 0 else 0.0\n")
+
+#: The champion's decomposition (reference `tests/test_scheduler.py:21-99`,
+#: score 0.4901): piecewise utilisation scores, GPU-milli remainder, cpu/mem
+#: ratio balance, "ample resources" / "big node" bonuses, GPU imbalance and
+#: the nearly-full penalty -- plus three best-fit style GPU terms.
+COMPOSITE_FEATURES: List[tuple] = [
+    ("bias", "1.0"),
+    ("cpu_free_lo", "(1.0 - cpu_u) if cpu_u < 0.7 else 0.0"),
+    ("cpu_free_hi", "(1.0 - cpu_u) if cpu_u >= 0.7 else 0.0"),
+    ("mem_free_lo", "(1.0 - mem_u) if mem_u < 0.7 else 0.0"),
+    ("mem_free_hi", "(1.0 - mem_u) if mem_u >= 0.7 else 0.0"),
+    ("gpu_free_lo", "((1.0 - gpu_u) if gpu_u < 0.7 else 0.0) if pod.num_gpu > 0 else 0.0"),
+    ("gpu_free_hi", "((1.0 - gpu_u) if gpu_u >= 0.7 else 0.0) if pod.num_gpu > 0 else 0.0"),
+    ("gpu_milli_remainder",
+     "(sum(g.gpu_milli_left for g in node.gpus) % max(1, pod.gpu_milli)) if pod.num_gpu > 0 else 0"),
+    ("cpu_mem_ratio_gap",
+     "abs(node.cpu_milli_left / max(1, node.memory_mib_left) - pod.cpu_milli / max(1, pod.memory_mib))"),
+    ("ample_resources",
+     "1.0 if (node.cpu_milli_left > pod.cpu_milli * 2 and node.memory_mib_left > pod.memory_mib * 2) else 0.0"),
+    ("gpu_imbalance",
+     "(max(g.gpu_milli_left for g in node.gpus) - min(g.gpu_milli_left for g in node.gpus))"
+     " if pod.num_gpu > 0 else 0"),
+    ("big_node", "1.0 if (node.cpu_milli_total > 10000 and node.memory_mib_total > 64) else 0.0"),
+    ("nearly_full", "1.0 if (cpu_u > 0.9 or mem_u > 0.9) else 0.0"),
+    ("best_fit_gpu_slack", FEATURES[10][1]),
+    ("idle_gpu_fraction", FEATURES[7][1]),
+    ("cpu_pod_on_gpu_node", FEATURES[9][1]),
+]
+N_COMPOSITE = len(COMPOSITE_FEATURES)
+
+#: The champion's weights in this basis (its scores differ only by the float
+#: summation order of the terms).
+CHAMPION_COMPOSITE = np.array([0.0, 100.0, 50.0, 100.0, 50.0, 200.0, 100.0, -0.2, -0.5, 25.0, -0.05, 15.0, -20.0,
+                               0.0, 0.0, 0.0])
+_COMPOSITE_SCALE = np.array([20.0, 50.0, 25.0, 50.0, 25.0, 100.0, 50.0, 0.1, 0.25, 12.0, 0.025, 8.0, 10.0,
+                             50.0, 50.0, 20.0])
+
+
+def composite_linear_program(w: Sequence[float]) -> str:
+    lines = [COMPOSITE_PREAMBLE + "    score = 0.0"]
+    for (name, expr), wk in zip(COMPOSITE_FEATURES, w):
+        wk = float(wk)
+        if wk != 0.0:
+            lines.append(f"    score += {wk!r} * ({expr})  # {name}")
+    return _HEAD + "\n".join(lines) + "\n    \n    return max(1, int(score))\n"
+
+
+def sample_composite_linear(n: int, rng: np.random.Generator) -> np.ndarray:
+    """Prior around the champion: log-normal rescaling of its terms, Gaussian
+    values for the terms it does not use, occasional sign flips."""
+    w = CHAMPION_COMPOSITE * np.exp(rng.normal(0.0, 0.6, size=(n, N_COMPOSITE)))
+    unused = CHAMPION_COMPOSITE == 0.0
+    w[:, unused] = rng.normal(0.0, 1.0, size=(n, int(unused.sum()))) * _COMPOSITE_SCALE[unused]
+    flip = rng.random(w.shape) < 0.05
+    w[flip] = -w[flip]
+    return w
+
+
+SAMPLERS = {"random_linear": sample_random_linear, "feature_linear": sample_feature_linear,
+            "composite_linear": sample_composite_linear}
+
+
 def to_program(family: str, w: Sequence[float]) -> str:
     if family == "random_linear":
         return random_linear_program(w)
     if family == "feature_linear":
         return feature_linear_program(w)
+    if family == "composite_linear":
+        return composite_linear_program(w)
     raise KeyError(family)
 
 

@@ -65,17 +65,40 @@ def build_cpu(force: bool = False) -> Path:
     return target
 
 
-def build_hip(force: bool = False) -> Path:
+#: Device translation units of _fks_hip: (object name, extra defines).  The
+#: replay kernels are split per NPASS and kind so their many template
+#: instances compile in parallel.
+HIP_UNITS = [("module", "module.hip", [])] + [
+    (f"replay_k{kind}_np{npass}", "replay_kernels.hip", [f"-DFKS_KIND={kind}", f"-DFKS_NPASS={npass}"])
+    for kind, npasses in ((0, (1, 2, 4)), (1, (1, 2, 4)), (2, (1,))) for npass in npasses]
+
+
+def _hip_flags() -> List[str]:
+    return [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-ffp-contract=off",
+            "-fno-fast-math", "-munsafe-fp-atomics", "-Wno-unused-result",
+            *_py_includes(), f"-I{CSRC_DIR / 'include'}", f"-I{CSRC_DIR / 'hip'}"]
+
+
+def build_hip(force: bool = False, jobs: int = 0) -> Path:
+    """Compile every HIP unit for gfx950 (in parallel) and link ``_fks_hip``."""
+    from concurrent.futures import ThreadPoolExecutor
     target = NATIVE_DIR / f"_fks_hip{_ext_suffix()}"
     srcs = _deps("hip/*.hip", "hip/*.h", "hip/*.cpp", "include/fks/*.hpp")
-    if force or _stale(target, srcs):
-        hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
-               "-fvisibility=hidden", "-ffp-contract=off", "-fno-fast-math",
-               "-munsafe-fp-atomics", "-Wno-unused-result",
-               *_py_includes(), f"-I{CSRC_DIR / 'include'}", f"-I{CSRC_DIR / 'hip'}",
-               str(CSRC_DIR / "hip" / "module.hip"), "-o", str(target)]
-        _run(cmd)
+    if not (force or _stale(target, srcs)):
+        return target
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    obj_dir = NATIVE_DIR.parent.parent / "build" / "hip_obj"
+    obj_dir.mkdir(parents=True, exist_ok=True)
+    flags = _hip_flags()
+    cmds, objs = [], []
+    for name, src, defs in HIP_UNITS:
+        obj = obj_dir / f"{name}.o"
+        objs.append(obj)
+        cmds.append([hipcc, *flags, *defs, "-c", str(CSRC_DIR / "hip" / src), "-o", str(obj)])
+    jobs = jobs or min(len(cmds), int(os.environ.get("MAX_JOBS", "0")) or os.cpu_count() or 1, 16)
+    with ThreadPoolExecutor(jobs) as ex:
+        list(ex.map(_run, cmds))
+    _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(target)])
     return target
 
 

@@ -18,7 +18,7 @@ from ..policy.compiler import CompiledPolicy
 
 _mod = None
 
-FAMILY = {"first_fit": 0, "best_fit": 1, "random_linear": 2, "feature_linear": 3}
+FAMILY = {"first_fit": 0, "best_fit": 1, "random_linear": 2, "feature_linear": 3, "composite_linear": 4}
 
 
 def native():

@@ -2,6 +2,7 @@
 import numpy as np
 import pytest
 
+from funsearch_kubernetes_simulator_amd.models import families as fam
 from funsearch_kubernetes_simulator_amd.models.library import reference_policies, reference_scores
 from funsearch_kubernetes_simulator_amd.ops import cpu_engine as ce
 from funsearch_kubernetes_simulator_amd.policy.compiler import compile_policy
@@ -42,6 +43,13 @@ def test_feature_linear_matches_cpu(dev, default_workload):
     w = rng.normal(0, 1000, size=(P, 12))
     gpu = dev.evaluate_builtin("feature_linear", w)
     cpu = ce.simulate_builtin_batch(default_workload, "feature_linear", w)
+    assert np.array_equal(gpu, cpu)
+
+
+def test_composite_linear_matches_cpu(dev, default_workload):
+    w = fam.sample_composite_linear(128, np.random.default_rng(12))
+    gpu = dev.evaluate_builtin("composite_linear", w)
+    cpu = ce.simulate_builtin_batch(default_workload, "composite_linear", w)
     assert np.array_equal(gpu, cpu)
 
 

@@ -38,17 +38,22 @@ def test_builtin_equals_vm_trace(default_workload):
     assert b["trace_hash"] == v["trace_hash"]
 
 
-@pytest.mark.parametrize("family", ["random_linear", "feature_linear"])
+@pytest.mark.parametrize("family", ["random_linear", "feature_linear", "composite_linear"])
 def test_family_text_matches_builtin(default_workload, family):
     rng = np.random.default_rng(42)
-    sampler = fam.sample_random_linear if family == "random_linear" else fam.sample_feature_linear
-    W = sampler(6, rng)
+    W = fam.SAMPLERS[family](6, rng)
     tab = ce.simulate_builtin_batch(default_workload, family, W, threads=4)
     progs = [compile_policy(fam.to_program(family, w)) for w in W]
     tab2 = ce.simulate_program_batch(default_workload, progs, threads=4)
     assert np.array_equal(tab, tab2)
     # and the object engine (CPython exec) agrees on one member
     assert object_engine_eval(fam.to_program(family, W[0]), default_workload).score == tab[0, 0]
+
+
+def test_composite_basis_contains_champion(default_workload):
+    """The champion (reference tests/test_scheduler.py:21) is a member of the composite basis."""
+    r = ce.simulate_builtin(default_workload, "composite_linear", list(fam.CHAMPION_COMPOSITE))
+    assert r["score"] == reference_scores()["funsearch_4901"]
 
 
 def test_exact_mean_matches_statistics():
