@@ -3,12 +3,21 @@
 OpenB trace (16-node / 64-GPU cluster), island-model search on MI355X.
 
 One step = one generation of every island on every GPU: each rank runs
-`--islands` islands x `--candidates` random-weight candidate policies (the
-reference's `_create_random_policy` family), evaluated exactly (bit-identical
-to the reference scorer) in one batched k_replay launch, followed by elite
-selection; every `--migrate-every` generations the islands exchange elites
-with an RCCL all-gather.  `value` = total evaluations per second over all
-ranks (weak scaling: per-GPU work is fixed).
+`--islands` islands x `--candidates` random-weight candidate policies,
+evaluated exactly (bit-identical to the reference scorer) in one batched
+k_replay launch, followed by elite selection; every `--migrate-every`
+generations the islands exchange elites with an RCCL all-gather.  `value` =
+total evaluations per second over all ranks (weak scaling: per-GPU work is
+fixed).  The second half of the headline metric -- the champion's
+utilisation / fragmentation -- is the best policy found during the run
+(all-gathered over ranks after the timed region); `--save-best` writes it as
+a policy program in the reference's results-JSON schema.
+
+Candidate families (models/families.py): `composite_linear` (default; the
+reference's `_create_random_policy` idea generalised to a 16-term linear
+basis that contains the README champion), `feature_linear`, and
+`random_linear` (exactly `_create_random_policy`,
+`funsearch/funsearch_integration.py:403-431`).
 
     python bench.py --gpus 1 --steps 10 --warmup 2
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
@@ -38,12 +47,15 @@ def main() -> None:
     ap.add_argument("--islands", type=int, default=4, help="islands per GPU")
     ap.add_argument("--candidates", type=int, default=1024, help="candidates per island per generation")
     ap.add_argument("--elite", type=int, default=32)
-    ap.add_argument("--family", default="random_linear", choices=["random_linear", "feature_linear", "composite_linear"])
+    ap.add_argument("--family", default="composite_linear", choices=["random_linear", "feature_linear", "composite_linear"])
     ap.add_argument("--migrate-every", type=int, default=5)
     ap.add_argument("--migrants", type=int, default=8)
     ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"])
     ap.add_argument("--heap-mode", default="auto", choices=["auto", "lds", "hbm"])
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--sync-islands", action="store_true",
+                    help="one launch per generation for all islands (default: one HIP stream per island)")
+    ap.add_argument("--save-best", default="", help="write the champion program (reference results-JSON schema)")
     args = ap.parse_args()
 
     from funsearch_kubernetes_simulator_amd.parallel import dist
@@ -58,7 +70,7 @@ def main() -> None:
 
     workload = load_default_workload()
     device = ctx.local_rank if args.device == "gpu" else "cpu"
-    ev = Evaluator(workload, device=device, options={"heap_mode": args.heap_mode})
+    ev = Evaluator(workload, device=device, options={"heap_mode": args.heap_mode}, n_slots=max(1, args.islands))
     if args.device == "gpu" and ev.device is None:
         raise SystemExit("no HIP device visible")
     islands = make_islands(args.islands, args.family, args.candidates, args.elite,
@@ -71,38 +83,89 @@ def main() -> None:
             torch.cuda.synchronize()
         dist.barrier()
 
-    best_row = [None, -1.0]
+    best_row = [None, -1.0, None, -1]   # table row, score, weights, generation
+    events = [0.0]
 
-    def step(gen: int) -> None:
-        props = [isl.propose() for isl in islands]
-        W = np.concatenate(props)
-        tab = ev.evaluate_family(args.family, W)
-        off = 0
-        for isl, p in zip(islands, props):
-            sc = tab[off:off + len(p), COLS["score"]]
-            isl.update(p, sc)
-            j = int(np.argmax(sc))
-            if sc[j] > best_row[1]:
-                best_row[0], best_row[1] = tab[off + j].copy(), float(sc[j])
-            off += len(p)
-        if args.migrate_every and (gen + 1) % args.migrate_every == 0:
-            migrate(islands, args.migrants, gather)
+    def absorb(isl, props, tab, gen: int) -> None:
+        sc = tab[:, COLS["score"]]
+        isl.update(props, sc)
+        events[0] += float(tab[:, COLS["n_events"]].sum())
+        j = int(np.argmax(sc))
+        if sc[j] > best_row[1]:
+            best_row[:] = [tab[j].copy(), float(sc[j]), props[j].copy(), gen]
 
-    for g in range(args.warmup):
-        step(g)
+    def epoch_sync(gen0: int, n: int) -> None:
+        """All islands in one launch per generation (--sync-islands)."""
+        for gen in range(gen0, gen0 + n):
+            props = [isl.propose() for isl in islands]
+            tab = ev.evaluate_family(args.family, np.concatenate(props))
+            off = 0
+            for isl, p in zip(islands, props):
+                absorb(isl, p, tab[off:off + len(p)], gen)
+                off += len(p)
+
+    def epoch_async(gen0: int, n: int) -> None:
+        """Each island advances n generations on its own HIP stream (slot): an
+        island whose batch holds long-replay stragglers does not hold back the
+        others, whose next launches fill the CUs its finished waves free."""
+        k = len(islands)
+        props, gens, left = [None] * k, [gen0] * k, [n] * k
+
+        def launch(i: int) -> None:
+            props[i] = islands[i].propose()
+            ev.submit_family(i, args.family, props[i])
+
+        for i in range(k):
+            launch(i)
+        pending = set(range(k))
+        while pending:
+            progressed = False
+            for i in sorted(pending):
+                if not ev.ready(i):
+                    continue
+                absorb(islands[i], props[i], ev.wait(i), gens[i])
+                gens[i] += 1
+                left[i] -= 1
+                progressed = True
+                if left[i]:
+                    launch(i)
+                else:
+                    pending.discard(i)
+            if not progressed:
+                time.sleep(0.0002)
+
+    def run(g0: int, count: int) -> None:
+        """`count` generations of every island; migration (an RCCL all-gather
+        across ranks) at every multiple of --migrate-every."""
+        M = args.migrate_every or (g0 + count + 1)
+        g = g0
+        while g < g0 + count:
+            n = min(M - g % M, g0 + count - g)
+            (epoch_sync if args.sync_islands else epoch_async)(g, n)
+            g += n
+            if args.migrate_every and g % M == 0:
+                migrate(islands, args.migrants, gather)
+
+    run(0, args.warmup)
     sync()
+    events[0] = 0.0
     t0 = time.perf_counter()
-    for g in range(args.warmup, args.warmup + args.steps):
-        step(g)
+    run(args.warmup, args.steps)
     sync()
     elapsed = dist.all_reduce_max(time.perf_counter() - t0)
+    events_total = dist.all_reduce_sum(events[0])
 
     per_step = args.islands * args.candidates
     total = per_step * args.steps * ctx.world_size
     value = total / elapsed
-    best_score = dist.all_reduce_max(best_row[1])
+    # champion over all ranks (outside the timed region): [score, generation, table row, weights]
+    from funsearch_kubernetes_simulator_amd.models import families as fam
+    rec = np.concatenate([[best_row[1], best_row[3]], best_row[0], fam.pad_weights(best_row[2])[0]])
+    allrec = dist.all_gather_array(rec[None]).reshape(-1, rec.size) if ctx.distributed else rec[None]
+    champ = allrec[int(np.argmax(allrec[:, 0]))]
+    ncol = len(COLS)
+    row, wbest = champ[2:2 + ncol], champ[2 + ncol:]
     if ctx.is_main:
-        row = best_row[0]
         out = {
             "metric": "policy evals/sec on 8,152-pod Alibaba trace at 1/2/4/8 GPUs; champion util/frag",
             "value": round(value, 2),
@@ -116,7 +179,7 @@ def main() -> None:
             "vs_baseline": round(value / BASELINE_EVALS_PER_S, 2),
             "dtype": "fp64",
             "data": "OpenB openb_pod_list_default.csv (8,152 pods) on gpu_models_filtered.csv (16 nodes/64 GPUs); "
-                    "random-weight candidate policies (reference _create_random_policy family)",
+                    f"random-weight candidate policies ({args.family} family, random init)",
             "config": {
                 "model": f"{args.family} policy family, exact replay (reference-bit-identical scores)",
                 "global_batch": per_step * ctx.world_size,
@@ -126,13 +189,25 @@ def main() -> None:
                 "candidates_per_island": args.candidates,
                 "backend": ev.backend,
                 "heap_mode": args.heap_mode,
+                "islands_async": not args.sync_islands,
             },
-            "best_score": best_score,
+            "events_per_s": round(events_total / elapsed, 1),
+            "best_score": float(champ[0]),
+            "champion": {"cpu_util": row[COLS["avg_cpu"]], "mem_util": row[COLS["avg_mem"]],
+                         "gpu_count_util": row[COLS["avg_gpu_count"]],
+                         "gpu_milli_util": row[COLS["avg_gpu_milli"]], "frag": row[COLS["frag"]]},
+            "reference_champion": {"score": 0.49013357497851473, "cpu_util": 0.459, "mem_util": 0.261,
+                                   "gpu_count_util": 0.734, "frag": 0.033},
         }
-        if row is not None and ctx.world_size == 1:
-            out["champion"] = {"cpu_util": row[COLS["avg_cpu"]], "mem_util": row[COLS["avg_mem"]],
-                               "gpu_count_util": row[COLS["avg_gpu_count"]],
-                               "gpu_milli_util": row[COLS["avg_gpu_milli"]], "frag": row[COLS["frag"]]}
+        if args.save_best:
+            k = {"random_linear": 4, "feature_linear": fam.N_FEATURES}.get(args.family, fam.N_COMPOSITE)
+            code = fam.to_program(args.family, wbest[:k])
+            with open(args.save_best, "w") as f:
+                json.dump({"score": float(champ[0]), "generation": int(champ[1]), "code": code,
+                           "timestamp": time.strftime("%Y%m%d_%H%M%S"), "family": args.family,
+                           "weights": [float(x) for x in wbest[:k]],
+                           "results": {c: float(row[i]) for c, i in COLS.items()}}, f, indent=2)
+            out["saved"] = args.save_best
         print(json.dumps(out), flush=True)
     dist.shutdown()
 

@@ -420,7 +420,7 @@ struct VmScorer {
     ScoreOut o;
     if (n == 0 || c.pod != cached_pod || c.pod_ctime != cached_time) {
       const Workload& w = c.w;
-      VmCore vm(prog, budget_total > 0 ? budget_left : 0);
+      VmCore vm(prog, budget_total);   // the budget bounds one priority evaluation
       vm.resize(w.n_nodes);
       VmCore::World W;
       W.pod[PF_CPU] = w.pcpu[c.pod]; W.pod[PF_MEM] = w.pmem[c.pod];
@@ -432,7 +432,6 @@ struct VmScorer {
       W.gmilli_left = c.s.gmilli_left.data(); W.gmilli_total = w.gmilli_total.data();
       W.gmem_left = w.gmem_left0.data(); W.gmem_total = w.gmem_total.data();
       bool ok = vm.run(W);
-      if (budget_total > 0) budget_left = vm.budget;
       if (!ok) { o.exc = vm.exc; exc = vm.exc; return o; }
       res = vm.result; has = vm.has_result;
       cached_pod = c.pod; cached_time = c.pod_ctime;

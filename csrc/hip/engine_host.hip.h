@@ -2,21 +2,30 @@
 //
 // Uploads the SoA workload once (pods relabelled by id rank, initial heap
 // pre-heapified on the host, snapshot schedule precomputed), then evaluates
-// policy batches on its own HIP stream: one k_replay workgroup (one wave) per
-// policy followed by k_eval_reduce.  Two heap placements:
+// policy batches: one k_replay workgroup (one wave) per policy followed by
+// k_eval_reduce.  Two heap placements:
 //   * LDS heap  -- the whole event heap in LDS (2 policies per CU on the
 //                  8,152-pod trace; lowest latency per event);
 //   * HBM heap  -- each policy's heap in its own slice of an HBM buffer, only
-//                  the deletion bitmap (and VM registers) in LDS, so 12+
+//                  the deletion bitmap (and VM registers) in LDS, so 16
 //                  policy waves share a CU and hide each other's latency;
 //                  also the only placement for traces beyond ~19k pods.
 // `heap_mode` = "auto" picks HBM for batches large enough to fill the chip.
+//
+// Batches run in *slots*: each slot owns a HIP stream, its device buffers and
+// pinned host staging.  `evaluate_*` is a synchronous round trip on slot 0;
+// `submit_*` / `ready` / `wait` let independent islands keep several batches
+// in flight on separate streams, so one island's long-replay stragglers do
+// not idle the CUs the other islands could use.
 #pragma once
 
 #include <hip/hip_runtime.h>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 
+#include <algorithm>
+#include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -62,11 +71,54 @@ struct DevBuf {
   T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+// pinned host staging (async copies need page-locked memory)
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  void reserve(size_t bytes) {
+    if (bytes <= cap) return;
+    if (p) HIP_OK(hipHostFree(p));
+    HIP_OK(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    cap = bytes;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct Slot {
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  DevBuf res, tab, fam, w, code, meta, kpay, ktag, gheap, prof;
+  HostBuf h_in, h_tab;
+  int P = 0;
+  int fam_spec = -1;    // family shared by the whole staged batch, or -1
+  bool busy = false;
+  void release() {
+    for (DevBuf* b : {&res, &tab, &fam, &w, &code, &meta, &kpay, &ktag, &gheap, &prof}) b->release();
+    h_in.release();
+    h_tab.release();
+    if (done) (void)hipEventDestroy(done);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
 class DeviceEngine {
  public:
-  DeviceEngine(py::dict d, int device) : device_(device) {
+  DeviceEngine(py::dict d, int device, int n_slots = 4) : device_(device) {
     HIP_OK(hipSetDevice(device_));
-    HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    if (n_slots < 1 || n_slots > 64) throw std::invalid_argument("n_slots must be in [1, 64]");
+    slots_.resize(n_slots);
+    for (auto& s : slots_) {
+      s = std::make_unique<Slot>();
+      HIP_OK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+      HIP_OK(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
+    }
+    hipStream_t st = slots_[0]->stream;
     auto geti = [&](const char* k) { return d[k].cast<int64_t>(); };
     auto arr = [&](const char* k) { return d[k].cast<py::array>(); };
     std::memset(&W_, 0, sizeof(W_));
@@ -75,20 +127,20 @@ class DeviceEngine {
     W_.n_classes = (int32_t)geti("n_classes");
     npass_ = (int)geti("npass");
     if (!(npass_ == 1 || npass_ == 2 || npass_ == 4)) throw std::invalid_argument("npass must be 1, 2 or 4");
-    W_.cpu_total = dev_upload<int32_t>(arr("cpu_total"), stream_, owned_);
-    W_.cpu_left0 = dev_upload<int32_t>(arr("cpu_left"), stream_, owned_);
-    W_.mem_total = dev_upload<int32_t>(arr("mem_total"), stream_, owned_);
-    W_.mem_left0 = dev_upload<int32_t>(arr("mem_left"), stream_, owned_);
-    W_.gpu_left0 = dev_upload<int32_t>(arr("gpu_left"), stream_, owned_);
-    W_.ngpus = dev_upload<int32_t>(arr("ngpus"), stream_, owned_);
-    W_.gml_total = dev_upload<int32_t>(arr("gml_total"), stream_, owned_);
-    W_.gml_left0 = dev_upload<int32_t>(arr("gml_left"), stream_, owned_);
-    W_.gmem_total = dev_upload<int64_t>(arr("gmem_total"), stream_, owned_);
-    W_.pod = dev_upload<int4>(arr("pod"), stream_, owned_);
-    W_.pod_ctime = dev_upload<int32_t>(arr("pod_ctime"), stream_, owned_);
-    W_.heap0 = dev_upload<uint64_t>(arr("heap0"), stream_, owned_);
-    W_.class_value = dev_upload<int32_t>(arr("class_value"), stream_, owned_);
-    W_.snap_fire = dev_upload<int64_t>(arr("snap_fire"), stream_, owned_);
+    W_.cpu_total = dev_upload<int32_t>(arr("cpu_total"), st, owned_);
+    W_.cpu_left0 = dev_upload<int32_t>(arr("cpu_left"), st, owned_);
+    W_.mem_total = dev_upload<int32_t>(arr("mem_total"), st, owned_);
+    W_.mem_left0 = dev_upload<int32_t>(arr("mem_left"), st, owned_);
+    W_.gpu_left0 = dev_upload<int32_t>(arr("gpu_left"), st, owned_);
+    W_.ngpus = dev_upload<int32_t>(arr("ngpus"), st, owned_);
+    W_.gml_total = dev_upload<int32_t>(arr("gml_total"), st, owned_);
+    W_.gml_left0 = dev_upload<int32_t>(arr("gml_left"), st, owned_);
+    W_.gmem_total = dev_upload<int64_t>(arr("gmem_total"), st, owned_);
+    W_.pod = dev_upload<int4>(arr("pod"), st, owned_);
+    W_.pod_ctime = dev_upload<int32_t>(arr("pod_ctime"), st, owned_);
+    W_.heap0 = dev_upload<uint64_t>(arr("heap0"), st, owned_);
+    W_.class_value = dev_upload<int32_t>(arr("class_value"), st, owned_);
+    W_.snap_fire = dev_upload<int64_t>(arr("snap_fire"), st, owned_);
     W_.n_fire = (int32_t)arr("snap_fire").size();
     W_.thr_after_fire = d["thr_after_fire"].cast<double>();
     W_.tot_cpu = geti("tot_cpu"); W_.tot_mem = geti("tot_mem");
@@ -98,7 +150,7 @@ class DeviceEngine {
     W_.rank_bits = (int32_t)geti("rank_bits"); W_.node_bits = (int32_t)geti("node_bits");
     W_.low_bits = (int32_t)geti("low_bits"); W_.time_bits = (int32_t)geti("time_bits");
     W_.snapshot_interval = 0.05;
-    HIP_OK(hipStreamSynchronize(stream_));
+    HIP_OK(hipStreamSynchronize(st));
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, device_));
     num_cus_ = prop.multiProcessorCount;
@@ -111,9 +163,11 @@ class DeviceEngine {
 
   ~DeviceEngine() {
     (void)hipSetDevice(device_);
+    for (auto& s : slots_) {
+      if (s->stream) (void)hipStreamSynchronize(s->stream);
+      s->release();
+    }
     for (void* p : owned_) (void)hipFree(p);
-    for (DevBuf* b : {&res_, &tab_, &fam_, &w_, &code_, &meta_, &kpay_, &ktag_, &gheap_, &prof_}) b->release();
-    (void)hipStreamDestroy(stream_);
   }
 
   void set_options(py::dict o) {
@@ -121,6 +175,7 @@ class DeviceEngine {
     if (o.contains("gpu_alloc")) W_.first_fit_alloc = o["gpu_alloc"].cast<std::string>() == "first_fit";
     if (o.contains("snapshot_interval")) W_.snapshot_interval = o["snapshot_interval"].cast<double>();
     if (o.contains("budget")) budget_ = o["budget"].cast<int64_t>();
+    if (o.contains("heap_top")) heap_top_opt_ = o["heap_top"].cast<int>();   // -1: auto
     if (o.contains("heap_mode")) {
       const std::string m = o["heap_mode"].cast<std::string>();
       if (m != "auto" && m != "lds" && m != "hbm") throw std::invalid_argument("heap_mode: auto | lds | hbm");
@@ -129,83 +184,125 @@ class DeviceEngine {
     }
   }
 
+  // ---- synchronous round trips (slot 0) -------------------------------------------------
   py::array_t<double> evaluate_builtin(py::array_t<int32_t, py::array::c_style | py::array::forcecast> fam,
                                        py::array_t<double, py::array::c_style | py::array::forcecast> weights) {
-    const int P = (int)fam.size();
-    stage_builtin(fam, weights);
-    {
-      py::gil_scoped_release rel;
-      launch_builtin(P);
-    }
-    return collect(P);
+    submit_builtin(0, fam, weights);
+    return wait(0);
   }
 
   py::array_t<double> evaluate_programs(py::bytes blob, py::array_t<int32_t> offsets, py::array_t<int32_t> lengths,
                                         py::array_t<int64_t> kpay, py::array_t<int32_t> koff,
                                         py::array_t<uint8_t> ktag, int nregs) {
-    const int P = (int)offsets.size();
-    stage_programs(blob, offsets, lengths, kpay, koff, ktag, nregs);
-    {
-      py::gil_scoped_release rel;
-      launch_vm(P, nregs);
-    }
-    return collect(P);
+    submit_programs(0, blob, offsets, lengths, kpay, koff, ktag, nregs);
+    return wait(0);
   }
 
-  // Stage a builtin batch once, then time repeated launches (no H2D/D2H).
-  void stage_builtin(py::array_t<int32_t, py::array::c_style | py::array::forcecast> fam,
-                     py::array_t<double, py::array::c_style | py::array::forcecast> weights) {
+  // ---- asynchronous slots ----------------------------------------------------------------
+  void submit_builtin(int slot, py::array_t<int32_t, py::array::c_style | py::array::forcecast> fam,
+                      py::array_t<double, py::array::c_style | py::array::forcecast> weights) {
+    Slot& s = idle_slot(slot);
     const int P = (int)fam.size();
     if (weights.ndim() != 2 || weights.shape(0) != P || weights.shape(1) != kWeights)
       throw std::invalid_argument("weights must be [P, 16] float64");
+    if (P < 1) throw std::invalid_argument("empty batch");
     HIP_OK(hipSetDevice(device_));
-    ensure_batch(P);
-    fam_spec_ = P > 0 ? fam.at(0) : -1;
-    for (int i = 1; i < P && fam_spec_ >= 0; ++i)
-      if (fam.at(i) != fam_spec_) fam_spec_ = -1;
-    HIP_OK(hipMemcpyAsync(fam_.p, fam.data(), (size_t)P * 4, hipMemcpyHostToDevice, stream_));
-    HIP_OK(hipMemcpyAsync(w_.p, weights.data(), (size_t)P * kWeights * 8, hipMemcpyHostToDevice, stream_));
-    HIP_OK(hipStreamSynchronize(stream_));
+    stage_builtin(s, fam.data(), weights.data(), P);
+    {
+      py::gil_scoped_release rel;
+      launch_builtin(s);
+      finish(s);
+    }
   }
-  void launch_builtin_async(int P) { launch_builtin(P); }
-  void synchronize() { HIP_OK(hipStreamSynchronize(stream_)); }
-  py::array_t<double> collect_table(int P) { return collect(P); }
+
+  void submit_programs(int slot, py::bytes blob, py::array_t<int32_t> offsets, py::array_t<int32_t> lengths,
+                       py::array_t<int64_t> kpay, py::array_t<int32_t> koff, py::array_t<uint8_t> ktag, int nregs) {
+    Slot& s = idle_slot(slot);
+    const int P = (int)offsets.size();
+    if (P < 1) throw std::invalid_argument("empty batch");
+    HIP_OK(hipSetDevice(device_));
+    stage_programs(s, blob, offsets, lengths, kpay, koff, ktag, nregs);
+    {
+      py::gil_scoped_release rel;
+      launch_vm(s, nregs);
+      finish(s);
+    }
+  }
+
+  bool ready(int slot) {
+    Slot& s = slot_at(slot);
+    if (!s.busy) return true;
+    const hipError_t e = hipEventQuery(s.done);
+    if (e == hipErrorNotReady) return false;
+    HIP_OK(e);
+    return true;
+  }
+
+  py::array_t<double> wait(int slot) {
+    Slot& s = slot_at(slot);
+    if (!s.busy) throw std::invalid_argument("slot has no batch in flight");
+    {
+      py::gil_scoped_release rel;
+      HIP_OK(hipEventSynchronize(s.done));
+    }
+    s.busy = false;
+    py::array_t<double> out({(py::ssize_t)s.P, (py::ssize_t)13});
+    std::memcpy(out.mutable_data(), s.h_tab.p, sizeof(double) * 13 * (size_t)s.P);
+    return out;
+  }
+
+  // Stage a builtin batch once, then time repeated launches (no H2D/D2H): tools/.
+  void stage_builtin_only(py::array_t<int32_t, py::array::c_style | py::array::forcecast> fam,
+                          py::array_t<double, py::array::c_style | py::array::forcecast> weights) {
+    Slot& s = idle_slot(0);
+    HIP_OK(hipSetDevice(device_));
+    stage_builtin(s, fam.data(), weights.data(), (int)fam.size());
+    HIP_OK(hipStreamSynchronize(s.stream));
+  }
+  void launch_builtin_async() {
+    py::gil_scoped_release rel;
+    launch_builtin(*slots_[0]);
+  }
+  void synchronize() {
+    for (auto& s : slots_) HIP_OK(hipStreamSynchronize(s->stream));
+  }
 
   py::tuple profile(py::object fam_or_none, py::object weights_or_none, py::object programs_or_none) {
     if (npass_ != 1) throw std::invalid_argument("profiling supports <= 64 nodes");
     HIP_OK(hipSetDevice(device_));
-    int P;
+    Slot& s = idle_slot(0);
     bool is_vm = !programs_or_none.is_none();
     int nregs = 0;
     if (is_vm) {
       py::tuple t = programs_or_none.cast<py::tuple>();
-      auto offsets = t[1].cast<py::array_t<int32_t>>();
-      P = (int)offsets.size();
       nregs = t[6].cast<int>();
-      stage_programs(t[0].cast<py::bytes>(), offsets, t[2].cast<py::array_t<int32_t>>(),
+      stage_programs(s, t[0].cast<py::bytes>(), t[1].cast<py::array_t<int32_t>>(), t[2].cast<py::array_t<int32_t>>(),
                      t[3].cast<py::array_t<int64_t>>(), t[4].cast<py::array_t<int32_t>>(),
                      t[5].cast<py::array_t<uint8_t>>(), nregs);
     } else {
       auto fam = fam_or_none.cast<py::array_t<int32_t, py::array::c_style | py::array::forcecast>>();
-      P = (int)fam.size();
-      stage_builtin(fam, weights_or_none.cast<py::array_t<double, py::array::c_style | py::array::forcecast>>());
+      auto w = weights_or_none.cast<py::array_t<double, py::array::c_style | py::array::forcecast>>();
+      stage_builtin(s, fam.data(), w.data(), (int)fam.size());
     }
-    prof_.reserve((size_t)P * 64);
+    const int P = s.P;
+    s.prof.reserve((size_t)P * 64);
     const bool g = use_gheap(P);
-    const size_t lds = lds_bytes(g, is_vm ? nregs : 0);
-    uint64_t* gh = g ? gheap_for(P) : nullptr;
+    const DevWorkload Wl = launch_workload(g, is_vm ? nregs : 0);
+    const size_t lds = lds_bytes(g, Wl.heap_top, is_vm ? nregs : 0);
+    uint64_t* gh = g ? gheap_for(s, P) : nullptr;
     if (is_vm) {
-      const fksk::VmArgs a{W_, table(), res_.as<DevResult>(), budget_, gh, prof_.as<uint64_t>()};
-      HIP_OK(fksk::launch_vm_prof(g, P, lds, stream_, a));
+      const fksk::VmArgs a{Wl, table(s), s.res.as<DevResult>(), budget_, gh, s.prof.as<uint64_t>()};
+      HIP_OK(fksk::launch_vm_prof(g, P, lds, s.stream, a));
     } else {
-      const fksk::BuiltinArgs a{W_, fam_.as<int32_t>(), w_.as<double>(), res_.as<DevResult>(), gh,
-                                prof_.as<uint64_t>()};
-      HIP_OK(fksk::launch_builtin_prof(g, P, lds, stream_, a));
+      const fksk::BuiltinArgs a{Wl, s.fam.as<int32_t>(), s.w.as<double>(), s.res.as<DevResult>(), gh,
+                                s.prof.as<uint64_t>()};
+      HIP_OK(fksk::launch_builtin_prof(g, P, lds, s.stream, a));
     }
-    reduce(P);
+    finish(s);
     py::array_t<uint64_t> prof({(py::ssize_t)P, (py::ssize_t)8});
-    HIP_OK(hipMemcpyAsync(prof.mutable_data(), prof_.p, (size_t)P * 64, hipMemcpyDeviceToHost, stream_));
-    py::array_t<double> tab = collect(P);
+    HIP_OK(hipMemcpyAsync(prof.mutable_data(), s.prof.p, (size_t)P * 64, hipMemcpyDeviceToHost, s.stream));
+    py::array_t<double> tab = wait(0);
+    HIP_OK(hipStreamSynchronize(s.stream));
     return py::make_tuple(tab, prof);
   }
 
@@ -216,13 +313,27 @@ class DeviceEngine {
     d["lds_heap_ok"] = lds_heap_ok_;
     d["npass"] = npass_;
     d["heap_mode"] = heap_mode_;
+    d["n_slots"] = (int)slots_.size();
+    d["heap_top_hbm"] = heap_top_for(0);
     return d;
   }
 
   bool would_use_hbm(int P) const { return use_gheap(P); }
+  int n_slots() const { return (int)slots_.size(); }
 
  private:
   static constexpr size_t kMaxLds = 160 * 1024;
+  static constexpr size_t kPoliciesPerCu = 16;   // HBM-heap kernels: 4 waves per SIMD
+
+  Slot& slot_at(int i) {
+    if (i < 0 || i >= (int)slots_.size()) throw std::out_of_range("slot index");
+    return *slots_[i];
+  }
+  Slot& idle_slot(int i) {
+    Slot& s = slot_at(i);
+    if (s.busy) throw std::runtime_error("slot busy: wait() for its batch first");
+    return s;
+  }
 
   void set_attrs() {
     const int mx = (int)kMaxLds;
@@ -241,105 +352,145 @@ class DeviceEngine {
     return P > 2 * num_cus_;
   }
 
-  size_t lds_bytes(bool g, int nregs) const {
+  size_t lds_bytes(bool g, int top, int nregs) const {
     const size_t vregs = (size_t)nregs * 64 * 8;
-    return g ? delmap_bytes_ + vregs : heap_bytes_ + delmap_bytes_ + vregs;
+    return g ? delmap_bytes_ + (size_t)top * 8 + vregs : heap_bytes_ + delmap_bytes_ + vregs;
   }
 
-  uint64_t* gheap_for(int P) {
-    gheap_.reserve(heap_bytes_ * (size_t)P);
-    return gheap_.as<uint64_t>();
+  // HBM-heap launches keep the top 2^L - 1 heap slots in LDS, as many levels as
+  // fit a 16-policies-per-CU share of the 160 KiB (or the `heap_top` option).
+  int heap_top_for(int nregs) const {
+    const int entries = (int)(heap_bytes_ / 8);
+    if (heap_top_opt_ >= 0) return std::min(heap_top_opt_, entries);
+    const size_t budget = kMaxLds / kPoliciesPerCu;
+    const size_t fixed = delmap_bytes_ + (size_t)nregs * 64 * 8;
+    int T = 0;
+    while (T < entries && fixed + (size_t)(2 * T + 1) * 8 <= budget) T = 2 * T + 1;
+    return std::min(T, entries);
   }
 
-  DevProgramTable table() const {
-    return DevProgramTable{code_.as<const uint64_t>(), meta_.as<const int32_t>(), kpay_.as<const int64_t>(),
-                           ktag_.as<const uint8_t>()};
+  DevWorkload launch_workload(bool g, int nregs) const {
+    DevWorkload Wl = W_;
+    Wl.heap_top = g ? heap_top_for(nregs) : 0;
+    return Wl;
   }
 
-  void ensure_batch(int P) {
-    res_.reserve(sizeof(DevResult) * (size_t)P);
-    tab_.reserve(sizeof(double) * 13 * (size_t)P);
-    fam_.reserve(sizeof(int32_t) * (size_t)P);
-    w_.reserve(sizeof(double) * kWeights * (size_t)P);
+  uint64_t* gheap_for(Slot& s, int P) {
+    s.gheap.reserve(heap_bytes_ * (size_t)P);
+    return s.gheap.as<uint64_t>();
   }
 
-  void stage_programs(py::bytes blob, py::array_t<int32_t> offsets, py::array_t<int32_t> lengths,
+  DevProgramTable table(const Slot& s) const {
+    return DevProgramTable{s.code.as<const uint64_t>(), s.meta.as<const int32_t>(), s.kpay.as<const int64_t>(),
+                           s.ktag.as<const uint8_t>()};
+  }
+
+  void ensure_batch(Slot& s, int P) {
+    s.res.reserve(sizeof(DevResult) * (size_t)P);
+    s.tab.reserve(sizeof(double) * 13 * (size_t)P);
+    s.fam.reserve(sizeof(int32_t) * (size_t)P);
+    s.w.reserve(sizeof(double) * kWeights * (size_t)P);
+    s.h_tab.reserve(sizeof(double) * 13 * (size_t)P);
+    s.P = P;
+  }
+
+  // numpy -> pinned staging -> device (async on the slot's stream)
+  void stage_builtin(Slot& s, const int32_t* fam, const double* weights, int P) {
+    HIP_OK(hipStreamSynchronize(s.stream));   // the previous batch no longer reads the staging
+    ensure_batch(s, P);
+    s.fam_spec = P > 0 ? fam[0] : -1;
+    for (int i = 1; i < P && s.fam_spec >= 0; ++i)
+      if (fam[i] != s.fam_spec) s.fam_spec = -1;
+    const size_t fb = (size_t)P * 4, wb = (size_t)P * kWeights * 8;
+    s.h_in.reserve(fb + wb + 16);
+    char* h = s.h_in.as<char>();
+    std::memcpy(h, weights, wb);
+    std::memcpy(h + wb, fam, fb);
+    HIP_OK(hipMemcpyAsync(s.w.p, h, wb, hipMemcpyHostToDevice, s.stream));
+    HIP_OK(hipMemcpyAsync(s.fam.p, h + wb, fb, hipMemcpyHostToDevice, s.stream));
+  }
+
+  void stage_programs(Slot& s, py::bytes blob, py::array_t<int32_t> offsets, py::array_t<int32_t> lengths,
                       py::array_t<int64_t> kpay, py::array_t<int32_t> koff, py::array_t<uint8_t> ktag, int nregs) {
     const int P = (int)offsets.size();
     if (nregs < 1 || nregs > 64) throw std::invalid_argument("nregs must be in [1, 64]");
-    HIP_OK(hipSetDevice(device_));
-    ensure_batch(P);
-    std::string code = blob;
-    code_.reserve(code.size() + 16);
-    meta_.reserve((size_t)P * 12 + 16);
-    kpay_.reserve((size_t)kpay.size() * 8 + 16);
-    ktag_.reserve((size_t)ktag.size() + 16);
+    HIP_OK(hipStreamSynchronize(s.stream));
+    ensure_batch(s, P);
+    s.fam_spec = -1;
+    const std::string code = blob;
     std::vector<int32_t> meta((size_t)P * 3);
     for (int i = 0; i < P; ++i) {
       meta[3 * i] = offsets.at(i);
       meta[3 * i + 1] = lengths.at(i);
       meta[3 * i + 2] = koff.at(i);
     }
-    HIP_OK(hipMemcpyAsync(code_.p, code.data(), code.size(), hipMemcpyHostToDevice, stream_));
-    HIP_OK(hipMemcpyAsync(meta_.p, meta.data(), meta.size() * 4, hipMemcpyHostToDevice, stream_));
-    HIP_OK(hipMemcpyAsync(kpay_.p, kpay.data(), (size_t)kpay.size() * 8, hipMemcpyHostToDevice, stream_));
-    HIP_OK(hipMemcpyAsync(ktag_.p, ktag.data(), (size_t)ktag.size(), hipMemcpyHostToDevice, stream_));
-    HIP_OK(hipStreamSynchronize(stream_));
+    const size_t cb = code.size(), mb = meta.size() * 4, kb = (size_t)kpay.size() * 8, tb = (size_t)ktag.size();
+    s.code.reserve(cb + 16);
+    s.meta.reserve(mb + 16);
+    s.kpay.reserve(kb + 16);
+    s.ktag.reserve(tb + 16);
+    s.h_in.reserve(cb + mb + kb + tb + 64);
+    char* h = s.h_in.as<char>();
+    size_t o = 0;
+    auto put = [&](DevBuf& d, const void* src, size_t n) {
+      std::memcpy(h + o, src, n);
+      HIP_OK(hipMemcpyAsync(d.p, h + o, n, hipMemcpyHostToDevice, s.stream));
+      o += (n + 15) & ~size_t(15);
+    };
+    put(s.code, code.data(), cb);
+    put(s.meta, meta.data(), mb);
+    put(s.kpay, kpay.data(), kb);
+    put(s.ktag, ktag.data(), tb);
   }
 
-  void launch_builtin(int P) {
+  void launch_builtin(Slot& s) {
+    const int P = s.P;
     const bool g = use_gheap(P);
-    const size_t lds = lds_bytes(g, 0);
-    uint64_t* gh = g ? gheap_for(P) : nullptr;
-    const fksk::BuiltinArgs a{W_, fam_.as<int32_t>(), w_.as<double>(), res_.as<DevResult>(), gh, nullptr};
-    if (npass_ == 1) HIP_OK(fksk::launch_builtin_np1(g, fam_spec_, P, lds, stream_, a));
-    else if (npass_ == 2) HIP_OK(fksk::launch_builtin_np2(g, fam_spec_, P, lds, stream_, a));
-    else HIP_OK(fksk::launch_builtin_np4(g, fam_spec_, P, lds, stream_, a));
-    reduce(P);
+    const DevWorkload Wl = launch_workload(g, 0);
+    const size_t lds = lds_bytes(g, Wl.heap_top, 0);
+    uint64_t* gh = g ? gheap_for(s, P) : nullptr;
+    const fksk::BuiltinArgs a{Wl, s.fam.as<int32_t>(), s.w.as<double>(), s.res.as<DevResult>(), gh, nullptr};
+    if (npass_ == 1) HIP_OK(fksk::launch_builtin_np1(g, s.fam_spec, P, lds, s.stream, a));
+    else if (npass_ == 2) HIP_OK(fksk::launch_builtin_np2(g, s.fam_spec, P, lds, s.stream, a));
+    else HIP_OK(fksk::launch_builtin_np4(g, s.fam_spec, P, lds, s.stream, a));
   }
 
-  void launch_vm(int P, int nregs) {
+  void launch_vm(Slot& s, int nregs) {
+    const int P = s.P;
     const bool g = use_gheap(P);
-    const size_t lds = lds_bytes(g, nregs);
+    const DevWorkload Wl = launch_workload(g, nregs);
+    const size_t lds = lds_bytes(g, Wl.heap_top, nregs);
     if (lds > kMaxLds) throw std::invalid_argument("heap + VM registers exceed the 160 KiB LDS");
-    uint64_t* gh = g ? gheap_for(P) : nullptr;
-    const fksk::VmArgs a{W_, table(), res_.as<DevResult>(), budget_, gh, nullptr};
-    if (npass_ == 1) HIP_OK(fksk::launch_vm_np1(g, P, lds, stream_, a));
-    else if (npass_ == 2) HIP_OK(fksk::launch_vm_np2(g, P, lds, stream_, a));
-    else HIP_OK(fksk::launch_vm_np4(g, P, lds, stream_, a));
-    reduce(P);
+    uint64_t* gh = g ? gheap_for(s, P) : nullptr;
+    const fksk::VmArgs a{Wl, table(s), s.res.as<DevResult>(), budget_, gh, nullptr};
+    if (npass_ == 1) HIP_OK(fksk::launch_vm_np1(g, P, lds, s.stream, a));
+    else if (npass_ == 2) HIP_OK(fksk::launch_vm_np2(g, P, lds, s.stream, a));
+    else HIP_OK(fksk::launch_vm_np4(g, P, lds, s.stream, a));
   }
 
-  void reduce(int P) {
-    hipLaunchKernelGGL(k_eval_reduce, dim3((P + 63) / 64), dim3(64), 0, stream_, res_.as<DevResult>(),
-                       tab_.as<double>(), P);
+  // k_eval_reduce, result table -> pinned host, completion event
+  void finish(Slot& s) {
+    const int P = s.P;
+    hipLaunchKernelGGL(k_eval_reduce, dim3((P + 63) / 64), dim3(64), 0, s.stream, s.res.as<DevResult>(),
+                       s.tab.as<double>(), P);
     HIP_OK(hipGetLastError());
-  }
-
-  py::array_t<double> collect(int P) {
-    py::array_t<double> out({(py::ssize_t)P, (py::ssize_t)13});
-    {
-      py::gil_scoped_release rel;
-      HIP_OK(hipMemcpyAsync(out.mutable_data(), tab_.p, sizeof(double) * 13 * (size_t)P, hipMemcpyDeviceToHost,
-                            stream_));
-      HIP_OK(hipStreamSynchronize(stream_));
-    }
-    return out;
+    HIP_OK(hipMemcpyAsync(s.h_tab.p, s.tab.p, sizeof(double) * 13 * (size_t)P, hipMemcpyDeviceToHost, s.stream));
+    HIP_OK(hipEventRecord(s.done, s.stream));
+    s.busy = true;
   }
 
   int device_ = 0;
-  hipStream_t stream_ = nullptr;
+  std::vector<std::unique_ptr<Slot>> slots_;
   DevWorkload W_;
   int npass_ = 1;
-  int fam_spec_ = -1;   // family shared by the whole staged batch, or -1
   size_t heap_bytes_ = 0, delmap_bytes_ = 0;
   bool lds_heap_ok_ = true;
   int num_cus_ = 0;
   std::string arch_;
   std::string heap_mode_ = "auto";
   int64_t budget_ = 0;
+  int heap_top_opt_ = -1;
   std::vector<void*> owned_;
-  DevBuf res_, tab_, fam_, w_, code_, meta_, kpay_, ktag_, gheap_, prof_;
 };
 
 }  // namespace fks_host

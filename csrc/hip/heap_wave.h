@@ -16,6 +16,11 @@
 // (the repush rule observes the layout), verified against the serial code
 // and the CPU oracle.  A parallel bitmap marks the slots holding DELETION
 // events so "first deletion in array order" is a ballot over 64-word chunks.
+//
+// Placement: slots [0, T) live in LDS (`top`), slots [T, n) in the policy's
+// HBM slice (`h`).  With the whole heap in LDS T covers everything; with an
+// HBM heap the top levels (the hottest: every pop walks root -> leaf) stay in
+// LDS so only the last round of a pop and the tail of a push touch HBM.
 #pragma once
 
 #include "device_common.h"
@@ -27,9 +32,17 @@ constexpr int kDelKind = 2;
 __device__ __forceinline__ bool key_lt(uint64_t a, uint64_t b, int lb) { return (a >> lb) < (b >> lb); }
 
 struct WaveHeap {
-  uint64_t* h;        // keys
-  uint32_t* delmap;   // bit p set <=> h[p] is a deletion
+  uint64_t* h;        // keys (slots >= T)
+  uint64_t* top;      // LDS copy of slots [0, T)
+  int T;
+  uint32_t* delmap;   // bit p set <=> slot p holds a deletion
   int lb;             // low (payload) bits below the (time, rank) compare key
+
+  __device__ __forceinline__ uint64_t ld(int i) const { return i < T ? top[i] : h[i]; }
+  __device__ __forceinline__ void st(int i, uint64_t v) const {
+    if (i < T) top[i] = v;
+    else h[i] = v;
+  }
 
   __device__ __forceinline__ void mark(int pos, uint64_t v) const {
     const uint32_t bit = 1u << (pos & 31);
@@ -64,7 +77,7 @@ struct WaveHeap {
       rounds = rd + 1;
       const int idx = ((pos + 1) << r) - 1 + i;
       const bool valid = lane < 62 && idx < n;
-      const uint64_t v = valid ? h[idx] : ~0ull;
+      const uint64_t v = valid ? ld(idx) : ~0ull;
       const uint64_t sib = swap_pairs64(v);
       const bool go_right = ((lane & 1) == 0) && valid && (idx + 1 < n) && !key_lt(v, sib, lb);
       const uint64_t right_mask = ballot(go_right);
@@ -110,11 +123,11 @@ struct WaveHeap {
       const bool above = jr < 0 || rd < jr || (rd == jr && lane < jl);
       if (on[rd] && above) {
         const int parent = (posv[rd] - 1) >> 1;
-        h[parent] = val[rd];
+        st(parent, val[rd]);
         mark(parent, val[rd]);
       }
     }
-    if (lane == 0) { h[target] = last; mark(target, last); }
+    if (lane == 0) { st(target, last); mark(target, last); }
   }
 
   // CPython heappush on a heap of n items (item lands at index <= n).
@@ -124,14 +137,14 @@ struct WaveHeap {
     const int l = lane + 1;
     const int anc = lane < 30 ? ((n + 1) >> l) - 1 : -1;
     const bool valid = anc >= 0 && n > 0;
-    const uint64_t v = valid ? h[anc] : 0;
+    const uint64_t v = valid ? ld(anc) : 0;
     const bool gt = valid && key_lt(item, v, lb);
     const int J = __popcll(ballot(gt));        // sorted path: a prefix from the bottom
     // moves: v_l -> a_{l-1} (a_0 = n) for l <= J ; item -> a_J
     const int dst = lane < 30 ? ((n + 1) >> (l - 1)) - 1 : 0;
-    if (gt) { h[dst] = v; mark(dst, v); }
+    if (gt) { st(dst, v); mark(dst, v); }
     const int aJ = J == 0 ? n : ((n + 1) >> J) - 1;
-    if (lane == 0) { h[aJ] = item; mark(aJ, item); }
+    if (lane == 0) { st(aJ, item); mark(aJ, item); }
   }
 
   // index of the first DELETION in h[0, n), or -1

@@ -189,15 +189,19 @@ PYBIND11_MODULE(_fks_hip, m) {
   m.def("test_wave_ops", &test_wave_ops);
   m.def("test_heap", &test_heap);
   py::class_<DeviceEngine>(m, "DeviceEngine")
-      .def(py::init<py::dict, int>(), py::arg("workload"), py::arg("device") = 0)
+      .def(py::init<py::dict, int, int>(), py::arg("workload"), py::arg("device") = 0, py::arg("n_slots") = 4)
       .def("set_options", &DeviceEngine::set_options)
       .def("evaluate_builtin", &DeviceEngine::evaluate_builtin)
       .def("evaluate_programs", &DeviceEngine::evaluate_programs)
+      .def("submit_builtin", &DeviceEngine::submit_builtin)
+      .def("submit_programs", &DeviceEngine::submit_programs)
+      .def("ready", &DeviceEngine::ready)
+      .def("wait", &DeviceEngine::wait)
+      .def("n_slots", &DeviceEngine::n_slots)
       .def("profile", &DeviceEngine::profile)
-      .def("stage_builtin", &DeviceEngine::stage_builtin)
-      .def("collect_table", &DeviceEngine::collect_table)
-      .def("would_use_hbm", &DeviceEngine::would_use_hbm)
+      .def("stage_builtin_only", &DeviceEngine::stage_builtin_only)
       .def("launch_builtin_async", &DeviceEngine::launch_builtin_async)
+      .def("would_use_hbm", &DeviceEngine::would_use_hbm)
       .def("synchronize", &DeviceEngine::synchronize)
       .def("info", &DeviceEngine::info);
   m.attr("WEIGHTS_PER_POLICY") = kWeights;

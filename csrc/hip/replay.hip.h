@@ -59,7 +59,8 @@ struct DevWorkload {
   int32_t rank_bits, node_bits, low_bits, time_bits;
   double snapshot_interval;
   double thr_after_fire;      // threshold value after the last precomputed snapshot
-  int32_t repush_earliest, first_fit_alloc, truncate, pad1;
+  int32_t repush_earliest, first_fit_alloc, truncate;
+  int32_t heap_top;           // heap slots kept in LDS when the heap lives in HBM
 };
 
 struct DevResult {
@@ -160,10 +161,11 @@ __device__ __forceinline__ int pick_gpus(const NodeRegs<NPASS>& nr, int ps, int 
 
 // ----------------------------------------------------------------------------
 template <int NPASS, class Scorer, class Prof = NoProf>
-__device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* hbuf, uint32_t* delmap, DevResult* out,
-                           uint64_t* prof_out = nullptr) {
+__device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* hbuf, uint64_t* htop, int T,
+                           uint32_t* delmap, DevResult* out, uint64_t* prof_out = nullptr) {
   // hbuf: the policy's heap array -- LDS (fast, 2 policies/CU on the 8k trace)
-  // or its private slice of an HBM buffer (any trace length, 12+ policies/CU)
+  // or its private slice of an HBM buffer (any trace length, 16 policies/CU);
+  // slots [0, T) are held in LDS at htop instead (T >= N: all of it)
   Prof prof;
   const int lane = lane_id();
   const int lb = W.low_bits, nb = W.node_bits;
@@ -174,9 +176,11 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* hbuf,
 
   WaveHeap heap;
   heap.h = hbuf;
+  heap.top = htop;
+  heap.T = T;
   heap.delmap = delmap;
   heap.lb = lb;
-  for (int i = lane; i < N; i += kWave) hbuf[i] = W.heap0[i];
+  for (int i = lane; i < N; i += kWave) heap.st(i, W.heap0[i]);
   for (int i = lane; i < lds_delmap_words(N); i += kWave) heap.delmap[i] = 0u;
 
   NodeRegs<NPASS> nr;
@@ -217,10 +221,10 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* hbuf,
 
   while (n > 0) {
     // ---------------- pop (pod record load issued first, consumed after the sift)
-    const uint64_t top = uniu64(hbuf[0]);
+    const uint64_t top = uniu64(heap.ld(0));
     const int rank = (int)((top >> lb) & ((1ull << rb) - 1));
     const int4 precv = load_vgpr(&W.pod[rank]);
-    const uint64_t last = uniu64(hbuf[n - 1]);
+    const uint64_t last = uniu64(heap.ld(n - 1));
     --n;
     if (n > 0) heap.pop_reinsert(n, last);
 
@@ -305,13 +309,13 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* hbuf,
         int64_t anchor = -1;
         if (!W.repush_earliest) {
           const int f = heap.first_deletion(n);
-          if (f >= 0) anchor = (int64_t)(uniu64(hbuf[f]) >> tshift);
+          if (f >= 0) anchor = (int64_t)(uniu64(heap.ld(f)) >> tshift);
         } else {
           uint64_t mn = ~0ull;
           for (int base = 0; base < n; base += kWave) {
             const int i = base + lane;
             uint64_t tv = ~0ull;
-            if (i < n) { const uint64_t k = hbuf[i]; if ((k & 3) == kDelete) tv = k >> tshift; }
+            if (i < n) { const uint64_t k = heap.ld(i); if ((k & 3) == kDelete) tv = k >> tshift; }
             tv = ~wave_max_u64(~tv);
             mn = tv < mn ? tv : mn;
           }

@@ -24,10 +24,13 @@ using namespace fksd;
 namespace {
 
 // Where a policy's heap, deletion bitmap and VM registers live.
-//   GHEAP = false: heap | bitmap | vregs all in LDS (2 policies/CU on the 8k trace)
-//   GHEAP = true : heap in its HBM slice, bitmap | vregs in LDS (12-16 policies/CU)
+//   GHEAP = false: LDS = heap | bitmap | vregs (2 policies/CU on the 8k trace)
+//   GHEAP = true : heap in its HBM slice, LDS = bitmap | heap top (W.heap_top
+//                  slots) | vregs (16 policies/CU)
 struct Slot {
   uint64_t* h;
+  uint64_t* top;
+  int T;
   uint32_t* delmap;
   uint64_t* vregs;
 };
@@ -39,9 +42,13 @@ __device__ __forceinline__ Slot policy_slot(const DevWorkload& W, uint64_t* ghea
   if (GHEAP) {
     s.h = gheap + (size_t)p * lds_heap_entries(N);
     s.delmap = reinterpret_cast<uint32_t*>(lds);
-    s.vregs = lds + lds_delmap_words(N) / 2;
+    s.top = lds + lds_delmap_words(N) / 2;
+    s.T = W.heap_top;
+    s.vregs = s.top + W.heap_top;
   } else {
     s.h = lds;
+    s.top = lds;
+    s.T = lds_heap_entries(N);
     s.delmap = reinterpret_cast<uint32_t*>(lds + lds_heap_entries(N));
     s.vregs = lds + lds_vreg_offset(N);
   }
@@ -64,7 +71,7 @@ __global__ FKS_BOUNDS(GHEAP) void k_replay_builtin(fksk::BuiltinArgs a) {
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   BuiltinScorerDev<FAM> sc;
   sc.load(a.fam[p], a.weights + (size_t)p * kWeights);
-  replay_one<NPASS>(a.W, sc, s.h, s.delmap, a.out + p);
+  replay_one<NPASS>(a.W, sc, s.h, s.top, s.T, s.delmap, a.out + p);
 }
 
 template <int NPASS, bool GHEAP>
@@ -104,7 +111,7 @@ __global__ FKS_BOUNDS(GHEAP) void k_replay_vm(fksk::VmArgs a) {
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   VmScorerDev sc;
   sc.init(a.T, p, a.W, a.budget, s.vregs);
-  replay_one<NPASS>(a.W, sc, s.h, s.delmap, a.out + p);
+  replay_one<NPASS>(a.W, sc, s.h, s.top, s.T, s.delmap, a.out + p);
 }
 #endif
 
@@ -115,7 +122,8 @@ __global__ FKS_BOUNDS(GHEAP) void k_replay_builtin_prof(fksk::BuiltinArgs a) {
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   BuiltinScorerDev<-1> sc;
   sc.load(a.fam[p], a.weights + (size_t)p * kWeights);
-  replay_one<1, BuiltinScorerDev<-1>, PhaseProf>(a.W, sc, s.h, s.delmap, a.out + p, a.prof + (size_t)p * 8);
+  replay_one<1, BuiltinScorerDev<-1>, PhaseProf>(a.W, sc, s.h, s.top, s.T, s.delmap, a.out + p,
+                                                 a.prof + (size_t)p * 8);
 }
 
 template <bool GHEAP>
@@ -124,7 +132,7 @@ __global__ FKS_BOUNDS(GHEAP) void k_replay_vm_prof(fksk::VmArgs a) {
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   VmScorerDev sc;
   sc.init(a.T, p, a.W, a.budget, s.vregs);
-  replay_one<1, VmScorerDev, PhaseProf>(a.W, sc, s.h, s.delmap, a.out + p, a.prof + (size_t)p * 8);
+  replay_one<1, VmScorerDev, PhaseProf>(a.W, sc, s.h, s.top, s.T, s.delmap, a.out + p, a.prof + (size_t)p * 8);
 }
 #endif
 

@@ -318,7 +318,7 @@ struct VmScorerDev {
   const uint8_t* ktag;
   const int64_t* gmem_total;
   int32_t n_nodes;
-  int64_t budget;      // remaining instruction budget (<= 0: unlimited)
+  int64_t budget_call;  // instruction budget of one priority evaluation (<= 0: unlimited)
   bool limited;
   uint64_t* vregs;     // LDS: [reg][64]
 
@@ -329,7 +329,7 @@ struct VmScorerDev {
     ktag = T.ktag + koff;
     gmem_total = W.gmem_total;
     n_nodes = W.n_nodes;
-    budget = bud;
+    budget_call = bud;
     limited = bud > 0;
     vregs = vreg_base;
   }
@@ -360,6 +360,7 @@ struct VmScorerDev {
     const int ngp = nr.ngpus[ps];
 
     int pc = 0;
+    int64_t budget = budget_call;   // runaway programs end here, so every wave drains
     for (;;) {
       if (limited && --budget < 0) { exc = EXC_BUDGET; return 0; }
       const uint64_t in = code[pc];

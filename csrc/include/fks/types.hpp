@@ -49,7 +49,7 @@ struct SimOptions {
   int32_t gpu_alloc = ALLOC_BEST_FIT;
   double snapshot_interval = 0.05;
   bool truncate = true;          // FunSearchScheduler: int(max(0, score))
-  int64_t budget = 0;            // VM instruction budget per replay (0 = unlimited)
+  int64_t budget = 0;            // VM instruction budget per priority evaluation (0 = unlimited)
   bool record_values = false;    // keep snapshot / frag values (exact fallback, tests)
   bool record_placements = false;
 };

@@ -7,10 +7,12 @@ Routing per program (every path yields the reference's score bit-for-bit):
 2. MI355X (`ops.hip_engine`): one k_replay wave per program, all programs of
    a call in one launch;
 3. native CPU VM (`ops.cpu_engine`): for no-GPU hosts, for programs the device
-   reports as EXC_UNSUPPORTED (bigint / complex / trig / near-tie math), and
-   for results whose exact-mean accumulator flagged `inexact`;
+   reports as EXC_UNSUPPORTED (bigint / complex / trig / near-tie math) or
+   EXC_BUDGET (per-call instruction budget), and for results whose exact-mean
+   accumulator flagged `inexact`;
 4. object engine (`simulator.KubernetesSimulator` + ``exec``), which *is* the
-   reference semantics, for whatever the native engines cannot express.
+   reference semantics, for whatever the native engines cannot express; it
+   runs under a wall-clock budget (``object_timeout_s``, default 600 s).
 
 Scores follow `evaluate_policy_standalone` (`funsearch/funsearch_integration.py:30-64`):
 any exception during the replay gives score 0.  `EvalResult.exc` tells which
@@ -70,10 +72,28 @@ def _row_to_result(row: np.ndarray, engine: str) -> EvalResult:
 
 
 # ---------------------------------------------------------------------------- object engine
+class ReplayTimeout(Exception):
+    """Raised inside an object-engine replay that exceeded its wall-clock budget."""
+
+
 def object_engine_eval(code: str, workload: Workload, budget_s: float = 0.0) -> EvalResult:
-    """Reference-semantics replay with CPython ``exec`` (the exact fallback)."""
+    """Reference-semantics replay with CPython ``exec`` (the exact fallback).
+
+    ``budget_s`` > 0 bounds the replay's wall-clock time with ``SIGALRM`` (as
+    the reference's `SafeExecutor`, `funsearch/safe_execution.py:81-96`, does
+    per call): a program that loops forever scores 0 with `Exc.BUDGET`
+    instead of hanging the search.  Only effective in a process's main thread.
+    """
+    import signal
+    import threading
     from .funsearch.scheduler import FunSearchScheduler
     from .simulator import DiscreteEventSimulator, KubernetesSimulator, SchedulingEvaluator
+    armed = budget_s > 0 and threading.current_thread() is threading.main_thread()
+    if armed:
+        def _expire(signum, frame):
+            raise ReplayTimeout(f"replay exceeded {budget_s} s")
+        old = signal.signal(signal.SIGALRM, _expire)
+        signal.setitimer(signal.ITIMER_REAL, budget_s)
     try:
         sched = FunSearchScheduler(code)
         cluster, pods = workload.to_objects()
@@ -84,9 +104,15 @@ def object_engine_eval(code: str, workload: Workload, budget_s: float = 0.0) -> 
         return EvalResult(float(ev.get_policy_score(pods)), 0, "object", res, sim.events_processed)
     except Exception as exc:  # any exception aborts the replay -> score 0
         return EvalResult(0.0, _exc_code(exc), "object")
+    finally:
+        if armed:
+            signal.setitimer(signal.ITIMER_REAL, 0)
+            signal.signal(signal.SIGALRM, old)
 
 
 def _exc_code(exc: BaseException) -> int:
+    if isinstance(exc, ReplayTimeout):
+        return int(Exc.BUDGET)
     if isinstance(exc, ZeroDivisionError):
         return int(Exc.ZERO_DIVISION)
     if isinstance(exc, OverflowError):
@@ -101,8 +127,8 @@ def _exc_code(exc: BaseException) -> int:
 
 
 def _object_worker(args):
-    code, workload = args
-    return object_engine_eval(code, workload)
+    code, workload, budget_s = args
+    return object_engine_eval(code, workload, budget_s)
 
 
 # ---------------------------------------------------------------------------- evaluator
@@ -114,7 +140,7 @@ class Evaluator:
     """
 
     def __init__(self, workload: Optional[Workload] = None, device="auto", options: Optional[dict] = None,
-                 cpu_threads: int = 0, object_workers: int = 0):
+                 cpu_threads: int = 0, object_workers: int = 0, n_slots: int = 4):
         self.workload = workload or load_default_workload()
         self.options = dict(options or {})
         self.cpu_threads = cpu_threads or os.cpu_count() or 1
@@ -129,11 +155,12 @@ class Evaluator:
                 raise RuntimeError("HIP device requested but none is visible")
             if available:
                 try:
-                    self.device = hip_engine.DeviceEvaluator(self.workload, idx, self.options)
+                    self.device = hip_engine.DeviceEvaluator(self.workload, idx, self.options, n_slots)
                 except hip_engine.UnsupportedWorkload:
                     if device != "auto":
                         raise
         self.stats = {"device": 0, "cpu_vm": 0, "object": 0, "compile_errors": 0}
+        self._done: Dict[int, np.ndarray] = {}   # CPU stand-in for in-flight slots
 
     @property
     def backend(self) -> str:
@@ -148,9 +175,25 @@ class Evaluator:
         return cpu_engine.simulate_builtin_batch(self.workload, family, weights,
                                                  cpu_engine.SimOptions(**self._cpu_opts()), self.cpu_threads)
 
+    # asynchronous form: several family batches in flight (one HIP stream per slot)
+    def submit_family(self, slot: int, family: str, weights: np.ndarray) -> None:
+        if self.device is not None:
+            self.device.submit_builtin(slot, family, weights)
+        else:
+            self._done[slot] = self.evaluate_family(family, weights)
+
+    def ready(self, slot: int) -> bool:
+        return self.device.ready(slot) if self.device is not None else True
+
+    def wait(self, slot: int) -> np.ndarray:
+        return self.device.wait(slot) if self.device is not None else self._done.pop(slot)
+
     def _cpu_opts(self) -> dict:
-        keep = ("repush", "gpu_alloc", "snapshot_interval", "budget")
-        return {k: v for k, v in self.options.items() if k in keep}
+        from .ops.cpu_engine import DEFAULT_CALL_BUDGET
+        keep = ("repush", "gpu_alloc", "snapshot_interval", "budget")   # (object_timeout_s: object engine only)
+        opts = {k: v for k, v in self.options.items() if k in keep}
+        opts.setdefault("budget", DEFAULT_CALL_BUDGET)
+        return opts
 
     # -- programs ---------------------------------------------------------------------
     def evaluate_programs(self, codes: Sequence[str]) -> List[EvalResult]:
@@ -169,7 +212,7 @@ class Evaluator:
             if dev_idx:
                 tab = self.device.evaluate_programs([compiled[i] for i in dev_idx])
                 for row, i in zip(tab, dev_idx):
-                    if int(row[COLS["exc"]]) == Exc.UNSUPPORTED or row[COLS["inexact"]]:
+                    if int(row[COLS["exc"]]) in (Exc.UNSUPPORTED, Exc.BUDGET) or row[COLS["inexact"]]:
                         continue
                     out[i] = _row_to_result(row, "hip")
                     self.stats["device"] += 1
@@ -180,7 +223,7 @@ class Evaluator:
             tab = cpu_engine.simulate_program_batch(self.workload, [compiled[i] for i in cpu_idx],
                                                     cpu_engine.SimOptions(**self._cpu_opts()), self.cpu_threads)
             for row, i in zip(tab, cpu_idx):
-                if int(row[COLS["exc"]]) == Exc.UNSUPPORTED or row[COLS["inexact"]]:
+                if int(row[COLS["exc"]]) in (Exc.UNSUPPORTED, Exc.BUDGET) or row[COLS["inexact"]]:
                     continue
                 out[i] = _row_to_result(row, "cpu")
                 self.stats["cpu_vm"] += 1
@@ -188,7 +231,8 @@ class Evaluator:
         rest = [i for i in range(n) if out[i] is None]
         if rest:
             if self._object_engine_ok():
-                jobs = [(codes[i], self.workload) for i in rest]
+                budget_s = float(self.options.get("object_timeout_s", 600.0))
+                jobs = [(codes[i], self.workload, budget_s) for i in rest]
                 if len(rest) > 1 and self.object_workers > 1:
                     with ProcessPoolExecutor(max_workers=min(self.object_workers, len(rest))) as ex:
                         results = list(ex.map(_object_worker, jobs))

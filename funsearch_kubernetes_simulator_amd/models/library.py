@@ -42,3 +42,17 @@ def policy(name: str) -> str:
         if name in _load(table):
             return _load(table)[name]["code"]
     raise KeyError(name)
+
+
+def discovered_policies() -> Dict[str, dict]:
+    """Policies found by this framework's searches, stored in the reference's
+    results-JSON schema (`save_best_policy`: score, generation, code,
+    timestamp; plus family / weights / results) under
+    ``data/policies/discovered``.  file stem -> record."""
+    out: Dict[str, dict] = {}
+    d = POLICIES_DIR / "discovered"
+    if d.is_dir():
+        for f in sorted(d.glob("*.json")):
+            with open(f) as fh:
+                out[f.stem] = json.load(fh)
+    return out

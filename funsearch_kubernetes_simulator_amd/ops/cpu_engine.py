@@ -18,6 +18,12 @@ from ..policy.compiler import CompiledPolicy
 
 _mod = None
 
+#: Default VM instruction budget of one priority evaluation (one pod, all
+#: nodes).  Runaway programs (``while True``) stop with EXC_BUDGET -- on the
+#: GPU this guarantees every replay wave drains -- and the evaluator hands
+#: them to the wall-clock-bounded object engine.
+DEFAULT_CALL_BUDGET = 1 << 22
+
 FAMILY = {"first_fit": 0, "best_fit": 1, "random_linear": 2, "feature_linear": 3, "composite_linear": 4}
 
 
@@ -68,7 +74,7 @@ class SimOptions:
     gpu_alloc: str = "best_fit"     # "best_fit" (reference) | "first_fit"
     snapshot_interval: float = 0.05
     truncate: bool = True           # FunSearchScheduler int(max(0, score))
-    budget: int = 0                 # VM instruction budget per replay (0 = unlimited)
+    budget: int = DEFAULT_CALL_BUDGET  # VM instructions per priority evaluation (0 = unlimited)
     record_values: bool = False
     record_placements: bool = False
 

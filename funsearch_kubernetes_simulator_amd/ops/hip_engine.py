@@ -22,7 +22,7 @@ import numpy as np
 
 from ..core.arrays import Workload
 from ..policy.compiler import CompiledPolicy
-from .cpu_engine import FAMILY, RESULT_COLUMNS  # noqa: F401  (same table layout)
+from .cpu_engine import DEFAULT_CALL_BUDGET, FAMILY, RESULT_COLUMNS  # noqa: F401  (same table layout)
 
 GMAX = 8
 WEIGHTS_PER_POLICY = 16
@@ -191,14 +191,15 @@ def pack_programs(progs: Sequence[CompiledPolicy]):
 class DeviceEvaluator:
     """A workload resident on one MI355X, evaluating policy batches."""
 
-    def __init__(self, workload: Workload, device: int = 0, options: Optional[dict] = None):
+    def __init__(self, workload: Workload, device: int = 0, options: Optional[dict] = None, n_slots: int = 4):
         self.workload = workload
         self.device = device
         options = dict(options or {})
         interval = float(options.get("snapshot_interval", 0.05))
         self.layout = prepare_device_workload(workload, interval)
-        self._eng = native().DeviceEngine(self.layout, device)
+        self._eng = native().DeviceEngine(self.layout, device, n_slots)
         options["snapshot_interval"] = interval
+        options.setdefault("budget", DEFAULT_CALL_BUDGET)
         self._eng.set_options(options)
         self.options = options
 
@@ -211,8 +212,8 @@ class DeviceEvaluator:
         self.options.update(opts)
         self._eng.set_options(opts)
 
-    def evaluate_builtin(self, family: "str | Sequence[str]", weights: Optional[np.ndarray] = None,
-                         n: Optional[int] = None) -> np.ndarray:
+    @staticmethod
+    def _builtin_args(family, weights, n=None):
         if isinstance(family, str):
             count = n if n is not None else (len(weights) if weights is not None else 1)
             fam = np.full(count, FAMILY[family], dtype=np.int32)
@@ -222,7 +223,30 @@ class DeviceEvaluator:
         if weights is not None:
             weights = np.asarray(weights, dtype=np.float64).reshape(len(fam), -1)
             W[:, :weights.shape[1]] = weights
-        return self._eng.evaluate_builtin(fam, W)
+        return fam, W
+
+    def evaluate_builtin(self, family: "str | Sequence[str]", weights: Optional[np.ndarray] = None,
+                         n: Optional[int] = None) -> np.ndarray:
+        return self._eng.evaluate_builtin(*self._builtin_args(family, weights, n))
+
+    # -- asynchronous slots: several batches in flight on separate HIP streams --------------
+    @property
+    def n_slots(self) -> int:
+        return self._eng.n_slots()
+
+    def submit_builtin(self, slot: int, family: str, weights: np.ndarray) -> None:
+        """Start a batch on `slot` (its own stream); returns immediately."""
+        self._eng.submit_builtin(slot, *self._builtin_args(family, weights))
+
+    def submit_programs(self, slot: int, progs: Sequence[CompiledPolicy]) -> None:
+        self._eng.submit_programs(slot, *pack_programs(progs), max(p.nregs for p in progs))
+
+    def ready(self, slot: int) -> bool:
+        return self._eng.ready(slot)
+
+    def wait(self, slot: int) -> np.ndarray:
+        """[P, 13] result table of the batch in flight on `slot`."""
+        return self._eng.wait(slot)
 
     def evaluate_programs(self, progs: Sequence[CompiledPolicy]) -> np.ndarray:
         if not progs:
@@ -243,8 +267,12 @@ class DeviceEvaluator:
         packed = pack_programs(progs) + (max(p.nregs for p in progs),)
         return self._eng.profile(None, None, packed)
 
-    def launch_builtin_async(self, n: int) -> None:
-        self._eng.launch_builtin_async(n)
+    def stage_builtin_only(self, family: str, weights: np.ndarray) -> None:
+        """Stage a batch on slot 0 for repeated timing launches (tools/)."""
+        self._eng.stage_builtin_only(*self._builtin_args(family, weights))
+
+    def launch_builtin_async(self) -> None:
+        self._eng.launch_builtin_async()
 
     def synchronize(self) -> None:
         self._eng.synchronize()

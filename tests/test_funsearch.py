@@ -131,3 +131,18 @@ def test_run_funsearch_islands_cpu(tmp_path):
     assert score >= reference_scores()["best_fit"]
     assert "def priority_function" in code
     assert os.path.exists(tmp_path / "ck" / "islands_rank0.json")
+
+
+def test_runaway_program_is_bounded():
+    """`while True` stops on the VM call budget, then on the object engine's wall clock."""
+    import numpy as np
+    from funsearch_kubernetes_simulator_amd.core import load_default_workload
+    from funsearch_kubernetes_simulator_amd.core.arrays import Workload
+    from funsearch_kubernetes_simulator_amd.engine import Evaluator
+    from funsearch_kubernetes_simulator_amd.policy.bytecode import Exc
+    w = load_default_workload()
+    sub = Workload(w.cluster, w.pods.subset(np.arange(0, 50)))
+    ev = Evaluator(sub, device="cpu", options={"object_timeout_s": 1.0})
+    code = "def priority_function(pod, node):\n    x = 0\n    while True:\n        x += 1\n    return 1\n"
+    r = ev.evaluate_programs([code])[0]
+    assert (r.score, r.exc, r.engine) == (0.0, int(Exc.BUDGET), "object")

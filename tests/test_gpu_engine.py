@@ -61,3 +61,17 @@ def test_vm_reference_programs_exact(dev, default_workload):
         assert tab[i, 0] == reference_scores()[n], n
         cpu = ce.simulate_program(default_workload, progs[i])
         assert tab[i, 12] == float(cpu["trace_hash"] >> 11), n
+
+
+def test_async_slots_match_sync(dev, default_workload):
+    """Batches in flight on separate streams give the same tables as round trips."""
+    rng = np.random.default_rng(5)
+    a = fam.sample_composite_linear(96, rng)
+    b = fam.sample_random_linear(80, rng)
+    dev.submit_builtin(1, "composite_linear", a)
+    dev.submit_builtin(2, "random_linear", b)
+    tb = dev.wait(2)
+    ta = dev.wait(1)
+    assert np.array_equal(ta, dev.evaluate_builtin("composite_linear", a))
+    assert np.array_equal(tb, dev.evaluate_builtin("random_linear", b))
+    assert dev.ready(1) and dev.ready(2)

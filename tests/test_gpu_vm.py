@@ -52,3 +52,15 @@ def test_device_vm_equals_cpu_vm(default_workload, mode):
         assert np.array_equal(gpu[i], cpu[i]), (i, p.source[-300:], gpu[i], cpu[i])
         compared += 1
     assert compared >= len(progs) - 6
+
+
+def test_device_vm_runaway_program_drains(default_workload):
+    """A non-terminating candidate must not hang the GPU: the per-call budget ends its wave."""
+    from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
+    w = default_workload
+    sub = Workload(w.cluster, w.pods.subset(np.arange(0, 64)))
+    dev = he.DeviceEvaluator(sub, options={"budget": 100000})
+    prog = compile_policy("def priority_function(pod, node):\n    x = 0\n    while True:\n        x += 1\n"
+                          "    return 1\n")
+    tab = dev.evaluate_programs([prog] * 4)
+    assert np.all(tab[:, 10] == Exc.BUDGET)
