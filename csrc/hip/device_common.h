@@ -135,6 +135,43 @@ struct FixedAccD {
   }
 };
 
+// The replay's five exact accumulators (4 utilisation means + fragmentation)
+// spread over lanes: accumulator k lives in lane k, so the whole set costs a
+// handful of VGPRs instead of ~35 loop-carried SGPRs (which the compiler
+// would otherwise spill through v_writelane / v_readlane on every event).
+// Same arithmetic as FixedAccD.
+struct LaneAcc {
+  i128 sum;
+  int64_t count;
+  int32_t inexact;
+  __device__ void init() { sum = 0; count = 0; inexact = 0; }
+  // v is wave-uniform; adds it to accumulator k
+  __device__ void add(int k, double v) {
+    const bool mine = lane_id() == k;
+    uint64_t bits = (uint64_t)__double_as_longlong(v);
+    const int E = (int)((bits >> 52) & 0x7FF);
+    const uint64_t frac = bits & ((1ull << 52) - 1);
+    if (mine) ++count;
+    if (E == 0 && frac == 0) return;
+    bool bad = (E == 0x7FF || E == 0);   // inf/nan, subnormal
+    uint64_t M = frac | (1ull << 52);
+    int shift = E - 979;  // v * 2^96 = M * 2^(E-1075+96)
+    if (!bad && shift < 0) {
+      if (shift <= -53 || (M & ((1ull << (-shift)) - 1))) bad = true;
+      else { M >>= (-shift); shift = 0; }
+    }
+    if (!bad && shift > 126 - 53) bad = true;
+    if (bad) { if (mine) inexact = 1; return; }
+    i128 t = (i128)(u128)M << shift;
+    if (bits >> 63) t = -t;
+    if (mine) {
+      sum += t;
+      const u128 mag = sum < 0 ? (u128)(-sum) : (u128)sum;
+      if (mag >> 126) inexact = 1;
+    }
+  }
+};
+
 // Correctly rounded A * 2^-96 / n  (bit-serial long division; no libcalls).
 __device__ inline double fixed_div_round_dev(i128 A, uint64_t n) {
   if (A == 0 || n == 0) return 0.0;

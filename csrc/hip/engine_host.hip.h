@@ -93,15 +93,16 @@ struct HostBuf {
 struct Slot {
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
-  DevBuf res, tab, fam, w, code, meta, kpay, ktag, gheap, prof;
-  HostBuf h_in, h_tab;
+  DevBuf res, tab, fam, w, code, meta, kpay, ktag, gheap, prof, wc;
+  HostBuf h_in, h_tab, h_wc;
   int P = 0;
   int fam_spec = -1;    // family shared by the whole staged batch, or -1
   bool busy = false;
   void release() {
-    for (DevBuf* b : {&res, &tab, &fam, &w, &code, &meta, &kpay, &ktag, &gheap, &prof}) b->release();
+    for (DevBuf* b : {&res, &tab, &fam, &w, &code, &meta, &kpay, &ktag, &gheap, &prof, &wc}) b->release();
     h_in.release();
     h_tab.release();
+    h_wc.release();
     if (done) (void)hipEventDestroy(done);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -287,14 +288,15 @@ class DeviceEngine {
     const int P = s.P;
     s.prof.reserve((size_t)P * 64);
     const bool g = use_gheap(P);
-    const DevWorkload Wl = launch_workload(g, is_vm ? nregs : 0);
+    const DevWorkload Wl = launch_workload(g, is_vm ? nregs : 0, is_vm);
     const size_t lds = lds_bytes(g, Wl.heap_top, is_vm ? nregs : 0);
     uint64_t* gh = g ? gheap_for(s, P) : nullptr;
+    const DevWorkload* wc = upload_workload(s, Wl);
     if (is_vm) {
-      const fksk::VmArgs a{Wl, table(s), s.res.as<DevResult>(), budget_, gh, s.prof.as<uint64_t>()};
+      const fksk::VmArgs a{Wl, wc, table(s), s.res.as<DevResult>(), budget_, gh, s.prof.as<uint64_t>()};
       HIP_OK(fksk::launch_vm_prof(g, P, lds, s.stream, a));
     } else {
-      const fksk::BuiltinArgs a{Wl, s.fam.as<int32_t>(), s.w.as<double>(), s.res.as<DevResult>(), gh,
+      const fksk::BuiltinArgs a{Wl, wc, s.fam.as<int32_t>(), s.w.as<double>(), s.res.as<DevResult>(), gh,
                                 s.prof.as<uint64_t>()};
       HIP_OK(fksk::launch_builtin_prof(g, P, lds, s.stream, a));
     }
@@ -314,7 +316,7 @@ class DeviceEngine {
     d["npass"] = npass_;
     d["heap_mode"] = heap_mode_;
     d["n_slots"] = (int)slots_.size();
-    d["heap_top_hbm"] = heap_top_for(0);
+    d["heap_top_hbm"] = heap_top_for(0, false);
     return d;
   }
 
@@ -323,7 +325,8 @@ class DeviceEngine {
 
  private:
   static constexpr size_t kMaxLds = 160 * 1024;
-  static constexpr size_t kPoliciesPerCu = 16;   // HBM-heap kernels: 4 waves per SIMD
+  static constexpr size_t kPoliciesPerCu = 16;   // HBM-heap builtin kernels: 4 waves per SIMD
+  static constexpr size_t kVmPoliciesPerCu = 8;  // HBM-heap VM kernels: 2 waves per SIMD
 
   Slot& slot_at(int i) {
     if (i < 0 || i >= (int)slots_.size()) throw std::out_of_range("slot index");
@@ -359,19 +362,19 @@ class DeviceEngine {
 
   // HBM-heap launches keep the top 2^L - 1 heap slots in LDS, as many levels as
   // fit a 16-policies-per-CU share of the 160 KiB (or the `heap_top` option).
-  int heap_top_for(int nregs) const {
+  int heap_top_for(int nregs, bool vm) const {
     const int entries = (int)(heap_bytes_ / 8);
     if (heap_top_opt_ >= 0) return std::min(heap_top_opt_, entries);
-    const size_t budget = kMaxLds / kPoliciesPerCu;
+    const size_t budget = kMaxLds / (vm ? kVmPoliciesPerCu : kPoliciesPerCu);
     const size_t fixed = delmap_bytes_ + (size_t)nregs * 64 * 8;
     int T = 0;
     while (T < entries && fixed + (size_t)(2 * T + 1) * 8 <= budget) T = 2 * T + 1;
     return std::min(T, entries);
   }
 
-  DevWorkload launch_workload(bool g, int nregs) const {
+  DevWorkload launch_workload(bool g, int nregs, bool vm) const {
     DevWorkload Wl = W_;
-    Wl.heap_top = g ? heap_top_for(nregs) : 0;
+    Wl.heap_top = g ? heap_top_for(nregs, vm) : 0;
     return Wl;
   }
 
@@ -446,10 +449,11 @@ class DeviceEngine {
   void launch_builtin(Slot& s) {
     const int P = s.P;
     const bool g = use_gheap(P);
-    const DevWorkload Wl = launch_workload(g, 0);
+    const DevWorkload Wl = launch_workload(g, 0, false);
     const size_t lds = lds_bytes(g, Wl.heap_top, 0);
     uint64_t* gh = g ? gheap_for(s, P) : nullptr;
-    const fksk::BuiltinArgs a{Wl, s.fam.as<int32_t>(), s.w.as<double>(), s.res.as<DevResult>(), gh, nullptr};
+    const fksk::BuiltinArgs a{Wl, upload_workload(s, Wl), s.fam.as<int32_t>(), s.w.as<double>(),
+                              s.res.as<DevResult>(), gh, nullptr};
     if (npass_ == 1) HIP_OK(fksk::launch_builtin_np1(g, s.fam_spec, P, lds, s.stream, a));
     else if (npass_ == 2) HIP_OK(fksk::launch_builtin_np2(g, s.fam_spec, P, lds, s.stream, a));
     else HIP_OK(fksk::launch_builtin_np4(g, s.fam_spec, P, lds, s.stream, a));
@@ -458,14 +462,23 @@ class DeviceEngine {
   void launch_vm(Slot& s, int nregs) {
     const int P = s.P;
     const bool g = use_gheap(P);
-    const DevWorkload Wl = launch_workload(g, nregs);
+    const DevWorkload Wl = launch_workload(g, nregs, true);
     const size_t lds = lds_bytes(g, Wl.heap_top, nregs);
     if (lds > kMaxLds) throw std::invalid_argument("heap + VM registers exceed the 160 KiB LDS");
     uint64_t* gh = g ? gheap_for(s, P) : nullptr;
-    const fksk::VmArgs a{Wl, table(s), s.res.as<DevResult>(), budget_, gh, nullptr};
+    const fksk::VmArgs a{Wl, upload_workload(s, Wl), table(s), s.res.as<DevResult>(), budget_, gh, nullptr};
     if (npass_ == 1) HIP_OK(fksk::launch_vm_np1(g, P, lds, s.stream, a));
     else if (npass_ == 2) HIP_OK(fksk::launch_vm_np2(g, P, lds, s.stream, a));
     else HIP_OK(fksk::launch_vm_np4(g, P, lds, s.stream, a));
+  }
+
+  // the launch's workload struct, also resident in HBM (the kernels' cold-field copy)
+  const DevWorkload* upload_workload(Slot& s, const DevWorkload& Wl) {
+    s.wc.reserve(sizeof(DevWorkload));
+    s.h_wc.reserve(sizeof(DevWorkload));
+    std::memcpy(s.h_wc.p, &Wl, sizeof(DevWorkload));
+    HIP_OK(hipMemcpyAsync(s.wc.p, s.h_wc.p, sizeof(DevWorkload), hipMemcpyHostToDevice, s.stream));
+    return s.wc.as<const DevWorkload>();
   }
 
   // k_eval_reduce, result table -> pinned host, completion event

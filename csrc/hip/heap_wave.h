@@ -37,6 +37,7 @@ struct WaveHeap {
   int T;
   uint32_t* delmap;   // bit p set <=> slot p holds a deletion
   int lb;             // low (payload) bits below the (time, rank) compare key
+  int lane;           // this lane's id, refreshed (opaquely) per event by the caller
 
   __device__ __forceinline__ uint64_t ld(int i) const { return i < T ? top[i] : h[i]; }
   __device__ __forceinline__ void st(int i, uint64_t v) const {
@@ -54,7 +55,6 @@ struct WaveHeap {
   // re-inserted (CPython: heap.pop(); heap[0] = last; _siftup(heap, 0)).
   // n = new size (>= 1).
   __device__ void pop_reinsert(int n, uint64_t last) const {
-    const int lane = lane_id();
     // lane l in [0, 62): subtree level r (1..5), index i within the level
     const int r = lane < 2 ? 1 : lane < 6 ? 2 : lane < 14 ? 3 : lane < 30 ? 4 : 5;
     const int i = lane - ((1 << r) - 2);
@@ -132,7 +132,6 @@ struct WaveHeap {
 
   // CPython heappush on a heap of n items (item lands at index <= n).
   __device__ void push(int n, uint64_t item) const {
-    const int lane = lane_id();
     // ancestors a_l = ((n+1) >> l) - 1, l >= 1, exist while (n+1) >> l >= 1
     const int l = lane + 1;
     const int anc = lane < 30 ? ((n + 1) >> l) - 1 : -1;
@@ -149,7 +148,6 @@ struct WaveHeap {
 
   // index of the first DELETION in h[0, n), or -1
   __device__ int first_deletion(int n) const {
-    const int lane = lane_id();
     const int words = (n + 31) >> 5;
     for (int base = 0; base < words; base += kWave) {
       const int wi = base + lane;

@@ -18,6 +18,7 @@ using fksd::DevWorkload;
 
 struct BuiltinArgs {
   DevWorkload W;
+  const DevWorkload* Wc;  // the same workload struct, resident in HBM (cold fields)
   const int32_t* fam;     // [P] family id per policy
   const double* weights;  // [P, kWeights]
   DevResult* out;
@@ -27,6 +28,7 @@ struct BuiltinArgs {
 
 struct VmArgs {
   DevWorkload W;
+  const DevWorkload* Wc;
   DevProgramTable T;
   DevResult* out;
   int64_t budget;

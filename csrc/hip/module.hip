@@ -90,8 +90,11 @@ __global__ __launch_bounds__(64) void k_test_heap(const uint64_t* init, int n0, 
   const int lane = lane_id();
   WaveHeap hp;
   hp.h = lds;
+  hp.top = lds;
+  hp.T = 1 << 30;   // all slots in LDS
   hp.delmap = reinterpret_cast<uint32_t*>(lds + 4096);
   hp.lb = lb;
+  hp.lane = lane;
   for (int i = lane; i < n0; i += 64) lds[i] = init[i];
   for (int i = lane; i < 256; i += 64) hp.delmap[i] = 0;
   __syncthreads();

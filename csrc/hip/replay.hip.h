@@ -161,8 +161,13 @@ __device__ __forceinline__ int pick_gpus(const NodeRegs<NPASS>& nr, int ps, int 
 
 // ----------------------------------------------------------------------------
 template <int NPASS, class Scorer, class Prof = NoProf>
-__device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* hbuf, uint64_t* htop, int T,
-                           uint32_t* delmap, DevResult* out, uint64_t* prof_out = nullptr) {
+__device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Scorer& scorer, uint64_t* hbuf,
+                           uint64_t* htop, int T, uint32_t* delmap, DevResult* out, uint64_t* prof_out = nullptr) {
+  // W: the kernel-argument copy (hot fields, kept in SGPRs); Wcold: the same
+  // struct in global memory for the fields only snapshots / failures / commits
+  // of multi-GPU pods need.  Its address is made opaque once per event so the
+  // compiler re-loads those fields (scalar-cache hits) where they are used
+  // instead of pinning ~30 SGPRs for the whole loop and spilling them.
   // hbuf: the policy's heap array -- LDS (fast, 2 policies/CU on the 8k trace)
   // or its private slice of an HBM buffer (any trace length, 16 policies/CU);
   // slots [0, T) are held in LDS at htop instead (T >= N: all of it)
@@ -206,12 +211,12 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* hbuf,
   for (int k = 0; k < KP; ++k) wcnt[k] = 0;
 
   int64_t used_cpu = W.used_cpu0, used_mem = W.used_mem0, used_gcnt = W.used_gcnt0, used_gml = W.used_gmilli0;
-  FixedAccD acc[5];
-#pragma unroll
-  for (int k = 0; k < 5; ++k) acc[k].init();
-  int64_t processed = 0, n_repush = 0, n_dropped = 0, max_nodes = 0;
+  LaneAcc acc;   // accumulators 0-3: utilisation snapshots, 4: fragmentation
+  acc.init();
+  int64_t processed = 0, n_repush = 0, n_dropped = 0;
   int ksnap = 0;
-  int64_t next_fire = W.n_fire > 0 ? W.snap_fire[0] : INT64_MAX;
+  const int n_fire = W.n_fire;
+  int64_t next_fire = n_fire > 0 ? W.snap_fire[0] : INT64_MAX;
   double thr = W.thr_after_fire;   // used once the precomputed schedule is exhausted
   uint64_t hsh = 0xcbf29ce484222325ull;
   int32_t exc = EXC_NONE;
@@ -219,7 +224,21 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* hbuf,
   __syncthreads();
   prof.start();
 
+  heap.lane = lane;
   while (n > 0) {
+    const DevWorkload* Wc = reinterpret_cast<const DevWorkload*>(uniu64(reinterpret_cast<uint64_t>(Wcold)));
+    asm volatile("" : "+s"(Wc));
+    // Lane-derived predicates (subtree slots of the heap walk, "GPU j exists")
+    // are loop-invariant; hoisted they become dozens of live 64-bit lane masks
+    // in SGPRs that get spilled every event.  Opaque copies are recomputed per
+    // event with a few VALU compares instead.
+    {
+      int ol = lane;
+      asm volatile("" : "+v"(ol));
+      heap.lane = ol;
+#pragma unroll
+      for (int ps = 0; ps < NPASS; ++ps) asm volatile("" : "+v"(nr.ngpus[ps]));
+    }
     // ---------------- pop (pod record load issued first, consumed after the sift)
     const uint64_t top = uniu64(heap.ld(0));
     const int rank = (int)((top >> lb) & ((1ull << rb) - 1));
@@ -292,7 +311,7 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* hbuf,
           if (mcls < 0 && b) mcls = k * kWave + first_lane(b);
         }
         if (mcls >= 0) {
-          const int m = W.class_value[mcls];
+          const int m = Wc->class_value[mcls];
           int64_t stranded = 0;
 #pragma unroll
           for (int ps = 0; ps < NPASS; ++ps)
@@ -302,12 +321,13 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* hbuf,
               if (j < nr.ngpus[ps] && 0 < l && l < m) stranded += l;
             }
           stranded = wave_sum_i64(stranded);
-          frag = W.tot_gmilli > 0 ? (double)stranded / (double)W.tot_gmilli : 0.0;
+          const int64_t tg = Wc->tot_gmilli;
+          frag = tg > 0 ? (double)stranded / (double)tg : 0.0;
         }
-        acc[4].add(frag);
+        acc.add(4, frag);
         // repush: first DELETION in heap-array order (or the earliest one)
         int64_t anchor = -1;
-        if (!W.repush_earliest) {
+        if (!Wc->repush_earliest) {
           const int f = heap.first_deletion(n);
           if (f >= 0) anchor = (int64_t)(uniu64(heap.ld(f)) >> tshift);
         } else {
@@ -341,7 +361,7 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* hbuf,
           int mymask = 0, myok = 1;
 #pragma unroll
           for (int ps = 0; ps < NPASS; ++ps)
-            if (ps == bp) mymask = pick_gpus<NPASS>(nr, ps, pod.gmilli, pod.ngpu, W.first_fit_alloc != 0, myok);
+            if (ps == bp) mymask = pick_gpus<NPASS>(nr, ps, pod.gmilli, pod.ngpu, Wc->first_fit_alloc != 0, myok);
           gmask = readlane(mymask, bl);
           ok = readlane(myok, bl);
         }
@@ -377,48 +397,39 @@ __device__ void replay_one(const DevWorkload& W, Scorer& scorer, uint64_t* hbuf,
     // ---------------- evaluator hook (snapshot schedule precomputed on the host)
     ++processed;
     bool fire;
-    if (ksnap < W.n_fire) fire = processed >= next_fire;
+    if (ksnap < n_fire) fire = processed >= next_fire;
     else fire = (double)processed / (double)N >= thr;
     if (fire) {
-      const double r0 = W.tot_cpu > 0 ? (double)used_cpu / (double)W.tot_cpu : 0.0;
-      const double r1 = W.tot_mem > 0 ? (double)used_mem / (double)W.tot_mem : 0.0;
-      const double r2 = W.tot_gcnt > 0 ? (double)used_gcnt / (double)W.tot_gcnt : 0.0;
-      const double r3 = W.tot_gmilli > 0 ? (double)used_gml / (double)W.tot_gmilli : 0.0;
-      acc[0].add(r0); acc[1].add(r1); acc[2].add(r2); acc[3].add(r3);
-      if (ksnap >= W.n_fire) thr += W.snapshot_interval;
+      const int64_t t0 = Wc->tot_cpu, t1 = Wc->tot_mem, t2 = Wc->tot_gcnt, t3 = Wc->tot_gmilli;
+      const double r0 = t0 > 0 ? (double)used_cpu / (double)t0 : 0.0;
+      const double r1 = t1 > 0 ? (double)used_mem / (double)t1 : 0.0;
+      const double r2 = t2 > 0 ? (double)used_gcnt / (double)t2 : 0.0;
+      const double r3 = t3 > 0 ? (double)used_gml / (double)t3 : 0.0;
+      acc.add(0, r0); acc.add(1, r1); acc.add(2, r2); acc.add(3, r3);
+      if (ksnap >= n_fire) thr += Wc->snapshot_interval;
       ++ksnap;
-      next_fire = ksnap < W.n_fire ? W.snap_fire[ksnap] : INT64_MAX;
+      next_fire = ksnap < n_fire ? Wc->snap_fire[ksnap] : INT64_MAX;
     }
-    // active nodes (max_nodes; informational)
-    int active = 0;
-#pragma unroll
-    for (int ps = 0; ps < NPASS; ++ps) {
-      const bool valid = (ps * kWave + lane) < W.n_nodes;
-      const bool a = valid && (nr.cpu_left[ps] < nr.cpu_total[ps] || nr.mem_left[ps] < nr.mem_total[ps] ||
-                               nr.gpu_left[ps] < nr.ngpus[ps]);
-      active += __popcll(ballot(a));
-    }
-    max_nodes = active > max_nodes ? active : max_nodes;
+    // (the reference's max_nodes counter feeds no metric: not tracked)
     prof.mark(PH_EVAL);
   }
   if (prof_out) prof.flush(prof_out);
 
+  const int64_t n_snap = readlane64(acc.count, 0), n_frag = readlane64(acc.count, 4);
+  const int inexact = ballot(lane < 5 && acc.inexact != 0) != 0;
+  if (lane < 5) {
+    out->acc_lo[lane] = (uint64_t)(u128)acc.sum;
+    out->acc_hi[lane] = (uint64_t)((u128)acc.sum >> 64);
+  }
   if (lane == 0) {
     out->n_events = processed;
-    out->n_snap = acc[0].count;
-    out->n_frag = acc[4].count;
+    out->n_snap = n_snap;
+    out->n_frag = n_frag;
     out->n_unplaced = n_dropped;
     out->n_repush = n_repush;
-    out->max_nodes = max_nodes;
+    out->max_nodes = 0;
     out->hash = hsh;
     out->exc = exc;
-    int inexact = 0;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      inexact |= acc[k].inexact;
-      out->acc_lo[k] = (uint64_t)(u128)acc[k].sum;
-      out->acc_hi[k] = (uint64_t)((u128)acc[k].sum >> 64);
-    }
     out->inexact = inexact;
   }
 }

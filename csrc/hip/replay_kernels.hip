@@ -58,6 +58,8 @@ __device__ __forceinline__ Slot policy_slot(const DevWorkload& W, uint64_t* ghea
 // Waves per SIMD the kernel is compiled for: the LDS-heap variant is LDS-bound at
 // 2 waves/CU anyway; the HBM-heap variant trades registers for occupancy.
 #define FKS_BOUNDS(G) __launch_bounds__(64, (G) ? 4 : 1)
+// The VM keeps its hot virtual registers in VGPRs (vm_dev.hip.h): 2 waves/SIMD.
+#define FKS_VM_BOUNDS(G) __launch_bounds__(64, (G) ? 2 : 1)
 
 template <class T>
 hipError_t raise_lds(T* f, int max_lds) {
@@ -65,13 +67,16 @@ hipError_t raise_lds(T* f, int max_lds) {
 }
 
 #if FKS_KIND == 0
+// the feature families carry ~40 more live values through scoring: 3 waves/SIMD
+// without spills beats 4 with scratch traffic
+#define FKS_FAM_BOUNDS(G, F) __launch_bounds__(64, (G) ? (((F) == 3 || (F) == 4 || (F) < 0) ? 3 : 4) : 1)
 template <int NPASS, bool GHEAP, int FAM>
-__global__ FKS_BOUNDS(GHEAP) void k_replay_builtin(fksk::BuiltinArgs a) {
+__global__ FKS_FAM_BOUNDS(GHEAP, FAM) void k_replay_builtin(fksk::BuiltinArgs a) {
   const int p = blockIdx.x;
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   BuiltinScorerDev<FAM> sc;
   sc.load(a.fam[p], a.weights + (size_t)p * kWeights);
-  replay_one<NPASS>(a.W, sc, s.h, s.top, s.T, s.delmap, a.out + p);
+  replay_one<NPASS>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, a.out + p);
 }
 
 template <int NPASS, bool GHEAP>
@@ -106,12 +111,12 @@ hipError_t attrs_g(int mx) {
 
 #if FKS_KIND == 1
 template <int NPASS, bool GHEAP>
-__global__ FKS_BOUNDS(GHEAP) void k_replay_vm(fksk::VmArgs a) {
+__global__ FKS_VM_BOUNDS(GHEAP) void k_replay_vm(fksk::VmArgs a) {
   const int p = blockIdx.x;
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   VmScorerDev sc;
   sc.init(a.T, p, a.W, a.budget, s.vregs);
-  replay_one<NPASS>(a.W, sc, s.h, s.top, s.T, s.delmap, a.out + p);
+  replay_one<NPASS>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, a.out + p);
 }
 #endif
 
@@ -122,17 +127,17 @@ __global__ FKS_BOUNDS(GHEAP) void k_replay_builtin_prof(fksk::BuiltinArgs a) {
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   BuiltinScorerDev<-1> sc;
   sc.load(a.fam[p], a.weights + (size_t)p * kWeights);
-  replay_one<1, BuiltinScorerDev<-1>, PhaseProf>(a.W, sc, s.h, s.top, s.T, s.delmap, a.out + p,
+  replay_one<1, BuiltinScorerDev<-1>, PhaseProf>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, a.out + p,
                                                  a.prof + (size_t)p * 8);
 }
 
 template <bool GHEAP>
-__global__ FKS_BOUNDS(GHEAP) void k_replay_vm_prof(fksk::VmArgs a) {
+__global__ FKS_VM_BOUNDS(GHEAP) void k_replay_vm_prof(fksk::VmArgs a) {
   const int p = blockIdx.x;
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   VmScorerDev sc;
   sc.init(a.T, p, a.W, a.budget, s.vregs);
-  replay_one<1, VmScorerDev, PhaseProf>(a.W, sc, s.h, s.top, s.T, s.delmap, a.out + p, a.prof + (size_t)p * 8);
+  replay_one<1, VmScorerDev, PhaseProf>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, a.out + p, a.prof + (size_t)p * 8);
 }
 #endif
 

@@ -47,17 +47,24 @@ __host__ __device__ constexpr int family_weights(int fam) {
 template <int FAM = -1>
 struct BuiltinScorerDev {
   int32_t family;
-  double w[kWeights];
+  const double* wp;   // this policy's kWeights weights (HBM)
 
-  __device__ void load(int32_t fam_id, const double* __restrict__ wp) {
+  __device__ void load(int32_t fam_id, const double* __restrict__ p) {
     family = FAM >= 0 ? FAM : fam_id;
-#pragma unroll
-    for (int k = 0; k < kWeights; ++k) w[k] = k < family_weights(FAM) ? wp[k] : 0.0;
+    wp = p;
   }
 
   template <int NPASS>
   __device__ int64_t score(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, int& exc) const {
     if (!feasible<NPASS>(ps, nr, pod)) return 0;
+    // weights are re-read (scalar-cache hits) at every call rather than held in
+    // SGPRs across the event loop: the opaque pointer stops the compiler from
+    // hoisting the loads and spilling 8-32 SGPRs per event
+    const double* q = reinterpret_cast<const double*>(uniu64(reinterpret_cast<uint64_t>(wp)));
+    asm volatile("" : "+s"(q));
+    double w[kWeights];
+#pragma unroll
+    for (int k = 0; k < kWeights; ++k) w[k] = k < family_weights(FAM) ? q[k] : 0.0;
     switch (FAM >= 0 ? FAM : family) {
       case FAM_FIRST_FIT:
         return 1000;
@@ -91,7 +98,7 @@ struct BuiltinScorerDev {
         return trunc_score(s, exc);
       }
       case FAM_COMPOSITE_LINEAR:
-        return trunc_score(composite<NPASS>(ps, nr, pod), exc);
+        return trunc_score(composite<NPASS>(ps, nr, pod, w), exc);
     }
     exc = EXC_UNSUPPORTED;
     return 0;
@@ -102,7 +109,7 @@ struct BuiltinScorerDev {
   // rounding as `score += w_k * (f_k)`), so no 16-double feature vector is
   // held live across the node loop.
   template <int NPASS>
-  __device__ double composite(int ps, const NodeRegs<NPASS>& nr, const PodView& pod) const {
+  __device__ double composite(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, const double* w) const {
     const int ng = nr.ngpus[ps];
     const bool gpod = pod.ngpu > 0;
     const int64_t ct = nr.cpu_total[ps], mt = nr.mem_total[ps];

@@ -311,6 +311,10 @@ __device__ inline int d_unop(int op, const PyN& a, PyN& r) {
 
 // ---- the interpreter ---------------------------------------------------------------
 constexpr uint32_t kBrk = 1, kCont = 2, kDone = 4;
+#ifndef FKS_VM_VGPR_REGS
+#define FKS_VM_VGPR_REGS 16
+#endif
+constexpr int kVgprRegs = FKS_VM_VGPR_REGS;   // virtual registers held in VGPRs
 
 struct VmScorerDev {
   const uint64_t* code;
@@ -345,13 +349,22 @@ struct VmScorerDev {
     PyN result = pi(0);
     bool has_result = false;
     uint64_t* R = vregs + lane;
-
-    auto get = [&](int r) -> PyN { return PyN{(int64_t)R[r * kWave], ((ftag >> r) & 1) != 0}; };
+    // registers [0, kVgprRegs) live in VGPRs (uniform index -> s_set_gpr_idx
+    // relative addressing, no LDS round trip); the compiler numbers registers
+    // by use count, so the hot ones land here.  The rest live in LDS.
+    typedef long long VRegs __attribute__((ext_vector_type(kVgprRegs)));
+    VRegs RV = (VRegs)0;   // vector value: dynamic element access stays in registers
+    auto rd = [&](int r) -> int64_t { return r < kVgprRegs ? (int64_t)RV[r] : (int64_t)R[r * kWave]; };
+    auto wr = [&](int r, int64_t v) {
+      if (r < kVgprRegs) RV[r] = v;
+      else R[r * kWave] = (uint64_t)v;
+    };
+    auto get = [&](int r) -> PyN { return PyN{rd(r), ((ftag >> r) & 1) != 0}; };
     auto put = [&](int r, const PyN& v) {
-      R[r * kWave] = (uint64_t)v.b;
+      wr(r, v.b);
       ftag = v.fl ? (ftag | (1ull << r)) : (ftag & ~(1ull << r));
     };
-    auto put_raw = [&](int r, int64_t v) { R[r * kWave] = (uint64_t)v; ftag &= ~(1ull << r); };
+    auto put_raw = [&](int r, int64_t v) { wr(r, v); ftag &= ~(1ull << r); };
 
     // per-lane node view (pass ps)
     int32_t gml[kGmax];

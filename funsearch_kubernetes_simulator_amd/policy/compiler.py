@@ -207,9 +207,31 @@ class Compiler:
             self.emit(Op.CONST, flag, imm=self.const(0))
         self.block(fn.body)
         self.emit(Op.END)
+        self._renumber_registers()
         nregs = max((c[1] for c in self.code if c[1] != NO_REG), default=0) + 1
         return CompiledPolicy(b"".join(pack_insn(*c) for c in self.code), self.fconst, self.iconst,
                               self.ctag, nregs, self.source, frozenset(self.features))
+
+    #: ops whose `imm` field names a register (or NO_REG)
+    _IMM_REG_OPS = (Op.GLIST_SLICE, Op.GLIST_INSERT)
+
+    def _renumber_registers(self) -> None:
+        """Renumber virtual registers by static use count (most used -> 0).
+
+        The device VM keeps the lowest-numbered registers in VGPRs and the
+        rest in LDS, so hot temporaries and loop variables get the fast file.
+        A pure renaming: both VMs execute the same instructions."""
+        from collections import Counter
+        uses: Counter = Counter()
+        for op, d, a, b, imm in self.code:
+            for r in (d, a, b) + ((imm,) if op in self._IMM_REG_OPS else ()):
+                if r != NO_REG:
+                    uses[r] += 1
+        order = sorted(uses, key=lambda r: (-uses[r], r))
+        perm = {r: i for i, r in enumerate(order)}
+        m = lambda r: NO_REG if r == NO_REG else perm[r]
+        self.code = [(op, m(d), m(a), m(b), m(imm) if op in self._IMM_REG_OPS else imm)
+                     for op, d, a, b, imm in self.code]
 
     def _fold_constant(self, node: ast.AST):
         """Module-level ``NAME = <numeric literal expression>``."""

@@ -75,3 +75,13 @@ def test_async_slots_match_sync(dev, default_workload):
     assert np.array_equal(ta, dev.evaluate_builtin("composite_linear", a))
     assert np.array_equal(tb, dev.evaluate_builtin("random_linear", b))
     assert dev.ready(1) and dev.ready(2)
+
+
+@pytest.mark.parametrize("top", [0, 63, 1023, 2047])
+def test_hbm_heap_with_lds_top_matches_cpu(default_workload, top):
+    """Heap slots split between LDS (top levels) and HBM give the CPU oracle's tables."""
+    from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
+    dev = he.DeviceEvaluator(default_workload, options={"heap_mode": "hbm", "heap_top": top})
+    w = fam.sample_composite_linear(64, np.random.default_rng(top))
+    assert np.array_equal(dev.evaluate_builtin("composite_linear", w),
+                          ce.simulate_builtin_batch(default_workload, "composite_linear", w))
