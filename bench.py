@@ -53,6 +53,10 @@ def main() -> None:
     ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"])
     ap.add_argument("--heap-mode", default="auto", choices=["auto", "lds", "hbm"])
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--trace", default="default", choices=["default", "synthetic"],
+                    help="default: 8,152-pod OpenB trace on 16 nodes; synthetic: BASELINE config 5 shape")
+    ap.add_argument("--nodes", type=int, default=256, help="synthetic trace: nodes")
+    ap.add_argument("--pods", type=int, default=65536, help="synthetic trace: pods")
     ap.add_argument("--sync-islands", action="store_true",
                     help="one launch per generation for all islands (default: one HIP stream per island)")
     ap.add_argument("--save-best", default="", help="write the champion program (reference results-JSON schema)")
@@ -68,7 +72,11 @@ def main() -> None:
     from funsearch_kubernetes_simulator_amd.engine import COLS, Evaluator
     from funsearch_kubernetes_simulator_amd.funsearch.param_islands import make_islands, migrate
 
-    workload = load_default_workload()
+    if args.trace == "synthetic":
+        from funsearch_kubernetes_simulator_amd.core import synthetic_workload
+        workload = synthetic_workload(n_nodes=args.nodes, n_pods=args.pods, seed=0)
+    else:
+        workload = load_default_workload()
     device = ctx.local_rank if args.device == "gpu" else "cpu"
     ev = Evaluator(workload, device=device, options={"heap_mode": args.heap_mode}, n_slots=max(1, args.islands))
     if args.device == "gpu" and ev.device is None:
@@ -178,8 +186,11 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_EVALS_PER_S, 2),
             "dtype": "fp64",
-            "data": "OpenB openb_pod_list_default.csv (8,152 pods) on gpu_models_filtered.csv (16 nodes/64 GPUs); "
-                    f"random-weight candidate policies ({args.family} family, random init)",
+            "data": ("OpenB openb_pod_list_default.csv (8,152 pods) on gpu_models_filtered.csv (16 nodes/64 GPUs)"
+                     if args.trace == "default" else
+                     f"synthetic scaled trace {workload.pods.n_pods} pods / {workload.cluster.n_nodes} nodes "
+                     "(BASELINE config 5 shape, tiled OpenB rows)")
+                    + f"; random-weight candidate policies ({args.family} family, random init)",
             "config": {
                 "model": f"{args.family} policy family, exact replay (reference-bit-identical scores)",
                 "global_batch": per_step * ctx.world_size,

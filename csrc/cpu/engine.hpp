@@ -158,6 +158,34 @@ inline bool feasible(const ScoreCtx& c, int n) {
   return true;
 }
 
+// Resource-accounting invariants (reference `_validate_cluster_invariants`,
+// simulator/main.py:201-272): every node's and GPU's remaining capacity is in
+// [0, total] and equals total minus what the pods with a pending DELETION
+// event (placed, not yet finished) hold.
+inline bool invariants_hold(const Workload& w, const ClusterState& st, const std::vector<HeapItem>& heap,
+                            const std::vector<int32_t>& assigned, const std::vector<int32_t>& assigned_gpus,
+                            const std::vector<int32_t>& gpu_off) {
+  const int N = w.n_nodes;
+  std::vector<int64_t> ucpu(N, 0), umem(N, 0), ugpu(N, 0), ugm(w.n_gpus, 0);
+  for (const HeapItem& it : heap) {
+    if (it.kind != 1) continue;
+    const int p = it.pod, n = assigned[p];
+    if (n < 0 || n >= N) return false;
+    ucpu[n] += w.pcpu[p]; umem[n] += w.pmem[p]; ugpu[n] += w.pngpu[p];
+    for (int k = gpu_off[p]; k < gpu_off[p + 1]; ++k) ugm[w.gpu_start[n] + assigned_gpus[k]] += w.pgmilli[p];
+  }
+  for (int n = 0; n < N; ++n) {
+    if (st.cpu_left[n] < 0 || st.cpu_left[n] > w.cpu_total[n] || ucpu[n] + st.cpu_left[n] != w.cpu_total[n]) return false;
+    if (st.mem_left[n] < 0 || st.mem_left[n] > w.mem_total[n] || umem[n] + st.mem_left[n] != w.mem_total[n]) return false;
+    if (st.gpu_left[n] < 0 || st.gpu_left[n] > w.ngpus[n] || ugpu[n] + st.gpu_left[n] != w.ngpus[n]) return false;
+  }
+  for (int g = 0; g < w.n_gpus; ++g)
+    if (st.gmilli_left[g] < 0 || st.gmilli_left[g] > w.gmilli_total[g] ||
+        ugm[g] + st.gmilli_left[g] != w.gmilli_total[g])
+      return false;
+  return true;
+}
+
 template <class Scorer>
 SimResult simulate(const Workload& w, Scorer& scorer, const SimOptions& opt) {
   SimResult res;
@@ -238,6 +266,14 @@ SimResult simulate(const Workload& w, Scorer& scorer, const SimOptions& opt) {
           }
         }
         if (py_gt(s, best)) { best = s; best_node = n; }
+      }
+      if (opt.record_states) {
+        res.states.push_back(p);
+        res.states.push_back(best_node);
+        res.states.insert(res.states.end(), st.cpu_left.begin(), st.cpu_left.end());
+        res.states.insert(res.states.end(), st.mem_left.begin(), st.mem_left.end());
+        res.states.insert(res.states.end(), st.gpu_left.begin(), st.gpu_left.end());
+        res.states.insert(res.states.end(), st.gmilli_left.begin(), st.gmilli_left.end());
       }
       if (best_node < 0) {
         // ---- failed placement
@@ -330,6 +366,15 @@ SimResult simulate(const Workload& w, Scorer& scorer, const SimOptions& opt) {
       active += (st.cpu_left[n] < w.cpu_total[n] || st.mem_left[n] < w.mem_total[n] ||
                  st.gpu_left[n] < w.ngpus[n]);
     if (active > res.max_nodes) res.max_nodes = active;
+    if (opt.check_invariants > 0 && processed % opt.check_invariants == 0 &&
+        !invariants_hold(w, st, heap, assigned, assigned_gpus, gpu_off)) {
+      res.exc = EXC_INVARIANT;
+      return res;
+    }
+  }
+  if (opt.check_invariants > 0 && !invariants_hold(w, st, heap, assigned, assigned_gpus, gpu_off)) {
+    res.exc = EXC_INVARIANT;
+    return res;
   }
 
   res.n_events = processed;

@@ -1,6 +1,7 @@
 // pybind11 bindings of the native CPU oracle engine (_fks_cpu).
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+#include <cstring>
 #include <pybind11/stl.h>
 
 #include <atomic>
@@ -57,12 +58,14 @@ SimOptions make_options(const py::dict& o) {
   if (o.contains("budget")) s.budget = o["budget"].cast<int64_t>();
   if (o.contains("record_values")) s.record_values = o["record_values"].cast<bool>();
   if (o.contains("record_placements")) s.record_placements = o["record_placements"].cast<bool>();
+  if (o.contains("check_invariants")) s.check_invariants = o["check_invariants"].cast<int64_t>();
+  if (o.contains("record_states")) s.record_states = o["record_states"].cast<bool>();
   return s;
 }
 
 py::dict to_dict(const SimResult& r) {
   py::dict d;
-  d["exc"] = r.exc; d["score"] = r.score;
+  d["exc"] = r.exc; d["score"] = r.score; d["vm_insns"] = r.vm_insns;
   d["avg_cpu"] = r.avg_cpu; d["avg_mem"] = r.avg_mem;
   d["avg_gpu_count"] = r.avg_gpu_count; d["avg_gpu_milli"] = r.avg_gpu_milli; d["frag"] = r.frag;
   d["n_snapshots"] = r.n_snapshots; d["n_frag_events"] = r.n_frag_events; d["n_events"] = r.n_events;
@@ -71,6 +74,11 @@ py::dict to_dict(const SimResult& r) {
   if (!r.snap_values.empty()) d["snap_values"] = r.snap_values;
   if (!r.frag_values.empty()) d["frag_values"] = r.frag_values;
   if (!r.placement.empty()) d["placement"] = r.placement;
+  if (!r.states.empty()) {
+    py::array_t<int32_t> a((py::ssize_t)r.states.size());
+    std::memcpy(a.mutable_data(), r.states.data(), r.states.size() * 4);
+    d["states"] = a;
+  }
   return d;
 }
 
@@ -137,7 +145,13 @@ PYBIND11_MODULE(_fks_cpu, m) {
     Program prog = make_program(code, fconst, iconst, ctag);
     SimOptions o = make_options(opts);
     SimResult r;
-    { py::gil_scoped_release rel; VmScorer sc(prog, o.budget); r = simulate(w, sc, o); if (r.exc == EXC_NONE && sc.exc) r.exc = sc.exc; }
+    {
+      py::gil_scoped_release rel;
+      VmScorer sc(prog, o.budget);
+      r = simulate(w, sc, o);
+      if (r.exc == EXC_NONE && sc.exc) r.exc = sc.exc;
+      r.vm_insns = sc.insns;
+    }
     return to_dict(r);
   }, py::arg("workload"), py::arg("code"), py::arg("fconst"), py::arg("iconst"), py::arg("ctag"), py::arg("options") = py::dict());
 

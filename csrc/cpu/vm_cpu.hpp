@@ -91,6 +91,7 @@ struct VmCore {
   std::vector<uint8_t> has_result;
 
   VmCore(const Program& p, int64_t b) : P(p), budget(b), limited(b > 0) {}
+  int64_t executed = 0;   // instructions dispatched (one per wave-uniform step)
 
   void resize(int lanes) {
     L = lanes;
@@ -136,6 +137,7 @@ struct VmCore {
     int pc = 0;
     for (;;) {
       if (limited && --budget < 0) { exc = EXC_BUDGET; return false; }
+      ++executed;
       const Insn in = code[pc];
       switch (in.op) {
         case OP_NOP: break;
@@ -415,6 +417,7 @@ struct VmScorer {
   std::vector<PyNum> res;
   std::vector<uint8_t> has;
   VmScorer(const Program& p, int64_t budget) : prog(p), budget_total(budget), budget_left(budget) {}
+  int64_t insns = 0;   // VM instructions executed over the replay
 
   ScoreOut operator()(const ScoreCtx& c, int n) {
     ScoreOut o;
@@ -432,6 +435,7 @@ struct VmScorer {
       W.gmilli_left = c.s.gmilli_left.data(); W.gmilli_total = w.gmilli_total.data();
       W.gmem_left = w.gmem_left0.data(); W.gmem_total = w.gmem_total.data();
       bool ok = vm.run(W);
+      insns += vm.executed;
       if (!ok) { o.exc = vm.exc; exc = vm.exc; return o; }
       res = vm.result; has = vm.has_result;
       cached_pod = c.pod; cached_time = c.pod_ctime;

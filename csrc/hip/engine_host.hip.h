@@ -177,6 +177,11 @@ class DeviceEngine {
     if (o.contains("snapshot_interval")) W_.snapshot_interval = o["snapshot_interval"].cast<double>();
     if (o.contains("budget")) budget_ = o["budget"].cast<int64_t>();
     if (o.contains("heap_top")) heap_top_opt_ = o["heap_top"].cast<int>();   // -1: auto
+    if (o.contains("check_invariants")) {
+      const int64_t k = o["check_invariants"].cast<int64_t>();
+      W_.check_every = (int32_t)std::max<int64_t>(0, std::min<int64_t>(k, INT32_MAX));
+      W_.inv_words = W_.check_every > 0 ? inv_words_for(npass_) : 0;
+    }
     if (o.contains("heap_mode")) {
       const std::string m = o["heap_mode"].cast<std::string>();
       if (m != "auto" && m != "lds" && m != "hbm") throw std::invalid_argument("heap_mode: auto | lds | hbm");
@@ -347,7 +352,7 @@ class DeviceEngine {
   }
 
   bool use_gheap(int P) const {
-    if (!lds_heap_ok_) return true;
+    if (!lds_heap_ok_ || lds_bytes(false, 0, 0) > kMaxLds) return true;
     if (heap_mode_ == "hbm") return true;
     if (heap_mode_ == "lds") return false;
     // auto: the HBM heap wins once the batch exceeds what the LDS heap can
@@ -357,7 +362,8 @@ class DeviceEngine {
 
   size_t lds_bytes(bool g, int top, int nregs) const {
     const size_t vregs = (size_t)nregs * 64 * 8;
-    return g ? delmap_bytes_ + (size_t)top * 8 + vregs : heap_bytes_ + delmap_bytes_ + vregs;
+    const size_t inv = (size_t)W_.inv_words * 8;
+    return inv + (g ? delmap_bytes_ + (size_t)top * 8 + vregs : heap_bytes_ + delmap_bytes_ + vregs);
   }
 
   // HBM-heap launches keep the top 2^L - 1 heap slots in LDS, as many levels as
@@ -365,8 +371,9 @@ class DeviceEngine {
   int heap_top_for(int nregs, bool vm) const {
     const int entries = (int)(heap_bytes_ / 8);
     if (heap_top_opt_ >= 0) return std::min(heap_top_opt_, entries);
-    const size_t budget = kMaxLds / (vm ? kVmPoliciesPerCu : kPoliciesPerCu);
-    const size_t fixed = delmap_bytes_ + (size_t)nregs * 64 * 8;
+    const size_t per_cu = vm ? kVmPoliciesPerCu : (npass_ >= 4 ? 8 : npass_ == 2 ? 12 : kPoliciesPerCu);
+    const size_t budget = kMaxLds / per_cu;
+    const size_t fixed = delmap_bytes_ + (size_t)nregs * 64 * 8 + (size_t)W_.inv_words * 8;
     int T = 0;
     while (T < entries && fixed + (size_t)(2 * T + 1) * 8 <= budget) T = 2 * T + 1;
     return std::min(T, entries);
@@ -451,6 +458,7 @@ class DeviceEngine {
     const bool g = use_gheap(P);
     const DevWorkload Wl = launch_workload(g, 0, false);
     const size_t lds = lds_bytes(g, Wl.heap_top, 0);
+    if (lds > kMaxLds) throw std::invalid_argument("replay layout exceeds the 160 KiB LDS");
     uint64_t* gh = g ? gheap_for(s, P) : nullptr;
     const fksk::BuiltinArgs a{Wl, upload_workload(s, Wl), s.fam.as<int32_t>(), s.w.as<double>(),
                               s.res.as<DevResult>(), gh, nullptr};

@@ -178,6 +178,53 @@ py::tuple test_heap(py::array_t<uint64_t, py::array::c_style | py::array::forcec
   return py::make_tuple(out, popped);
 }
 
+// Surrogate screening on one device (ops/screening.py): X [S*Np, KP], Wt [KP, Ppad],
+// R [S*Np], Rfail [S] (float32) -> fit [Ppad].
+py::array_t<float> screen_linear(py::array_t<float, py::array::c_style | py::array::forcecast> X,
+                                 py::array_t<float, py::array::c_style | py::array::forcecast> Wt,
+                                 py::array_t<float, py::array::c_style | py::array::forcecast> R,
+                                 py::array_t<float, py::array::c_style | py::array::forcecast> Rfail, int Np,
+                                 int device) {
+  if (X.ndim() != 2 || Wt.ndim() != 2 || X.shape(1) != Wt.shape(0)) throw std::invalid_argument("X [M,K] / Wt [K,P]");
+  const int KP = (int)X.shape(1), Ppad = (int)Wt.shape(1);
+  const int64_t M = X.shape(0);
+  if (Np <= 0 || M % Np != 0 || R.size() != M) throw std::invalid_argument("R must have S*Np entries");
+  const int S = (int)(M / Np);
+  if (Rfail.size() != S) throw std::invalid_argument("Rfail must have S entries");
+  HIP_OK(hipSetDevice(device));
+  float *dX, *dW, *dR, *dF, *dfit;
+  HIP_OK(hipMalloc(&dX, X.size() * 4));
+  HIP_OK(hipMalloc(&dW, Wt.size() * 4));
+  HIP_OK(hipMalloc(&dR, R.size() * 4));
+  HIP_OK(hipMalloc(&dF, Rfail.size() * 4 + 4));
+  HIP_OK(hipMalloc(&dfit, (size_t)Ppad * 4));
+  HIP_OK(hipMemcpy(dX, X.data(), X.size() * 4, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(dW, Wt.data(), Wt.size() * 4, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(dR, R.data(), R.size() * 4, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(dF, Rfail.data(), Rfail.size() * 4, hipMemcpyHostToDevice));
+  HIP_OK(hipMemset(dfit, 0, (size_t)Ppad * 4));
+  {
+    py::gil_scoped_release rel;
+    HIP_OK(fksk::launch_screen_linear(dX, dW, dR, dF, S, Np, KP, Ppad, dfit, nullptr));
+    HIP_OK(hipDeviceSynchronize());
+  }
+  py::array_t<float> out(Ppad);
+  HIP_OK(hipMemcpy(out.mutable_data(), dfit, (size_t)Ppad * 4, hipMemcpyDeviceToHost));
+  for (void* p : {(void*)dX, (void*)dW, (void*)dR, (void*)dF, (void*)dfit}) (void)hipFree(p);
+  return out;
+}
+
+py::array_t<float> mfma_probe(int device) {
+  HIP_OK(hipSetDevice(device));
+  float* d;
+  HIP_OK(hipMalloc(&d, 64 * 16 * 4));
+  HIP_OK(fksk::launch_mfma_probe(d, nullptr));
+  py::array_t<float> out({64, 16});
+  HIP_OK(hipMemcpy(out.mutable_data(), d, 64 * 16 * 4, hipMemcpyDeviceToHost));
+  (void)hipFree(d);
+  return out;
+}
+
 int device_count() {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -191,6 +238,9 @@ PYBIND11_MODULE(_fks_hip, m) {
   m.def("device_count", &device_count);
   m.def("test_wave_ops", &test_wave_ops);
   m.def("test_heap", &test_heap);
+  m.def("screen_linear", &screen_linear, py::arg("X"), py::arg("Wt"), py::arg("R"), py::arg("Rfail"), py::arg("Np"),
+        py::arg("device") = 0);
+  m.def("mfma_probe", &mfma_probe, py::arg("device") = 0);
   py::class_<DeviceEngine>(m, "DeviceEngine")
       .def(py::init<py::dict, int, int>(), py::arg("workload"), py::arg("device") = 0, py::arg("n_slots") = 4)
       .def("set_options", &DeviceEngine::set_options)

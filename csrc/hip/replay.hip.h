@@ -35,7 +35,7 @@ constexpr int kFresh = 0, kRetry = 1, kDelete = 2;
 
 enum ExcCode : int32_t {
   EXC_NONE = 0, EXC_ZERO_DIVISION = 1, EXC_VALUE = 2, EXC_OVERFLOW = 3, EXC_TYPE = 4,
-  EXC_INDEX = 5, EXC_ALLOC = 6, EXC_NAME = 7, EXC_UNSUPPORTED = 100, EXC_BUDGET = 101,
+  EXC_INDEX = 5, EXC_ALLOC = 6, EXC_NAME = 7, EXC_UNSUPPORTED = 100, EXC_BUDGET = 101, EXC_INVARIANT = 102,
 };
 
 struct DevWorkload {
@@ -61,6 +61,8 @@ struct DevWorkload {
   double thr_after_fire;      // threshold value after the last precomputed snapshot
   int32_t repush_earliest, first_fit_alloc, truncate;
   int32_t heap_top;           // heap slots kept in LDS when the heap lives in HBM
+  int32_t check_every;        // k_check_invariants cadence in events (0: off)
+  int32_t inv_words;          // LDS u64 words reserved for the invariant check (0: off)
 };
 
 struct DevResult {
@@ -160,9 +162,62 @@ __device__ __forceinline__ int pick_gpus(const NodeRegs<NPASS>& nr, int ps, int 
 }
 
 // ----------------------------------------------------------------------------
+// Debug check (the reference's `_validate_cluster_invariants`,
+// simulator/main.py:201-272): every node's / GPU's remaining capacity lies in
+// [0, total] and equals total minus what the pods with a pending DELETION in
+// the heap hold.  Per-node "used" sums are built with LDS atomics from the
+// heap's deletion keys (node, GPU mask and pod rank are packed in the key).
+constexpr int kInvCols = 3 + kGmax;   // cpu, mem, gpu count, per-GPU milli
+__host__ __device__ inline int inv_words_for(int npass) { return (kWave * npass * kInvCols * 4 + 7) / 8; }
+
+template <int NPASS>
+__device__ bool invariants_hold(const DevWorkload& W, const WaveHeap& heap, int n, const NodeRegs<NPASS>& nr,
+                                int32_t* inv, int lane) {
+  for (int i = lane; i < kWave * NPASS * kInvCols; i += kWave) inv[i] = 0;
+  __syncthreads();
+  const int lb = W.low_bits, nb = W.node_bits, rb = W.rank_bits;
+  for (int i = lane; i < n; i += kWave) {
+    const uint64_t k = heap.ld(i);
+    if ((int)(k & 3) != kDelete) continue;
+    const int node = (int)((k >> 2) & ((1u << nb) - 1));
+    const int mask = (int)((k >> (2 + nb)) & 0xFF);
+    const int rank = (int)((k >> lb) & ((1ull << rb) - 1));
+    const int4 pr = W.pod[rank];
+    int32_t* row = inv + node * kInvCols;
+    atomicAdd(&row[0], pr.x);
+    atomicAdd(&row[1], pr.y);
+    atomicAdd(&row[2], (pr.w >> 16) & 0xFF);
+#pragma unroll
+    for (int j = 0; j < kGmax; ++j)
+      if ((mask >> j) & 1) atomicAdd(&row[3 + j], pr.w & 0xFFFF);
+  }
+  __syncthreads();
+  bool bad = false;
+#pragma unroll
+  for (int ps = 0; ps < NPASS; ++ps) {
+    const int node = ps * kWave + lane;
+    if (node >= W.n_nodes) continue;
+    const int32_t* row = inv + node * kInvCols;
+    const int32_t cl = nr.cpu_left[ps], ml = nr.mem_left[ps], gl = nr.gpu_left[ps];
+    bad |= cl < 0 || cl > nr.cpu_total[ps] || row[0] + cl != nr.cpu_total[ps];
+    bad |= ml < 0 || ml > nr.mem_total[ps] || row[1] + ml != nr.mem_total[ps];
+    bad |= gl < 0 || gl > nr.ngpus[ps] || row[2] + gl != nr.ngpus[ps];
+#pragma unroll
+    for (int j = 0; j < kGmax; ++j)
+      if (j < nr.ngpus[ps]) {
+        const int32_t l = nr.gml[ps][j], t = nr.gmt[ps][j];
+        bad |= l < 0 || l > t || row[3 + j] + l != t;
+      }
+  }
+  __syncthreads();
+  return ballot(bad) == 0;
+}
+
+// ----------------------------------------------------------------------------
 template <int NPASS, class Scorer, class Prof = NoProf>
 __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Scorer& scorer, uint64_t* hbuf,
-                           uint64_t* htop, int T, uint32_t* delmap, DevResult* out, uint64_t* prof_out = nullptr) {
+                           uint64_t* htop, int T, uint32_t* delmap, int32_t* inv, DevResult* out,
+                           uint64_t* prof_out = nullptr) {
   // W: the kernel-argument copy (hot fields, kept in SGPRs); Wcold: the same
   // struct in global memory for the fields only snapshots / failures / commits
   // of multi-GPU pods need.  Its address is made opaque once per event so the
@@ -411,6 +466,11 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
       next_fire = ksnap < n_fire ? Wc->snap_fire[ksnap] : INT64_MAX;
     }
     // (the reference's max_nodes counter feeds no metric: not tracked)
+    if (W.check_every > 0 && (processed % W.check_every == 0 || n == 0) &&
+        !invariants_hold<NPASS>(W, heap, n, nr, inv, lane)) {
+      exc = EXC_INVARIANT;
+      break;
+    }
     prof.mark(PH_EVAL);
   }
   if (prof_out) prof.flush(prof_out);

@@ -33,12 +33,15 @@ struct Slot {
   int T;
   uint32_t* delmap;
   uint64_t* vregs;
+  int32_t* inv;   // invariant-check scratch (debug; nullptr when off)
 };
 template <bool GHEAP>
 __device__ __forceinline__ Slot policy_slot(const DevWorkload& W, uint64_t* gheap, int p) {
-  extern __shared__ uint64_t lds[];
+  extern __shared__ uint64_t lds_raw[];
+  uint64_t* lds = lds_raw + W.inv_words;   // [invariant scratch | policy layout]
   const int N = W.n_pods;
   Slot s;
+  s.inv = W.inv_words > 0 ? reinterpret_cast<int32_t*>(lds_raw) : nullptr;
   if (GHEAP) {
     s.h = gheap + (size_t)p * lds_heap_entries(N);
     s.delmap = reinterpret_cast<uint32_t*>(lds);
@@ -69,14 +72,17 @@ hipError_t raise_lds(T* f, int max_lds) {
 #if FKS_KIND == 0
 // the feature families carry ~40 more live values through scoring: 3 waves/SIMD
 // without spills beats 4 with scratch traffic
-#define FKS_FAM_BOUNDS(G, F) __launch_bounds__(64, (G) ? (((F) == 3 || (F) == 4 || (F) < 0) ? 3 : 4) : 1)
+// without spills beats 4 with scratch traffic; 128 / 256 nodes (NPASS 2 / 4)
+// hold 2 / 4 node slots per lane: 3 / 2 waves per SIMD.
+#define FKS_FAM_BOUNDS(G, F, NP) \
+  __launch_bounds__(64, !(G) ? 1 : (NP) >= 4 ? 2 : (NP) == 2 ? 3 : (((F) == 3 || (F) == 4 || (F) < 0) ? 3 : 4))
 template <int NPASS, bool GHEAP, int FAM>
-__global__ FKS_FAM_BOUNDS(GHEAP, FAM) void k_replay_builtin(fksk::BuiltinArgs a) {
+__global__ FKS_FAM_BOUNDS(GHEAP, FAM, NPASS) void k_replay_builtin(fksk::BuiltinArgs a) {
   const int p = blockIdx.x;
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   BuiltinScorerDev<FAM> sc;
   sc.load(a.fam[p], a.weights + (size_t)p * kWeights);
-  replay_one<NPASS>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, a.out + p);
+  replay_one<NPASS>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p);
 }
 
 template <int NPASS, bool GHEAP>
@@ -116,7 +122,7 @@ __global__ FKS_VM_BOUNDS(GHEAP) void k_replay_vm(fksk::VmArgs a) {
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   VmScorerDev sc;
   sc.init(a.T, p, a.W, a.budget, s.vregs);
-  replay_one<NPASS>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, a.out + p);
+  replay_one<NPASS>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p);
 }
 #endif
 
@@ -127,7 +133,7 @@ __global__ FKS_BOUNDS(GHEAP) void k_replay_builtin_prof(fksk::BuiltinArgs a) {
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   BuiltinScorerDev<-1> sc;
   sc.load(a.fam[p], a.weights + (size_t)p * kWeights);
-  replay_one<1, BuiltinScorerDev<-1>, PhaseProf>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, a.out + p,
+  replay_one<1, BuiltinScorerDev<-1>, PhaseProf>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p,
                                                  a.prof + (size_t)p * 8);
 }
 
@@ -137,7 +143,7 @@ __global__ FKS_VM_BOUNDS(GHEAP) void k_replay_vm_prof(fksk::VmArgs a) {
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   VmScorerDev sc;
   sc.init(a.T, p, a.W, a.budget, s.vregs);
-  replay_one<1, VmScorerDev, PhaseProf>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, a.out + p, a.prof + (size_t)p * 8);
+  replay_one<1, VmScorerDev, PhaseProf>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p, a.prof + (size_t)p * 8);
 }
 #endif
 

@@ -50,13 +50,8 @@ __device__ __forceinline__ bool truthy(const PyN& x) { return x.fl ? (__longlong
 constexpr double kTwo63d = 9223372036854775808.0;
 constexpr int64_t kTwo53i = (int64_t)1 << 53;
 
-__device__ inline int d_cmp(const PyN& a, const PyN& b) {
-  if (!a.fl && !b.fl) return a.b < b.b ? -1 : (a.b > b.b ? 1 : 0);
-  if (a.fl && b.fl) {
-    const double x = __longlong_as_double(a.b), y = __longlong_as_double(b.b);
-    if (isnan(x) || isnan(y)) return 2;
-    return x < y ? -1 : (x > y ? 1 : 0);
-  }
+// int-vs-float comparison (exact, CPython float_richcompare): out of line
+__device__ __noinline__ int d_cmp_mixed(const PyN& a, const PyN& b) {
   const bool swap = !a.fl;
   const double x = __longlong_as_double(swap ? b.b : a.b);
   const int64_t y = swap ? a.b : b.b;
@@ -74,9 +69,19 @@ __device__ inline int d_cmp(const PyN& a, const PyN& b) {
   return swap ? -c : c;
 }
 
+__device__ __forceinline__ int d_cmp(const PyN& a, const PyN& b) {
+  if (!a.fl && !b.fl) return a.b < b.b ? -1 : (a.b > b.b ? 1 : 0);
+  if (a.fl && b.fl) {
+    const double x = __longlong_as_double(a.b), y = __longlong_as_double(b.b);
+    if (isnan(x) || isnan(y)) return 2;
+    return x < y ? -1 : (x > y ? 1 : 0);
+  }
+  return d_cmp_mixed(a, b);
+}
+
 __device__ __forceinline__ bool dbl_odd_int(double x) { return fmod(fabs(x), 2.0) == 1.0; }
 
-__device__ inline int d_float_pow(double iv, double iw, PyN& r) {
+__device__ __noinline__ int d_float_pow(double iv, double iw, PyN& r) {
   if (iw == 0.0) { r = pf(1.0); return EXC_NONE; }
   if (isnan(iv)) { r = pf(iv); return EXC_NONE; }
   if (isnan(iw)) { r = pf(iv == 1.0 ? 1.0 : iw); return EXC_NONE; }
@@ -114,7 +119,11 @@ __device__ inline int d_float_pow(double iv, double iw, PyN& r) {
   return EXC_NONE;
 }
 
-__device__ inline int d_binop(int op, const PyN& a, const PyN& b, PyN& r) {
+// Full Python binary-operator semantics.  The interpreter inlines the common
+// cases (int/int and float add, sub, mul, true division) and calls this out
+// of line for the rest, which keeps the dispatch loop small enough for the
+// instruction cache.
+__device__ __noinline__ int d_binop(int op, const PyN& a, const PyN& b, PyN& r) {
   const bool ii = !a.fl && !b.fl;
   switch (op) {
     case OP_ADD: {
@@ -243,7 +252,7 @@ __device__ inline int d_binop(int op, const PyN& a, const PyN& b, PyN& r) {
   return EXC_UNSUPPORTED;
 }
 
-__device__ inline int d_unop(int op, const PyN& a, PyN& r) {
+__device__ __noinline__ int d_unop(int op, const PyN& a, PyN& r) {
   switch (op) {
     case OP_NEG:
       if (a.fl) { r = pf(-__longlong_as_double(a.b)); return EXC_NONE; }
@@ -374,9 +383,12 @@ struct VmScorerDev {
 
     int pc = 0;
     int64_t budget = budget_call;   // runaway programs end here, so every wave drains
+    const uint64_t* cp = reinterpret_cast<const uint64_t*>(uniu64(reinterpret_cast<uint64_t>(code)));
+    uint64_t nxt = cp[0];
     for (;;) {
       if (limited && --budget < 0) { exc = EXC_BUDGET; return 0; }
-      const uint64_t in = code[pc];
+      const uint64_t in = nxt;
+      nxt = cp[pc + 1];   // prefetch the fall-through instruction while this one executes
       const int op = uni((int)(in & 0xFF));
       const int d = uni((int)((in >> 8) & 0xFF));
       const int a = uni((int)((in >> 16) & 0xFF));
@@ -500,8 +512,35 @@ struct VmScorerDev {
             put_raw(d, (nb << 4) | (n + 1));
           }
           break;
-        case OP_ADD: case OP_SUB: case OP_MUL: case OP_TDIV: case OP_FDIV: case OP_MOD: case OP_POW:
-        case OP_LOGB: case OP_MPOW:
+        case OP_ADD: case OP_SUB: case OP_MUL:
+          if (act) {
+            const PyN x = get(a), y = get(b);
+            PyN r;
+            if (!x.fl && !y.fl) {
+              int64_t v;
+              const bool ovf = op == OP_ADD ? __builtin_add_overflow(x.b, y.b, &v)
+                             : op == OP_SUB ? __builtin_sub_overflow(x.b, y.b, &v)
+                                            : __builtin_mul_overflow(x.b, y.b, &v);
+              if (ovf) { lexc = EXC_UNSUPPORTED; st |= kDone; break; }   // bigint: host decides
+              r = pi(v);
+            } else {
+              const double p = fv(x), q = fv(y);
+              r = pf(op == OP_ADD ? p + q : op == OP_SUB ? p - q : p * q);
+            }
+            put(d, r);
+          }
+          break;
+        case OP_TDIV:
+          if (act) {
+            const PyN x = get(a), y = get(b);
+            const bool big = !x.fl && !y.fl && (x.b > kTwo53i || x.b < -kTwo53i || y.b > kTwo53i || y.b < -kTwo53i);
+            const double q = fv(y);
+            if (q == 0.0) { lexc = EXC_ZERO_DIVISION; st |= kDone; break; }
+            if (big) { lexc = EXC_UNSUPPORTED; st |= kDone; break; }
+            put(d, pf(fv(x) / q));
+          }
+          break;
+        case OP_FDIV: case OP_MOD: case OP_POW: case OP_LOGB: case OP_MPOW:
           if (act) {
             PyN r;
             const int e = d_binop(op, get(a), get(b), r);
@@ -509,9 +548,20 @@ struct VmScorerDev {
             put(d, r);
           }
           break;
-        case OP_NEG: case OP_POS: case OP_NOT: case OP_TRUTH: case OP_ABS: case OP_INT: case OP_FLOAT:
-        case OP_ROUND: case OP_SQRT: case OP_LOG: case OP_EXP: case OP_SIN: case OP_COS: case OP_TAN:
+        case OP_NOT:
+          if (act) put(d, pi(truthy(get(a)) ? 0 : 1));
+          break;
+        case OP_TRUTH:
+          if (act) put(d, pi(truthy(get(a)) ? 1 : 0));
+          break;
         case OP_ISINT:
+          if (act) put(d, pi(get(a).fl ? 0 : 1));
+          break;
+        case OP_FLOAT:
+          if (act) put(d, pf(fv(get(a))));
+          break;
+        case OP_NEG: case OP_POS: case OP_ABS: case OP_INT: case OP_ROUND: case OP_SQRT: case OP_LOG: case OP_EXP:
+        case OP_SIN: case OP_COS: case OP_TAN:
           if (act) {
             PyN r;
             const int e = d_unop(op, get(a), r);
@@ -545,12 +595,12 @@ struct VmScorerDev {
         case OP_IF: {
           if (act) { if (!truthy(get(a))) off = 1; }
           else off += 1;
-          if (!ballot(off == 0 && st == 0)) { pc = imm; continue; }
+          if (!ballot(off == 0 && st == 0)) { pc = imm; nxt = cp[pc]; continue; }
           break;
         }
         case OP_ELSE:
           if (off == 1) off = 0; else if (off == 0) off = 1;
-          if (!ballot(off == 0 && st == 0)) { pc = imm; continue; }
+          if (!ballot(off == 0 && st == 0)) { pc = imm; nxt = cp[pc]; continue; }
           break;
         case OP_ENDIF:
           if (off > 0) off -= 1;
@@ -562,13 +612,14 @@ struct VmScorerDev {
           break;
         case OP_LOOP_TEST:
           if (act && !truthy(get(a))) st |= kBrk;
-          if (!ballot(off == 0 && st == 0)) { pc = imm; continue; }
+          if (!ballot(off == 0 && st == 0)) { pc = imm; nxt = cp[pc]; continue; }
           break;
         case OP_LOOP_CONT:
           st &= ~kCont;
           break;
         case OP_LOOP_NEXT:
           pc = imm;
+          nxt = cp[pc];
           continue;
         case OP_LOOP_EXIT: {
           if (off > 0) off -= 1;

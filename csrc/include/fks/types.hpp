@@ -25,7 +25,8 @@ enum ExcCode : int32_t {
   EXC_ALLOC = 6,           // ValueError from the GPU allocator (not enough GPUs)
   EXC_NAME = 7,            // NameError / UnboundLocalError
   EXC_UNSUPPORTED = 100,   // semantics outside the native subset (bigint, ...): re-run exactly on host
-  EXC_BUDGET = 101,        // instruction budget exhausted (runaway program)
+  EXC_BUDGET = 101,
+  EXC_INVARIANT = 102,     // resource accounting invariant violated (debug check)        // instruction budget exhausted (runaway program)
 };
 
 enum RepushMode : int32_t { REPUSH_FIRST = 0, REPUSH_EARLIEST = 1 };
@@ -52,6 +53,8 @@ struct SimOptions {
   int64_t budget = 0;            // VM instruction budget per priority evaluation (0 = unlimited)
   bool record_values = false;    // keep snapshot / frag values (exact fallback, tests)
   bool record_placements = false;
+  int64_t check_invariants = 0;  // verify resource accounting every K events and at the end (0 = off)
+  bool record_states = false;    // per creation event: pod + node/GPU state + decision (screening data)
 };
 
 struct SimResult {
@@ -60,11 +63,15 @@ struct SimResult {
   double avg_cpu = 0, avg_mem = 0, avg_gpu_count = 0, avg_gpu_milli = 0, frag = 0;
   int64_t n_snapshots = 0, n_frag_events = 0, n_events = 0, n_unplaced = 0;
   int64_t max_nodes = 0, n_repush = 0, n_dropped = 0;
+  int64_t vm_insns = 0;              // bytecode instructions executed (VM scorers)
   bool inexact = false;
   uint64_t trace_hash = 0;
   std::vector<double> snap_values;   // 4 per snapshot (record_values)
   std::vector<double> frag_values;   // record_values
   std::vector<int32_t> placement;    // node per pod (-1 never placed; record_placements)
+  // record_states: per creation event, [pod, chosen node (-1 failed), cpu_left[N],
+  // mem_left[N], gpu_left[N], gmilli_left[G]]
+  std::vector<int32_t> states;
 };
 
 // FNV-1a style mixing of the event stream; identical on host and device so a

@@ -77,6 +77,8 @@ class SimOptions:
     budget: int = DEFAULT_CALL_BUDGET  # VM instructions per priority evaluation (0 = unlimited)
     record_values: bool = False
     record_placements: bool = False
+    check_invariants: int = 0       # verify resource accounting every K events + at the end (debug)
+    record_states: bool = False     # per creation event: pod, decision, node/GPU state (screening data)
 
     def as_dict(self) -> dict:
         return dict(self.__dict__)

@@ -95,8 +95,8 @@ def prepare_device_workload(w: Workload, snapshot_interval: float = 0.05) -> Dic
         raise UnsupportedWorkload(f"more than {GMAX} GPUs on a node")
     if len(np.unique(p.pod_rank)) != P:
         raise UnsupportedWorkload("duplicate pod ids")
-    if P * 8 > LDS_BYTES_PER_CU - 4096:
-        raise UnsupportedWorkload("trace longer than the LDS-resident heap")
+    if P >= 2 ** 20:
+        raise UnsupportedWorkload("more than 2^20 pods (heap depth > 20 levels)")
     for name, arr in (("cpu", c.node_cpu_total), ("mem", c.node_mem_total), ("pcpu", p.pod_cpu),
                       ("pmem", p.pod_mem), ("dur", p.pod_dur), ("ctime", p.pod_ctime)):
         if arr.size and (arr.max() >= 2 ** 31 or arr.min() < -(2 ** 31)):

@@ -96,6 +96,7 @@ class Exc(enum.IntEnum):
     NAME = 7
     UNSUPPORTED = 100
     BUDGET = 101
+    INVARIANT = 102
 
 
 _INSN = struct.Struct("<BBBBi")

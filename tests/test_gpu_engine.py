@@ -85,3 +85,29 @@ def test_hbm_heap_with_lds_top_matches_cpu(default_workload, top):
     w = fam.sample_composite_linear(64, np.random.default_rng(top))
     assert np.array_equal(dev.evaluate_builtin("composite_linear", w),
                           ce.simulate_builtin_batch(default_workload, "composite_linear", w))
+
+
+@pytest.mark.parametrize("mode", ["lds", "hbm"])
+def test_device_invariant_checker(default_workload, mode):
+    """k_check_invariants: resource accounting holds on device replays and does not perturb them."""
+    from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
+    w = fam.sample_composite_linear(32, np.random.default_rng(3))
+    plain = he.DeviceEvaluator(default_workload, options={"heap_mode": mode}).evaluate_builtin("composite_linear", w)
+    dev = he.DeviceEvaluator(default_workload, options={"heap_mode": mode, "check_invariants": 61})
+    checked = dev.evaluate_builtin("composite_linear", w)
+    assert np.all(checked[:, 10] == 0)
+    assert np.array_equal(checked, plain)
+
+
+def test_scaled_synthetic_256_nodes_matches_cpu():
+    """Config-5 shape (256 nodes -> 4 node slots per lane, HBM heap): device == CPU oracle."""
+    from funsearch_kubernetes_simulator_amd.core import synthetic_workload
+    from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
+    w = synthetic_workload(n_nodes=256, n_pods=24000, seed=5)
+    dev = he.DeviceEvaluator(w)
+    assert dev.info()["npass"] == 4
+    for family in ("first_fit", "best_fit", "random_linear", "composite_linear"):
+        W = fam.SAMPLERS[family](48, np.random.default_rng(1)) if family in fam.SAMPLERS else None
+        gpu = dev.evaluate_builtin(family, W, n=48)
+        cpu = ce.simulate_builtin_batch(w, family, fam.pad_weights(W) if W is not None else np.zeros((48, 16)))
+        assert np.array_equal(gpu, cpu), family

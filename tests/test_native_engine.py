@@ -6,6 +6,7 @@ import numpy as np
 import pytest
 
 from funsearch_kubernetes_simulator_amd.core import load_default_workload
+from funsearch_kubernetes_simulator_amd.core.arrays import Workload
 from funsearch_kubernetes_simulator_amd.engine import Evaluator, object_engine_eval
 from funsearch_kubernetes_simulator_amd.models import families as fam
 from funsearch_kubernetes_simulator_amd.models.library import reference_policies, reference_scores
@@ -126,3 +127,16 @@ def test_exception_semantics(default_workload):
     assert res[3].score == 0 and res[3].exc == 0
     # no feasibility check: a GPU pod lands on a node without enough GPUs -> allocator raises
     assert res[4].score == 0 and res[4].exc == 6
+
+
+def test_invariant_checker_passes_and_is_transparent(default_workload):
+    """`check_invariants` (reference _validate_cluster_invariants) holds at every event of real replays."""
+    sub = Workload(default_workload.cluster, default_workload.pods.subset(np.arange(0, 1500)))
+    opts = ce.SimOptions(check_invariants=1)
+    for name in ("first_fit", "best_fit"):
+        a = ce.simulate_builtin(sub, name, options=opts)
+        b = ce.simulate_builtin(sub, name)
+        assert a["exc"] == 0 and a["score"] == b["score"] and a["trace_hash"] == b["trace_hash"]
+    prog = compile_policy(reference_policies()["funsearch_4901"])
+    a = ce.simulate_program(sub, prog, options=opts)
+    assert a["exc"] == 0 and a["score"] == ce.simulate_program(sub, prog)["score"]
