@@ -298,7 +298,7 @@ class DeviceEngine {
     uint64_t* gh = g ? gheap_for(s, P) : nullptr;
     const DevWorkload* wc = upload_workload(s, Wl);
     if (is_vm) {
-      const fksk::VmArgs a{Wl, wc, table(s), s.res.as<DevResult>(), budget_, gh, s.prof.as<uint64_t>()};
+      const fksk::VmArgs a{Wl, wc, table(s), s.res.as<DevResult>(), budget_, nregs, gh, s.prof.as<uint64_t>()};
       HIP_OK(fksk::launch_vm_prof(g, P, lds, s.stream, a));
     } else {
       const fksk::BuiltinArgs a{Wl, wc, s.fam.as<int32_t>(), s.w.as<double>(), s.res.as<DevResult>(), gh,
@@ -474,7 +474,7 @@ class DeviceEngine {
     const size_t lds = lds_bytes(g, Wl.heap_top, nregs);
     if (lds > kMaxLds) throw std::invalid_argument("heap + VM registers exceed the 160 KiB LDS");
     uint64_t* gh = g ? gheap_for(s, P) : nullptr;
-    const fksk::VmArgs a{Wl, upload_workload(s, Wl), table(s), s.res.as<DevResult>(), budget_, gh, nullptr};
+    const fksk::VmArgs a{Wl, upload_workload(s, Wl), table(s), s.res.as<DevResult>(), budget_, nregs, gh, nullptr};
     if (npass_ == 1) HIP_OK(fksk::launch_vm_np1(g, P, lds, s.stream, a));
     else if (npass_ == 2) HIP_OK(fksk::launch_vm_np2(g, P, lds, s.stream, a));
     else HIP_OK(fksk::launch_vm_np4(g, P, lds, s.stream, a));

@@ -32,6 +32,7 @@ struct VmArgs {
   DevProgramTable T;
   DevResult* out;
   int64_t budget;
+  int32_t nregs;          // max virtual registers over the batch's programs
   uint64_t* gheap;
   uint64_t* prof;
 };

@@ -51,7 +51,7 @@ constexpr double kTwo63d = 9223372036854775808.0;
 constexpr int64_t kTwo53i = (int64_t)1 << 53;
 
 // int-vs-float comparison (exact, CPython float_richcompare): out of line
-__device__ __noinline__ int d_cmp_mixed(const PyN& a, const PyN& b) {
+__device__ __noinline__ int d_cmp_mixed(PyN a, PyN b) {
   const bool swap = !a.fl;
   const double x = __longlong_as_double(swap ? b.b : a.b);
   const int64_t y = swap ? a.b : b.b;
@@ -123,7 +123,7 @@ __device__ __noinline__ int d_float_pow(double iv, double iw, PyN& r) {
 // cases (int/int and float add, sub, mul, true division) and calls this out
 // of line for the rest, which keeps the dispatch loop small enough for the
 // instruction cache.
-__device__ __noinline__ int d_binop(int op, const PyN& a, const PyN& b, PyN& r) {
+__device__ __forceinline__ int d_binop_impl(int op, const PyN& a, const PyN& b, PyN& r) {
   const bool ii = !a.fl && !b.fl;
   switch (op) {
     case OP_ADD: {
@@ -252,7 +252,7 @@ __device__ __noinline__ int d_binop(int op, const PyN& a, const PyN& b, PyN& r) 
   return EXC_UNSUPPORTED;
 }
 
-__device__ __noinline__ int d_unop(int op, const PyN& a, PyN& r) {
+__device__ __forceinline__ int d_unop_impl(int op, const PyN& a, PyN& r) {
   switch (op) {
     case OP_NEG:
       if (a.fl) { r = pf(-__longlong_as_double(a.b)); return EXC_NONE; }
@@ -318,14 +318,41 @@ __device__ __noinline__ int d_unop(int op, const PyN& a, PyN& r) {
   return EXC_UNSUPPORTED;
 }
 
+// Out-of-line entry points: arguments and results travel by value (registers),
+// so the interpreter's result slot never has to live in scratch memory.
+struct PyR {
+  int64_t b;
+  int32_t fl;
+  int32_t e;
+};
+__device__ __noinline__ PyR d_binop(int op, PyN a, PyN b) {
+  PyN r = pi(0);
+  const int e = d_binop_impl(op, a, b, r);
+  return PyR{r.b, r.fl ? 1 : 0, e};
+}
+__device__ __noinline__ PyR d_unop(int op, PyN a) {
+  PyN r = pi(0);
+  const int e = d_unop_impl(op, a, r);
+  return PyR{r.b, r.fl ? 1 : 0, e};
+}
+
 // ---- the interpreter ---------------------------------------------------------------
 constexpr uint32_t kBrk = 1, kCont = 2, kDone = 4;
-#ifndef FKS_VM_VGPR_REGS
-#define FKS_VM_VGPR_REGS 16
-#endif
-constexpr int kVgprRegs = FKS_VM_VGPR_REGS;   // virtual registers held in VGPRs
 
+// Scalar (SMEM) load of a wave-uniform 64-bit word.  The program table is
+// reached through a generic pointer, which the compiler would fetch with a
+// vector flat_load per instruction; the scalar cache path is much shorter.
+__device__ __forceinline__ uint64_t sload64(const uint64_t* p) {
+  uint64_t v;
+  asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  return v;
+}
+// The 16 most-used virtual registers (the compiler numbers them by use count)
+// live in VGPRs, the rest in LDS.  (A 32-register all-VGPR file measured
+// slower: 32-bit halves double the relative-addressing work and the extra
+// VGPRs cost spills; the interpreter is dispatch-bound, not register-bound.)
 struct VmScorerDev {
+  static constexpr int kVgprRegs = 16;
   const uint64_t* code;
   const int64_t* kpay;
   const uint8_t* ktag;
@@ -384,55 +411,62 @@ struct VmScorerDev {
     int pc = 0;
     int64_t budget = budget_call;   // runaway programs end here, so every wave drains
     const uint64_t* cp = reinterpret_cast<const uint64_t*>(uniu64(reinterpret_cast<uint64_t>(code)));
-    uint64_t nxt = cp[0];
     for (;;) {
       if (limited && --budget < 0) { exc = EXC_BUDGET; return 0; }
-      const uint64_t in = nxt;
-      nxt = cp[pc + 1];   // prefetch the fall-through instruction while this one executes
+      // pc is wave-uniform by construction; say so, so the fetch is a scalar load
+      pc = uni(pc);
+      const uint64_t in = sload64(cp + pc);
       const int op = uni((int)(in & 0xFF));
       const int d = uni((int)((in >> 8) & 0xFF));
       const int a = uni((int)((in >> 16) & 0xFF));
       const int b = uni((int)((in >> 24) & 0xFF));
       const int imm = uni((int)(in >> 32));
       const bool act = off == 0 && st == 0;
+      // Every case computes at most one result; it is written back once, after
+      // the switch (one write site keeps the VGPR register file from being
+      // copied along every arm).  wmode: 0 none, 1 active lanes, 2 all lanes.
+      PyN res = pi(0);
+      int wmode = 0;
+      int jump = -1;   // >= 0: uniform branch target
+      bool fin = false;
       switch (op) {
         case OP_NOP: break;
-        case OP_CONST: {
-          const PyN k{kpay[imm], ktag[imm] != 0};
-          if (act) put(d, k);
+        case OP_CONST:
+          res = PyN{kpay[imm], ktag[imm] != 0};
+          wmode = 1;
+          break;
+        case OP_MOV:
+          res = get(a);
+          wmode = 1;
+          break;
+        case OP_POD: {
+          int64_t v;
+          switch (imm) {
+            case 0: v = pod.cpu; break;
+            case 1: v = pod.mem; break;
+            case 2: v = pod.ngpu; break;
+            case 3: v = pod.gmilli; break;
+            case 4: v = pod.ctime; break;
+            default: v = pod.dur; break;
+          }
+          res = pi(v);
+          wmode = 1;
           break;
         }
-        case OP_MOV:
-          if (act) put(d, get(a));
-          break;
-        case OP_POD:
-          if (act) {
-            int64_t v;
-            switch (imm) {
-              case 0: v = pod.cpu; break;
-              case 1: v = pod.mem; break;
-              case 2: v = pod.ngpu; break;
-              case 3: v = pod.gmilli; break;
-              case 4: v = pod.ctime; break;
-              default: v = pod.dur; break;
-            }
-            put(d, pi(v));
+        case OP_NODE: {
+          int64_t v;
+          switch (imm) {
+            case 0: v = nr.cpu_left[ps]; break;
+            case 1: v = nr.cpu_total[ps]; break;
+            case 2: v = nr.mem_left[ps]; break;
+            case 3: v = nr.mem_total[ps]; break;
+            case 4: v = nr.gpu_left[ps]; break;
+            default: v = ngp; break;
           }
+          res = pi(v);
+          wmode = 1;
           break;
-        case OP_NODE:
-          if (act) {
-            int64_t v;
-            switch (imm) {
-              case 0: v = nr.cpu_left[ps]; break;
-              case 1: v = nr.cpu_total[ps]; break;
-              case 2: v = nr.mem_left[ps]; break;
-              case 3: v = nr.mem_total[ps]; break;
-              case 4: v = nr.gpu_left[ps]; break;
-              default: v = ngp; break;
-            }
-            put(d, pi(v));
-          }
-          break;
+        }
         case OP_GPU:
           if (act) {
             const int j = (int)(get(a).b & 0xF);
@@ -446,25 +480,29 @@ struct VmScorerDev {
             } else {
               v = gmem_total[node * kGmax + j];
             }
-            put(d, pi(v));
+            res = pi(v);
           }
+          wmode = 1;
           break;
         case OP_GLIST_ALL:
-          if (act) put_raw(d, (int64_t)ngp | ((int64_t)(0x76543210u & (uint32_t)((1ull << (4 * ngp)) - 1)) << 4));
+          res = pi((int64_t)ngp | ((int64_t)(0x76543210u & (uint32_t)((1ull << (4 * ngp)) - 1)) << 4));
+          wmode = 1;
           break;
         case OP_GLIST_LEN:
-          if (act) put(d, pi(get(a).b & 0xF));
+          res = pi(get(a).b & 0xF);
+          wmode = 1;
           break;
         case OP_GLIST_GET:
           if (act) {
             const PyN i = get(b);
             const int64_t lst = get(a).b;
             const int n = (int)(lst & 0xF);
-            if (i.fl) { lexc = EXC_TYPE; st |= kDone; break; }
             const int64_t k = i.b < 0 ? i.b + n : i.b;
-            if (k < 0 || k >= n) { lexc = EXC_INDEX; st |= kDone; break; }
-            put_raw(d, (lst >> (4 + 4 * k)) & 0xF);
+            if (i.fl) { lexc = EXC_TYPE; st |= kDone; }
+            else if (k < 0 || k >= n) { lexc = EXC_INDEX; st |= kDone; }
+            else res = pi((lst >> (4 + 4 * k)) & 0xF);
           }
+          wmode = 1;
           break;
         case OP_GLIST_SLICE:
           if (act) {
@@ -472,159 +510,173 @@ struct VmScorerDev {
             const int n = (int)(lst & 0xF);
             int64_t lo = 0, hi = n;
             bool bad = false;
-            if (b != kNoRegDev) { const PyN s = get(b); bad |= s.fl; lo = s.b; }
-            if (imm != kNoRegDev) { const PyN s = get(imm); bad |= s.fl; hi = s.b; }
-            if (bad) { lexc = EXC_TYPE; st |= kDone; break; }
-            if (lo < 0) { lo += n; if (lo < 0) lo = 0; } else if (lo > n) lo = n;
-            if (hi < 0) { hi += n; if (hi < 0) hi = 0; } else if (hi > n) hi = n;
-            int64_t outv = 0;
-            int m = 0;
-            for (int64_t k = lo; k < hi; ++k, ++m) outv |= ((lst >> (4 + 4 * k)) & 0xF) << (4 + 4 * m);
-            put_raw(d, outv | m);
+            if (b != kNoRegDev) { const PyN s_ = get(b); bad |= s_.fl; lo = s_.b; }
+            if (imm != kNoRegDev) { const PyN s_ = get(imm); bad |= s_.fl; hi = s_.b; }
+            if (bad) {
+              lexc = EXC_TYPE; st |= kDone;
+            } else {
+              if (lo < 0) { lo += n; if (lo < 0) lo = 0; } else if (lo > n) lo = n;
+              if (hi < 0) { hi += n; if (hi < 0) hi = 0; } else if (hi > n) hi = n;
+              int64_t outv = 0;
+              int m = 0;
+              for (int64_t k = lo; k < hi; ++k, ++m) outv |= ((lst >> (4 + 4 * k)) & 0xF) << (4 + 4 * m);
+              res = pi(outv | m);
+            }
           }
+          wmode = 1;
           break;
         case OP_GLIST_NEW:
-          if (act) put_raw(d, 0);
+          wmode = 1;
           break;
         case OP_GLIST_APPEND:
           if (act) {
             int64_t lst = get(a).b;
             const int n = (int)(lst & 0xF);
-            if (n >= 15) { lexc = EXC_UNSUPPORTED; st |= kDone; break; }
-            lst = (lst & ~(int64_t)0xF) | (n + 1);
-            lst |= (get(b).b & 0xF) << (4 + 4 * n);
-            put_raw(d, lst);
+            if (n >= 15) {
+              lexc = EXC_UNSUPPORTED; st |= kDone;
+            } else {
+              lst = (lst & ~(int64_t)0xF) | (n + 1);
+              lst |= (get(b).b & 0xF) << (4 + 4 * n);
+              res = pi(lst);
+            }
           }
+          wmode = 1;
           break;
         case OP_GLIST_INSERT:
           if (act) {
             const int64_t lst = get(a).b;
             const int n = (int)(lst & 0xF);
             const PyN ps_ = get(imm);
-            if (n >= 15) { lexc = EXC_UNSUPPORTED; st |= kDone; break; }
-            if (ps_.fl) { lexc = EXC_TYPE; st |= kDone; break; }
-            int64_t pos = ps_.b;
-            if (pos < 0) { pos += n; if (pos < 0) pos = 0; } else if (pos > n) pos = n;
-            const int64_t item = get(b).b & 0xF;
-            const int64_t body = lst >> 4;
-            const int64_t lowmask = (pos == 0) ? 0 : (((int64_t)1 << (4 * pos)) - 1);
-            const int64_t nb = (body & lowmask) | (item << (4 * pos)) | ((body & ~lowmask) << 4);
-            put_raw(d, (nb << 4) | (n + 1));
+            if (n >= 15) { lexc = EXC_UNSUPPORTED; st |= kDone; }
+            else if (ps_.fl) { lexc = EXC_TYPE; st |= kDone; }
+            else {
+              int64_t pos = ps_.b;
+              if (pos < 0) { pos += n; if (pos < 0) pos = 0; } else if (pos > n) pos = n;
+              const int64_t item = get(b).b & 0xF;
+              const int64_t body = lst >> 4;
+              const int64_t lowmask = (pos == 0) ? 0 : (((int64_t)1 << (4 * pos)) - 1);
+              const int64_t nb = (body & lowmask) | (item << (4 * pos)) | ((body & ~lowmask) << 4);
+              res = pi((nb << 4) | (n + 1));
+            }
           }
+          wmode = 1;
           break;
         case OP_ADD: case OP_SUB: case OP_MUL:
           if (act) {
             const PyN x = get(a), y = get(b);
-            PyN r;
             if (!x.fl && !y.fl) {
               int64_t v;
               const bool ovf = op == OP_ADD ? __builtin_add_overflow(x.b, y.b, &v)
                              : op == OP_SUB ? __builtin_sub_overflow(x.b, y.b, &v)
                                             : __builtin_mul_overflow(x.b, y.b, &v);
-              if (ovf) { lexc = EXC_UNSUPPORTED; st |= kDone; break; }   // bigint: host decides
-              r = pi(v);
+              if (ovf) { lexc = EXC_UNSUPPORTED; st |= kDone; }   // bigint: host decides
+              else res = pi(v);
             } else {
               const double p = fv(x), q = fv(y);
-              r = pf(op == OP_ADD ? p + q : op == OP_SUB ? p - q : p * q);
+              res = pf(op == OP_ADD ? p + q : op == OP_SUB ? p - q : p * q);
             }
-            put(d, r);
           }
+          wmode = 1;
           break;
         case OP_TDIV:
           if (act) {
             const PyN x = get(a), y = get(b);
             const bool big = !x.fl && !y.fl && (x.b > kTwo53i || x.b < -kTwo53i || y.b > kTwo53i || y.b < -kTwo53i);
             const double q = fv(y);
-            if (q == 0.0) { lexc = EXC_ZERO_DIVISION; st |= kDone; break; }
-            if (big) { lexc = EXC_UNSUPPORTED; st |= kDone; break; }
-            put(d, pf(fv(x) / q));
+            if (q == 0.0) { lexc = EXC_ZERO_DIVISION; st |= kDone; }
+            else if (big) { lexc = EXC_UNSUPPORTED; st |= kDone; }
+            else res = pf(fv(x) / q);
           }
+          wmode = 1;
           break;
         case OP_FDIV: case OP_MOD: case OP_POW: case OP_LOGB: case OP_MPOW:
           if (act) {
-            PyN r;
-            const int e = d_binop(op, get(a), get(b), r);
-            if (e) { lexc = e; st |= kDone; break; }
-            put(d, r);
+            const PyR o = d_binop(op, get(a), get(b));
+            if (o.e) { lexc = o.e; st |= kDone; }
+            else res = PyN{o.b, o.fl != 0};
           }
+          wmode = 1;
           break;
         case OP_NOT:
-          if (act) put(d, pi(truthy(get(a)) ? 0 : 1));
+          res = pi(truthy(get(a)) ? 0 : 1);
+          wmode = 1;
           break;
         case OP_TRUTH:
-          if (act) put(d, pi(truthy(get(a)) ? 1 : 0));
+          res = pi(truthy(get(a)) ? 1 : 0);
+          wmode = 1;
           break;
         case OP_ISINT:
-          if (act) put(d, pi(get(a).fl ? 0 : 1));
+          res = pi(get(a).fl ? 0 : 1);
+          wmode = 1;
           break;
         case OP_FLOAT:
-          if (act) put(d, pf(fv(get(a))));
+          res = pf(fv(get(a)));
+          wmode = 1;
           break;
         case OP_NEG: case OP_POS: case OP_ABS: case OP_INT: case OP_ROUND: case OP_SQRT: case OP_LOG: case OP_EXP:
         case OP_SIN: case OP_COS: case OP_TAN:
           if (act) {
-            PyN r;
-            const int e = d_unop(op, get(a), r);
-            if (e) { lexc = e; st |= kDone; break; }
-            put(d, r);
+            const PyR o = d_unop(op, get(a));
+            if (o.e) { lexc = o.e; st |= kDone; }
+            else res = PyN{o.b, o.fl != 0};
           }
+          wmode = 1;
           break;
-        case OP_LT: case OP_LE: case OP_GT: case OP_GE: case OP_EQ: case OP_NE:
-          if (act) {
-            const int c = d_cmp(get(a), get(b));
-            bool v;
-            switch (op) {
-              case OP_LT: v = c == -1; break;
-              case OP_LE: v = c == -1 || c == 0; break;
-              case OP_GT: v = c == 1; break;
-              case OP_GE: v = c == 1 || c == 0; break;
-              case OP_EQ: v = c == 0; break;
-              default: v = c != 0; break;
-            }
-            put(d, pi(v ? 1 : 0));
+        case OP_LT: case OP_LE: case OP_GT: case OP_GE: case OP_EQ: case OP_NE: {
+          const int c = d_cmp(get(a), get(b));
+          bool v;
+          switch (op) {
+            case OP_LT: v = c == -1; break;
+            case OP_LE: v = c == -1 || c == 0; break;
+            case OP_GT: v = c == 1; break;
+            case OP_GE: v = c == 1 || c == 0; break;
+            case OP_EQ: v = c == 0; break;
+            default: v = c != 0; break;
           }
-          break;
-        case OP_MIN2: case OP_MAX2:
-          if (act) {
-            const PyN x = get(a), y = get(b);
-            const int c = d_cmp(y, x);
-            const bool take = op == OP_MAX2 ? c == 1 : c == -1;
-            put(d, take ? y : x);
-          }
-          break;
-        case OP_IF: {
-          if (act) { if (!truthy(get(a))) off = 1; }
-          else off += 1;
-          if (!ballot(off == 0 && st == 0)) { pc = imm; nxt = cp[pc]; continue; }
+          res = pi(v ? 1 : 0);
+          wmode = 1;
           break;
         }
+        case OP_MIN2: case OP_MAX2: {
+          const PyN x = get(a), y = get(b);
+          const int c = d_cmp(y, x);
+          const bool take = op == OP_MAX2 ? c == 1 : c == -1;
+          res = take ? y : x;
+          wmode = 1;
+          break;
+        }
+        case OP_IF:
+          if (act) { if (!truthy(get(a))) off = 1; }
+          else off += 1;
+          if (!ballot(off == 0 && st == 0)) jump = imm;
+          break;
         case OP_ELSE:
           if (off == 1) off = 0; else if (off == 0) off = 1;
-          if (!ballot(off == 0 && st == 0)) { pc = imm; nxt = cp[pc]; continue; }
+          if (!ballot(off == 0 && st == 0)) jump = imm;
           break;
         case OP_ENDIF:
           if (off > 0) off -= 1;
           break;
         case OP_LOOP_BEGIN:
-          put_raw(d, (int64_t)(st & (kBrk | kCont)));
+          res = pi((int64_t)(st & (kBrk | kCont)));
+          wmode = 2;
           if (!act) off += 1;
           st &= ~(kBrk | kCont);
           break;
         case OP_LOOP_TEST:
           if (act && !truthy(get(a))) st |= kBrk;
-          if (!ballot(off == 0 && st == 0)) { pc = imm; nxt = cp[pc]; continue; }
+          if (!ballot(off == 0 && st == 0)) jump = imm;
           break;
         case OP_LOOP_CONT:
           st &= ~kCont;
           break;
         case OP_LOOP_NEXT:
-          pc = imm;
-          nxt = cp[pc];
-          continue;
+          jump = imm;
+          break;
         case OP_LOOP_EXIT: {
           if (off > 0) off -= 1;
-          const uint32_t s = (uint32_t)get(a).b & (kBrk | kCont);
-          st = (st & kDone) | s;
+          const uint32_t s_ = (uint32_t)get(a).b & (kBrk | kCont);
+          st = (st & kDone) | s_;
           break;
         }
         case OP_BREAK:
@@ -635,20 +687,25 @@ struct VmScorerDev {
           break;
         case OP_RET:
           if (act) { result = get(a); has_result = true; st |= kDone; }
-          if (!ballot((st & kDone) == 0)) goto finished;
+          fin = !ballot((st & kDone) == 0);
           break;
         case OP_RAISE:
           if (act) { lexc = imm; st |= kDone; }
           break;
         case OP_END:
-          goto finished;
+          fin = true;
+          break;
         default:
           lexc = EXC_UNSUPPORTED;
-          goto finished;
+          fin = true;
+          break;
       }
-      ++pc;
+      // single write-back (lanes that raised above are no longer active)
+      if (wmode == 2 || (wmode == 1 && act && st == 0)) put(d, res);
+      if (fin) break;
+      pc = jump >= 0 ? jump : pc + 1;
     }
-  finished:
+    // finished
     if (node >= n_nodes) return 0;
     if (lexc != EXC_NONE) { exc = lexc; return 0; }
     if (!has_result) { exc = EXC_TYPE; return 0; }  // returned None

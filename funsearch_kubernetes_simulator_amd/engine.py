@@ -143,8 +143,12 @@ class Evaluator:
                  cpu_threads: int = 0, object_workers: int = 0, n_slots: int = 4):
         self.workload = workload or load_default_workload()
         self.options = dict(options or {})
-        self.cpu_threads = cpu_threads or os.cpu_count() or 1
-        self.object_workers = object_workers or min(8, os.cpu_count() or 1)
+        from .ops.cpu_engine import default_threads
+        self.cpu_threads = cpu_threads or default_threads()
+        self.object_workers = object_workers or min(8, self.cpu_threads)
+        # below this many programs a batch runs faster on the CPU VM (one replay per
+        # core, ~0.1 s each) than as a handful of latency-bound device waves
+        self.device_min_batch = int(self.options.pop("device_min_batch", 128))
         self.device = None
         want_gpu = device not in ("cpu", None)
         if want_gpu:
@@ -209,7 +213,7 @@ class Evaluator:
         pending = [i for i, p in enumerate(compiled) if p is not None]
         if self.device is not None:
             dev_idx = [i for i in pending if compiled[i].device_ok]
-            if dev_idx:
+            if len(dev_idx) >= self.device_min_batch:
                 tab = self.device.evaluate_programs([compiled[i] for i in dev_idx])
                 for row, i in zip(tab, dev_idx):
                     if int(row[COLS["exc"]]) in (Exc.UNSUPPORTED, Exc.BUDGET) or row[COLS["inexact"]]:

@@ -24,6 +24,8 @@ def main() -> None:
     ap.add_argument("--checkpoint-dir")
     ap.add_argument("--log")
     ap.add_argument("--save", help="write the top-5 JSON (reference schema) here")
+    ap.add_argument("--device-min-batch", type=int,
+                    help="smallest program batch sent to the device VM (smaller ones run on the CPU VM)")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args()
     cfg = load_config(a.config)
@@ -36,6 +38,8 @@ def main() -> None:
         cfg["funsearch"]["policies_per_generation"] = a.policies_per_generation
     if a.device:
         cfg.setdefault("device", {})["kind"] = a.device
+    if a.device_min_batch is not None:
+        cfg.setdefault("device", {})["min_batch"] = a.device_min_batch
     if a.checkpoint_dir:
         cfg.setdefault("checkpoint", {})["dir"] = a.checkpoint_dir
     if a.log:

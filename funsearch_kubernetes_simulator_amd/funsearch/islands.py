@@ -45,7 +45,10 @@ class IslandFunSearch:
         dev = (self.config.get("device") or {}).get("kind", "auto")
         if dev == "auto" and self.ctx.backend == "nccl":
             dev = self.ctx.local_rank
-        self.evaluator = evaluator or Evaluator(device=dev)
+        opts = {}
+        if "min_batch" in (self.config.get("device") or {}):
+            opts["device_min_batch"] = int(self.config["device"]["min_batch"])
+        self.evaluator = evaluator or Evaluator(device=dev, options=opts)
         llm_cfg = dict(self.config.get("llm") or {})
         base_seed = int(llm_cfg.get("seed", 0)) + 1000003 * self.ctx.rank
         self.islands: List[SimpleFunSearch] = []

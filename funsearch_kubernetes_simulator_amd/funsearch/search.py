@@ -111,6 +111,19 @@ class SimpleFunSearch:
     def initialize_population(self) -> None:
         seeds = seed_policies()
         baseline = [seeds["first_fit"], seeds["best_fit"]]
+        # optional extra seeds (not in the reference): "discovered" = the policies
+        # under data/policies/discovered, "reference" = the published champions,
+        # or any seed/library policy name
+        for extra in self.config.get("funsearch", {}).get("extra_seeds", []) or []:
+            if extra == "discovered":
+                from ..models.library import discovered_policies
+                baseline += [r["code"] for r in discovered_policies().values()]
+            elif extra == "reference":
+                from ..models.library import reference_policies
+                baseline += [c for n, c in reference_policies().items() if n.startswith("funsearch")]
+            else:
+                from ..models.library import policy
+                baseline.append(policy(extra))
         self._print("Evaluating baseline policies on OpenB dataset...")
         for i, code in enumerate(baseline):
             score = self._evaluate_policy_full(code)

@@ -24,6 +24,18 @@ _mod = None
 #: them to the wall-clock-bounded object engine.
 DEFAULT_CALL_BUDGET = 1 << 22
 
+
+def default_threads() -> int:
+    """Worker threads for the native CPU engine: the process's CPU share
+    (OMP_NUM_THREADS / affinity) rather than every core of a shared machine."""
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
 FAMILY = {"first_fit": 0, "best_fit": 1, "random_linear": 2, "feature_linear": 3, "composite_linear": 4}
 
 
@@ -92,7 +104,7 @@ def simulate_builtin(w: Workload, family: str, weights: Sequence[float] = (),
 
 def simulate_builtin_batch(w: Workload, family: str, weights: np.ndarray,
                            options: Optional[SimOptions] = None, threads: int = 0) -> np.ndarray:
-    threads = threads or os.cpu_count() or 1
+    threads = threads or default_threads()
     return native().simulate_builtin_batch(native_workload(w), FAMILY[family],
                                            np.ascontiguousarray(weights, dtype=np.float64),
                                            (options or SimOptions()).as_dict(), threads)
@@ -105,7 +117,7 @@ def simulate_program(w: Workload, prog: CompiledPolicy, options: Optional[SimOpt
 
 def simulate_program_batch(w: Workload, progs: Sequence[CompiledPolicy],
                            options: Optional[SimOptions] = None, threads: int = 0) -> np.ndarray:
-    threads = threads or os.cpu_count() or 1
+    threads = threads or default_threads()
     return native().simulate_program_batch(native_workload(w), [p.code for p in progs],
                                            [p.fconst for p in progs], [p.iconst for p in progs],
                                            [p.ctag for p in progs], (options or SimOptions()).as_dict(),

@@ -64,3 +64,23 @@ def test_device_vm_runaway_program_drains(default_workload):
                           "    return 1\n")
     tab = dev.evaluate_programs([prog] * 4)
     assert np.all(tab[:, 10] == Exc.BUDGET)
+
+
+def test_device_vm_wide_register_file(default_workload):
+    """Programs with > 32 virtual registers take the VGPR + LDS register-file kernel."""
+    from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
+    body = "".join(f"    v{i} = node.cpu_milli_left * {i + 1} + pod.cpu_milli\n" for i in range(40))
+    total = " + ".join(f"v{i}" for i in range(40))
+    code = ("def priority_function(pod, node):\n"
+            "    if pod.cpu_milli > node.cpu_milli_left or pod.memory_mib > node.memory_mib_left:\n"
+            "        return 0\n"
+            "    if pod.num_gpu > 0 and sum(1 for g in node.gpus if g.gpu_milli_left >= pod.gpu_milli) < pod.num_gpu:\n"
+            "        return 0\n" + body + f"    return ({total}) % 1000 + 1\n")
+    prog = compile_policy(code)
+    assert prog.nregs > 32
+    w = default_workload
+    sub = Workload(w.cluster, w.pods.subset(np.arange(0, 800)))
+    dev = he.DeviceEvaluator(sub)
+    gpu = dev.evaluate_programs([prog, prog])
+    cpu = ce.simulate_program_batch(sub, [prog, prog], threads=2)
+    assert np.array_equal(gpu, cpu)
