@@ -72,6 +72,7 @@ def main() -> None:
     from funsearch_kubernetes_simulator_amd.core import load_default_workload
     from funsearch_kubernetes_simulator_amd.engine import COLS, Evaluator
     from funsearch_kubernetes_simulator_amd.funsearch.param_islands import make_islands, migrate
+    from funsearch_kubernetes_simulator_amd.utils.trace import roctx_range
 
     if args.trace == "synthetic":
         from funsearch_kubernetes_simulator_amd.core import synthetic_workload
@@ -79,7 +80,9 @@ def main() -> None:
     else:
         workload = load_default_workload()
     device = ctx.local_rank if args.device == "gpu" else "cpu"
-    ev = Evaluator(workload, device=device, options={"heap_mode": args.heap_mode}, n_slots=max(1, args.islands))
+    # the per-event trace hash only serves cross-engine equality tests: off here
+    ev = Evaluator(workload, device=device, options={"heap_mode": args.heap_mode, "trace_hash": False},
+                   n_slots=max(1, args.islands))
     if args.device == "gpu" and ev.device is None:
         raise SystemExit("no HIP device visible")
     islands = make_islands(args.islands, args.family, args.candidates, args.elite,
@@ -150,10 +153,12 @@ def main() -> None:
         g = g0
         while g < g0 + count:
             n = min(M - g % M, g0 + count - g)
-            (epoch_sync if args.sync_islands else epoch_async)(g, n)
+            with roctx_range(f"bench.generations {g}-{g + n - 1}"):
+                (epoch_sync if args.sync_islands else epoch_async)(g, n)
             g += n
             if args.migrate_every and g % M == 0:
-                migrate(islands, args.migrants, gather)
+                with roctx_range("bench.migrate"):
+                    migrate(islands, args.migrants, gather)
 
     run(0, args.warmup)
     sync()

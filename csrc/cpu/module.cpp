@@ -9,6 +9,7 @@
 
 #include "builtin_scorers.hpp"
 #include "engine.hpp"
+#include "trace_io.hpp"
 #include "vm_cpu.hpp"
 
 namespace py = pybind11;
@@ -103,7 +104,40 @@ void parallel_for(int64_t n, int threads, Fn fn) {
 
 }  // namespace
 
+template <class T>
+py::array_t<T> np_of(const std::vector<T>& v) {
+  py::array_t<T> a((py::ssize_t)v.size());
+  if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(T));
+  return a;
+}
+
 PYBIND11_MODULE(_fks_cpu, m) {
+  m.def("load_pod_csv", [](const std::string& path) {
+    fks::PodColumns p;
+    try {
+      p = fks::load_pods(path);
+    } catch (const fks::MissingColumn& e) {
+      throw py::key_error(e.what());
+    }
+    py::dict d;
+    d["name"] = p.name; d["gpu_spec"] = p.gpu_spec;
+    d["cpu"] = np_of(p.cpu); d["mem"] = np_of(p.mem); d["ngpu"] = np_of(p.ngpu); d["gmilli"] = np_of(p.gmilli);
+    d["ctime"] = np_of(p.ctime); d["dur"] = np_of(p.dur);
+    return d;
+  }, py::arg("path"));
+  m.def("load_node_csv", [](const std::string& path, const std::unordered_map<std::string, int64_t>& mem_map) {
+    fks::NodeColumns n;
+    try {
+      n = fks::load_nodes(path, mem_map);
+    } catch (const fks::MissingColumn& e) {
+      throw py::key_error(e.what());
+    }
+    py::dict d;
+    d["sn"] = n.sn;
+    d["cpu"] = np_of(n.cpu); d["mem"] = np_of(n.mem); d["gpu_count"] = np_of(n.gpu_count);
+    d["ngpus"] = np_of(n.ngpus); d["gpu_mem"] = np_of(n.gpu_mem);
+    return d;
+  }, py::arg("path"), py::arg("gpu_mem_mapping"));
   m.doc() = "Native CPU oracle engine of funsearch_kubernetes_simulator_amd";
   py::class_<Workload>(m, "Workload")
       .def(py::init(&make_workload))

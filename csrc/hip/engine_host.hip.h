@@ -21,6 +21,7 @@
 
 #include <hip/hip_runtime.h>
 #include <pybind11/numpy.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include <pybind11/pybind11.h>
 
 #include <algorithm>
@@ -98,6 +99,7 @@ struct Slot {
   int P = 0;
   int fam_spec = -1;    // family shared by the whole staged batch, or -1
   bool busy = false;
+  roctx_range_id_t range = 0;   // roctx range spanning submit -> wait (rocprofv3 --marker-trace)
   void release() {
     for (DevBuf* b : {&res, &tab, &fam, &w, &code, &meta, &kpay, &ktag, &gheap, &prof, &wc}) b->release();
     h_in.release();
@@ -151,6 +153,7 @@ class DeviceEngine {
     W_.rank_bits = (int32_t)geti("rank_bits"); W_.node_bits = (int32_t)geti("node_bits");
     W_.low_bits = (int32_t)geti("low_bits"); W_.time_bits = (int32_t)geti("time_bits");
     W_.snapshot_interval = 0.05;
+    W_.trace_hash = 1;
     HIP_OK(hipStreamSynchronize(st));
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, device_));
@@ -177,6 +180,7 @@ class DeviceEngine {
     if (o.contains("snapshot_interval")) W_.snapshot_interval = o["snapshot_interval"].cast<double>();
     if (o.contains("budget")) budget_ = o["budget"].cast<int64_t>();
     if (o.contains("heap_top")) heap_top_opt_ = o["heap_top"].cast<int>();   // -1: auto
+    if (o.contains("trace_hash")) W_.trace_hash = o["trace_hash"].cast<bool>() ? 1 : 0;
     if (o.contains("check_invariants")) {
       const int64_t k = o["check_invariants"].cast<int64_t>();
       W_.check_every = (int32_t)std::max<int64_t>(0, std::min<int64_t>(k, INT32_MAX));
@@ -213,6 +217,7 @@ class DeviceEngine {
       throw std::invalid_argument("weights must be [P, 16] float64");
     if (P < 1) throw std::invalid_argument("empty batch");
     HIP_OK(hipSetDevice(device_));
+    s.range = roctxRangeStartA("fks.batch.builtin");
     stage_builtin(s, fam.data(), weights.data(), P);
     {
       py::gil_scoped_release rel;
@@ -227,6 +232,7 @@ class DeviceEngine {
     const int P = (int)offsets.size();
     if (P < 1) throw std::invalid_argument("empty batch");
     HIP_OK(hipSetDevice(device_));
+    s.range = roctxRangeStartA("fks.batch.vm");
     stage_programs(s, blob, offsets, lengths, kpay, koff, ktag, nregs);
     {
       py::gil_scoped_release rel;
@@ -252,6 +258,8 @@ class DeviceEngine {
       HIP_OK(hipEventSynchronize(s.done));
     }
     s.busy = false;
+    if (s.range) roctxRangeStop(s.range);
+    s.range = 0;
     py::array_t<double> out({(py::ssize_t)s.P, (py::ssize_t)13});
     std::memcpy(out.mutable_data(), s.h_tab.p, sizeof(double) * 13 * (size_t)s.P);
     return out;

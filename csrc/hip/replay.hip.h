@@ -63,6 +63,7 @@ struct DevWorkload {
   int32_t heap_top;           // heap slots kept in LDS when the heap lives in HBM
   int32_t check_every;        // k_check_invariants cadence in events (0: off)
   int32_t inv_words;          // LDS u64 words reserved for the invariant check (0: off)
+  int32_t trace_hash;         // 1: fold every event into DevResult.hash (cross-engine trace check)
 };
 
 struct DevResult {
@@ -327,7 +328,7 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
       }
       used_cpu -= pod.cpu; used_mem -= pod.mem; used_gcnt -= pod.ngpu;
       used_gml -= (int64_t)pod.gmilli * __builtin_popcount(mask);
-      hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 1, (uint64_t)t);
+      if (W.trace_hash) hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 1, (uint64_t)t);
       prof.mark(PH_DELETE);
     } else {
       // ---------------- creation: score all nodes, argmax (first node wins ties)
@@ -405,7 +406,7 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
         } else {
           ++n_dropped;
         }
-        hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 2, (uint64_t)t);
+        if (W.trace_hash) hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 2, (uint64_t)t);
         prof.mark(PH_FAIL);
       } else {
         // ---------------- commit on best_node
@@ -444,7 +445,7 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
         heap.push(n, (dt << tshift) | ((uint64_t)rank << lb) | ((uint64_t)gmask << (2 + nb)) |
                          ((uint64_t)best_node << 2) | kDelete);
         ++n;
-        hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2), ((uint64_t)t << 8) ^ (uint64_t)best_node);
+        if (W.trace_hash) hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2), ((uint64_t)t << 8) ^ (uint64_t)best_node);
         prof.mark(PH_COMMIT);
       }
     }

@@ -74,8 +74,15 @@ hipError_t raise_lds(T* f, int max_lds) {
 // without spills beats 4 with scratch traffic
 // without spills beats 4 with scratch traffic; 128 / 256 nodes (NPASS 2 / 4)
 // hold 2 / 4 node slots per lane: 3 / 2 waves per SIMD.
-#define FKS_FAM_BOUNDS(G, F, NP) \
-  __launch_bounds__(64, !(G) ? 1 : (NP) >= 4 ? 2 : (NP) == 2 ? 3 : (((F) == 3 || (F) == 4 || (F) < 0) ? 3 : 4))
+#ifndef FKS_LIGHT_WAVES
+#define FKS_LIGHT_WAVES 4   // first-fit / best-fit / random_linear (build-time knob for A/B runs)
+#endif
+#ifndef FKS_HEAVY_WAVES
+#define FKS_HEAVY_WAVES 3   // feature / composite families and mixed batches
+#endif
+#define FKS_FAM_BOUNDS(G, F, NP)                                               \
+  __launch_bounds__(64, !(G) ? 1 : (NP) >= 4 ? 2 : (NP) == 2 ? 3              \
+                           : (((F) == 3 || (F) == 4 || (F) < 0) ? FKS_HEAVY_WAVES : FKS_LIGHT_WAVES))
 template <int NPASS, bool GHEAP, int FAM>
 __global__ FKS_FAM_BOUNDS(GHEAP, FAM, NPASS) void k_replay_builtin(fksk::BuiltinArgs a) {
   const int p = blockIdx.x;

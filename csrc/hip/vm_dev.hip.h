@@ -402,11 +402,16 @@ struct VmScorerDev {
     };
     auto put_raw = [&](int r, int64_t v) { wr(r, v); ftag &= ~(1ull << r); };
 
-    // per-lane node view (pass ps)
-    int32_t gml[kGmax];
+    // per-lane node view (pass ps), copied into registers once per call
+    // (score() is out of line, so `nr` arrives through memory)
+    int32_t gml[kGmax], gmt[kGmax];
 #pragma unroll
-    for (int j = 0; j < kGmax; ++j) gml[j] = nr.gml[ps][j];
+    for (int j = 0; j < kGmax; ++j) { gml[j] = nr.gml[ps][j]; gmt[j] = nr.gmt[ps][j]; }
     const int ngp = nr.ngpus[ps];
+    const int64_t n_cpu_left = nr.cpu_left[ps], n_cpu_total = nr.cpu_total[ps];
+    const int64_t n_mem_left = nr.mem_left[ps], n_mem_total = nr.mem_total[ps], n_gpu_left = nr.gpu_left[ps];
+    const int64_t p_cpu = pod.cpu, p_mem = pod.mem, p_ngpu = pod.ngpu, p_gmilli = pod.gmilli;
+    const int64_t p_ctime = pod.ctime, p_dur = pod.dur;
 
     int pc = 0;
     int64_t budget = budget_call;   // runaway programs end here, so every wave drains
@@ -442,12 +447,12 @@ struct VmScorerDev {
         case OP_POD: {
           int64_t v;
           switch (imm) {
-            case 0: v = pod.cpu; break;
-            case 1: v = pod.mem; break;
-            case 2: v = pod.ngpu; break;
-            case 3: v = pod.gmilli; break;
-            case 4: v = pod.ctime; break;
-            default: v = pod.dur; break;
+            case 0: v = p_cpu; break;
+            case 1: v = p_mem; break;
+            case 2: v = p_ngpu; break;
+            case 3: v = p_gmilli; break;
+            case 4: v = p_ctime; break;
+            default: v = p_dur; break;
           }
           res = pi(v);
           wmode = 1;
@@ -456,11 +461,11 @@ struct VmScorerDev {
         case OP_NODE: {
           int64_t v;
           switch (imm) {
-            case 0: v = nr.cpu_left[ps]; break;
-            case 1: v = nr.cpu_total[ps]; break;
-            case 2: v = nr.mem_left[ps]; break;
-            case 3: v = nr.mem_total[ps]; break;
-            case 4: v = nr.gpu_left[ps]; break;
+            case 0: v = n_cpu_left; break;
+            case 1: v = n_cpu_total; break;
+            case 2: v = n_mem_left; break;
+            case 3: v = n_mem_total; break;
+            case 4: v = n_gpu_left; break;
             default: v = ngp; break;
           }
           res = pi(v);
@@ -476,7 +481,7 @@ struct VmScorerDev {
               for (int jj = 0; jj < kGmax; ++jj) v = (jj == j) ? gml[jj] : v;
             } else if (imm == 1) {
 #pragma unroll
-              for (int jj = 0; jj < kGmax; ++jj) v = (jj == j) ? nr.gmt[ps][jj] : v;
+              for (int jj = 0; jj < kGmax; ++jj) v = (jj == j) ? gmt[jj] : v;
             } else {
               v = gmem_total[node * kGmax + j];
             }

@@ -100,10 +100,48 @@ class TraceParser:
         return self.parse_cluster(node_file), self.parse_pods(pod_file)
 
     def load_workload(self, node_file: str = DEFAULT_NODE_FILE,
-                      pod_file: str = DEFAULT_POD_FILE) -> Workload:
-        """Parse straight into SoA arrays (what the engines consume)."""
+                      pod_file: str = DEFAULT_POD_FILE, native: Optional[bool] = None) -> Workload:
+        """Parse straight into SoA arrays (what the engines consume).
+
+        ``native`` (default: when the C++ extension is built) reads the CSVs with
+        the C++ loader (csrc/cpu/trace_io.hpp) without building the object
+        graph; the result is identical to the object path."""
+        name = f"{Path(node_file).stem}/{Path(pod_file).stem}"
+        if native is None or native:
+            try:
+                from ..ops.cpu_engine import native as _native
+                mod = _native()
+            except Exception:
+                if native:
+                    raise
+                mod = None
+            if mod is not None:
+                return self._load_native(mod, node_file, pod_file, name)
         cluster, pods = self.parse_workload(node_file, pod_file)
-        return Workload.from_objects(cluster, pods, name=f"{Path(node_file).stem}/{Path(pod_file).stem}")
+        return Workload.from_objects(cluster, pods, name=name)
+
+    def _load_native(self, mod, node_file: str, pod_file: str, name: str) -> Workload:
+        n = mod.load_node_csv(str(self.csv_dir / node_file), self.gpu_mem_mapping)
+        p = mod.load_pod_csv(str(self.csv_dir / pod_file))
+        ngpus = np.asarray(n["ngpus"], dtype=np.int32)
+        start = np.zeros(ngpus.size + 1, dtype=np.int32)
+        np.cumsum(ngpus, out=start[1:])
+        G = int(start[-1])
+        gmem = np.repeat(np.asarray(n["gpu_mem"], dtype=np.int64), ngpus)
+        cpu, mem = np.asarray(n["cpu"], dtype=np.int64), np.asarray(n["mem"], dtype=np.int64)
+        cluster = ClusterArrays(
+            node_ids=list(n["sn"]), node_cpu_total=cpu, node_cpu_left=cpu.copy(),
+            node_mem_total=mem, node_mem_left=mem.copy(),
+            node_gpu_left=np.asarray(n["gpu_count"], dtype=np.int32), node_ngpus=ngpus, gpu_start=start,
+            gpu_milli_total=np.full(G, GPU_MILLI_PER_CARD, dtype=np.int32),
+            gpu_milli_left=np.full(G, GPU_MILLI_PER_CARD, dtype=np.int32),
+            gpu_mem_total=gmem, gpu_mem_left=gmem.copy())
+        ids = list(p["name"])
+        pods = PodArrays(ids, np.asarray(p["cpu"], dtype=np.int64), np.asarray(p["mem"], dtype=np.int64),
+                         np.asarray(p["ngpu"], dtype=np.int32), np.asarray(p["gmilli"], dtype=np.int32),
+                         np.asarray(p["ctime"], dtype=np.int64), np.asarray(p["dur"], dtype=np.int64),
+                         dense_rank(ids), list(p["gpu_spec"]))
+        return Workload(cluster, pods, name=name)
 
     # -- Kubernetes Node YAML (bundled with the reference, unused there) ----
     def parse_node_yaml(self, yaml_file: str = "openb_node_list_gpu_node.yaml") -> Cluster:

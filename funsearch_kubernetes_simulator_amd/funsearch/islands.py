@@ -30,6 +30,7 @@ from typing import List, Optional, Tuple
 from ..engine import Evaluator
 from ..parallel import dist
 from ..utils.metrics import MetricsLog
+from ..utils.trace import roctx_range
 from .llm import make_client
 from .search import FEEDBACK, SimpleFunSearch, load_config
 
@@ -105,7 +106,8 @@ class IslandFunSearch:
                 ki[1], plans[ki[0]][1], FEEDBACK), jobs))
         children = [(k, code) for k, _, code in outs if code]
         t_gen = time.time()
-        results = self.evaluator.evaluate_programs([c for _, c in children]) if children else []
+        with roctx_range(f"funsearch.evaluate gen {self.generation} ({len(children)} programs)"):
+            results = self.evaluator.evaluate_programs([c for _, c in children]) if children else []
         t_eval = time.time()
         self.evaluations += len(children)
         for k, (s, elites, _) in enumerate(plans):
@@ -118,7 +120,8 @@ class IslandFunSearch:
                     s.best_score, s.best_policy = res.score, code
             s.population = sorted(elites + new, key=lambda x: x[1], reverse=True)[:s.population_size]
         if self.migrate_every and self.generation % self.migrate_every == 0:
-            self.migrate()
+            with roctx_range(f"funsearch.migrate gen {self.generation}"):
+                self.migrate()
         best_local = self.best[1]
         best_global = dist.all_reduce_max(best_local)
         rec = dict(kind="generation", rank=self.ctx.rank, generation=self.generation, best=best_local,

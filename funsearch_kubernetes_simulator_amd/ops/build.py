@@ -74,8 +74,10 @@ HIP_UNITS = [("module", "module.hip", []), ("screen", "screen.hip", [])] + [
 
 
 def _hip_flags() -> List[str]:
+    # occupancy knobs of the replay kernels (waves per SIMD), for A/B builds
+    knobs = [f"-D{k}={os.environ[k]}" for k in ("FKS_LIGHT_WAVES", "FKS_HEAVY_WAVES") if os.environ.get(k)]
     return [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-ffp-contract=off",
-            "-fno-fast-math", "-munsafe-fp-atomics", "-Wno-unused-result",
+            "-fno-fast-math", "-munsafe-fp-atomics", "-Wno-unused-result", *knobs,
             *_py_includes(), f"-I{CSRC_DIR / 'include'}", f"-I{CSRC_DIR / 'hip'}"]
 
 
@@ -98,7 +100,8 @@ def build_hip(force: bool = False, jobs: int = 0) -> Path:
     jobs = jobs or min(len(cmds), int(os.environ.get("MAX_JOBS", "0")) or os.cpu_count() or 1, 16)
     with ThreadPoolExecutor(jobs) as ex:
         list(ex.map(_run, cmds))
-    _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(target)])
+    _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(target),
+          "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"])
     return target
 
 

@@ -104,3 +104,22 @@ def test_bench_two_ranks_cpu():
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["value"] > 0 and line["scaling"] == "weak"
     assert line["config"]["global_batch"] == 8
+
+
+def test_native_csv_loader_matches_python_parser():
+    """C++ trace loader (csrc/cpu/trace_io.hpp) == the object-graph parser, field by field."""
+    p = TraceParser()
+    for nf in ("gpu_models_filtered.csv", "openb_node_list_all_node.csv"):
+        for pf in ("openb_pod_list_default.csv", "openb_pod_list_gpuspec33.csv", "openb_pod_list_cpu050.csv"):
+            a = p.load_workload(nf, pf, native=False)
+            b = p.load_workload(nf, pf, native=True)
+            assert a.cluster.node_ids == b.cluster.node_ids and a.pods.pod_ids == b.pods.pod_ids
+            assert a.pods.gpu_spec == b.pods.gpu_spec
+            for name in ("node_cpu_total", "node_cpu_left", "node_mem_total", "node_mem_left", "node_gpu_left",
+                         "node_ngpus", "gpu_start", "gpu_milli_total", "gpu_milli_left", "gpu_mem_total",
+                         "gpu_mem_left"):
+                assert np.array_equal(getattr(a.cluster, name), getattr(b.cluster, name)), name
+            for name in ("pod_cpu", "pod_mem", "pod_ngpu", "pod_gmilli", "pod_ctime", "pod_dur", "pod_rank"):
+                assert np.array_equal(getattr(a.pods, name), getattr(b.pods, name)), name
+    with pytest.raises(KeyError):
+        p.load_workload("gpu_models_filtered.csv", "openb_pod_list_multigpu20.csv", native=True)
