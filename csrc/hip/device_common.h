@@ -10,6 +10,20 @@ namespace fksd {
 
 constexpr int kWave = 64;
 
+// Address-space qualified pointers: generic pointers make the compiler emit
+// FLAT memory instructions (one path for LDS and global, both counters, the
+// slower one's latency).  LDS data goes through ds_*, HBM through global_*,
+// and read-only launch data through scalar s_load.
+#define FKS_LDS __attribute__((address_space(3)))
+#define FKS_GLOBAL __attribute__((address_space(1)))
+#define FKS_CONST __attribute__((address_space(4)))
+template <class T>
+__device__ __forceinline__ FKS_LDS T* lds_ptr(T* p) { return (FKS_LDS T*)p; }
+template <class T>
+__device__ __forceinline__ FKS_GLOBAL T* global_ptr(T* p) { return (FKS_GLOBAL T*)p; }
+template <class T>
+__device__ __forceinline__ const FKS_CONST T* const_ptr(const T* p) { return (const FKS_CONST T*)p; }
+
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -95,8 +109,10 @@ __device__ __forceinline__ int4 load_vgpr(const int4* p) {
   const uint64_t a = (uint64_t)p;
   uint32_t lo = (uint32_t)a;
   asm volatile("v_mov_b32 %0, %0" : "+v"(lo));
-  const int4* q = reinterpret_cast<const int4*>((a & 0xFFFFFFFF00000000ull) | lo);
-  return *q;
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  const FKS_GLOBAL v4i* q = reinterpret_cast<const FKS_GLOBAL v4i*>((a & 0xFFFFFFFF00000000ull) | lo);
+  const v4i v = *q;   // global_load_dwordx4
+  return make_int4(v.x, v.y, v.z, v.w);
 }
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }

@@ -32,14 +32,17 @@ constexpr int kDelKind = 2;
 __device__ __forceinline__ bool key_lt(uint64_t a, uint64_t b, int lb) { return (a >> lb) < (b >> lb); }
 
 struct WaveHeap {
-  uint64_t* h;        // keys (slots >= T)
-  uint64_t* top;      // LDS copy of slots [0, T)
+  FKS_GLOBAL uint64_t* h;   // keys (slots >= T), the policy's HBM slice
+  FKS_LDS uint64_t* top;    // LDS copy of slots [0, T)
   int T;
-  uint32_t* delmap;   // bit p set <=> slot p holds a deletion
+  FKS_LDS uint32_t* delmap; // bit p set <=> slot p holds a deletion
   int lb;             // low (payload) bits below the (time, rank) compare key
   int lane;           // this lane's id, refreshed (opaquely) per event by the caller
 
-  __device__ __forceinline__ uint64_t ld(int i) const { return i < T ? top[i] : h[i]; }
+  __device__ __forceinline__ uint64_t ld(int i) const {
+    if (i < T) return top[i];
+    return h[i];
+  }
   __device__ __forceinline__ void st(int i, uint64_t v) const {
     if (i < T) top[i] = v;
     else h[i] = v;
@@ -47,8 +50,8 @@ struct WaveHeap {
 
   __device__ __forceinline__ void mark(int pos, uint64_t v) const {
     const uint32_t bit = 1u << (pos & 31);
-    if ((v & 3) == kDelKind) atomicOr(&delmap[pos >> 5], bit);
-    else atomicAnd(&delmap[pos >> 5], ~bit);
+    if ((v & 3) == kDelKind) __hip_atomic_fetch_or(&delmap[pos >> 5], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else __hip_atomic_fetch_and(&delmap[pos >> 5], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 
   // Removes the root of a heap that holds n+1 items; `last` (= old h[n]) is

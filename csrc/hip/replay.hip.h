@@ -173,7 +173,7 @@ __host__ __device__ inline int inv_words_for(int npass) { return (kWave * npass 
 
 template <int NPASS>
 __device__ bool invariants_hold(const DevWorkload& W, const WaveHeap& heap, int n, const NodeRegs<NPASS>& nr,
-                                int32_t* inv, int lane) {
+                                FKS_LDS int32_t* inv, int lane) {
   for (int i = lane; i < kWave * NPASS * kInvCols; i += kWave) inv[i] = 0;
   __syncthreads();
   const int lb = W.low_bits, nb = W.node_bits, rb = W.rank_bits;
@@ -184,13 +184,13 @@ __device__ bool invariants_hold(const DevWorkload& W, const WaveHeap& heap, int 
     const int mask = (int)((k >> (2 + nb)) & 0xFF);
     const int rank = (int)((k >> lb) & ((1ull << rb) - 1));
     const int4 pr = W.pod[rank];
-    int32_t* row = inv + node * kInvCols;
-    atomicAdd(&row[0], pr.x);
-    atomicAdd(&row[1], pr.y);
-    atomicAdd(&row[2], (pr.w >> 16) & 0xFF);
+    FKS_LDS int32_t* row = inv + node * kInvCols;
+    __hip_atomic_fetch_add(&row[0], pr.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add(&row[1], pr.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add(&row[2], (pr.w >> 16) & 0xFF, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
     for (int j = 0; j < kGmax; ++j)
-      if ((mask >> j) & 1) atomicAdd(&row[3 + j], pr.w & 0xFFFF);
+      if ((mask >> j) & 1) __hip_atomic_fetch_add(&row[3 + j], pr.w & 0xFFFF, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   __syncthreads();
   bool bad = false;
@@ -198,7 +198,7 @@ __device__ bool invariants_hold(const DevWorkload& W, const WaveHeap& heap, int 
   for (int ps = 0; ps < NPASS; ++ps) {
     const int node = ps * kWave + lane;
     if (node >= W.n_nodes) continue;
-    const int32_t* row = inv + node * kInvCols;
+    const FKS_LDS int32_t* row = inv + node * kInvCols;
     const int32_t cl = nr.cpu_left[ps], ml = nr.mem_left[ps], gl = nr.gpu_left[ps];
     bad |= cl < 0 || cl > nr.cpu_total[ps] || row[0] + cl != nr.cpu_total[ps];
     bad |= ml < 0 || ml > nr.mem_total[ps] || row[1] + ml != nr.mem_total[ps];
@@ -216,8 +216,9 @@ __device__ bool invariants_hold(const DevWorkload& W, const WaveHeap& heap, int 
 
 // ----------------------------------------------------------------------------
 template <int NPASS, class Scorer, class Prof = NoProf>
-__device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Scorer& scorer, uint64_t* hbuf,
-                           uint64_t* htop, int T, uint32_t* delmap, int32_t* inv, DevResult* out,
+__device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Scorer& scorer, FKS_GLOBAL uint64_t* hbuf,
+                           FKS_LDS uint64_t* htop, int T, FKS_LDS uint32_t* delmap, FKS_LDS int32_t* inv,
+                           DevResult* out,
                            uint64_t* prof_out = nullptr) {
   // W: the kernel-argument copy (hot fields, kept in SGPRs); Wcold: the same
   // struct in global memory for the fields only snapshots / failures / commits
@@ -282,8 +283,9 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
 
   heap.lane = lane;
   while (n > 0) {
-    const DevWorkload* Wc = reinterpret_cast<const DevWorkload*>(uniu64(reinterpret_cast<uint64_t>(Wcold)));
-    asm volatile("" : "+s"(Wc));
+    const DevWorkload* Wg = reinterpret_cast<const DevWorkload*>(uniu64(reinterpret_cast<uint64_t>(Wcold)));
+    asm volatile("" : "+s"(Wg));
+    const FKS_CONST DevWorkload* Wc = const_ptr(Wg);   // scalar loads (read-only during the launch)
     // Lane-derived predicates (subtree slots of the heap walk, "GPU j exists")
     // are loop-invariant; hoisted they become dozens of live 64-bit lane masks
     // in SGPRs that get spilled every event.  Opaque copies are recomputed per
@@ -367,7 +369,7 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
           if (mcls < 0 && b) mcls = k * kWave + first_lane(b);
         }
         if (mcls >= 0) {
-          const int m = Wc->class_value[mcls];
+          const int m = const_ptr(Wc->class_value)[mcls];
           int64_t stranded = 0;
 #pragma unroll
           for (int ps = 0; ps < NPASS; ++ps)
@@ -464,7 +466,7 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
       acc.add(0, r0); acc.add(1, r1); acc.add(2, r2); acc.add(3, r3);
       if (ksnap >= n_fire) thr += Wc->snapshot_interval;
       ++ksnap;
-      next_fire = ksnap < n_fire ? Wc->snap_fire[ksnap] : INT64_MAX;
+      next_fire = ksnap < n_fire ? const_ptr(Wc->snap_fire)[ksnap] : INT64_MAX;
     }
     // (the reference's max_nodes counter feeds no metric: not tracked)
     if (W.check_every > 0 && (processed % W.check_every == 0 || n == 0) &&

@@ -28,32 +28,33 @@ namespace {
 //   GHEAP = true : heap in its HBM slice, LDS = bitmap | heap top (W.heap_top
 //                  slots) | vregs (16 policies/CU)
 struct Slot {
-  uint64_t* h;
-  uint64_t* top;
+  FKS_GLOBAL uint64_t* h;
+  FKS_LDS uint64_t* top;
   int T;
-  uint32_t* delmap;
+  FKS_LDS uint32_t* delmap;
   uint64_t* vregs;
-  int32_t* inv;   // invariant-check scratch (debug; nullptr when off)
+  FKS_LDS int32_t* inv;   // invariant-check scratch (debug; unused when off)
 };
 template <bool GHEAP>
 __device__ __forceinline__ Slot policy_slot(const DevWorkload& W, uint64_t* gheap, int p) {
   extern __shared__ uint64_t lds_raw[];
-  uint64_t* lds = lds_raw + W.inv_words;   // [invariant scratch | policy layout]
+  FKS_LDS uint64_t* lds0 = lds_ptr(lds_raw);
+  FKS_LDS uint64_t* lds = lds0 + W.inv_words;   // [invariant scratch | policy layout]
   const int N = W.n_pods;
   Slot s;
-  s.inv = W.inv_words > 0 ? reinterpret_cast<int32_t*>(lds_raw) : nullptr;
+  s.inv = reinterpret_cast<FKS_LDS int32_t*>(lds0);
   if (GHEAP) {
-    s.h = gheap + (size_t)p * lds_heap_entries(N);
-    s.delmap = reinterpret_cast<uint32_t*>(lds);
+    s.h = global_ptr(gheap + (size_t)p * lds_heap_entries(N));
+    s.delmap = reinterpret_cast<FKS_LDS uint32_t*>(lds);
     s.top = lds + lds_delmap_words(N) / 2;
     s.T = W.heap_top;
-    s.vregs = s.top + W.heap_top;
+    s.vregs = lds_raw + W.inv_words + lds_delmap_words(N) / 2 + W.heap_top;
   } else {
-    s.h = lds;
+    s.h = global_ptr(gheap);   // never dereferenced: T covers the whole heap
     s.top = lds;
     s.T = lds_heap_entries(N);
-    s.delmap = reinterpret_cast<uint32_t*>(lds + lds_heap_entries(N));
-    s.vregs = lds + lds_vreg_offset(N);
+    s.delmap = reinterpret_cast<FKS_LDS uint32_t*>(lds + lds_heap_entries(N));
+    s.vregs = lds_raw + W.inv_words + lds_vreg_offset(N);
   }
   return s;
 }

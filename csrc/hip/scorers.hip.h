@@ -60,8 +60,9 @@ struct BuiltinScorerDev {
     // weights are re-read (scalar-cache hits) at every call rather than held in
     // SGPRs across the event loop: the opaque pointer stops the compiler from
     // hoisting the loads and spilling 8-32 SGPRs per event
-    const double* q = reinterpret_cast<const double*>(uniu64(reinterpret_cast<uint64_t>(wp)));
-    asm volatile("" : "+s"(q));
+    const double* qg = reinterpret_cast<const double*>(uniu64(reinterpret_cast<uint64_t>(wp)));
+    asm volatile("" : "+s"(qg));
+    const FKS_CONST double* q = const_ptr(qg);   // scalar loads
     double w[kWeights];
 #pragma unroll
     for (int k = 0; k < kWeights; ++k) w[k] = k < family_weights(FAM) ? q[k] : 0.0;

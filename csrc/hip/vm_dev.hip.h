@@ -384,7 +384,7 @@ struct VmScorerDev {
     int lexc = EXC_NONE;
     PyN result = pi(0);
     bool has_result = false;
-    uint64_t* R = vregs + lane;
+    FKS_LDS uint64_t* R = lds_ptr(vregs) + lane;
     // registers [0, kVgprRegs) live in VGPRs (uniform index -> s_set_gpr_idx
     // relative addressing, no LDS round trip); the compiler numbers registers
     // by use count, so the hot ones land here.  The rest live in LDS.
