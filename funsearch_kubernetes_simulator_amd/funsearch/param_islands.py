@@ -107,15 +107,25 @@ def make_islands(n: int, family: str, n_candidates: int, elite_size: int, seed: 
             for i in range(n)]
 
 
-def migrate(islands: List[ParamIsland], k: int, all_gather=None) -> None:
-    """Ring migration over the global island index (rank-major)."""
-    local = np.stack([isl.migrants(k) for isl in islands])      # [I, k, R]
-    glob = all_gather(local) if all_gather is not None else local[None]   # [W, I, k, R]
-    W, I = glob.shape[0], glob.shape[1]
+def migration_records(islands: List[ParamIsland], k: int) -> np.ndarray:
+    """[I, k, 1 + K]: every local island's best k members (score, weights)."""
+    return np.stack([isl.migrants(k) for isl in islands])
+
+
+def inject(islands: List[ParamIsland], glob: np.ndarray, rank: int = 0) -> None:
+    """Ring migration over the global island index (rank-major): island g
+    receives island g-1's migrants.  glob: [W, I, k, R] all-gathered records."""
+    W, I, k = glob.shape[0], glob.shape[1], glob.shape[2]
     flat = glob.reshape(W * I, k, -1)
-    from .. parallel.dist import context
-    rank = context().rank if all_gather is not None else 0
     for li, isl in enumerate(islands):
         g = rank * I + li
         src = (g - 1) % (W * I)
         isl.accept(flat[src])
+
+
+def migrate(islands: List[ParamIsland], k: int, all_gather=None) -> None:
+    """Synchronous ring migration (an RCCL all-gather across ranks)."""
+    local = migration_records(islands, k)
+    glob = all_gather(local) if all_gather is not None else local[None]   # [W, I, k, R]
+    from ..parallel.dist import context
+    inject(islands, glob, context().rank if all_gather is not None else 0)

@@ -96,6 +96,33 @@ def all_gather_array(x: np.ndarray) -> np.ndarray:
     return np.stack([o.cpu().numpy() for o in out])
 
 
+class PendingGather:
+    """Handle of a non-blocking all-gather; `wait()` -> [world, *shape]."""
+
+    def __init__(self, work=None, out=None, ready: Optional[np.ndarray] = None):
+        self._work, self._out, self._ready = work, out, ready
+
+    def wait(self) -> np.ndarray:
+        if self._ready is None:
+            self._work.wait()
+            self._ready = np.stack([o.cpu().numpy() for o in self._out])
+        return self._ready
+
+
+def all_gather_array_async(x: np.ndarray) -> PendingGather:
+    """Start an all-gather and return at once (RCCL runs it on its own stream
+    while the caller keeps the GPU busy); the result is read with `.wait()`."""
+    ctx = context()
+    if not ctx.distributed:
+        return PendingGather(ready=x[None].copy())
+    import torch
+    import torch.distributed as dist
+    t = torch.from_numpy(np.ascontiguousarray(x)).to(ctx.device)
+    out = [torch.empty_like(t) for _ in range(ctx.world_size)]
+    work = dist.all_gather(out, t, async_op=True)
+    return PendingGather(work, out)
+
+
 def all_reduce_max(v: float) -> float:
     ctx = context()
     if not ctx.distributed:

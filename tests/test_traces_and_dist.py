@@ -75,6 +75,8 @@ def test_gloo_collectives_and_migration(tmp_path):
         "x = np.full((2, 3), ctx.rank, dtype=np.float64)\n"
         "g = dist.all_gather_array(x)\n"
         "assert g.shape == (2, 2, 3) and g[1].max() == 1\n"
+        "pg = dist.all_gather_array_async(x + 5)\n"
+        "assert np.array_equal(pg.wait(), g + 5)\n"
         "assert dist.all_reduce_max(ctx.rank * 10.0) == 10.0\n"
         "isl = make_islands(2, 'random_linear', 4, 3, seed=ctx.rank)\n"
         "for i in isl:\n"
