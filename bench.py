@@ -79,7 +79,11 @@ def main() -> None:
         workload = synthetic_workload(n_nodes=args.nodes, n_pods=args.pods, seed=0)
     else:
         workload = load_default_workload()
-    device = ctx.local_rank if args.device == "gpu" else "cpu"
+    if args.device == "gpu":
+        import torch
+        device = ctx.local_rank % max(1, torch.cuda.device_count())   # one rank per GPU (wraps on smaller boxes)
+    else:
+        device = "cpu"
     # the per-event trace hash only serves cross-engine equality tests: off here
     ev = Evaluator(workload, device=device, options={"heap_mode": args.heap_mode, "trace_hash": False},
                    n_slots=max(1, args.islands))
@@ -91,7 +95,7 @@ def main() -> None:
     def sync():
         if args.device == "gpu":
             import torch
-            torch.cuda.synchronize()
+            torch.cuda.synchronize(device)
         dist.barrier()
 
     best_row = [None, -1.0, None, -1]   # table row, score, weights, generation

@@ -56,7 +56,8 @@ def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = No
     if use_gpu is None:
         use_gpu = torch.cuda.is_available()
     if backend is None:
-        backend = "nccl" if use_gpu else "gloo"
+        # FKS_DIST_BACKEND=gloo rehearses multi-rank GPU runs on a single-GPU box
+        backend = os.environ.get("FKS_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     device = torch.device("cpu")
     if backend == "nccl":
         torch.cuda.set_device(local)
