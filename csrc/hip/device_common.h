@@ -3,8 +3,28 @@
 // event-key layout of the LDS heap.
 #pragma once
 
+#ifndef __HIPCC_RTC__   // hiprtc (policy JIT) provides these itself
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#else
+using __hip_internal::int8_t;
+using __hip_internal::int16_t;
+using __hip_internal::int32_t;
+using __hip_internal::int64_t;
+using __hip_internal::uint8_t;
+using __hip_internal::uint16_t;
+using __hip_internal::uint32_t;
+using __hip_internal::uint64_t;
+#ifndef INT64_MAX
+#define INT64_MAX 0x7fffffffffffffffLL
+#endif
+#ifndef INT64_MIN
+#define INT64_MIN (-INT64_MAX - 1)
+#endif
+#ifndef INT32_MAX
+#define INT32_MAX 0x7fffffff
+#endif
+#endif
 
 namespace fksd {
 

@@ -72,23 +72,30 @@ struct DevBuf {
   T* as() const { return reinterpret_cast<T*>(p); }
 };
 
-// pinned host staging (async copies need page-locked memory)
+// Pinned, device-mapped host memory.  Batch inputs (family ids, weights) are
+// read by the kernels straight from here and the result table is written
+// straight back (zero-copy): no copy kernels queue behind the replay waves
+// that already fill the CUs.
 struct HostBuf {
-  void* p = nullptr;
+  void* p = nullptr;   // host address
+  void* d = nullptr;   // device address of the same pages
   size_t cap = 0;
   void reserve(size_t bytes) {
     if (bytes <= cap) return;
     if (p) HIP_OK(hipHostFree(p));
-    HIP_OK(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc(&p, bytes, hipHostMallocMapped));
+    HIP_OK(hipHostGetDevicePointer(&d, p, 0));
     cap = bytes;
   }
   void release() {
     if (p) (void)hipHostFree(p);
-    p = nullptr;
+    p = d = nullptr;
     cap = 0;
   }
   template <class T>
   T* as() const { return reinterpret_cast<T*>(p); }
+  template <class T>
+  T* dev() const { return reinterpret_cast<T*>(d); }
 };
 
 struct Slot {
@@ -309,7 +316,9 @@ class DeviceEngine {
       const fksk::VmArgs a{Wl, wc, table(s), s.res.as<DevResult>(), budget_, nregs, gh, s.prof.as<uint64_t>()};
       HIP_OK(fksk::launch_vm_prof(g, P, lds, s.stream, a));
     } else {
-      const fksk::BuiltinArgs a{Wl, wc, s.fam.as<int32_t>(), s.w.as<double>(), s.res.as<DevResult>(), gh,
+      const size_t wb = (size_t)P * kWeights * 8;
+      const fksk::BuiltinArgs a{Wl, wc, reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + wb),
+                                s.h_in.dev<double>(), s.w.as<double>(), s.res.as<DevResult>(), gh,
                                 s.prof.as<uint64_t>()};
       HIP_OK(fksk::launch_builtin_prof(g, P, lds, s.stream, a));
     }
@@ -338,6 +347,7 @@ class DeviceEngine {
 
  private:
   static constexpr size_t kMaxLds = 160 * 1024;
+  static constexpr int kWeightWords = kWeights;   // LDS copy of a builtin policy's weights
   static constexpr size_t kPoliciesPerCu = 16;   // HBM-heap builtin kernels: 4 waves per SIMD
   static constexpr size_t kVmPoliciesPerCu = 8;  // HBM-heap VM kernels: 2 waves per SIMD
 
@@ -370,7 +380,7 @@ class DeviceEngine {
 
   size_t lds_bytes(bool g, int top, int nregs) const {
     const size_t vregs = (size_t)nregs * 64 * 8;
-    const size_t inv = (size_t)W_.inv_words * 8;
+    const size_t inv = (size_t)(W_.inv_words + kWeightWords) * 8;
     return inv + (g ? delmap_bytes_ + (size_t)top * 8 + vregs : heap_bytes_ + delmap_bytes_ + vregs);
   }
 
@@ -381,7 +391,7 @@ class DeviceEngine {
     if (heap_top_opt_ >= 0) return std::min(heap_top_opt_, entries);
     const size_t per_cu = vm ? kVmPoliciesPerCu : (npass_ >= 4 ? 8 : npass_ == 2 ? 12 : kPoliciesPerCu);
     const size_t budget = kMaxLds / per_cu;
-    const size_t fixed = delmap_bytes_ + (size_t)nregs * 64 * 8 + (size_t)W_.inv_words * 8;
+    const size_t fixed = delmap_bytes_ + (size_t)nregs * 64 * 8 + (size_t)(W_.inv_words + kWeightWords) * 8;
     int T = 0;
     while (T < entries && fixed + (size_t)(2 * T + 1) * 8 <= budget) T = 2 * T + 1;
     return std::min(T, entries);
@@ -405,10 +415,8 @@ class DeviceEngine {
 
   void ensure_batch(Slot& s, int P) {
     s.res.reserve(sizeof(DevResult) * (size_t)P);
-    s.tab.reserve(sizeof(double) * 13 * (size_t)P);
-    s.fam.reserve(sizeof(int32_t) * (size_t)P);
-    s.w.reserve(sizeof(double) * kWeights * (size_t)P);
     s.h_tab.reserve(sizeof(double) * 13 * (size_t)P);
+    s.w.reserve(sizeof(double) * kWeights * (size_t)P);
     s.P = P;
   }
 
@@ -422,10 +430,8 @@ class DeviceEngine {
     const size_t fb = (size_t)P * 4, wb = (size_t)P * kWeights * 8;
     s.h_in.reserve(fb + wb + 16);
     char* h = s.h_in.as<char>();
-    std::memcpy(h, weights, wb);
+    std::memcpy(h, weights, wb);   // read by the kernel prologue through the mapping
     std::memcpy(h + wb, fam, fb);
-    HIP_OK(hipMemcpyAsync(s.w.p, h, wb, hipMemcpyHostToDevice, s.stream));
-    HIP_OK(hipMemcpyAsync(s.fam.p, h + wb, fb, hipMemcpyHostToDevice, s.stream));
   }
 
   void stage_programs(Slot& s, py::bytes blob, py::array_t<int32_t> offsets, py::array_t<int32_t> lengths,
@@ -468,8 +474,9 @@ class DeviceEngine {
     const size_t lds = lds_bytes(g, Wl.heap_top, 0);
     if (lds > kMaxLds) throw std::invalid_argument("replay layout exceeds the 160 KiB LDS");
     uint64_t* gh = g ? gheap_for(s, P) : nullptr;
-    const fksk::BuiltinArgs a{Wl, upload_workload(s, Wl), s.fam.as<int32_t>(), s.w.as<double>(),
-                              s.res.as<DevResult>(), gh, nullptr};
+    const size_t wb = (size_t)P * kWeights * 8;
+    const fksk::BuiltinArgs a{Wl, upload_workload(s, Wl), reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + wb),
+                              s.h_in.dev<double>(), s.w.as<double>(), s.res.as<DevResult>(), gh, nullptr};
     if (npass_ == 1) HIP_OK(fksk::launch_builtin_np1(g, s.fam_spec, P, lds, s.stream, a));
     else if (npass_ == 2) HIP_OK(fksk::launch_builtin_np2(g, s.fam_spec, P, lds, s.stream, a));
     else HIP_OK(fksk::launch_builtin_np4(g, s.fam_spec, P, lds, s.stream, a));
@@ -490,10 +497,14 @@ class DeviceEngine {
 
   // the launch's workload struct, also resident in HBM (the kernels' cold-field copy)
   const DevWorkload* upload_workload(Slot& s, const DevWorkload& Wl) {
+    // the device copy is re-sent only when the launch configuration changes
+    const bool fresh = s.wc.p == nullptr;
     s.wc.reserve(sizeof(DevWorkload));
     s.h_wc.reserve(sizeof(DevWorkload));
-    std::memcpy(s.h_wc.p, &Wl, sizeof(DevWorkload));
-    HIP_OK(hipMemcpyAsync(s.wc.p, s.h_wc.p, sizeof(DevWorkload), hipMemcpyHostToDevice, s.stream));
+    if (fresh || std::memcmp(s.h_wc.p, &Wl, sizeof(DevWorkload)) != 0) {
+      std::memcpy(s.h_wc.p, &Wl, sizeof(DevWorkload));
+      HIP_OK(hipMemcpyAsync(s.wc.p, s.h_wc.p, sizeof(DevWorkload), hipMemcpyHostToDevice, s.stream));
+    }
     return s.wc.as<const DevWorkload>();
   }
 
@@ -501,9 +512,8 @@ class DeviceEngine {
   void finish(Slot& s) {
     const int P = s.P;
     hipLaunchKernelGGL(k_eval_reduce, dim3((P + 63) / 64), dim3(64), 0, s.stream, s.res.as<DevResult>(),
-                       s.tab.as<double>(), P);
+                       s.h_tab.dev<double>(), P);   // zero-copy into the pinned result table
     HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(s.h_tab.p, s.tab.p, sizeof(double) * 13 * (size_t)P, hipMemcpyDeviceToHost, s.stream));
     HIP_OK(hipEventRecord(s.done, s.stream));
     s.busy = true;
   }

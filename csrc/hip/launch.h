@@ -20,7 +20,8 @@ struct BuiltinArgs {
   DevWorkload W;
   const DevWorkload* Wc;  // the same workload struct, resident in HBM (cold fields)
   const int32_t* fam;     // [P] family id per policy
-  const double* weights;  // [P, kWeights]
+  const double* weights;  // [P, kWeights] (pinned host memory, device-mapped)
+  double* wdev;           // [P, kWeights] device copy written by the kernel prologue
   DevResult* out;
   uint64_t* gheap;        // HBM heap slices (GHEAP) or nullptr
   uint64_t* prof;         // [P, 8] phase cycles (profiling launches only)

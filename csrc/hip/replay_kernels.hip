@@ -28,6 +28,7 @@ namespace {
 //   GHEAP = true : heap in its HBM slice, LDS = bitmap | heap top (W.heap_top
 //                  slots) | vregs (16 policies/CU)
 struct Slot {
+  FKS_LDS double* w;       // builtin policy weights, copied in by the prologue
   FKS_GLOBAL uint64_t* h;
   FKS_LDS uint64_t* top;
   int T;
@@ -39,22 +40,24 @@ template <bool GHEAP>
 __device__ __forceinline__ Slot policy_slot(const DevWorkload& W, uint64_t* gheap, int p) {
   extern __shared__ uint64_t lds_raw[];
   FKS_LDS uint64_t* lds0 = lds_ptr(lds_raw);
-  FKS_LDS uint64_t* lds = lds0 + W.inv_words;   // [invariant scratch | policy layout]
+  // [invariant scratch | builtin weights (kWeights doubles) | policy layout]
+  FKS_LDS uint64_t* lds = lds0 + W.inv_words + kWeights;
   const int N = W.n_pods;
   Slot s;
   s.inv = reinterpret_cast<FKS_LDS int32_t*>(lds0);
+  s.w = reinterpret_cast<FKS_LDS double*>(lds0 + W.inv_words);
   if (GHEAP) {
     s.h = global_ptr(gheap + (size_t)p * lds_heap_entries(N));
     s.delmap = reinterpret_cast<FKS_LDS uint32_t*>(lds);
     s.top = lds + lds_delmap_words(N) / 2;
     s.T = W.heap_top;
-    s.vregs = lds_raw + W.inv_words + lds_delmap_words(N) / 2 + W.heap_top;
+    s.vregs = lds_raw + W.inv_words + kWeights + lds_delmap_words(N) / 2 + W.heap_top;
   } else {
     s.h = global_ptr(gheap);   // never dereferenced: T covers the whole heap
     s.top = lds;
     s.T = lds_heap_entries(N);
     s.delmap = reinterpret_cast<FKS_LDS uint32_t*>(lds + lds_heap_entries(N));
-    s.vregs = lds_raw + W.inv_words + lds_vreg_offset(N);
+    s.vregs = lds_raw + W.inv_words + kWeights + lds_vreg_offset(N);
   }
   return s;
 }
@@ -64,6 +67,21 @@ __device__ __forceinline__ Slot policy_slot(const DevWorkload& W, uint64_t* ghea
 #define FKS_BOUNDS(G) __launch_bounds__(64, (G) ? 4 : 1)
 // The VM keeps its hot virtual registers in VGPRs (vm_dev.hip.h): 2 waves/SIMD.
 #define FKS_VM_BOUNDS(G) __launch_bounds__(64, (G) ? 2 : 1)
+
+// Prologue: the batch's family ids / weights live in pinned host memory
+// (zero-copy, no copy kernel queued behind busy CUs); each policy moves its 16
+// weights into its slot of a device buffer once, which the scorer then reads
+// through the scalar cache.
+template <int FAM>
+__device__ __forceinline__ void load_policy(BuiltinScorerDev<FAM>& sc, const Slot&, const fksk::BuiltinArgs& a,
+                                            int p) {
+  const int lane = lane_id();
+  double* wd = a.wdev + (size_t)p * kWeights;
+  if (lane < kWeights) wd[lane] = a.weights[(size_t)p * kWeights + lane];
+  const int fam = uni(lane == 0 ? a.fam[p] : 0);
+  __threadfence();   // stores visible to the scalar loads that follow
+  sc.load(fam, wd);
+}
 
 template <class T>
 hipError_t raise_lds(T* f, int max_lds) {
@@ -89,7 +107,7 @@ __global__ FKS_FAM_BOUNDS(GHEAP, FAM, NPASS) void k_replay_builtin(fksk::Builtin
   const int p = blockIdx.x;
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   BuiltinScorerDev<FAM> sc;
-  sc.load(a.fam[p], a.weights + (size_t)p * kWeights);
+  load_policy<FAM>(sc, s, a, p);
   replay_one<NPASS>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p);
 }
 
@@ -140,7 +158,7 @@ __global__ FKS_BOUNDS(GHEAP) void k_replay_builtin_prof(fksk::BuiltinArgs a) {
   const int p = blockIdx.x;
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   BuiltinScorerDev<-1> sc;
-  sc.load(a.fam[p], a.weights + (size_t)p * kWeights);
+  load_policy<-1>(sc, s, a, p);
   replay_one<1, BuiltinScorerDev<-1>, PhaseProf>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p,
                                                  a.prof + (size_t)p * 8);
 }

@@ -47,9 +47,9 @@ __host__ __device__ constexpr int family_weights(int fam) {
 template <int FAM = -1>
 struct BuiltinScorerDev {
   int32_t family;
-  const double* wp;   // this policy's kWeights weights (HBM)
+  const double* wp;   // this policy's kWeights weights (device copy, HBM)
 
-  __device__ void load(int32_t fam_id, const double* __restrict__ p) {
+  __device__ void load(int32_t fam_id, const double* p) {
     family = FAM >= 0 ? FAM : fam_id;
     wp = p;
   }
@@ -57,6 +57,9 @@ struct BuiltinScorerDev {
   template <int NPASS>
   __device__ int64_t score(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, int& exc) const {
     if (!feasible<NPASS>(ps, nr, pod)) return 0;
+    // weights are re-read (scalar-cache hits) at every call rather than held in
+    // SGPRs across the event loop: the opaque pointer stops the compiler from
+    // hoisting the loads and spilling 8-32 SGPRs per event
     // weights are re-read (scalar-cache hits) at every call rather than held in
     // SGPRs across the event loop: the opaque pointer stops the compiler from
     // hoisting the loads and spilling 8-32 SGPRs per event

@@ -106,17 +106,21 @@ class OpenAICompatibleClient(BaseClient):
             try:
                 r = requests.post(f"{self.base_url}/chat/completions", headers=headers, data=json.dumps(body),
                                   timeout=self.timeout_s)
+            except Exception as exc:  # network errors are retried
+                err = exc
+            else:
                 if r.status_code == 200:
                     text = r.json()["choices"][0]["message"]["content"]
                     with self._lock:
                         self.calls += 1
                     return _response(text, time.time() - t0)
                 if r.status_code not in (408, 409, 425, 429, 500, 502, 503, 504):
-                    raise RuntimeError(f"LLM HTTP {r.status_code}: {r.text[:200]}")
+                    with self._lock:
+                        self.failures += 1
+                    raise RuntimeError(f"LLM HTTP {r.status_code}: {r.text[:200]}")   # not retryable
                 err = RuntimeError(f"LLM HTTP {r.status_code}")
-            except Exception as exc:  # network errors are retried
-                err = exc
-            time.sleep(self.backoff_s * (2 ** attempt) * (0.5 + random.random()))
+            if attempt < self.max_retries:
+                time.sleep(self.backoff_s * (2 ** attempt) * (0.5 + random.random()))
         with self._lock:
             self.failures += 1
         raise RuntimeError(f"LLM request failed after {self.max_retries + 1} attempts: {err}")

@@ -146,3 +146,44 @@ def test_runaway_program_is_bounded():
     code = "def priority_function(pod, node):\n    x = 0\n    while True:\n        x += 1\n    return 1\n"
     r = ev.evaluate_programs([code])[0]
     assert (r.score, r.exc, r.engine) == (0.0, int(Exc.BUDGET), "object")
+
+
+def test_openai_compatible_client_retries_and_parses():
+    """OpenAI-compatible HTTP backend against a local stub server: 503 is retried, 401 is not."""
+    import http.server
+    import threading
+    from funsearch_kubernetes_simulator_amd.funsearch.llm import OpenAICompatibleClient
+    seen = []
+
+    class H(http.server.BaseHTTPRequestHandler):
+        def log_message(self, *a):
+            pass
+
+        def do_POST(self):
+            body = json.loads(self.rfile.read(int(self.headers["Content-Length"])))
+            seen.append((self.path, self.headers.get("Authorization"), body["model"]))
+            if body["model"] == "deny":
+                self.send_response(401); self.end_headers(); self.wfile.write(b"no"); return
+            if len(seen) == 1:
+                self.send_response(503); self.end_headers(); return
+            out = json.dumps({"choices": [{"message": {"content": "    score = 1.0"}}]}).encode()
+            self.send_response(200)
+            self.send_header("Content-Type", "application/json")
+            self.send_header("Content-Length", str(len(out)))
+            self.end_headers()
+            self.wfile.write(out)
+
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        c = OpenAICompatibleClient("k123", f"http://127.0.0.1:{srv.server_address[1]}/v1", timeout_s=5,
+                                   max_retries=2, backoff_s=0.01)
+        r = c.chat.completions.create(model="m", messages=[{"role": "user", "content": "hi"}])
+        assert r.choices[0].message.content == "    score = 1.0"
+        assert seen[0] == ("/v1/chat/completions", "Bearer k123", "m") and len(seen) == 2
+        n = len(seen)
+        with pytest.raises(RuntimeError):
+            c.chat.completions.create(model="deny", messages=[])
+        assert len(seen) == n + 1      # not retried
+    finally:
+        srv.shutdown()
