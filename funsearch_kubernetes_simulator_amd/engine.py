@@ -149,6 +149,10 @@ class Evaluator:
         # below this many programs a batch runs faster on the CPU VM (one replay per
         # core, ~0.1 s each) than as a handful of latency-bound device waves
         self.device_min_batch = int(self.options.pop("device_min_batch", 128))
+        # fault-injection hook: fail this fraction of program
+        # evaluations as if the replay had raised -> score 0, like the reference
+        self.fault_rate = float(self.options.pop("fault_rate", 0.0) or 0.0)
+        self._fault_rng = np.random.default_rng(int(self.options.pop("fault_seed", 0)))
         self.device = None
         want_gpu = device not in ("cpu", None)
         if want_gpu:
@@ -247,6 +251,11 @@ class Evaluator:
             for i, r in zip(rest, results):
                 out[i] = r
                 self.stats["object"] += 1
+        if self.fault_rate > 0:
+            for i in range(n):
+                if self._fault_rng.random() < self.fault_rate:
+                    out[i] = EvalResult(0.0, int(Exc.VALUE), "fault-injection")
+                    self.stats["faults"] = self.stats.get("faults", 0) + 1
         return out  # type: ignore[return-value]
 
     def _object_engine_ok(self) -> bool:

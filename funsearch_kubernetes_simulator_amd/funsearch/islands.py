@@ -49,6 +49,12 @@ class IslandFunSearch:
         opts = {}
         if "min_batch" in (self.config.get("device") or {}):
             opts["device_min_batch"] = int(self.config["device"]["min_batch"])
+        fi = self.config.get("fault_injection") or {}
+        if fi.get("eval_failure_rate"):
+            opts["fault_rate"] = float(fi["eval_failure_rate"])
+            opts["fault_seed"] = int(fi.get("seed", 0))
+        if fi.get("llm_failure_rate"):
+            self.config.setdefault("llm", {})["fault_rate"] = float(fi["llm_failure_rate"])
         self.evaluator = evaluator or Evaluator(device=dev, options=opts)
         llm_cfg = dict(self.config.get("llm") or {})
         base_seed = int(llm_cfg.get("seed", 0)) + 1000003 * self.ctx.rank

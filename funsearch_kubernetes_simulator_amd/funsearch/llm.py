@@ -285,12 +285,37 @@ class MutationClient(BaseClient):
         return "\n".join(out).lstrip()
 
 
+class FaultInjectingClient(BaseClient):
+    """Wraps a client and fails a fraction of requests (SURVEY section 5.3
+    fault-injection hook): the search must treat them like real LLM errors."""
+
+    def __init__(self, inner: BaseClient, rate: float, seed: int = 0):
+        super().__init__()
+        self.inner, self.rate = inner, float(rate)
+        self._rng = random.Random(seed)
+        self.injected = 0
+
+    def _create(self, **kw) -> ChatResponse:
+        with self._lock:
+            fail = self._rng.random() < self.rate
+            if fail:
+                self.injected += 1
+        if fail:
+            raise RuntimeError("injected LLM failure")
+        return self.inner._create(**kw)
+
+
 def make_client(cfg: dict) -> BaseClient:
-    """Client from the ``llm`` / ``openrouter`` section of a config."""
+    """Client from the ``llm`` / ``openrouter`` section of a config
+    (``fault_rate`` > 0 wraps it in a `FaultInjectingClient`)."""
     backend = cfg.get("backend", "openai")
     if backend in ("mutation", "offline"):
-        return MutationClient(int(cfg.get("seed", 0)))
-    if backend == "scripted":
-        return ScriptedClient(cfg["responses"])
-    return OpenAICompatibleClient(cfg.get("api_key"), cfg.get("base_url", "https://openrouter.ai/api/v1"),
-                                  float(cfg.get("timeout_s", 60)), int(cfg.get("max_retries", 4)))
+        client: BaseClient = MutationClient(int(cfg.get("seed", 0)))
+    elif backend == "scripted":
+        client = ScriptedClient(cfg["responses"])
+    else:
+        client = OpenAICompatibleClient(cfg.get("api_key"), cfg.get("base_url", "https://openrouter.ai/api/v1"),
+                                        float(cfg.get("timeout_s", 60)), int(cfg.get("max_retries", 4)))
+    if float(cfg.get("fault_rate", 0) or 0) > 0:
+        client = FaultInjectingClient(client, float(cfg["fault_rate"]), int(cfg.get("seed", 0)) + 17)
+    return client

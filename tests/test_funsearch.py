@@ -187,3 +187,14 @@ def test_openai_compatible_client_retries_and_parses():
         assert len(seen) == n + 1      # not retried
     finally:
         srv.shutdown()
+
+
+def test_search_survives_injected_faults(tmp_path):
+    """Fault-injection hooks (LLM failures, failing evaluations) do not stop the search."""
+    cfg = _cfg(tmp_path)
+    cfg["islands"] = {"per_rank": 2, "migrate_every": 1, "migrants": 1}
+    cfg["fault_injection"] = {"llm_failure_rate": 0.3, "eval_failure_rate": 0.3, "seed": 1}
+    code, score = run_funsearch(cfg, generations=3)
+    assert score >= reference_scores()["best_fit"]
+    logs = [json.loads(l) for l in open(tmp_path / "log.jsonl")]
+    assert logs[-1]["generation"] == 3
