@@ -9,6 +9,7 @@
 
 #include "builtin_scorers.hpp"
 #include "engine.hpp"
+#include "parallel.hpp"
 #include "trace_io.hpp"
 #include "vm_cpu.hpp"
 
@@ -92,15 +93,6 @@ void fill_row(double* row, const SimResult& r) {
   row[10] = (double)r.exc; row[11] = r.inexact ? 1.0 : 0.0; row[12] = (double)(r.trace_hash >> 11);
 }
 
-template <class Fn>
-void parallel_for(int64_t n, int threads, Fn fn) {
-  if (threads <= 1 || n <= 1) { for (int64_t i = 0; i < n; ++i) fn(i); return; }
-  std::atomic<int64_t> next{0};
-  std::vector<std::thread> pool;
-  for (int t = 0; t < threads; ++t)
-    pool.emplace_back([&] { for (int64_t i; (i = next.fetch_add(1)) < n;) fn(i); });
-  for (auto& th : pool) th.join();
-}
 
 }  // namespace
 
@@ -110,6 +102,38 @@ py::array_t<T> np_of(const std::vector<T>& v) {
   if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(T));
   return a;
 }
+
+namespace fks {
+
+// One-shot evaluation for compiler unit tests: a single node.
+static pybind11::object vm_score_once(const Program& prog, const pybind11::dict& pod, const pybind11::dict& node,
+                                      const std::vector<int64_t>& gl, const std::vector<int64_t>& gt,
+                                      const std::vector<int64_t>& gm) {
+  namespace py = pybind11;
+  VmCore vm(prog, 1000000);
+  vm.resize(1);
+  std::vector<int32_t> gl32(gl.begin(), gl.end()), gt32(gt.begin(), gt.end());
+  int64_t cpu_left = node["cpu_milli_left"].cast<int64_t>(), cpu_total = node["cpu_milli_total"].cast<int64_t>();
+  int64_t mem_left = node["memory_mib_left"].cast<int64_t>(), mem_total = node["memory_mib_total"].cast<int64_t>();
+  int32_t gpu_left = node["gpu_left"].cast<int32_t>();
+  int32_t ngpus = (int32_t)gl.size();
+  int32_t gstart[2] = {0, ngpus};
+  VmCore::World W;
+  W.pod[PF_CPU] = pod["cpu_milli"].cast<int64_t>(); W.pod[PF_MEM] = pod["memory_mib"].cast<int64_t>();
+  W.pod[PF_NGPU] = pod["num_gpu"].cast<int64_t>(); W.pod[PF_GMILLI] = pod["gpu_milli"].cast<int64_t>();
+  W.pod[PF_CTIME] = pod["creation_time"].cast<int64_t>(); W.pod[PF_DUR] = pod["duration_time"].cast<int64_t>();
+  W.cpu_left = &cpu_left; W.cpu_total = &cpu_total; W.mem_left = &mem_left; W.mem_total = &mem_total;
+  W.gpu_left = &gpu_left; W.ngpus = &ngpus; W.gpu_start = gstart;
+  W.gmilli_left = gl32.data(); W.gmilli_total = gt32.data(); W.gmem_left = gm.data(); W.gmem_total = gm.data();
+  bool ok = vm.run(W);
+  if (!ok) return py::make_tuple("exc", vm.exc);
+  if (!vm.has_result[0]) return py::make_tuple("none", 0);
+  const PyNum& v = vm.result[0];
+  if (v.fl) return py::make_tuple("float", v.f);
+  return py::make_tuple("int", v.i);
+}
+
+}  // namespace fks
 
 PYBIND11_MODULE(_fks_cpu, m) {
   m.def("load_pod_csv", [](const std::string& path) {
@@ -176,7 +200,7 @@ PYBIND11_MODULE(_fks_cpu, m) {
 
   m.def("simulate_program", [](const Workload& w, py::bytes code, std::vector<double> fconst,
                                std::vector<int64_t> iconst, std::vector<uint8_t> ctag, py::dict opts) {
-    Program prog = make_program(code, fconst, iconst, ctag);
+    Program prog = make_program(std::string(code), fconst, iconst, ctag);
     SimOptions o = make_options(opts);
     SimResult r;
     {
@@ -195,7 +219,7 @@ PYBIND11_MODULE(_fks_cpu, m) {
                                      std::vector<std::vector<uint8_t>> ctags, py::dict opts, int threads) {
     const int64_t P = (int64_t)codes.size();
     std::vector<Program> progs;
-    for (int64_t i = 0; i < P; ++i) progs.push_back(make_program(codes[i], fconsts[i], iconsts[i], ctags[i]));
+    for (int64_t i = 0; i < P; ++i) progs.push_back(make_program(std::string(codes[i]), fconsts[i], iconsts[i], ctags[i]));
     SimOptions o = make_options(opts);
     py::array_t<double> out({P, (int64_t)kCols});
     double* op = out.mutable_data();
@@ -216,7 +240,7 @@ PYBIND11_MODULE(_fks_cpu, m) {
                                  std::vector<uint8_t> ctag, py::dict pod, py::dict node, std::vector<int64_t> gpu_left,
                                  std::vector<int64_t> gpu_total, std::vector<int64_t> gpu_mem) {
     // Single (pod, node) evaluation of a program; used by compiler unit tests.
-    Program prog = make_program(code, fconst, iconst, ctag);
+    Program prog = make_program(std::string(code), fconst, iconst, ctag);
     return vm_score_once(prog, pod, node, gpu_left, gpu_total, gpu_mem);
   });
 

@@ -6,10 +6,9 @@
 // one of them, and tests diff them event by event (trace_hash).
 #pragma once
 
-#include <pybind11/pybind11.h>
-#include <pybind11/stl.h>
-
+#include <algorithm>
 #include <cstring>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -26,10 +25,9 @@ struct Program {
   int nregs = 0;
 };
 
-inline Program make_program(const pybind11::bytes& code, const std::vector<double>& fconst,
+inline Program make_program(const std::string& s, const std::vector<double>& fconst,
                             const std::vector<int64_t>& iconst, const std::vector<uint8_t>& ctag) {
   Program p;
-  std::string s = code;
   if (s.size() % sizeof(Insn)) throw std::invalid_argument("bytecode length must be a multiple of 8");
   p.code.resize(s.size() / sizeof(Insn));
   std::memcpy(p.code.data(), s.data(), s.size());
@@ -446,33 +444,5 @@ struct VmScorer {
     return o;
   }
 };
-
-// One-shot evaluation for compiler unit tests: a single node.
-inline pybind11::object vm_score_once(const Program& prog, const pybind11::dict& pod, const pybind11::dict& node,
-                                      const std::vector<int64_t>& gl, const std::vector<int64_t>& gt,
-                                      const std::vector<int64_t>& gm) {
-  namespace py = pybind11;
-  VmCore vm(prog, 1000000);
-  vm.resize(1);
-  std::vector<int32_t> gl32(gl.begin(), gl.end()), gt32(gt.begin(), gt.end());
-  int64_t cpu_left = node["cpu_milli_left"].cast<int64_t>(), cpu_total = node["cpu_milli_total"].cast<int64_t>();
-  int64_t mem_left = node["memory_mib_left"].cast<int64_t>(), mem_total = node["memory_mib_total"].cast<int64_t>();
-  int32_t gpu_left = node["gpu_left"].cast<int32_t>();
-  int32_t ngpus = (int32_t)gl.size();
-  int32_t gstart[2] = {0, ngpus};
-  VmCore::World W;
-  W.pod[PF_CPU] = pod["cpu_milli"].cast<int64_t>(); W.pod[PF_MEM] = pod["memory_mib"].cast<int64_t>();
-  W.pod[PF_NGPU] = pod["num_gpu"].cast<int64_t>(); W.pod[PF_GMILLI] = pod["gpu_milli"].cast<int64_t>();
-  W.pod[PF_CTIME] = pod["creation_time"].cast<int64_t>(); W.pod[PF_DUR] = pod["duration_time"].cast<int64_t>();
-  W.cpu_left = &cpu_left; W.cpu_total = &cpu_total; W.mem_left = &mem_left; W.mem_total = &mem_total;
-  W.gpu_left = &gpu_left; W.ngpus = &ngpus; W.gpu_start = gstart;
-  W.gmilli_left = gl32.data(); W.gmilli_total = gt32.data(); W.gmem_left = gm.data(); W.gmem_total = gm.data();
-  bool ok = vm.run(W);
-  if (!ok) return py::make_tuple("exc", vm.exc);
-  if (!vm.has_result[0]) return py::make_tuple("none", 0);
-  const PyNum& v = vm.result[0];
-  if (v.fl) return py::make_tuple("float", v.f);
-  return py::make_tuple("int", v.i);
-}
 
 }  // namespace fks
