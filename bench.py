@@ -46,7 +46,7 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--islands", type=int, default=4, help="islands per GPU")
-    ap.add_argument("--candidates", type=int, default=1536, help="candidates per island per generation")
+    ap.add_argument("--candidates", type=int, default=4096, help="candidates per island per generation")
     ap.add_argument("--elite", type=int, default=32)
     ap.add_argument("--family", default="composite_linear", choices=["random_linear", "feature_linear", "composite_linear"])
     ap.add_argument("--migrate-every", type=int, default=5)

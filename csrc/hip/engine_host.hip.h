@@ -149,6 +149,17 @@ class DeviceEngine {
     W_.pod = dev_upload<int4>(arr("pod"), st, owned_);
     W_.pod_ctime = dev_upload<int32_t>(arr("pod_ctime"), st, owned_);
     W_.heap0 = dev_upload<uint64_t>(arr("heap0"), st, owned_);
+    {
+      // row-kernel image of the initial heap: slot i at address i + 1
+      py::array_t<uint64_t, py::array::c_style | py::array::forcecast> h0(arr("heap0"));
+      const int np = (int)geti("n_pods");
+      py::array_t<uint64_t> shifted((py::ssize_t)row_heap_entries(np));
+      uint64_t* sp = shifted.mutable_data();
+      std::memset(sp, 0, sizeof(uint64_t) * (size_t)row_heap_entries(np));
+      std::memcpy(sp + 1, h0.data(), sizeof(uint64_t) * (size_t)std::min<py::ssize_t>(np, h0.size()));
+      W_.heap0p = dev_upload<uint64_t>(shifted, st, owned_);
+      HIP_OK(hipStreamSynchronize(st));   // `shifted` dies with this scope
+    }
     W_.class_value = dev_upload<int32_t>(arr("class_value"), st, owned_);
     W_.snap_fire = dev_upload<int64_t>(arr("snap_fire"), st, owned_);
     W_.n_fire = (int32_t)arr("snap_fire").size();
@@ -169,6 +180,8 @@ class DeviceEngine {
     heap_bytes_ = (size_t)lds_heap_entries(W_.n_pods) * sizeof(uint64_t);
     delmap_bytes_ = (size_t)lds_delmap_words(W_.n_pods) * 4;
     lds_heap_ok_ = heap_bytes_ + delmap_bytes_ <= kMaxLds;
+    rows_ok_ = npass_ == 1 && W_.n_nodes <= kRow && W_.n_classes <= kRow * kRowClassSlots &&
+               W_.n_pods <= kRowMaxHeap;
     set_attrs();
   }
 
@@ -193,6 +206,13 @@ class DeviceEngine {
       W_.check_every = (int32_t)std::max<int64_t>(0, std::min<int64_t>(k, INT32_MAX));
       W_.inv_words = W_.check_every > 0 ? inv_words_for(npass_) : 0;
     }
+    if (o.contains("row_kernel")) {
+      const std::string m = o["row_kernel"].cast<std::string>();
+      if (m != "auto" && m != "on" && m != "off") throw std::invalid_argument("row_kernel: auto | on | off");
+      if (m == "on" && !rows_ok_) throw std::invalid_argument("row kernel needs <= 16 nodes, <= 64 gpu_milli classes");
+      row_mode_ = m;
+    }
+    if (o.contains("row_heap_top")) row_top_opt_ = o["row_heap_top"].cast<int>();   // -1: auto
     if (o.contains("heap_mode")) {
       const std::string m = o["heap_mode"].cast<std::string>();
       if (m != "auto" && m != "lds" && m != "hbm") throw std::invalid_argument("heap_mode: auto | lds | hbm");
@@ -339,10 +359,14 @@ class DeviceEngine {
     d["heap_mode"] = heap_mode_;
     d["n_slots"] = (int)slots_.size();
     d["heap_top_hbm"] = heap_top_for(0, false);
+    d["row_kernel_ok"] = rows_ok_;
+    d["row_kernel"] = row_mode_;
+    d["row_heap_top"] = row_top();
     return d;
   }
 
   bool would_use_hbm(int P) const { return use_gheap(P); }
+  bool would_use_rows(int P) const { return use_rows(P); }
   int n_slots() const { return (int)slots_.size(); }
 
  private:
@@ -350,6 +374,7 @@ class DeviceEngine {
   static constexpr int kWeightWords = kWeights;   // LDS copy of a builtin policy's weights
   static constexpr size_t kPoliciesPerCu = 16;   // HBM-heap builtin kernels: 4 waves per SIMD
   static constexpr size_t kVmPoliciesPerCu = 8;  // HBM-heap VM kernels: 2 waves per SIMD
+  static constexpr size_t kRowWavesPerCu = 12;   // row kernel: 12 waves = 48 policies per CU (3 per SIMD)
 
   Slot& slot_at(int i) {
     if (i < 0 || i >= (int)slots_.size()) throw std::out_of_range("slot index");
@@ -367,6 +392,30 @@ class DeviceEngine {
     HIP_OK(fksk::set_builtin_attrs_np4(mx));
     HIP_OK(fksk::set_vm_attrs_np1(mx)); HIP_OK(fksk::set_vm_attrs_np2(mx)); HIP_OK(fksk::set_vm_attrs_np4(mx));
     HIP_OK(fksk::set_prof_attrs(mx));
+    HIP_OK(fksk::set_rows_attrs(mx));
+  }
+
+  // 4-policies-per-wave row kernel: clusters of <= 16 nodes, exact repush
+  // rule, no invariant checking (those stay on the wave kernel)
+  bool use_rows(int P) const {
+    (void)P;
+    if (!rows_ok_ || row_mode_ == "off") return false;
+    if (row_mode_ == "on") return true;
+    return heap_mode_ != "lds" && W_.check_every == 0 && !W_.repush_earliest;
+  }
+
+  // heap slots each row keeps in LDS: 2^k - 1, as many levels as fit the
+  // per-wave LDS budget (kRowWavesPerCu waves of 4 policies per CU)
+  int row_top() const {
+    const int entries = row_heap_entries(W_.n_pods);
+    int T = 1;
+    if (row_top_opt_ > 0) {
+      while (2 * T + 1 <= row_top_opt_ && T < entries) T = 2 * T + 1;
+      return T;
+    }
+    const size_t budget = kMaxLds / kRowWavesPerCu;
+    while (T < entries && rows_lds_bytes(W_.n_pods, 2 * T + 1) <= budget) T = 2 * T + 1;
+    return T;
   }
 
   bool use_gheap(int P) const {
@@ -469,6 +518,19 @@ class DeviceEngine {
 
   void launch_builtin(Slot& s) {
     const int P = s.P;
+    if (use_rows(P)) {
+      DevWorkload Wl = W_;
+      Wl.heap_top = row_top();
+      const size_t lds = rows_lds_bytes(W_.n_pods, Wl.heap_top);
+      if (lds > kMaxLds) throw std::invalid_argument("row kernel layout exceeds the 160 KiB LDS");
+      s.gheap.reserve((size_t)row_heap_entries(W_.n_pods) * 8 * (size_t)P);
+      const size_t wb = (size_t)P * kWeights * 8;
+      const fksk::BuiltinArgs a{Wl, upload_workload(s, Wl), reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + wb),
+                                s.h_in.dev<double>(), s.w.as<double>(), s.res.as<DevResult>(), s.gheap.as<uint64_t>(),
+                                nullptr};
+      HIP_OK(fksk::launch_builtin_rows(s.fam_spec, P, lds, s.stream, a));
+      return;
+    }
     const bool g = use_gheap(P);
     const DevWorkload Wl = launch_workload(g, 0, false);
     const size_t lds = lds_bytes(g, Wl.heap_top, 0);
@@ -524,6 +586,9 @@ class DeviceEngine {
   int npass_ = 1;
   size_t heap_bytes_ = 0, delmap_bytes_ = 0;
   bool lds_heap_ok_ = true;
+  bool rows_ok_ = false;
+  std::string row_mode_ = "auto";
+  int row_top_opt_ = -1;
   int num_cus_ = 0;
   std::string arch_;
   std::string heap_mode_ = "auto";

@@ -52,6 +52,10 @@ FKS_DECLARE_NPASS(2)
 FKS_DECLARE_NPASS(4)
 #undef FKS_DECLARE_NPASS
 
+// row kernels: 4 policies per wave (clusters of <= 16 nodes, replay_rows.hip.h)
+hipError_t launch_builtin_rows(int fam_spec, int P, size_t lds, hipStream_t s, const BuiltinArgs& a);
+hipError_t set_rows_attrs(int max_lds);
+
 // phase-profiled variants (NPASS = 1)
 hipError_t launch_builtin_prof(bool gheap, int P, size_t lds, hipStream_t s, const BuiltinArgs& a);
 hipError_t launch_vm_prof(bool gheap, int P, size_t lds, hipStream_t s, const VmArgs& a);

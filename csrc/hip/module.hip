@@ -19,6 +19,7 @@
 
 #include "launch.h"
 #include "replay.hip.h"
+#include "replay_rows.hip.h"
 #include "scorers.hip.h"
 #include "vm_dev.hip.h"
 
@@ -255,6 +256,7 @@ PYBIND11_MODULE(_fks_hip, m) {
       .def("stage_builtin_only", &DeviceEngine::stage_builtin_only)
       .def("launch_builtin_async", &DeviceEngine::launch_builtin_async)
       .def("would_use_hbm", &DeviceEngine::would_use_hbm)
+      .def("would_use_rows", &DeviceEngine::would_use_rows)
       .def("synchronize", &DeviceEngine::synchronize)
       .def("info", &DeviceEngine::info);
   m.attr("WEIGHTS_PER_POLICY") = kWeights;

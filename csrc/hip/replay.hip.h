@@ -64,6 +64,7 @@ struct DevWorkload {
   int32_t check_every;        // k_check_invariants cadence in events (0: off)
   int32_t inv_words;          // LDS u64 words reserved for the invariant check (0: off)
   int32_t trace_hash;         // 1: fold every event into DevResult.hash (cross-engine trace check)
+  const uint64_t* heap0p;     // initial heap shifted by one slot (row kernel layout: address = slot + 1)
 };
 
 struct DevResult {

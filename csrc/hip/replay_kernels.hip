@@ -4,6 +4,7 @@
 //   FKS_KIND 0 -> built-in family kernels for FKS_NPASS (one instance per family + a mixed one)
 //   FKS_KIND 1 -> bytecode-VM kernels for FKS_NPASS
 //   FKS_KIND 2 -> phase-profiled diagnostics kernels (NPASS = 1)
+//   FKS_KIND 3 -> row kernels (4 policies per wave, <= 16 nodes; replay_rows.hip.h)
 // Each unit defines the matching launchers of launch.h.
 #include <hip/hip_runtime.h>
 
@@ -11,6 +12,7 @@
 #include "replay.hip.h"
 #include "scorers.hip.h"
 #include "vm_dev.hip.h"
+#include "replay_rows.hip.h"
 
 #ifndef FKS_KIND
 #define FKS_KIND 0
@@ -173,6 +175,22 @@ __global__ FKS_VM_BOUNDS(GHEAP) void k_replay_vm_prof(fksk::VmArgs a) {
 }
 #endif
 
+
+#if FKS_KIND == 3
+// Row kernels: the LDS share per wave (4 heap tops + bitmaps) is what bounds
+// residency; registers are capped so LDS, not VGPRs, stays the limit.
+#ifndef FKS_ROW_WAVES
+#define FKS_ROW_WAVES 4        // first-fit / best-fit / random_linear
+#endif
+#ifndef FKS_ROW_HEAVY_WAVES
+#define FKS_ROW_HEAVY_WAVES 3  // feature / composite families
+#endif
+template <int FAM>
+__global__ __launch_bounds__(64, FAM < 0 ? 2 : (FAM == 3 || FAM == 4) ? FKS_ROW_HEAVY_WAVES : FKS_ROW_WAVES) void k_replay_rows(fksk::BuiltinArgs a, int P) {
+  replay_rows<FAM>(a.W, a.fam, a.weights, a.gheap, a.out, P);
+}
+#endif
+
 }  // namespace
 
 namespace fksk {
@@ -217,6 +235,34 @@ hipError_t set_prof_attrs(int mx) {
   hipError_t e = hipSuccess;
   for (hipError_t r : {raise_lds(&k_replay_builtin_prof<true>, mx), raise_lds(&k_replay_builtin_prof<false>, mx),
                        raise_lds(&k_replay_vm_prof<true>, mx), raise_lds(&k_replay_vm_prof<false>, mx)})
+    if (r != hipSuccess) e = r;
+  return e;
+}
+#endif
+
+
+#if FKS_KIND == 3
+hipError_t launch_builtin_rows(int fam, int P, size_t lds, hipStream_t st, const BuiltinArgs& a) {
+  const dim3 grid((P + kRowsPerWave - 1) / kRowsPerWave);
+#define FKS_CASE(F) \
+  case F: hipLaunchKernelGGL((k_replay_rows<F>), grid, dim3(64), lds, st, a, P); break;
+  switch (fam) {
+    FKS_CASE(FAM_FIRST_FIT)
+    FKS_CASE(FAM_BEST_FIT)
+    FKS_CASE(FAM_RANDOM_LINEAR)
+    FKS_CASE(FAM_FEATURE_LINEAR)
+    FKS_CASE(FAM_COMPOSITE_LINEAR)
+    default: hipLaunchKernelGGL((k_replay_rows<-1>), grid, dim3(64), lds, st, a, P);
+  }
+#undef FKS_CASE
+  return hipGetLastError();
+}
+hipError_t set_rows_attrs(int mx) {
+  hipError_t e = hipSuccess;
+  for (hipError_t r : {raise_lds(&k_replay_rows<-1>, mx), raise_lds(&k_replay_rows<FAM_FIRST_FIT>, mx),
+                       raise_lds(&k_replay_rows<FAM_BEST_FIT>, mx), raise_lds(&k_replay_rows<FAM_RANDOM_LINEAR>, mx),
+                       raise_lds(&k_replay_rows<FAM_FEATURE_LINEAR>, mx),
+                       raise_lds(&k_replay_rows<FAM_COMPOSITE_LINEAR>, mx)})
     if (r != hipSuccess) e = r;
   return e;
 }

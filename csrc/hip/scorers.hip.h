@@ -60,15 +60,21 @@ struct BuiltinScorerDev {
     // weights are re-read (scalar-cache hits) at every call rather than held in
     // SGPRs across the event loop: the opaque pointer stops the compiler from
     // hoisting the loads and spilling 8-32 SGPRs per event
-    // weights are re-read (scalar-cache hits) at every call rather than held in
-    // SGPRs across the event loop: the opaque pointer stops the compiler from
-    // hoisting the loads and spilling 8-32 SGPRs per event
     const double* qg = reinterpret_cast<const double*>(uniu64(reinterpret_cast<uint64_t>(wp)));
     asm volatile("" : "+s"(qg));
     const FKS_CONST double* q = const_ptr(qg);   // scalar loads
     double w[kWeights];
 #pragma unroll
     for (int k = 0; k < kWeights; ++k) w[k] = k < family_weights(FAM) ? q[k] : 0.0;
+    return score_weights<NPASS>(family, w, ps, nr, pod, exc);
+  }
+
+  // The family formulas on an already-loaded weight vector (shared with the
+  // 4-policies-per-wave row kernel, replay_rows.hip.h, whose weights come
+  // from LDS).  The caller has checked feasibility.
+  template <int NPASS>
+  __device__ static int64_t score_weights(int family, const double* w, int ps, const NodeRegs<NPASS>& nr,
+                                          const PodView& pod, int& exc) {
     switch (FAM >= 0 ? FAM : family) {
       case FAM_FIRST_FIT:
         return 1000;
@@ -113,7 +119,7 @@ struct BuiltinScorerDev {
   // rounding as `score += w_k * (f_k)`), so no 16-double feature vector is
   // held live across the node loop.
   template <int NPASS>
-  __device__ double composite(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, const double* w) const {
+  __device__ static double composite(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, const double* w) {
     const int ng = nr.ngpus[ps];
     const bool gpod = pod.ngpu > 0;
     const int64_t ct = nr.cpu_total[ps], mt = nr.mem_total[ps];

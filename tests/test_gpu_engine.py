@@ -81,7 +81,8 @@ def test_async_slots_match_sync(dev, default_workload):
 def test_hbm_heap_with_lds_top_matches_cpu(default_workload, top):
     """Heap slots split between LDS (top levels) and HBM give the CPU oracle's tables."""
     from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
-    dev = he.DeviceEvaluator(default_workload, options={"heap_mode": "hbm", "heap_top": top})
+    dev = he.DeviceEvaluator(default_workload, options={"heap_mode": "hbm", "heap_top": top, "row_kernel": "off"})
+    assert not dev._eng.would_use_rows(64)
     w = fam.sample_composite_linear(64, np.random.default_rng(top))
     assert np.array_equal(dev.evaluate_builtin("composite_linear", w),
                           ce.simulate_builtin_batch(default_workload, "composite_linear", w))
@@ -110,4 +111,55 @@ def test_scaled_synthetic_256_nodes_matches_cpu():
         W = fam.SAMPLERS[family](48, np.random.default_rng(1)) if family in fam.SAMPLERS else None
         gpu = dev.evaluate_builtin(family, W, n=48)
         cpu = ce.simulate_builtin_batch(w, family, fam.pad_weights(W) if W is not None else np.zeros((48, 16)))
+        assert np.array_equal(gpu, cpu), family
+
+
+# ---- row kernel: 4 policies per wave (clusters of <= 16 nodes) --------------------------
+
+def test_row_kernel_is_default_for_16_nodes(dev):
+    assert dev.info()["row_kernel_ok"] and dev._eng.would_use_rows(4096)
+
+
+@pytest.mark.parametrize("top", [1, 63, 511, 4095])
+def test_row_kernel_matches_cpu(default_workload, top):
+    """Row kernel with heaps split between LDS and HBM at every depth == CPU oracle;
+    P = 37 leaves a partly empty last wave."""
+    from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
+    dev = he.DeviceEvaluator(default_workload, options={"row_kernel": "on", "row_heap_top": top})
+    assert dev._eng.would_use_rows(37)
+    w = fam.sample_composite_linear(37, np.random.default_rng(100 + top))
+    assert np.array_equal(dev.evaluate_builtin("composite_linear", w),
+                          ce.simulate_builtin_batch(default_workload, "composite_linear", w))
+
+
+def test_row_kernel_mixed_families_and_exceptions(default_workload):
+    """Mixed-family batch (one kernel, divergent scorers per row) incl. rows that raise."""
+    from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
+    rng = np.random.default_rng(9)
+    names = ["first_fit", "best_fit", "random_linear", "feature_linear", "composite_linear"] * 6
+    W = np.zeros((len(names), 16))
+    for i, n in enumerate(names):
+        if n in fam.SAMPLERS:
+            W[i] = fam.pad_weights(fam.SAMPLERS[n](1, rng))[0]
+    W[3, :12] = 1e308          # feature_linear overflow -> OverflowError (score 0, exception column)
+    rows = he.DeviceEvaluator(default_workload, options={"row_kernel": "on"}).evaluate_builtin(names, W)
+    wave = he.DeviceEvaluator(default_workload, options={"row_kernel": "off"}).evaluate_builtin(names, W)
+    assert np.array_equal(rows, wave)
+    assert rows[3, 10] != 0
+    for n in set(names):
+        idx = [i for i, m in enumerate(names) if m == n]
+        assert np.array_equal(rows[idx], ce.simulate_builtin_batch(default_workload, n, W[idx])), n
+
+
+def test_row_kernel_deep_heap_synthetic():
+    """16 nodes, 40,000 pods: 16-level heaps (4 pop rounds) in the row kernel == CPU oracle."""
+    from funsearch_kubernetes_simulator_amd.core import synthetic_workload
+    from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
+    w = synthetic_workload(n_nodes=16, n_pods=40000, seed=3)
+    w.pods.pod_ctime[:] = w.pods.pod_ctime * 5   # 5x the pods over 5x the time: the 16 nodes keep up
+    dev = he.DeviceEvaluator(w, options={"row_kernel": "on"})
+    for family in ("best_fit", "random_linear"):
+        W = fam.SAMPLERS[family](12, np.random.default_rng(2)) if family in fam.SAMPLERS else None
+        gpu = dev.evaluate_builtin(family, W, n=12)
+        cpu = ce.simulate_builtin_batch(w, family, fam.pad_weights(W) if W is not None else np.zeros((12, 16)))
         assert np.array_equal(gpu, cpu), family
