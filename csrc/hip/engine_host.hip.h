@@ -101,14 +101,14 @@ struct HostBuf {
 struct Slot {
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
-  DevBuf res, tab, fam, w, code, meta, kpay, ktag, gheap, prof, wc;
+  DevBuf res, tab, fam, w, code, meta, kpay, ktag, gheap, prof, wc, queue;
   HostBuf h_in, h_tab, h_wc;
   int P = 0;
   int fam_spec = -1;    // family shared by the whole staged batch, or -1
   bool busy = false;
   roctx_range_id_t range = 0;   // roctx range spanning submit -> wait (rocprofv3 --marker-trace)
   void release() {
-    for (DevBuf* b : {&res, &tab, &fam, &w, &code, &meta, &kpay, &ktag, &gheap, &prof, &wc}) b->release();
+    for (DevBuf* b : {&res, &tab, &fam, &w, &code, &meta, &kpay, &ktag, &gheap, &prof, &wc, &queue}) b->release();
     h_in.release();
     h_tab.release();
     h_wc.release();
@@ -350,6 +350,22 @@ class DeviceEngine {
     return py::make_tuple(tab, prof);
   }
 
+  // row kernel, s_memtime build: (result table, per-wave phase cycles [waves, 8])
+  py::tuple profile_rows(py::array_t<int32_t, py::array::c_style | py::array::forcecast> fam,
+                         py::array_t<double, py::array::c_style | py::array::forcecast> weights) {
+    if (!rows_ok_) throw std::invalid_argument("row kernel needs <= 16 nodes");
+    HIP_OK(hipSetDevice(device_));
+    Slot& s = idle_slot(0);
+    stage_builtin(s, fam.data(), weights.data(), (int)fam.size());
+    const int waves = launch_rows(s, true);
+    finish(s);
+    py::array_t<uint64_t> prof({(py::ssize_t)waves, (py::ssize_t)8});
+    HIP_OK(hipMemcpyAsync(prof.mutable_data(), s.prof.p, (size_t)waves * 64, hipMemcpyDeviceToHost, s.stream));
+    py::array_t<double> tab = wait(0);
+    HIP_OK(hipStreamSynchronize(s.stream));
+    return py::make_tuple(tab, prof);
+  }
+
   py::dict info() const {
     py::dict d;
     d["device"] = device_; d["arch"] = arch_; d["num_cus"] = num_cus_;
@@ -362,6 +378,7 @@ class DeviceEngine {
     d["row_kernel_ok"] = rows_ok_;
     d["row_kernel"] = row_mode_;
     d["row_heap_top"] = row_top();
+    d["row_waves_per_cu"] = row_layout(FAM_COMPOSITE_LINEAR).second;
     return d;
   }
 
@@ -374,7 +391,6 @@ class DeviceEngine {
   static constexpr int kWeightWords = kWeights;   // LDS copy of a builtin policy's weights
   static constexpr size_t kPoliciesPerCu = 16;   // HBM-heap builtin kernels: 4 waves per SIMD
   static constexpr size_t kVmPoliciesPerCu = 8;  // HBM-heap VM kernels: 2 waves per SIMD
-  static constexpr size_t kRowWavesPerCu = 12;   // row kernel: 12 waves = 48 policies per CU (3 per SIMD)
 
   Slot& slot_at(int i) {
     if (i < 0 || i >= (int)slots_.size()) throw std::out_of_range("slot index");
@@ -404,18 +420,39 @@ class DeviceEngine {
     return heap_mode_ != "lds" && W_.check_every == 0 && !W_.repush_earliest;
   }
 
-  // heap slots each row keeps in LDS: 2^k - 1, as many levels as fit the
-  // per-wave LDS budget (kRowWavesPerCu waves of 4 policies per CU)
-  int row_top() const {
+  // Heap slots each row keeps in LDS (2^k - 1) for a family's kernel: the
+  // largest top among those that keep the most waves resident per CU (the
+  // kernel's register use and the LDS layout both bound residency), or the
+  // `row_heap_top` option.  Returns {T, resident waves per CU}.
+  std::pair<int, int> row_layout(int fam) const {
     const int entries = row_heap_entries(W_.n_pods);
-    int T = 1;
     if (row_top_opt_ > 0) {
+      int T = 1;
       while (2 * T + 1 <= row_top_opt_ && T < entries) T = 2 * T + 1;
-      return T;
+      return {T, std::max(1, row_waves(fam, T))};
     }
-    const size_t budget = kMaxLds / kRowWavesPerCu;
-    while (T < entries && rows_lds_bytes(W_.n_pods, 2 * T + 1) <= budget) T = 2 * T + 1;
-    return T;
+    const int key = fam + 1;
+    if (key >= 0 && key < (int)row_layout_cache_.size() && row_layout_cache_[key].first > 0)
+      return row_layout_cache_[key];
+    std::pair<int, int> best{1, 0};
+    for (int T = 63; T < entries && rows_lds_bytes(W_.n_pods, T) <= kMaxLds; T = 2 * T + 1) {
+      // residency as measured: the occupancy query is optimistic about LDS
+      // (allocation granules); count 2 KiB granules as well
+      const int w = row_waves(fam, T);
+      if (w >= best.second && w > 0) best = {T, w};
+    }
+    if (best.second == 0) best = {1, std::max(1, row_waves(fam, 1))};
+    if (key >= 0 && key < (int)row_layout_cache_.size()) row_layout_cache_[key] = best;
+    return best;
+  }
+  int row_top() const { return row_layout(FAM_COMPOSITE_LINEAR).first; }
+
+  // resident row-kernel waves per CU at heap top T: the occupancy query
+  // (registers, LDS) is optimistic about LDS allocation granules, so LDS is
+  // also counted in 2 KiB granules (what the measured residency follows)
+  int row_waves(int fam, int T) const {
+    const size_t lds = rows_lds_bytes(W_.n_pods, T);
+    return std::min<int>(fksk::rows_waves_per_cu(fam, lds), (int)(kMaxLds / ((lds + 2047) & ~size_t(2047))));
   }
 
   bool use_gheap(int P) const {
@@ -519,16 +556,7 @@ class DeviceEngine {
   void launch_builtin(Slot& s) {
     const int P = s.P;
     if (use_rows(P)) {
-      DevWorkload Wl = W_;
-      Wl.heap_top = row_top();
-      const size_t lds = rows_lds_bytes(W_.n_pods, Wl.heap_top);
-      if (lds > kMaxLds) throw std::invalid_argument("row kernel layout exceeds the 160 KiB LDS");
-      s.gheap.reserve((size_t)row_heap_entries(W_.n_pods) * 8 * (size_t)P);
-      const size_t wb = (size_t)P * kWeights * 8;
-      const fksk::BuiltinArgs a{Wl, upload_workload(s, Wl), reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + wb),
-                                s.h_in.dev<double>(), s.w.as<double>(), s.res.as<DevResult>(), s.gheap.as<uint64_t>(),
-                                nullptr};
-      HIP_OK(fksk::launch_builtin_rows(s.fam_spec, P, lds, s.stream, a));
+      launch_rows(s, false);
       return;
     }
     const bool g = use_gheap(P);
@@ -542,6 +570,29 @@ class DeviceEngine {
     if (npass_ == 1) HIP_OK(fksk::launch_builtin_np1(g, s.fam_spec, P, lds, s.stream, a));
     else if (npass_ == 2) HIP_OK(fksk::launch_builtin_np2(g, s.fam_spec, P, lds, s.stream, a));
     else HIP_OK(fksk::launch_builtin_np4(g, s.fam_spec, P, lds, s.stream, a));
+  }
+
+  // row kernel launch (optionally the phase-profiled build); returns the wave count
+  int launch_rows(Slot& s, bool profiled) {
+    const int P = s.P;
+    DevWorkload Wl = W_;
+    const std::pair<int, int> lay = row_layout(s.fam_spec);
+    Wl.heap_top = lay.first;
+    const size_t lds = rows_lds_bytes(W_.n_pods, Wl.heap_top) + (profiled ? kRowProfBytes : 0);
+    if (lds > kMaxLds) throw std::invalid_argument("row kernel layout exceeds the 160 KiB LDS");
+    // persistent waves: as many as stay resident, each row draining the policy queue
+    const int waves = std::max(1, std::min((P + kRowsPerWave - 1) / kRowsPerWave, lay.second * num_cus_));
+    s.gheap.reserve((size_t)row_heap_entries(W_.n_pods) * 8 * (size_t)waves * kRowsPerWave);
+    s.queue.reserve(64);
+    if (profiled) s.prof.reserve((size_t)waves * 64);
+    HIP_OK(hipMemsetAsync(s.queue.p, 0, sizeof(int), s.stream));
+    const size_t wb = (size_t)P * kWeights * 8;
+    const fksk::BuiltinArgs a{Wl, upload_workload(s, Wl), reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + wb),
+                              s.h_in.dev<double>(), s.w.as<double>(), s.res.as<DevResult>(), s.gheap.as<uint64_t>(),
+                              profiled ? s.prof.as<uint64_t>() : nullptr};
+    if (profiled) HIP_OK(fksk::launch_builtin_rows_prof(s.fam_spec, P, waves, s.queue.as<int>(), lds, s.stream, a));
+    else HIP_OK(fksk::launch_builtin_rows(s.fam_spec, P, waves, s.queue.as<int>(), lds, s.stream, a));
+    return waves;
   }
 
   void launch_vm(Slot& s, int nregs) {
@@ -589,6 +640,7 @@ class DeviceEngine {
   bool rows_ok_ = false;
   std::string row_mode_ = "auto";
   int row_top_opt_ = -1;
+  mutable std::vector<std::pair<int, int>> row_layout_cache_ = std::vector<std::pair<int, int>>(8, {0, 0});
   int num_cus_ = 0;
   std::string arch_;
   std::string heap_mode_ = "auto";

@@ -257,6 +257,7 @@ PYBIND11_MODULE(_fks_hip, m) {
       .def("launch_builtin_async", &DeviceEngine::launch_builtin_async)
       .def("would_use_hbm", &DeviceEngine::would_use_hbm)
       .def("would_use_rows", &DeviceEngine::would_use_rows)
+      .def("profile_rows", &DeviceEngine::profile_rows)
       .def("synchronize", &DeviceEngine::synchronize)
       .def("info", &DeviceEngine::info);
   m.attr("WEIGHTS_PER_POLICY") = kWeights;

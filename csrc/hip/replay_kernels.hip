@@ -180,14 +180,23 @@ __global__ FKS_VM_BOUNDS(GHEAP) void k_replay_vm_prof(fksk::VmArgs a) {
 // Row kernels: the LDS share per wave (4 heap tops + bitmaps) is what bounds
 // residency; registers are capped so LDS, not VGPRs, stays the limit.
 #ifndef FKS_ROW_WAVES
-#define FKS_ROW_WAVES 4        // first-fit / best-fit / random_linear
+#define FKS_ROW_WAVES 5        // first-fit / best-fit / random_linear
 #endif
 #ifndef FKS_ROW_HEAVY_WAVES
-#define FKS_ROW_HEAVY_WAVES 3  // feature / composite families
+#define FKS_ROW_HEAVY_WAVES 4  // feature / composite families (composite: only loop-invariant snapshot
+                               // divisors spill, reloaded on the rare snapshot path)
 #endif
 template <int FAM>
-__global__ __launch_bounds__(64, FAM < 0 ? 2 : (FAM == 3 || FAM == 4) ? FKS_ROW_HEAVY_WAVES : FKS_ROW_WAVES) void k_replay_rows(fksk::BuiltinArgs a, int P) {
-  replay_rows<FAM>(a.W, a.fam, a.weights, a.gheap, a.out, P);
+__global__ __launch_bounds__(64, FAM < 0 ? 2 : (FAM == 3 || FAM == 4) ? FKS_ROW_HEAVY_WAVES : FKS_ROW_WAVES) void k_replay_rows(fksk::BuiltinArgs a, int P, int* queue) {
+  replay_rows<FAM>(a.W, a.Wc, a.fam, a.weights, a.gheap, a.out, P, queue);
+}
+#endif
+
+#if FKS_KIND == 3
+template <int FAM>
+__global__ __launch_bounds__(64, FAM < 0 ? 2 : (FAM == 3 || FAM == 4) ? FKS_ROW_HEAVY_WAVES : FKS_ROW_WAVES)
+void k_replay_rows_prof(fksk::BuiltinArgs a, int P, int* queue) {
+  replay_rows<FAM, RowProf>(a.W, a.Wc, a.fam, a.weights, a.gheap, a.out, P, queue, a.prof);
 }
 #endif
 
@@ -242,23 +251,52 @@ hipError_t set_prof_attrs(int mx) {
 
 
 #if FKS_KIND == 3
-hipError_t launch_builtin_rows(int fam, int P, size_t lds, hipStream_t st, const BuiltinArgs& a) {
-  const dim3 grid((P + kRowsPerWave - 1) / kRowsPerWave);
+hipError_t launch_builtin_rows(int fam, int P, int waves, int* queue, size_t lds, hipStream_t st,
+                              const BuiltinArgs& a) {
+  const dim3 grid(waves);
 #define FKS_CASE(F) \
-  case F: hipLaunchKernelGGL((k_replay_rows<F>), grid, dim3(64), lds, st, a, P); break;
+  case F: hipLaunchKernelGGL((k_replay_rows<F>), grid, dim3(64), lds, st, a, P, queue); break;
   switch (fam) {
     FKS_CASE(FAM_FIRST_FIT)
     FKS_CASE(FAM_BEST_FIT)
     FKS_CASE(FAM_RANDOM_LINEAR)
     FKS_CASE(FAM_FEATURE_LINEAR)
     FKS_CASE(FAM_COMPOSITE_LINEAR)
-    default: hipLaunchKernelGGL((k_replay_rows<-1>), grid, dim3(64), lds, st, a, P);
+    default: hipLaunchKernelGGL((k_replay_rows<-1>), grid, dim3(64), lds, st, a, P, queue);
   }
 #undef FKS_CASE
   return hipGetLastError();
 }
+int rows_waves_per_cu(int fam, size_t lds) {
+  int n = 0;
+  hipError_t e;
+  switch (fam) {
+    case FAM_FIRST_FIT: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_replay_rows<FAM_FIRST_FIT>, 64, lds); break;
+    case FAM_BEST_FIT: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_replay_rows<FAM_BEST_FIT>, 64, lds); break;
+    case FAM_RANDOM_LINEAR:
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_replay_rows<FAM_RANDOM_LINEAR>, 64, lds); break;
+    case FAM_FEATURE_LINEAR:
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_replay_rows<FAM_FEATURE_LINEAR>, 64, lds); break;
+    case FAM_COMPOSITE_LINEAR:
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_replay_rows<FAM_COMPOSITE_LINEAR>, 64, lds); break;
+    default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_replay_rows<-1>, 64, lds);
+  }
+  return e == hipSuccess ? n : -1;
+}
+hipError_t launch_builtin_rows_prof(int fam, int P, int waves, int* queue, size_t lds, hipStream_t st,
+                                   const BuiltinArgs& a) {
+  const dim3 grid(waves);
+  if (fam == FAM_RANDOM_LINEAR) hipLaunchKernelGGL((k_replay_rows_prof<FAM_RANDOM_LINEAR>), grid, dim3(64), lds, st, a, P, queue);
+  else if (fam == FAM_COMPOSITE_LINEAR)
+    hipLaunchKernelGGL((k_replay_rows_prof<FAM_COMPOSITE_LINEAR>), grid, dim3(64), lds, st, a, P, queue);
+  else hipLaunchKernelGGL((k_replay_rows_prof<-1>), grid, dim3(64), lds, st, a, P, queue);
+  return hipGetLastError();
+}
 hipError_t set_rows_attrs(int mx) {
   hipError_t e = hipSuccess;
+  for (hipError_t r : {raise_lds(&k_replay_rows_prof<-1>, mx), raise_lds(&k_replay_rows_prof<FAM_RANDOM_LINEAR>, mx),
+                       raise_lds(&k_replay_rows_prof<FAM_COMPOSITE_LINEAR>, mx)})
+    if (r != hipSuccess) e = r;
   for (hipError_t r : {raise_lds(&k_replay_rows<-1>, mx), raise_lds(&k_replay_rows<FAM_FIRST_FIT>, mx),
                        raise_lds(&k_replay_rows<FAM_BEST_FIT>, mx), raise_lds(&k_replay_rows<FAM_RANDOM_LINEAR>, mx),
                        raise_lds(&k_replay_rows<FAM_FEATURE_LINEAR>, mx),

@@ -97,6 +97,9 @@ struct RowHeap {
     else __hip_atomic_fetch_and(&delmap[pos >> 5], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 
+  // Keys compare as plain u64: a pod has at most one entry in the heap, so two
+  // entries never share (time, rank) and the payload bits below `lb` never
+  // decide an order.
   // CPython heappop's re-insertion of `last` (= old h[n]) at the root of a
   // heap of n >= 1 items: same algorithm as WaveHeap::pop_reinsert with
   // 4-level rounds (lane j < 15 = the j-th node, BFS order, of the 4-level
@@ -104,18 +107,17 @@ struct RowHeap {
   __device__ void pop_reinsert(int n, uint64_t last) const {
     const int k = j == 0 ? 0 : j < 3 ? 1 : j < 7 ? 2 : 3;   // depth of node j in the subtree
     const int ki = j - ((1 << k) - 1);
-    constexpr int kRounds = 5;   // 20 levels: n < 2^20 (host guarantees n < 2^17)
-    uint64_t val[kRounds];
-    int par[kRounds];
-    bool on[kRounds];
-    int start[kRounds];
-    int pos = 0;
-    bool leaf = false;
+    // The path values grow downwards, so the bubble-up of `last` ends at the
+    // first path entry greater than it: rounds above that entry move their
+    // path up as soon as they are walked (nothing is carried between rounds),
+    // the round holding it moves the entries before it and places `last` on
+    // its parent, and the walk stops there -- the entries below keep their
+    // slots, exactly as after CPython's full descent and bubble-up.
+    constexpr int kRounds = 5;   // 20 levels (host guarantees n < 2^17)
+    int pos = 0, target = -1;
 #pragma unroll
     for (int rd = 0; rd < kRounds; ++rd) {
-      start[rd] = pos;
-      val[rd] = 0; par[rd] = 0; on[rd] = false;
-      if (leaf || 2 * pos + 1 >= n) { leaf = true; continue; }
+      if (2 * pos + 1 >= n) break;   // pos is a leaf
       const int q = ((pos + 1) << k) - 1 + ki;
       const int c = 2 * q + 1;
       const bool valid = j < 15 && c < n;
@@ -125,7 +127,7 @@ struct RowHeap {
         vl = pr.x;
         vr = pr.y;
       }
-      const bool go_r = valid && (c + 1 < n) && !key_lt(vl, vr, lb);
+      const bool go_r = valid && (c + 1 < n) && !(vl < vr);
       const uint32_t m = row_ballot(go_r, rbase);
       const uint32_t ex = row_ballot(valid, rbase);
       int cj = 0, taken = 0, idx = 0;
@@ -139,34 +141,23 @@ struct RowHeap {
           taken = lv + 1;
         }
       }
-      on[rd] = (onm >> j) & 1;
-      val[rd] = go_r ? vr : vl;
-      par[rd] = q;
-      pos = ((pos + 1) << taken) - 1 + idx;
-      if (taken < 4) leaf = true;
-    }
-    // bubble `last` up: the first path entry (path order = round, then lane)
-    // with last < v and everything below keep their slots; `last` lands on
-    // that entry's parent, the entries above move up one level
-    int jr = -1, jl = 0, target = pos;
-#pragma unroll
-    for (int rd = 0; rd < kRounds; ++rd) {
-      const uint32_t g = row_ballot(on[rd] && key_lt(last, val[rd], lb), rbase);
-      if (jr < 0 && g) {
-        jr = rd;
-        jl = __ffs(g) - 1;
+      const bool on = (onm >> j) & 1;
+      const uint64_t v = go_r ? vr : vl;
+      const uint32_t g = row_ballot(on && last < v, rbase);
+      const int jl = g ? __ffs(g) - 1 : kRow;
+      if (on && j < jl) {   // moves up one level
+        st(q, v);
+        mark(q, v);
+      }
+      if (g) {
         const int kk = jl == 0 ? 0 : jl < 3 ? 1 : jl < 7 ? 2 : 3;
-        target = ((start[rd] + 1) << kk) - 1 + (jl - ((1 << kk) - 1));
+        target = ((pos + 1) << kk) - 1 + (jl - ((1 << kk) - 1));
+        break;
       }
+      pos = ((pos + 1) << taken) - 1 + idx;
+      if (taken < 4) break;   // reached a leaf
     }
-#pragma unroll
-    for (int rd = 0; rd < kRounds; ++rd) {
-      const bool above = jr < 0 || rd < jr || (rd == jr && j < jl);
-      if (on[rd] && above) {
-        st(par[rd], val[rd]);
-        mark(par[rd], val[rd]);
-      }
-    }
+    if (target < 0) target = pos;
     if (j == 0) { st(target, last); mark(target, last); }
   }
 
@@ -176,7 +167,7 @@ struct RowHeap {
     const int anc = ((n + 1) >> l) - 1;
     const bool valid = n > 0 && anc >= 0;
     const uint64_t v = valid ? ld(anc) : 0;
-    const bool gt = valid && key_lt(item, v, lb);
+    const bool gt = valid && item < v;
     const int J = __popc(row_ballot(gt, rbase));
     const int dst = ((n + 1) >> (l - 1)) - 1;
     if (gt) { st(dst, v); mark(dst, v); }
@@ -235,256 +226,367 @@ struct RowAcc {
   }
 };
 
-// LDS per wave: [4 x 16 weights] then per row [deletion bitmap | heap top].
+// LDS per wave: [4 x 16 weights | 64 class values | 16 x 11 node constants] then
+// per row [deletion bitmap | heap top].
+constexpr int kNodeConsts = 3 + kGmax;
+constexpr int kRowClassBytes = (kRow * kRowClassSlots * 4 + kRow * kNodeConsts * 4 + 15) & ~15;
 __host__ __device__ inline size_t rows_row_bytes(int n_pods, int T) {
   return (size_t)lds_delmap_words(n_pods) * 4 + (size_t)(T + 1) * 8;
 }
 __host__ __device__ inline size_t rows_lds_bytes(int n_pods, int T) {
-  return (size_t)kRowsPerWave * kWeights * 8 + kRowsPerWave * rows_row_bytes(n_pods, T);
+  return (size_t)kRowsPerWave * kWeights * 8 + kRowClassBytes + kRowsPerWave * rows_row_bytes(n_pods, T);
 }
 
-// The row kernel body.  P policies, wave w replays policies 4w .. 4w+3.
-// fam: per-policy family ids (FAM = -1), weights: [P, kWeights] (device-mapped
-// pinned host memory), gheap: [P, row_heap_entries(N)] HBM heap slices,
-// heap0p: the initial heap shifted by one slot (address = slot + 1).
-template <int FAM>
-__device__ void replay_rows(const DevWorkload& W, const int32_t* fam, const double* weights, uint64_t* gheap,
-                            DevResult* out, int P) {
+// Wave-level phase profiler for the row kernel (diagnostics build only): each
+// instrumented region, whenever the wave executes it (for any of its rows),
+// charges the s_memtime cycles since the previous mark to its phase.  The
+// counters live in the wave's LDS tail so masked-off rows do not matter.
+struct RowNoProf {
+  __device__ void start(FKS_LDS uint64_t*) {}
+  __device__ void mark(int) {}
+  __device__ void flush(uint64_t*) {}
+};
+struct RowProf {
+  FKS_LDS uint64_t* c;   // [0, 8): phase cycles, [8]: last timestamp
+  __device__ void start(FKS_LDS uint64_t* at) {
+    c = at;
+    if (lane_id() < 9) c[lane_id()] = lane_id() == 8 ? __builtin_amdgcn_s_memtime() : 0;
+  }
+  __device__ void mark(int ph) {
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    if (lane_id() == __builtin_amdgcn_readfirstlane(lane_id())) {
+      c[ph] += now - c[8];
+      c[8] = now;
+    }
+  }
+  __device__ void flush(uint64_t* o) {
+    if (lane_id() < 8) o[lane_id()] = c[lane_id()];
+  }
+};
+constexpr int kRowProfBytes = 128;
+
+// The row kernel body: a persistent work queue of policies.  Every row claims
+// policies with atomicAdd(queue, 1); a row that finishes its replay (or
+// aborts on a policy exception) writes the result and claims the next one, so
+// the four rows of a wave stay busy until the batch is drained instead of
+// idling behind their wave's longest replay, and waves that only become
+// resident once others exit find the queue empty and leave at once.  fam: per-policy family ids (FAM = -1), weights: [P, kWeights]
+// (device-mapped pinned host memory), gheap: [4 * gridDim.x,
+// row_heap_entries(N)] HBM heap slices (one per row slot), heap0p: the
+// initial heap shifted by one slot (address = slot + 1).
+template <int FAM, class Prof = RowNoProf>
+__device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const int32_t* fam, const double* weights,
+                            uint64_t* gheap, DevResult* out, int P, int* queue, uint64_t* prof_out = nullptr) {
+  // W: the kernel-argument copy, read once for the hot scalars below; every
+  // other field is re-read where it is used through an opaque pointer to the
+  // HBM copy (scalar loads), so the loop carries no spilled SGPR copies of it
+  auto cold = [&]() {
+    const DevWorkload* g = reinterpret_cast<const DevWorkload*>(uniu64(reinterpret_cast<uint64_t>(Wdev)));
+    asm volatile("" : "+s"(g));
+    return const_ptr(g);
+  };
   extern __shared__ uint64_t lds_raw[];
   const int lane = lane_id();
   const int row = lane >> 4;
   const int rbase = lane & 48;
-  const int p = blockIdx.x * kRowsPerWave + row;
-  const bool live = p < P;
+  const int slot = blockIdx.x * kRowsPerWave + row;
   const int N = W.n_pods;
   const int T = W.heap_top;
   const int lb = W.low_bits, nb = W.node_bits, rb = W.rank_bits;
   const int tshift = rb + lb;
   const uint64_t time_max = (W.time_bits >= 63) ? ~0ull : ((1ull << W.time_bits) - 1);
   int jv = lane & 15;
+  const bool node_valid = jv < W.n_nodes;
 
   FKS_LDS uint64_t* lds = lds_ptr(lds_raw);
   FKS_LDS double* wl = reinterpret_cast<FKS_LDS double*>(lds) + row * kWeights;
-  FKS_LDS char* rowbase = reinterpret_cast<FKS_LDS char*>(lds + kRowsPerWave * kWeights) +
+  FKS_LDS int32_t* cls_lds = reinterpret_cast<FKS_LDS int32_t*>(lds + kRowsPerWave * kWeights);
+  FKS_LDS char* rowbase = reinterpret_cast<FKS_LDS char*>(lds + kRowsPerWave * kWeights) + kRowClassBytes +
                           (size_t)row * rows_row_bytes(N, T);
+  // the waiting-class values (gpu_milli of each class) for the fragmentation minimum
+  if (lane < W.n_classes) cls_lds[lane] = *global_ptr(&W.class_value[lane]);
+  // per-node constants shared by the four rows: cpu / mem totals, GPU count,
+  // per-GPU milli totals -- read back only by creation events, so they hold no
+  // registers through the pop
+  FKS_LDS int32_t* ntab = cls_lds + kRow * kRowClassSlots;
+  if (lane < kRow) {
+    ntab[lane * kNodeConsts + 0] = W.cpu_total[lane];
+    ntab[lane * kNodeConsts + 1] = W.mem_total[lane];
+    ntab[lane * kNodeConsts + 2] = W.ngpus[lane];
+#pragma unroll
+    for (int g = 0; g < kGmax; ++g) ntab[lane * kNodeConsts + 3 + g] = W.gml_total[lane * kGmax + g];
+  }
   RowHeap heap;
   heap.delmap = reinterpret_cast<FKS_LDS uint32_t*>(rowbase);
   heap.top = reinterpret_cast<FKS_LDS uint64_t*>(rowbase + (size_t)lds_delmap_words(N) * 4);
-  heap.h = global_ptr(gheap + (size_t)(live ? p : 0) * row_heap_entries(N));
+  heap.h = global_ptr(gheap + (size_t)slot * row_heap_entries(N));
   heap.T = T;
   heap.lb = lb;
   heap.j = jv;
   heap.rbase = rbase;
+  const FKS_GLOBAL u64x2* heap_src = reinterpret_cast<const FKS_GLOBAL u64x2*>(global_ptr(W.heap0p));
 
-  // ---- prologue: weights, heap image, bitmap, node state
+  auto claim = [&]() {
+    const int c = jv == 0 ? __hip_atomic_fetch_add(queue, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    return row_read(c, rbase, 0);
+  };
+  // per-policy state (row-uniform except the node registers / lane-owned slots)
+  int p = claim();
   int family = FAM;
-  if (live) {
+  NodeRegs<1> nr;
+  auto load_consts = [&]() {
+    const FKS_LDS int32_t* e = ntab + jv * kNodeConsts;
+    nr.cpu_total[0] = e[0];
+    nr.mem_total[0] = e[1];
+    nr.ngpus[0] = e[2];
+#pragma unroll
+    for (int g = 0; g < kGmax; ++g) nr.gmt[0][g] = e[3 + g];
+  };
+  int32_t wcnt[kRowClassSlots];
+  int32_t used_cpu = 0, used_mem = 0, used_gcnt = 0, used_gml = 0;   // host: totals < 2^31
+  RowAcc acc;
+  int32_t processed = 0, next_fire = INT32_MAX;
+  int n_repush = 0, n_dropped = 0, ksnap = 0, n = 0;
+  double thr = 0.0;
+  uint64_t hsh = 0;
+  int32_t exc = EXC_NONE;
+  
+  // start policy p on this row: weights, heap image, bitmap, node state, counters
+  auto begin = [&]() {
     wl[jv] = *global_ptr(&weights[(size_t)p * kWeights + jv]);
-    if (FAM < 0) family = fam[p];
+    if (FAM < 0) family = *global_ptr(&fam[p]);
     const int words = row_heap_entries(N) / 2;   // 16-byte pairs of the shifted heap
-    const FKS_GLOBAL u64x2* src = reinterpret_cast<const FKS_GLOBAL u64x2*>(global_ptr(W.heap0p));
     for (int i = jv; i < words; i += kRow) {
-      const u64x2 v = src[i];
+      const u64x2 v = heap_src[i];
       if (2 * i < T + 1) *reinterpret_cast<FKS_LDS u64x2*>(heap.top + 2 * i) = v;
       else *reinterpret_cast<FKS_GLOBAL u64x2*>(heap.h + 2 * i) = v;
     }
     for (int i = jv; i < lds_delmap_words(N); i += kRow) heap.delmap[i] = 0u;
-  }
-  NodeRegs<1> nr;
-  nr.cpu_left[0] = W.cpu_left0[jv];
-  nr.mem_left[0] = W.mem_left0[jv];
-  nr.gpu_left[0] = W.gpu_left0[jv];
-  nr.cpu_total[0] = W.cpu_total[jv];
-  nr.mem_total[0] = W.mem_total[jv];
-  nr.ngpus[0] = W.ngpus[jv];
+    const FKS_CONST DevWorkload* Wb = cold();
+    nr.cpu_left[0] = Wb->cpu_left0[jv];
+    nr.mem_left[0] = Wb->mem_left0[jv];
+    nr.gpu_left[0] = Wb->gpu_left0[jv];
 #pragma unroll
-  for (int g = 0; g < kGmax; ++g) {
-    nr.gml[0][g] = W.gml_left0[jv * kGmax + g];
-    nr.gmt[0][g] = W.gml_total[jv * kGmax + g];
-  }
-  const bool node_valid = jv < W.n_nodes;
-  int32_t wcnt[kRowClassSlots];
+    for (int g = 0; g < kGmax; ++g) {
+      nr.gml[0][g] = Wb->gml_left0[jv * kGmax + g];
+    }
 #pragma unroll
-  for (int s = 0; s < kRowClassSlots; ++s) wcnt[s] = 0;
+    for (int sl = 0; sl < kRowClassSlots; ++sl) wcnt[sl] = 0;
+    used_cpu = (int32_t)Wb->used_cpu0; used_mem = (int32_t)Wb->used_mem0;
+    used_gcnt = (int32_t)Wb->used_gcnt0; used_gml = (int32_t)Wb->used_gmilli0;
+    acc.init();
+    processed = 0; n_repush = 0; n_dropped = 0; ksnap = 0;
+    thr = Wb->thr_after_fire;
+    if (Wb->n_fire > 0) {
+      next_fire = (int32_t)*global_ptr(&Wb->snap_fire[0]);
+    } else {
+      int32_t c = 1;
+      while ((double)c / (double)N < thr) ++c;
+      next_fire = c;
+    }
+    hsh = 0xcbf29ce484222325ull;
+    exc = EXC_NONE;
+    n = N;
+    __builtin_amdgcn_s_waitcnt(0);   // heap image stored before the first pop reads it
+  };
 
-  int64_t used_cpu = W.used_cpu0, used_mem = W.used_mem0, used_gcnt = W.used_gcnt0, used_gml = W.used_gmilli0;
-  RowAcc acc;
-  acc.init();
-  int64_t processed = 0;
-  int n_repush = 0, n_dropped = 0;
-  int ksnap = 0;
-  const int n_fire = W.n_fire;
-  int64_t next_fire = n_fire > 0 ? W.snap_fire[0] : INT64_MAX;
-  double thr = W.thr_after_fire;
-  uint64_t hsh = 0xcbf29ce484222325ull;
-  int32_t exc = EXC_NONE;
-  int n = live ? N : 0;
-  __syncthreads();
+  Prof prof;
+  prof.start(reinterpret_cast<FKS_LDS uint64_t*>(reinterpret_cast<FKS_LDS char*>(lds) + rows_lds_bytes(N, T)));
+  bool have = p < P;
+  if (have) begin();
+  prof.mark(PH_EVAL);
 
-  while (n > 0) {
+  while (have) {
     // opaque lane id: keeps the lane-derived subtree predicates out of SGPRs
     asm volatile("" : "+v"(jv));
     heap.j = jv;
-    // ---------------- pop
-    const uint64_t top = heap.ld(0);
-    const int rank = (int)((top >> lb) & ((1ull << rb) - 1));
-    typedef int v4i __attribute__((ext_vector_type(4)));
-    const v4i precv = *reinterpret_cast<const FKS_GLOBAL v4i*>(global_ptr(&W.pod[rank]));
-    const uint64_t last = heap.ld(n - 1);
-    --n;
-    if (n > 0) heap.pop_reinsert(n, last);
-    const int kind = (int)(top & 3);
-    const int64_t t = (int64_t)(top >> tshift);
-    PodView pod;
-    pod.cpu = precv.x; pod.mem = precv.y; pod.dur = precv.z;
-    pod.gmilli = precv.w & 0xFFFF; pod.ngpu = (precv.w >> 16) & 0xFF; pod.cls = (precv.w >> 24) & 0xFF;
-    pod.ctime = t; pod.rank = rank;
+    do {   // one event; `break` = abort the replay (exc set) or end of the event
+      // ---------------- pop
+      const uint64_t top = heap.ld(0);
+      const int rank = (int)((top >> lb) & ((1ull << rb) - 1));
+      typedef int v4i __attribute__((ext_vector_type(4)));
+      const v4i precv = *reinterpret_cast<const FKS_GLOBAL v4i*>(global_ptr(&W.pod[rank]));
+      const uint64_t last = heap.ld(n - 1);
+      --n;
+      if (n > 0) heap.pop_reinsert(n, last);
+      const int kind = (int)(top & 3);
+      const int64_t t = (int64_t)(top >> tshift);
+      PodView pod;
+      pod.cpu = precv.x; pod.mem = precv.y; pod.dur = precv.z;
+      pod.gmilli = precv.w & 0xFFFF; pod.ngpu = (precv.w >> 16) & 0xFF; pod.cls = (precv.w >> 24) & 0xFF;
+      pod.ctime = t; pod.rank = rank;
+      prof.mark(PH_POP);
 
-    if (kind == kDelete) {
-      const int node = (int)((top >> 2) & ((1u << nb) - 1));
-      const int mask = (int)((top >> (2 + nb)) & 0xFF);
-      if (jv == node) {
-        nr.cpu_left[0] += pod.cpu;
-        nr.mem_left[0] += pod.mem;
-        nr.gpu_left[0] += pod.ngpu;
-#pragma unroll
-        for (int g = 0; g < kGmax; ++g)
-          if ((mask >> g) & 1) nr.gml[0][g] += pod.gmilli;
-      }
-      used_cpu -= pod.cpu; used_mem -= pod.mem; used_gcnt -= pod.ngpu;
-      used_gml -= (int64_t)pod.gmilli * __popc(mask);
-      if (W.trace_hash) hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 1, (uint64_t)t);
-    } else {
-      // ---------------- creation: score the row's nodes, first maximum wins
-      int lexc = EXC_NONE;
-      int64_t s = 0;
-      if (node_valid && feasible<1>(0, nr, pod)) {
-        double w[kWeights];
-#pragma unroll
-        for (int q = 0; q < kWeights; ++q) w[q] = q < family_weights(FAM) ? wl[q] : 0.0;
-        s = BuiltinScorerDev<FAM>::template score_weights<1>(family, w, 0, nr, pod, lexc);
-        if (lexc != EXC_NONE) s = 0;
-      }
-      const uint32_t bad = row_ballot(lexc != EXC_NONE, rbase);
-      if (bad) {
-        exc = row_read(lexc, rbase, __ffs(bad) - 1);
-        break;
-      }
-      const int64_t m = (int64_t)row_max_u64((uint64_t)s);   // scores are >= 0
-      const int best_node = m > 0 ? __ffs(row_ballot(s == m, rbase)) - 1 : -1;
-
-      if (best_node < 0) {
-        // ---------------- failed placement
-        if (kind == kFresh && pod.ngpu > 0) {
-#pragma unroll
-          for (int sl = 0; sl < kRowClassSlots; ++sl)
-            if (sl == (pod.cls >> 4) && jv == (pod.cls & 15)) wcnt[sl] += 1;
-        }
-        double frag = 0.0;
-        int mcls = -1;
-#pragma unroll
-        for (int sl = 0; sl < kRowClassSlots; ++sl) {
-          const uint32_t b = row_ballot(wcnt[sl] > 0, rbase);
-          if (mcls < 0 && b) mcls = sl * kRow + __ffs(b) - 1;
-        }
-        if (mcls >= 0) {
-          const int mv = *global_ptr(&W.class_value[mcls]);
-          int64_t stranded = 0;
-#pragma unroll
-          for (int g = 0; g < kGmax; ++g) {
-            const int l = nr.gml[0][g];
-            if (g < nr.ngpus[0] && 0 < l && l < mv) stranded += l;
-          }
-          stranded = row_sum_i64(node_valid ? stranded : 0);
-          const int64_t tg = W.tot_gmilli;
-          frag = tg > 0 ? (double)stranded / (double)tg : 0.0;
-        }
-        acc.add(4, frag, jv);
-        const int f = heap.first_deletion(n);
-        if (f >= 0) {
-          const uint64_t nt = (heap.ld(f) >> tshift) + 1;
-          if (nt > time_max) { exc = EXC_UNSUPPORTED; break; }
-          heap.push(n, (nt << tshift) | ((uint64_t)rank << lb) | kRetry);
-          ++n;
-          ++n_repush;
-        } else {
-          ++n_dropped;
-        }
-        if (W.trace_hash) hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 2, (uint64_t)t);
-      } else {
-        // ---------------- commit on best_node
-        int gmask = 0, ok = 1;
-        if (pod.ngpu > 0) {
-          int myok = 1;
-          const int mymask = pick_gpus<1>(nr, 0, pod.gmilli, pod.ngpu, W.first_fit_alloc != 0, myok);
-          const int packed = row_read(mymask | (myok << 8), rbase, best_node);
-          gmask = packed & 0xFF;
-          ok = packed >> 8;
-        }
-        if (!ok) { exc = EXC_ALLOC; break; }
-        if (jv == best_node) {
-          nr.cpu_left[0] -= pod.cpu;
-          nr.mem_left[0] -= pod.mem;
-          nr.gpu_left[0] -= pod.ngpu;
+      if (kind == kDelete) {
+        const int node = (int)((top >> 2) & ((1u << nb) - 1));
+        const int mask = (int)((top >> (2 + nb)) & 0xFF);
+        if (jv == node) {
+          nr.cpu_left[0] += pod.cpu;
+          nr.mem_left[0] += pod.mem;
+          nr.gpu_left[0] += pod.ngpu;
 #pragma unroll
           for (int g = 0; g < kGmax; ++g)
-            if ((gmask >> g) & 1) nr.gml[0][g] -= pod.gmilli;
+            if ((mask >> g) & 1) nr.gml[0][g] += pod.gmilli;
         }
-        used_cpu += pod.cpu; used_mem += pod.mem; used_gcnt += pod.ngpu;
-        used_gml += (int64_t)pod.gmilli * __popc(gmask);
-        if (kind == kRetry && pod.ngpu > 0) {
+        used_cpu -= pod.cpu; used_mem -= pod.mem; used_gcnt -= pod.ngpu;
+        used_gml -= pod.gmilli * __popc(mask);
+        if (cold()->trace_hash) hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 1, (uint64_t)t);
+        prof.mark(PH_DELETE);
+      } else {
+        // ---------------- creation: score the row's nodes, first maximum wins
+        load_consts();
+        int lexc = EXC_NONE;
+        int64_t s = 0;
+        if (node_valid && feasible<1>(0, nr, pod)) {
+          // weights read from LDS where each term uses them (no 32-VGPR weight vector)
+          const FKS_LDS double* wq = wl;
+          s = BuiltinScorerDev<FAM>::template score_weights<1>(family, wq, 0, nr, pod, lexc);
+          if (lexc != EXC_NONE) s = 0;
+        }
+        const uint32_t bad = row_ballot(lexc != EXC_NONE, rbase);
+        if (bad) {
+          exc = row_read(lexc, rbase, __ffs(bad) - 1);
+          break;
+        }
+        const int64_t m = (int64_t)row_max_u64((uint64_t)s);   // scores are >= 0
+        const int best_node = m > 0 ? __ffs(row_ballot(s == m, rbase)) - 1 : -1;
+        uint64_t push_item = 0;   // never 0 for a real entry: keys hold the pod rank's time > 0 or kind
+        prof.mark(PH_SCORE);
+
+        if (best_node < 0) {
+          // ---------------- failed placement
+          if (kind == kFresh && pod.ngpu > 0) {
 #pragma unroll
-          for (int sl = 0; sl < kRowClassSlots; ++sl)
-            if (sl == (pod.cls >> 4) && jv == (pod.cls & 15)) wcnt[sl] -= 1;
+            for (int sl = 0; sl < kRowClassSlots; ++sl)
+              if (sl == (pod.cls >> 4) && jv == (pod.cls & 15)) wcnt[sl] += 1;
+          }
+          double frag = 0.0;
+          int mcls = -1;
+#pragma unroll
+          for (int sl = 0; sl < kRowClassSlots; ++sl) {
+            const uint32_t b = row_ballot(wcnt[sl] > 0, rbase);
+            if (mcls < 0 && b) mcls = sl * kRow + __ffs(b) - 1;
+          }
+          if (mcls >= 0) {
+            const int mv = cls_lds[mcls];
+            int64_t stranded = 0;
+#pragma unroll
+            for (int g = 0; g < kGmax; ++g) {
+              const int l = nr.gml[0][g];
+              if (g < nr.ngpus[0] && 0 < l && l < mv) stranded += l;
+            }
+            stranded = row_sum_i64(node_valid ? stranded : 0);
+            const int64_t tg = cold()->tot_gmilli;
+            frag = tg > 0 ? (double)stranded / (double)tg : 0.0;
+          }
+          acc.add(4, frag, jv);
+          const int f = heap.first_deletion(n);
+          if (f >= 0) {
+            const uint64_t nt = (heap.ld(f) >> tshift) + 1;
+            if (nt > time_max) { exc = EXC_UNSUPPORTED; break; }
+            push_item = (nt << tshift) | ((uint64_t)rank << lb) | kRetry;
+            ++n_repush;
+          } else {
+            ++n_dropped;
+          }
+          if (cold()->trace_hash) hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 2, (uint64_t)t);
+          prof.mark(PH_FAIL);
+        } else {
+          // ---------------- commit on best_node
+          int gmask = 0, ok = 1;
+          if (pod.ngpu > 0) {
+            int myok = 1;
+            const int mymask = pick_gpus<1>(nr, 0, pod.gmilli, pod.ngpu, cold()->first_fit_alloc != 0, myok);
+            const int packed = row_read(mymask | (myok << 8), rbase, best_node);
+            gmask = packed & 0xFF;
+            ok = packed >> 8;
+          }
+          if (!ok) { exc = EXC_ALLOC; break; }
+          if (jv == best_node) {
+            nr.cpu_left[0] -= pod.cpu;
+            nr.mem_left[0] -= pod.mem;
+            nr.gpu_left[0] -= pod.ngpu;
+#pragma unroll
+            for (int g = 0; g < kGmax; ++g)
+              if ((gmask >> g) & 1) nr.gml[0][g] -= pod.gmilli;
+          }
+          used_cpu += pod.cpu; used_mem += pod.mem; used_gcnt += pod.ngpu;
+          used_gml += pod.gmilli * __popc(gmask);
+          if (kind == kRetry && pod.ngpu > 0) {
+#pragma unroll
+            for (int sl = 0; sl < kRowClassSlots; ++sl)
+              if (sl == (pod.cls >> 4) && jv == (pod.cls & 15)) wcnt[sl] -= 1;
+          }
+          const uint64_t dt = (uint64_t)(t + pod.dur);
+          if (t + pod.dur < 0 || dt > time_max) { exc = EXC_UNSUPPORTED; break; }
+          push_item = (dt << tshift) | ((uint64_t)rank << lb) | ((uint64_t)gmask << (2 + nb)) |
+                      ((uint64_t)best_node << 2) | kDelete;
+          if (cold()->trace_hash)
+            hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2), ((uint64_t)t << 8) ^ (uint64_t)best_node);
+          prof.mark(PH_COMMIT);
         }
-        const uint64_t dt = (uint64_t)(t + pod.dur);
-        if (t + pod.dur < 0 || dt > time_max) { exc = EXC_UNSUPPORTED; break; }
-        heap.push(n, (dt << tshift) | ((uint64_t)rank << lb) | ((uint64_t)gmask << (2 + nb)) |
-                         ((uint64_t)best_node << 2) | kDelete);
-        ++n;
-        if (W.trace_hash) hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2), ((uint64_t)t << 8) ^ (uint64_t)best_node);
+        // one heappush for both outcomes (re-queued creation or deletion): rows
+        // that placed and rows that failed share the ancestor gather
+        if (push_item != 0) {
+          heap.push(n, push_item);
+          ++n;
+        }
       }
-    }
 
-    // ---------------- evaluator hook (host-precomputed snapshot schedule)
-    ++processed;
-    bool fire;
-    if (ksnap < n_fire) fire = processed >= next_fire;
-    else fire = (double)processed / (double)N >= thr;
-    if (fire) {
-      const double r0 = W.tot_cpu > 0 ? (double)used_cpu / (double)W.tot_cpu : 0.0;
-      const double r1 = W.tot_mem > 0 ? (double)used_mem / (double)W.tot_mem : 0.0;
-      const double r2 = W.tot_gcnt > 0 ? (double)used_gcnt / (double)W.tot_gcnt : 0.0;
-      const double r3 = W.tot_gmilli > 0 ? (double)used_gml / (double)W.tot_gmilli : 0.0;
-      acc.add(0, r0, jv); acc.add(1, r1, jv); acc.add(2, r2, jv); acc.add(3, r3, jv);
-      if (ksnap >= n_fire) thr += W.snapshot_interval;
-      ++ksnap;
-      next_fire = ksnap < n_fire ? *global_ptr(&W.snap_fire[ksnap]) : INT64_MAX;
-    }
-  }
-  if (!live) return;
+      // ---------------- evaluator hook (host-precomputed snapshot schedule)
+      ++processed;
+      if (processed >= next_fire) {
+        const FKS_CONST DevWorkload* Ws = cold();
+        const double r0 = Ws->tot_cpu > 0 ? (double)used_cpu / (double)Ws->tot_cpu : 0.0;
+        const double r1 = Ws->tot_mem > 0 ? (double)used_mem / (double)Ws->tot_mem : 0.0;
+        const double r2 = Ws->tot_gcnt > 0 ? (double)used_gcnt / (double)Ws->tot_gcnt : 0.0;
+        const double r3 = Ws->tot_gmilli > 0 ? (double)used_gml / (double)Ws->tot_gmilli : 0.0;
+        acc.add(0, r0, jv); acc.add(1, r1, jv); acc.add(2, r2, jv); acc.add(3, r3, jv);
+        ++ksnap;
+        if (ksnap < Ws->n_fire) {
+          next_fire = (int32_t)*global_ptr(&Ws->snap_fire[ksnap]);
+        } else {
+          // past the host's precomputed schedule: the next count c > processed
+          // with c / N >= thr (the evaluator's IEEE test), thr += interval after
+          // every snapshot beyond it (simulator/evaluator.py:55-67)
+          if (ksnap > Ws->n_fire) thr += Ws->snapshot_interval;
+          int32_t c = processed + 1;
+          while ((double)c / (double)N < thr) ++c;
+          next_fire = c;
+        }
+      }
+      prof.mark(PH_EVAL);
+    } while (0);
 
-  const int64_t n_snap = (int64_t)(((uint64_t)(uint32_t)row_read((int)(acc.count >> 32), rbase, 0) << 32) |
-                                   (uint32_t)row_read((int)acc.count, rbase, 0));
-  const int64_t n_frag = (int64_t)(((uint64_t)(uint32_t)row_read((int)(acc.count >> 32), rbase, 4) << 32) |
-                                   (uint32_t)row_read((int)acc.count, rbase, 4));
-  const int inexact = row_ballot(jv < 5 && acc.inexact != 0, rbase) != 0;
-  DevResult* o = out + p;
-  if (jv < 5) {
-    o->acc_lo[jv] = (uint64_t)(u128)acc.sum;
-    o->acc_hi[jv] = (uint64_t)((u128)acc.sum >> 64);
+    if (n > 0 && exc == EXC_NONE) continue;
+    // ---------------- replay done (or aborted): result, then the next policy
+    const int64_t n_snap = (int64_t)(((uint64_t)(uint32_t)row_read((int)(acc.count >> 32), rbase, 0) << 32) |
+                                     (uint32_t)row_read((int)acc.count, rbase, 0));
+    const int64_t n_frag = (int64_t)(((uint64_t)(uint32_t)row_read((int)(acc.count >> 32), rbase, 4) << 32) |
+                                     (uint32_t)row_read((int)acc.count, rbase, 4));
+    const int inexact = row_ballot(jv < 5 && acc.inexact != 0, rbase) != 0;
+    DevResult* o = out + p;
+    if (jv < 5) {
+      o->acc_lo[jv] = (uint64_t)(u128)acc.sum;
+      o->acc_hi[jv] = (uint64_t)((u128)acc.sum >> 64);
+    }
+    if (jv == 0) {
+      o->n_events = processed;
+      o->n_snap = n_snap;
+      o->n_frag = n_frag;
+      o->n_unplaced = n_dropped;
+      o->n_repush = n_repush;
+      o->max_nodes = 0;
+      o->hash = hsh;
+      o->exc = exc;
+      o->inexact = inexact;
+    }
+    p = claim();
+    have = p < P;
+    if (have) begin();
+    prof.mark(PH_EVAL + 1);   // result write-back + next policy's prologue
   }
-  if (jv == 0) {
-    o->n_events = processed;
-    o->n_snap = n_snap;
-    o->n_frag = n_frag;
-    o->n_unplaced = n_dropped;
-    o->n_repush = n_repush;
-    o->max_nodes = 0;
-    o->hash = hsh;
-    o->exc = exc;
-    o->inexact = inexact;
-  }
+  if (prof_out) prof.flush(prof_out + (size_t)blockIdx.x * 8);
 }
 
 }  // namespace fksd

@@ -66,14 +66,14 @@ struct BuiltinScorerDev {
     double w[kWeights];
 #pragma unroll
     for (int k = 0; k < kWeights; ++k) w[k] = k < family_weights(FAM) ? q[k] : 0.0;
-    return score_weights<NPASS>(family, w, ps, nr, pod, exc);
+    return score_weights<NPASS>(family, (const double*)w, ps, nr, pod, exc);
   }
 
   // The family formulas on an already-loaded weight vector (shared with the
   // 4-policies-per-wave row kernel, replay_rows.hip.h, whose weights come
   // from LDS).  The caller has checked feasibility.
-  template <int NPASS>
-  __device__ static int64_t score_weights(int family, const double* w, int ps, const NodeRegs<NPASS>& nr,
+  template <int NPASS, class WP>
+  __device__ static int64_t score_weights(int family, WP w, int ps, const NodeRegs<NPASS>& nr,
                                           const PodView& pod, int& exc) {
     switch (FAM >= 0 ? FAM : family) {
       case FAM_FIRST_FIT:
@@ -118,19 +118,21 @@ struct BuiltinScorerDev {
   // the weighted terms are accumulated as they are produced (same order and
   // rounding as `score += w_k * (f_k)`), so no 16-double feature vector is
   // held live across the node loop.
-  template <int NPASS>
-  __device__ static double composite(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, const double* w) {
+  template <int NPASS, class WP>
+  __device__ static double composite(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, WP w) {
     const int ng = nr.ngpus[ps];
     const bool gpod = pod.ngpu > 0;
-    const int64_t ct = nr.cpu_total[ps], mt = nr.mem_total[ps];
-    const int64_t cl = nr.cpu_left[ps], ml = nr.mem_left[ps];
-    const double cpu_u = (double)(ct - cl) / (double)(ct > 1 ? ct : 1);
-    const double mem_u = (double)(mt - ml) / (double)(mt > 1 ? mt : 1);
-    int64_t free_m = 0, idle = 0, gmax = 0, gmin = 0, best = -1;
+    // 32-bit temporaries: GPU milli totals < 2^20 (prepare_device_workload),
+    // so sums over <= 8 GPUs cannot overflow; differences widen where formed
+    const int32_t ct = nr.cpu_total[ps], mt = nr.mem_total[ps];
+    const int32_t cl = nr.cpu_left[ps], ml = nr.mem_left[ps];
+    const double cpu_u = (double)((int64_t)ct - cl) / (double)(ct > 1 ? ct : 1);
+    const double mem_u = (double)((int64_t)mt - ml) / (double)(mt > 1 ? mt : 1);
+    int32_t free_m = 0, idle = 0, gmax = 0, gmin = 0, best = -1;
 #pragma unroll
     for (int j = 0; j < kGmax; ++j) {
       if (j < ng) {
-        const int64_t l = nr.gml[ps][j];
+        const int32_t l = nr.gml[ps][j];
         free_m += l;
         idle += (l == nr.gmt[ps][j]);
         gmax = (j == 0 || l > gmax) ? l : gmax;
@@ -141,7 +143,7 @@ struct BuiltinScorerDev {
     double gpu_u = 0.0;
     if (gpod) {
       const int64_t cap = (int64_t)nr.gpu_left[ps] * nr.gmt[ps][0];
-      gpu_u = (double)(cap - free_m) / (double)(cap > 1 ? cap : 1);
+      gpu_u = (double)(cap - free_m) / (double)(cap > 1 ? cap : 1);   // cap is int64
     }
     double s = 0.0;
     auto acc = [&](int k, double f) { if (w[k] != 0.0) s = s + w[k] * f; };
@@ -153,10 +155,9 @@ struct BuiltinScorerDev {
     acc(5, gpod ? (gpu_u < 0.7 ? 1.0 - gpu_u : 0.0) : 0.0);
     acc(6, gpod ? (gpu_u >= 0.7 ? 1.0 - gpu_u : 0.0) : 0.0);
     {
-      const int64_t d = pod.gmilli > 1 ? pod.gmilli : 1;
-      int64_t m = free_m % d;
-      if (m != 0 && ((m < 0) != (d < 0))) m += d;
-      acc(7, gpod ? (double)m : 0.0);
+      // free_m >= 0, d >= 1: Python's floor modulo is the unsigned remainder
+      const uint32_t d = pod.gmilli > 1 ? (uint32_t)pod.gmilli : 1u;
+      acc(7, gpod ? (double)((uint32_t)free_m % d) : 0.0);
     }
     const double a = (double)cl / (double)(ml > 1 ? ml : 1);
     const double b = (double)pod.cpu / (double)(pod.mem > 1 ? pod.mem : 1);
@@ -184,7 +185,7 @@ struct BuiltinScorerDev {
     f[2] = rm;
     f[3] = (double)((int64_t)nr.gpu_left[ps] - pod.ngpu) / (double)ngd;
     f[4] = fabs(rc - rm);
-    int64_t free_m = 0, idle = 0, part = 0, best = -1;
+    int32_t free_m = 0, idle = 0, part = 0, best = -1;
 #pragma unroll
     for (int j = 0; j < kGmax; ++j) {
       if (j < ng) {
@@ -197,10 +198,8 @@ struct BuiltinScorerDev {
     }
     f[5] = (double)free_m / 1000.0;
     {
-      const int64_t d = pod.gmilli > 1 ? pod.gmilli : 1;
-      int64_t m = free_m % d;
-      if (m != 0 && ((m < 0) != (d < 0))) m += d;
-      f[6] = (double)m / 1000.0;
+      const uint32_t d = pod.gmilli > 1 ? (uint32_t)pod.gmilli : 1u;
+      f[6] = (double)((uint32_t)free_m % d) / 1000.0;
     }
     f[7] = (double)idle / (double)ngd;
     f[8] = (double)part / (double)ngd;

@@ -93,6 +93,8 @@ def prepare_device_workload(w: Workload, snapshot_interval: float = 0.05) -> Dic
         raise UnsupportedWorkload("more than 256 nodes")
     if c.max_gpus_per_node > GMAX:
         raise UnsupportedWorkload(f"more than {GMAX} GPUs on a node")
+    if c.gpu_milli_total.size and (c.gpu_milli_total.max() >= 2 ** 20 or c.gpu_milli_total.min() < 0):
+        raise UnsupportedWorkload("GPU milli totals outside [0, 2^20) (32-bit per-node sums on device)")
     if len(np.unique(p.pod_rank)) != P:
         raise UnsupportedWorkload("duplicate pod ids")
     if P >= 2 ** 20:
@@ -262,6 +264,12 @@ class DeviceEvaluator:
         W = np.zeros((len(fam), WEIGHTS_PER_POLICY), dtype=np.float64)
         W[:, :np.asarray(weights).shape[1]] = weights
         return self._eng.profile(fam, W, None)
+
+    ROW_PHASES = ("pop", "delete", "score", "fail", "commit", "eval", "next_policy")
+
+    def profile_rows(self, family: str, weights: np.ndarray):
+        """Row kernel, s_memtime build: (result table, per-wave cycles [waves, 8] by ROW_PHASES)."""
+        return self._eng.profile_rows(*self._builtin_args(family, weights))
 
     def profile_programs(self, progs: Sequence[CompiledPolicy]):
         packed = pack_programs(progs) + (max(p.nregs for p in progs),)
