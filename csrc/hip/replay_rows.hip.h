@@ -79,6 +79,7 @@ struct RowHeap {
   FKS_LDS uint32_t* delmap;   // bit p set <=> slot p holds a deletion
   int lb;
   int j, rbase;               // lane within the row, first lane of the row
+  uint32_t anc, dir;          // subtree node j: BFS indices of its ancestors / of those stepping right
 
   __device__ __forceinline__ uint64_t ld(int i) const { return i < T ? top[i + 1] : h[i + 1]; }
   __device__ __forceinline__ void st(int i, uint64_t v) const {
@@ -130,18 +131,16 @@ struct RowHeap {
       const bool go_r = valid && (c + 1 < n) && !(vl < vr);
       const uint32_t m = row_ballot(go_r, rbase);
       const uint32_t ex = row_ballot(valid, rbase);
-      int cj = 0, taken = 0, idx = 0;
-      uint32_t onm = 0;
-#pragma unroll
-      for (int lv = 0; lv < 4; ++lv) {
-        if (taken == lv && ((ex >> cj) & 1)) {
-          onm |= 1u << cj;
-          idx = 2 * (cj - ((1 << lv) - 1)) + (int)((m >> cj) & 1);
-          cj = (1 << (lv + 1)) - 1 + idx;
-          taken = lv + 1;
-        }
-      }
-      const bool on = (onm >> j) & 1;
+      // node j is on the path iff every ancestor in the subtree has children
+      // and chooses the child towards j (lane constants anc / dir), and it
+      // is a path *parent* iff it has children itself: no serial walk
+      const bool on = valid && (ex & anc) == anc && ((m ^ dir) & anc) == 0;
+      const uint32_t onm = row_ballot(on, rbase);
+      const int jd = 31 - __clz(onm);                 // deepest path parent
+      const int kd = jd == 0 ? 0 : jd < 3 ? 1 : jd < 7 ? 2 : 3;
+      const int taken = kd + 1;                       // levels descended this round
+      const int qd = ((pos + 1) << kd) - 1 + (jd - ((1 << kd) - 1));
+      const int next = 2 * qd + 1 + (int)((m >> jd) & 1);   // its chosen child: the new path end
       const uint64_t v = go_r ? vr : vl;
       const uint32_t g = row_ballot(on && last < v, rbase);
       const int jl = g ? __ffs(g) - 1 : kRow;
@@ -154,7 +153,7 @@ struct RowHeap {
         target = ((pos + 1) << kk) - 1 + (jl - ((1 << kk) - 1));
         break;
       }
-      pos = ((pos + 1) << taken) - 1 + idx;
+      pos = next;
       if (taken < 4) break;   // reached a leaf
     }
     if (target < 0) target = pos;
@@ -324,6 +323,12 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
   heap.lb = lb;
   heap.j = jv;
   heap.rbase = rbase;
+  heap.anc = heap.dir = 0;
+  for (int x = jv; x > 0 && x < 15; x = (x - 1) >> 1) {
+    const int a = (x - 1) >> 1;
+    heap.anc |= 1u << a;
+    if ((x & 1) == 0) heap.dir |= 1u << a;   // even BFS index = right child
+  }
   const FKS_GLOBAL u64x2* heap_src = reinterpret_cast<const FKS_GLOBAL u64x2*>(global_ptr(W.heap0p));
 
   auto claim = [&]() {
