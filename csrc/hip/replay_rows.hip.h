@@ -92,10 +92,15 @@ struct RowHeap {
     if (c < T) return *reinterpret_cast<const FKS_LDS u64x2*>(top + c + 1);
     return *reinterpret_cast<const FKS_GLOBAL u64x2*>(h + c + 1);
   }
+  // bit `pos` of the deletion bitmap := (v is a DELETION): one LDS masked-OR
+  // atomic (word = (word & ~bit) | data), safe when several lanes of the row
+  // hit the same word in one instruction.  LDS operations of a wave complete
+  // in order, so later bitmap reads see it without an extra wait.
   __device__ __forceinline__ void mark(int pos, uint64_t v) const {
     const uint32_t bit = 1u << (pos & 31);
-    if ((v & 3) == kDelKind) __hip_atomic_fetch_or(&delmap[pos >> 5], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    else __hip_atomic_fetch_and(&delmap[pos >> 5], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t data = (v & 3) == kDelKind ? bit : 0u;
+    const uint32_t addr = (uint32_t)(uintptr_t)(delmap + (pos >> 5));
+    asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(addr), "v"(bit), "v"(data) : "memory");
   }
 
   // Keys compare as plain u64: a pod has at most one entry in the heap, so two
@@ -192,35 +197,43 @@ struct RowHeap {
   }
 };
 
-// Exact fixed-point accumulators 0-4 on lanes 0-4 of the row (LaneAcc's
-// arithmetic, lane-within-row ownership).
+// Exact fixed-point accumulators 0-4 on lanes 0-4 of the row: sum of v * 2^96
+// over the added doubles (LaneAcc's grid and contract).  Everything the row
+// kernel accumulates -- utilisation ratios and fragmentation -- is >= +0.0,
+// so the sum is an unsigned 128-bit pair (lo, hi) and the conversion is a
+// two-word shift; a negative, subnormal, non-finite or off-grid value marks
+// the replay inexact (the host then re-runs it on the CPU oracle).
 struct RowAcc {
-  i128 sum;
-  int64_t count;
+  uint64_t lo, hi;
+  int32_t count;
   int32_t inexact;
-  __device__ void init() { sum = 0; count = 0; inexact = 0; }
+  __device__ void init() { lo = hi = 0; count = 0; inexact = 0; }
   __device__ void add(int k, double v, int j) {
     const bool mine = j == k;
     const uint64_t bits = (uint64_t)__double_as_longlong(v);
-    const int E = (int)((bits >> 52) & 0x7FF);
-    const uint64_t frac = bits & ((1ull << 52) - 1);
     if (mine) ++count;
-    if (E == 0 && frac == 0) return;
-    bool bad = (E == 0x7FF || E == 0);
-    uint64_t M = frac | (1ull << 52);
-    int shift = E - 979;
-    if (!bad && shift < 0) {
-      if (shift <= -53 || (M & ((1ull << (-shift)) - 1))) bad = true;
-      else { M >>= (-shift); shift = 0; }
+    if (bits == 0) return;                                   // +0.0
+    const int E = (int)(bits >> 52);                         // sign bit set -> E >= 2048
+    const uint64_t M = (bits & ((1ull << 52) - 1)) | (1ull << 52);
+    const int shift = E - 979;                               // v * 2^96 = M << shift
+    bool bad = E == 0 || E >= 0x7FF || shift > 126 - 53;
+    uint64_t tl, th;
+    if (shift >= 0) {
+      tl = shift < 64 ? M << shift : 0ull;
+      th = shift == 0 ? 0ull : shift < 64 ? M >> (64 - shift) : M << (shift - 64);
+    } else {
+      bad = bad || shift <= -53 || (M & ((1ull << (-shift)) - 1)) != 0;
+      tl = M >> (-shift & 63);
+      th = 0;
     }
-    if (!bad && shift > 126 - 53) bad = true;
-    if (bad) { if (mine) inexact = 1; return; }
-    i128 t = (i128)(u128)M << shift;
-    if (bits >> 63) t = -t;
+    if (bad) {
+      if (mine) inexact = 1;
+      return;
+    }
     if (mine) {
-      sum += t;
-      const u128 mag = sum < 0 ? (u128)(-sum) : (u128)sum;
-      if (mag >> 126) inexact = 1;
+      lo += tl;
+      hi += th + (lo < tl);
+      if (hi >> 62) inexact = 1;   // keep LaneAcc's 2^126 headroom
     }
   }
 };
@@ -565,15 +578,13 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
 
     if (n > 0 && exc == EXC_NONE) continue;
     // ---------------- replay done (or aborted): result, then the next policy
-    const int64_t n_snap = (int64_t)(((uint64_t)(uint32_t)row_read((int)(acc.count >> 32), rbase, 0) << 32) |
-                                     (uint32_t)row_read((int)acc.count, rbase, 0));
-    const int64_t n_frag = (int64_t)(((uint64_t)(uint32_t)row_read((int)(acc.count >> 32), rbase, 4) << 32) |
-                                     (uint32_t)row_read((int)acc.count, rbase, 4));
+    const int64_t n_snap = row_read(acc.count, rbase, 0);
+    const int64_t n_frag = row_read(acc.count, rbase, 4);
     const int inexact = row_ballot(jv < 5 && acc.inexact != 0, rbase) != 0;
     DevResult* o = out + p;
     if (jv < 5) {
-      o->acc_lo[jv] = (uint64_t)(u128)acc.sum;
-      o->acc_hi[jv] = (uint64_t)((u128)acc.sum >> 64);
+      o->acc_lo[jv] = acc.lo;
+      o->acc_hi[jv] = acc.hi;
     }
     if (jv == 0) {
       o->n_events = processed;
