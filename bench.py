@@ -46,13 +46,18 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--islands", type=int, default=4, help="islands per GPU")
-    ap.add_argument("--candidates", type=int, default=4096, help="candidates per island per generation")
+    # 12,288 per island: each row of the persistent row kernel drains ~3 policies
+    # per launch, so short replays backfill behind long ones (4,096: one policy
+    # per row, every wave waits for its longest replay; profiles/README.md)
+    ap.add_argument("--candidates", type=int, default=12288, help="candidates per island per generation")
     ap.add_argument("--elite", type=int, default=32)
     ap.add_argument("--family", default="composite_linear", choices=["random_linear", "feature_linear", "composite_linear"])
     ap.add_argument("--migrate-every", type=int, default=5)
     ap.add_argument("--migrants", type=int, default=8)
     ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"])
     ap.add_argument("--heap-mode", default="auto", choices=["auto", "lds", "hbm"])
+    ap.add_argument("--row-wave-share", type=float, default=1.0,
+                    help="fraction of the chip's resident waves one island launch takes (row kernel)")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--trace", default="default", choices=["default", "synthetic"],
                     help="default: 8,152-pod OpenB trace on 16 nodes; synthetic: BASELINE config 5 shape")
@@ -85,7 +90,8 @@ def main() -> None:
     else:
         device = "cpu"
     # the per-event trace hash only serves cross-engine equality tests: off here
-    ev = Evaluator(workload, device=device, options={"heap_mode": args.heap_mode, "trace_hash": False},
+    ev = Evaluator(workload, device=device, options={"heap_mode": args.heap_mode, "trace_hash": False,
+                                                     "row_wave_share": args.row_wave_share},
                    n_slots=max(1, args.islands))
     if args.device == "gpu" and ev.device is None:
         raise SystemExit("no HIP device visible")

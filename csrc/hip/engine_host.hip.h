@@ -105,6 +105,7 @@ struct Slot {
   HostBuf h_in, h_tab, h_wc;
   int P = 0;
   int fam_spec = -1;    // family shared by the whole staged batch, or -1
+  uint32_t qbase = 0;   // row-kernel queue counter value at the next launch
   bool busy = false;
   roctx_range_id_t range = 0;   // roctx range spanning submit -> wait (rocprofv3 --marker-trace)
   void release() {
@@ -213,6 +214,11 @@ class DeviceEngine {
       row_mode_ = m;
     }
     if (o.contains("row_heap_top")) row_top_opt_ = o["row_heap_top"].cast<int>();   // -1: auto
+    if (o.contains("row_wave_share")) {
+      const double f = o["row_wave_share"].cast<double>();
+      if (!(f > 0.0 && f <= 4.0)) throw std::invalid_argument("row_wave_share must be in (0, 4]");
+      row_share_ = f;
+    }
     if (o.contains("heap_mode")) {
       const std::string m = o["heap_mode"].cast<std::string>();
       if (m != "auto" && m != "lds" && m != "hbm") throw std::invalid_argument("heap_mode: auto | lds | hbm");
@@ -379,6 +385,7 @@ class DeviceEngine {
     d["row_kernel"] = row_mode_;
     d["row_heap_top"] = row_top();
     d["row_waves_per_cu"] = row_layout(FAM_COMPOSITE_LINEAR).second;
+    d["row_wave_share"] = row_share_;
     return d;
   }
 
@@ -580,18 +587,27 @@ class DeviceEngine {
     Wl.heap_top = lay.first;
     const size_t lds = rows_lds_bytes(W_.n_pods, Wl.heap_top) + (profiled ? kRowProfBytes : 0);
     if (lds > kMaxLds) throw std::invalid_argument("row kernel layout exceeds the 160 KiB LDS");
-    // persistent waves: as many as stay resident, each row draining the policy queue
-    const int waves = std::max(1, std::min((P + kRowsPerWave - 1) / kRowsPerWave, lay.second * num_cus_));
+    // persistent waves: at most `row_wave_share` of what stays resident on the
+    // chip, each row draining the policy queue.  A wave holds its slot until
+    // its last row is done, so fewer waves (more policies per row) shrink the
+    // idle tail of every launch; concurrent launches of other slots (islands)
+    // fill the rest of the chip.
+    const int cap = std::max(1, (int)(row_share_ * lay.second * num_cus_));
+    const int waves = std::max(1, std::min((P + kRowsPerWave - 1) / kRowsPerWave, cap));
     s.gheap.reserve((size_t)row_heap_entries(W_.n_pods) * 8 * (size_t)waves * kRowsPerWave);
-    s.queue.reserve(64);
+    if (s.queue.p == nullptr) {   // zeroed once; launches then offset their claims
+      s.queue.reserve(64);
+      HIP_OK(hipMemsetAsync(s.queue.p, 0, 64, s.stream));
+      s.qbase = 0;
+    }
     if (profiled) s.prof.reserve((size_t)waves * 64);
-    HIP_OK(hipMemsetAsync(s.queue.p, 0, sizeof(int), s.stream));
     const size_t wb = (size_t)P * kWeights * 8;
     const fksk::BuiltinArgs a{Wl, upload_workload(s, Wl), reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + wb),
                               s.h_in.dev<double>(), s.w.as<double>(), s.res.as<DevResult>(), s.gheap.as<uint64_t>(),
                               profiled ? s.prof.as<uint64_t>() : nullptr};
-    if (profiled) HIP_OK(fksk::launch_builtin_rows_prof(s.fam_spec, P, waves, s.queue.as<int>(), lds, s.stream, a));
-    else HIP_OK(fksk::launch_builtin_rows(s.fam_spec, P, waves, s.queue.as<int>(), lds, s.stream, a));
+    if (profiled) HIP_OK(fksk::launch_builtin_rows_prof(s.fam_spec, P, waves, s.queue.as<uint32_t>(), s.qbase, lds, s.stream, a));
+    else HIP_OK(fksk::launch_builtin_rows(s.fam_spec, P, waves, s.queue.as<uint32_t>(), s.qbase, lds, s.stream, a));
+    s.qbase += (uint32_t)P + (uint32_t)waves * kRowsPerWave;   // every row makes one final, empty claim
     return waves;
   }
 
@@ -640,6 +656,7 @@ class DeviceEngine {
   bool rows_ok_ = false;
   std::string row_mode_ = "auto";
   int row_top_opt_ = -1;
+  double row_share_ = 1.0;
   mutable std::vector<std::pair<int, int>> row_layout_cache_ = std::vector<std::pair<int, int>>(8, {0, 0});
   int num_cus_ = 0;
   std::string arch_;

@@ -53,11 +53,13 @@ FKS_DECLARE_NPASS(4)
 #undef FKS_DECLARE_NPASS
 
 // row kernels: 4 policies per wave (clusters of <= 16 nodes, replay_rows.hip.h)
-// `waves` persistent waves drain the P-policy queue (`queue`: one zeroed int).
-hipError_t launch_builtin_rows(int fam_spec, int P, int waves, int* queue, size_t lds, hipStream_t s,
+// `waves` persistent waves drain the P-policy queue: claims are
+// atomicAdd(queue) - qbase (the counter runs on across launches; a launch
+// makes exactly P + 4 * waves claims).
+hipError_t launch_builtin_rows(int fam_spec, int P, int waves, uint32_t* queue, uint32_t qbase, size_t lds, hipStream_t s,
                               const BuiltinArgs& a);
 // s_memtime phase-profiled variant (random_linear / composite_linear / mixed); a.prof: [waves, 8]
-hipError_t launch_builtin_rows_prof(int fam_spec, int P, int waves, int* queue, size_t lds, hipStream_t s,
+hipError_t launch_builtin_rows_prof(int fam_spec, int P, int waves, uint32_t* queue, uint32_t qbase, size_t lds, hipStream_t s,
                                    const BuiltinArgs& a);
 // resident row-kernel waves per CU for a family's instance at `lds` bytes (-1: error)
 int rows_waves_per_cu(int fam_spec, size_t lds);

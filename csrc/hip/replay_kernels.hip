@@ -187,16 +187,16 @@ __global__ FKS_VM_BOUNDS(GHEAP) void k_replay_vm_prof(fksk::VmArgs a) {
                                // divisors spill, reloaded on the rare snapshot path)
 #endif
 template <int FAM>
-__global__ __launch_bounds__(64, FAM < 0 ? 2 : (FAM == 3 || FAM == 4) ? FKS_ROW_HEAVY_WAVES : FKS_ROW_WAVES) void k_replay_rows(fksk::BuiltinArgs a, int P, int* queue) {
-  replay_rows<FAM>(a.W, a.Wc, a.fam, a.weights, a.gheap, a.out, P, queue);
+__global__ __launch_bounds__(64, FAM < 0 ? 2 : (FAM == 3 || FAM == 4) ? FKS_ROW_HEAVY_WAVES : FKS_ROW_WAVES) void k_replay_rows(fksk::BuiltinArgs a, int P, uint32_t* queue, uint32_t qbase) {
+  replay_rows<FAM>(a.W, a.Wc, a.fam, a.weights, a.gheap, a.out, P, queue, qbase);
 }
 #endif
 
 #if FKS_KIND == 3
 template <int FAM>
 __global__ __launch_bounds__(64, FAM < 0 ? 2 : (FAM == 3 || FAM == 4) ? FKS_ROW_HEAVY_WAVES : FKS_ROW_WAVES)
-void k_replay_rows_prof(fksk::BuiltinArgs a, int P, int* queue) {
-  replay_rows<FAM, RowProf>(a.W, a.Wc, a.fam, a.weights, a.gheap, a.out, P, queue, a.prof);
+void k_replay_rows_prof(fksk::BuiltinArgs a, int P, uint32_t* queue, uint32_t qbase) {
+  replay_rows<FAM, RowProf>(a.W, a.Wc, a.fam, a.weights, a.gheap, a.out, P, queue, qbase, a.prof);
 }
 #endif
 
@@ -251,18 +251,18 @@ hipError_t set_prof_attrs(int mx) {
 
 
 #if FKS_KIND == 3
-hipError_t launch_builtin_rows(int fam, int P, int waves, int* queue, size_t lds, hipStream_t st,
+hipError_t launch_builtin_rows(int fam, int P, int waves, uint32_t* queue, uint32_t qbase, size_t lds, hipStream_t st,
                               const BuiltinArgs& a) {
   const dim3 grid(waves);
 #define FKS_CASE(F) \
-  case F: hipLaunchKernelGGL((k_replay_rows<F>), grid, dim3(64), lds, st, a, P, queue); break;
+  case F: hipLaunchKernelGGL((k_replay_rows<F>), grid, dim3(64), lds, st, a, P, queue, qbase); break;
   switch (fam) {
     FKS_CASE(FAM_FIRST_FIT)
     FKS_CASE(FAM_BEST_FIT)
     FKS_CASE(FAM_RANDOM_LINEAR)
     FKS_CASE(FAM_FEATURE_LINEAR)
     FKS_CASE(FAM_COMPOSITE_LINEAR)
-    default: hipLaunchKernelGGL((k_replay_rows<-1>), grid, dim3(64), lds, st, a, P, queue);
+    default: hipLaunchKernelGGL((k_replay_rows<-1>), grid, dim3(64), lds, st, a, P, queue, qbase);
   }
 #undef FKS_CASE
   return hipGetLastError();
@@ -283,13 +283,13 @@ int rows_waves_per_cu(int fam, size_t lds) {
   }
   return e == hipSuccess ? n : -1;
 }
-hipError_t launch_builtin_rows_prof(int fam, int P, int waves, int* queue, size_t lds, hipStream_t st,
+hipError_t launch_builtin_rows_prof(int fam, int P, int waves, uint32_t* queue, uint32_t qbase, size_t lds, hipStream_t st,
                                    const BuiltinArgs& a) {
   const dim3 grid(waves);
-  if (fam == FAM_RANDOM_LINEAR) hipLaunchKernelGGL((k_replay_rows_prof<FAM_RANDOM_LINEAR>), grid, dim3(64), lds, st, a, P, queue);
+  if (fam == FAM_RANDOM_LINEAR) hipLaunchKernelGGL((k_replay_rows_prof<FAM_RANDOM_LINEAR>), grid, dim3(64), lds, st, a, P, queue, qbase);
   else if (fam == FAM_COMPOSITE_LINEAR)
-    hipLaunchKernelGGL((k_replay_rows_prof<FAM_COMPOSITE_LINEAR>), grid, dim3(64), lds, st, a, P, queue);
-  else hipLaunchKernelGGL((k_replay_rows_prof<-1>), grid, dim3(64), lds, st, a, P, queue);
+    hipLaunchKernelGGL((k_replay_rows_prof<FAM_COMPOSITE_LINEAR>), grid, dim3(64), lds, st, a, P, queue, qbase);
+  else hipLaunchKernelGGL((k_replay_rows_prof<-1>), grid, dim3(64), lds, st, a, P, queue, qbase);
   return hipGetLastError();
 }
 hipError_t set_rows_attrs(int mx) {

@@ -288,7 +288,8 @@ constexpr int kRowProfBytes = 128;
 // initial heap shifted by one slot (address = slot + 1).
 template <int FAM, class Prof = RowNoProf>
 __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const int32_t* fam, const double* weights,
-                            uint64_t* gheap, DevResult* out, int P, int* queue, uint64_t* prof_out = nullptr) {
+                            uint64_t* gheap, DevResult* out, int P, uint32_t* queue, uint32_t qbase,
+                            uint64_t* prof_out = nullptr) {
   // W: the kernel-argument copy, read once for the hot scalars below; every
   // other field is re-read where it is used through an opaque pointer to the
   // HBM copy (scalar loads), so the loop carries no spilled SGPR copies of it
@@ -345,7 +346,10 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
   const FKS_GLOBAL u64x2* heap_src = reinterpret_cast<const FKS_GLOBAL u64x2*>(global_ptr(W.heap0p));
 
   auto claim = [&]() {
-    const int c = jv == 0 ? __hip_atomic_fetch_add(queue, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    // the counter is never reset: this launch's claims start at qbase (the
+    // host adds every launch's P + rows claims), so no fill kernel has to
+    // queue for a CU slot before the replay can start
+    const int c = jv == 0 ? (int)(__hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - qbase) : 0;
     return row_read(c, rbase, 0);
   };
   // per-policy state (row-uniform except the node registers / lane-owned slots)
