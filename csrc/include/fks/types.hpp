@@ -25,8 +25,8 @@ enum ExcCode : int32_t {
   EXC_ALLOC = 6,           // ValueError from the GPU allocator (not enough GPUs)
   EXC_NAME = 7,            // NameError / UnboundLocalError
   EXC_UNSUPPORTED = 100,   // semantics outside the native subset (bigint, ...): re-run exactly on host
-  EXC_BUDGET = 101,
-  EXC_INVARIANT = 102,     // resource accounting invariant violated (debug check)        // instruction budget exhausted (runaway program)
+  EXC_BUDGET = 101,        // instruction budget exhausted (runaway program)
+  EXC_INVARIANT = 102,     // resource accounting invariant violated (debug check)
 };
 
 enum RepushMode : int32_t { REPUSH_FIRST = 0, REPUSH_EARLIEST = 1 };
