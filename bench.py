@@ -109,7 +109,7 @@ def main() -> None:
 
     def absorb(isl, props, tab, gen: int) -> None:
         sc = tab[:, COLS["score"]]
-        isl.update(props, sc)
+        isl.update(props, sc, tab[:, COLS["n_events"]])
         events[0] += float(tab[:, COLS["n_events"]].sum())
         j = int(np.argmax(sc))
         if sc[j] > best_row[1]:

@@ -34,12 +34,14 @@ class ParamIsland:
     fresh_fraction: float = 0.1
     elites: np.ndarray = field(default=None)       # [E, K]
     elite_scores: np.ndarray = field(default=None)  # [E]
+    elite_events: np.ndarray = field(default=None)  # [E] replay events of each elite (NaN: unknown)
     generation: int = 0
 
     def __post_init__(self):
         k = self.sampler(1, self.rng).shape[1]
         self.elites = np.zeros((0, k))
         self.elite_scores = np.zeros(0)
+        self.elite_events = np.zeros(0)
 
     @property
     def best(self) -> Tuple[Optional[np.ndarray], float]:
@@ -49,6 +51,13 @@ class ParamIsland:
         return self.elites[i], float(self.elite_scores[i])
 
     def propose(self) -> np.ndarray:
+        """A generation of candidates, longest predicted replay first.
+
+        The device drains a batch through a persistent queue in index order,
+        so handing out the long replays first and the short ones last (LPT
+        scheduling) keeps the rows of a wave finishing close together.  A
+        mutant is predicted to replay as many events as its parent, a
+        crossover as its longer parent; fresh samples (unknown) go first."""
         n = self.n_candidates
         if len(self.elites) == 0:
             return self.sampler(n, self.rng)
@@ -60,29 +69,38 @@ class ParamIsland:
         order = np.argsort(-self.elite_scores)
         p = 1.0 / (np.arange(E) + 1.0)
         p /= p.sum()
-        pa = self.elites[order[self.rng.choice(E, n_mut, p=p)]]
+        ia = order[self.rng.choice(E, n_mut, p=p)]
+        pa = self.elites[ia]
         scale = self.sigma * self.rng.standard_normal(pa.shape)
         mut = pa * np.exp(scale) + self.rng.normal(0, self.sigma * 0.05, pa.shape) * np.abs(pa).mean(0)
         flip = self.rng.random(pa.shape) < 0.02
         mut[flip] = -mut[flip]
         zero = self.rng.random(pa.shape) < 0.02
         mut[zero] = 0.0
-        a = self.elites[order[self.rng.choice(E, n_cross, p=p)]]
-        b = self.elites[order[self.rng.choice(E, n_cross, p=p)]]
+        ca = order[self.rng.choice(E, n_cross, p=p)]
+        cb = order[self.rng.choice(E, n_cross, p=p)]
+        a, b = self.elites[ca], self.elites[cb]
         mask = self.rng.random(a.shape) < 0.5
         cross = np.where(mask, a, b)
         fresh = self.sampler(n_fresh, self.rng)
-        return np.concatenate([mut, cross, fresh])
+        ev = self.elite_events
+        pred = np.concatenate([ev[ia], np.fmax(ev[ca], ev[cb]), np.full(n_fresh, np.nan)])
+        pred = np.where(np.isnan(pred), np.inf, pred)
+        lpt = np.argsort(-pred, kind="stable")
+        return np.concatenate([mut, cross, fresh])[lpt]
 
-    def update(self, weights: np.ndarray, scores: np.ndarray) -> None:
+    def update(self, weights: np.ndarray, scores: np.ndarray, events: Optional[np.ndarray] = None) -> None:
         self.generation += 1
+        if events is None:
+            events = np.full(len(scores), np.nan)
         allw = np.concatenate([self.elites, weights])
         alls = np.concatenate([self.elite_scores, scores])
+        alle = np.concatenate([self.elite_events, np.asarray(events, dtype=np.float64)])
         # dedup exact duplicates, keep the best elite_size
         _, uniq = np.unique(np.round(allw, 12), axis=0, return_index=True)
-        allw, alls = allw[uniq], alls[uniq]
+        allw, alls, alle = allw[uniq], alls[uniq], alle[uniq]
         keep = np.argsort(-alls, kind="stable")[:self.elite_size]
-        self.elites, self.elite_scores = allw[keep], alls[keep]
+        self.elites, self.elite_scores, self.elite_events = allw[keep], alls[keep], alle[keep]
 
     def migrants(self, k: int) -> np.ndarray:
         """[k, 1 + K] records: score, weights (best first; -inf padded)."""
