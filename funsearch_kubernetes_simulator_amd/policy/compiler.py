@@ -112,6 +112,7 @@ class Compiler:
         self.free: List[int] = list(range(MAX_REGS - 1, -1, -1))
         self.features = set()
         self.globals: Dict[str, Val] = {}
+        self._walk_memo: Dict[int, tuple] = {}
         self.scope = _Scope()
         self.pod_name = self.node_name = None
         self.loop_depth = 0
@@ -248,7 +249,7 @@ class Compiler:
 
     def _check_names(self, fn: ast.FunctionDef) -> None:
         reserved = {self.pod_name, self.node_name, "math", "operator"} | SAFE_BUILTINS
-        for node in ast.walk(fn):
+        for node in self._walk(fn):
             if isinstance(node, ast.Name) and isinstance(node.ctx, ast.Store) and node.id in reserved:
                 raise CompileError(f"assignment to reserved name {node.id}")
             if isinstance(node, (ast.Global, ast.Nonlocal, ast.FunctionDef, ast.AsyncFunctionDef,
@@ -259,6 +260,26 @@ class Compiler:
                     raise CompileError(f"unsupported construct {type(node).__name__}")
 
     # ------------------------------------------------------------------ analysis
+    def _walk(self, node) -> list:
+        """`ast.walk(node)` as a list, memoised per subtree: the analysis passes
+        re-walk the same statements (kind planning runs three rounds, the unbound
+        analysis nests per statement), which made walking ~55% of compile time.
+        The node is kept in the entry so an id() cannot be reused while cached."""
+        hit = self._walk_memo.get(id(node))
+        if hit is None or hit[0] is not node:
+            out, i = [node], 0
+            while i < len(out):                 # breadth-first, the order of ast.walk
+                n = out[i]
+                i += 1
+                for f in n._fields:
+                    v = getattr(n, f, None)
+                    if isinstance(v, ast.AST):
+                        out.append(v)
+                    elif isinstance(v, list):
+                        out.extend(x for x in v if isinstance(x, ast.AST))
+            hit = self._walk_memo[id(node)] = (node, out)
+        return hit[1]
+
     @staticmethod
     def _assigned_names(body) -> set:
         names = set()
@@ -273,7 +294,7 @@ class Compiler:
         self.kinds: Dict[str, str] = {}
         for _ in range(3):
             for stmt in body:
-                for node in ast.walk(stmt):
+                for node in self._walk(stmt):
                     if isinstance(node, (ast.Assign, ast.AnnAssign)):
                         targets = node.targets if isinstance(node, ast.Assign) else [node.target]
                         for t in targets:
@@ -347,17 +368,17 @@ class Compiler:
         risky = set()
 
         def expr_reads(e, defined):
-            for n in ast.walk(e):
+            for n in self._walk(e):
                 if isinstance(n, ast.Name) and isinstance(n.ctx, ast.Load) and n.id in assigned \
                         and n.id not in defined:
                     risky.add(n.id)
 
         def comp_locals(e):
             out = set()
-            for n in ast.walk(e):
+            for n in self._walk(e):
                 if isinstance(n, (ast.ListComp, ast.GeneratorExp)):
                     for g in n.generators:
-                        for t in ast.walk(g.target):
+                        for t in self._walk(g.target):
                             if isinstance(t, ast.Name):
                                 out.add(t.id)
                 if isinstance(n, ast.Lambda):
@@ -371,7 +392,7 @@ class Compiler:
                 if isinstance(s, ast.Assign):
                     expr_reads(s.value, defined | local)
                     for t in s.targets:
-                        for n in ast.walk(t):
+                        for n in self._walk(t):
                             if isinstance(n, ast.Name):
                                 defined.add(n.id)
                 elif isinstance(s, ast.AugAssign):
@@ -387,7 +408,7 @@ class Compiler:
                 elif isinstance(s, (ast.For, ast.While)):
                     if isinstance(s, ast.For):
                         expr_reads(s.iter, defined | local)
-                        tgt = {n.id for n in ast.walk(s.target) if isinstance(n, ast.Name)}
+                        tgt = {n.id for n in self._walk(s.target) if isinstance(n, ast.Name)}
                         visit(s.body, defined | tgt)
                         visit(s.body, defined | tgt | set())
                     else:
@@ -398,7 +419,7 @@ class Compiler:
                     if s.value is not None:
                         expr_reads(s.value, defined | local)
                 else:
-                    for n in ast.walk(s):
+                    for n in self._walk(s):
                         if isinstance(n, ast.expr):
                             expr_reads(n, defined | local)
             return defined
