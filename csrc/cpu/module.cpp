@@ -10,6 +10,7 @@
 #include "builtin_scorers.hpp"
 #include "engine.hpp"
 #include "parallel.hpp"
+#include "seqmatch.hpp"
 #include "trace_io.hpp"
 #include "vm_cpu.hpp"
 
@@ -244,6 +245,14 @@ PYBIND11_MODULE(_fks_cpu, m) {
     return vm_score_once(prog, pod, node, gpu_left, gpu_total, gpu_mem);
   });
 
+  m.def("seq_ratio", [](const std::u32string& a, const std::u32string& b) {
+    // difflib.SequenceMatcher(None, a, b).ratio(), exactly
+    return SeqMatcher(a, b).ratio();
+  });
+  m.def("similar_at_least", [](const std::u32string& a, const std::u32string& b, double threshold) {
+    // difflib.SequenceMatcher(None, a, b).ratio() >= threshold
+    return SeqMatcher(a, b).at_least(threshold);
+  });
   m.def("exact_mean", [](std::vector<double> xs) {
     FixedAcc a; for (double x : xs) a.add(x);
     return py::make_tuple(fixed_mean(a), a.inexact);

