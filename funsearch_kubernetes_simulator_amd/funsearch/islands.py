@@ -17,11 +17,21 @@ populations per process.  Each generation:
 With ``islands.per_rank = 1`` on one process this is exactly `SimpleFunSearch`.
 Checkpoints (``checkpoint.dir``) hold every island's population so a run can
 `resume` after a crash, which the reference cannot.
+
+Failure handling (the reference has none): a collective that
+fails because a peer rank died makes the survivors checkpoint, log a
+``rank_failure`` record and continue as single-rank jobs
+(``islands.elastic``, on by default).  ``--resume`` is elastic: it re-shards
+the saved islands of a run with any world size / islands-per-rank onto the
+current layout (surplus islands are merged, missing ones are cloned), so a
+job restarted on fewer or more GPUs (e.g. by ``torchrun --max-restarts``)
+keeps every population.
 """
 
 from __future__ import annotations
 
 import concurrent.futures
+import glob
 import json
 import os
 import time
@@ -43,6 +53,8 @@ class IslandFunSearch:
         self.n_islands = int(isl.get("per_rank", 1))
         self.migrate_every = int(isl.get("migrate_every", 50))
         self.n_migrants = int(isl.get("migrants", 2))
+        self.elastic = bool(isl.get("elastic", True))
+        self.failures: List[dict] = []
         dev = (self.config.get("device") or {}).get("kind", "auto")
         if dev == "auto" and self.ctx.backend == "nccl":
             dev = self.ctx.local_rank
@@ -127,9 +139,9 @@ class IslandFunSearch:
             s.population = sorted(elites + new, key=lambda x: x[1], reverse=True)[:s.population_size]
         if self.migrate_every and self.generation % self.migrate_every == 0:
             with roctx_range(f"funsearch.migrate gen {self.generation}"):
-                self.migrate()
+                self._collective("migrate", self.migrate, None)
         best_local = self.best[1]
-        best_global = dist.all_reduce_max(best_local)
+        best_global = self._collective("all_reduce_max", lambda: dist.all_reduce_max(best_local), best_local)
         rec = dict(kind="generation", rank=self.ctx.rank, generation=self.generation, best=best_local,
                    best_global=best_global, children=len(children),
                    islands=[round(s.best_score, 6) for s in self.islands],
@@ -139,6 +151,26 @@ class IslandFunSearch:
         if self.ck_dir and self.ck_every and self.generation % self.ck_every == 0:
             self.save_checkpoint()
         return rec
+
+    def _collective(self, what: str, fn, fallback):
+        """Run a collective; if a peer is gone, survive as a single-rank job."""
+        if not self.ctx.distributed:
+            return fn()
+        try:
+            return fn()
+        except Exception as exc:        # DistBackendError / RuntimeError from a dead or timed-out peer
+            if not self.elastic:
+                raise
+            rec = dict(kind="rank_failure", rank=self.ctx.rank, generation=self.generation, collective=what,
+                       world_size=self.ctx.world_size, error=f"{type(exc).__name__}: {str(exc)[:300]}")
+            self.failures.append(rec)
+            self.log.write(**rec)
+            if self.verbose:
+                print(json.dumps(rec), flush=True)
+            self.ctx = dist.degrade_to_local(what)
+            if self.ck_dir:
+                self.save_checkpoint()
+            return fn() if fallback is None else fallback
 
     def migrate(self) -> None:
         """Ring migration of each island's best programs across all ranks."""
@@ -167,9 +199,7 @@ class IslandFunSearch:
 
     def run(self, generations: Optional[int] = None, resume: bool = False) -> Tuple[Optional[str], float]:
         if resume and self.ck_dir:
-            path = os.path.join(self.ck_dir, f"islands_rank{self.ctx.rank}.json")
-            if os.path.exists(path):
-                self.load_checkpoint(path)
+            self.load_elastic(self.ck_dir)
         self.initialize()
         generations = generations or self.islands[0].max_generations
         threshold = self.islands[0].early_stop_threshold
@@ -187,7 +217,7 @@ class IslandFunSearch:
         if not self.ctx.distributed:
             return code, score
         rec = dist.pack_programs([code or ""], [score])
-        allr = dist.all_gather_array(rec)
+        allr = self._collective("global_best", lambda: dist.all_gather_array(rec), rec[None])
         best = max(dist.unpack_programs(allr), key=lambda cs: cs[1], default=(code, score))
         return best
 
@@ -196,6 +226,7 @@ class IslandFunSearch:
         os.makedirs(self.ck_dir, exist_ok=True)
         path = os.path.join(self.ck_dir, f"islands_rank{self.ctx.rank}.json")
         state = {"format": "fks-islands-checkpoint-v1", "generation": self.generation,
+                 "rank": self.ctx.rank, "world_size": self.ctx.world_size,
                  "evaluations": self.evaluations, "islands": [s.state_dict() for s in self.islands]}
         tmp = path + ".tmp"
         with open(tmp, "w") as fh:
@@ -214,6 +245,63 @@ class IslandFunSearch:
             s.generation = int(ss["generation"])
             s.population = [(p["code"], float(p["score"])) for p in ss["population"]]
             s.best_policy, s.best_score = ss["best_policy"], float(ss["best_score"])
+
+
+    def load_elastic(self, ck_dir: str) -> bool:
+        """Resume from the newest complete checkpoint set in `ck_dir`, whatever
+        world size and islands-per-rank wrote it.  Saved islands are numbered
+        globally (rank-major); with T islands now, saved island j goes to global
+        island j % T (populations merged: union, best first, truncated), and
+        when fewer were saved than exist now, island g clones saved island
+        g % J.  Returns False when there is nothing to resume."""
+        sets = {}
+        for path in glob.glob(os.path.join(ck_dir, "islands_rank*.json")):
+            try:
+                with open(path) as fh:
+                    st = json.load(fh)
+            except (OSError, ValueError):
+                continue
+            if st.get("format") != "fks-islands-checkpoint-v1":
+                continue
+            rank = int(st.get("rank", os.path.basename(path)[len("islands_rank"):-len(".json")]))
+            key = (int(st["generation"]), int(st.get("world_size", 1)))
+            sets.setdefault(key, {})[rank] = st
+        if not sets:
+            return False
+        complete = [k for k, v in sets.items() if len(v) >= k[1]]
+        gen, ws = max(complete or sets)
+        saved = sets[(gen, ws)]
+        own = saved.get(self.ctx.rank)
+        if ws == self.ctx.world_size and own is not None and len(own["islands"]) == len(self.islands):
+            self.generation = gen
+            self.evaluations = int(own.get("evaluations", 0))
+            for s, ss in zip(self.islands, own["islands"]):
+                self._load_island(s, [ss])
+            return True
+        flat = [ss for r in sorted(saved) for ss in saved[r]["islands"]]
+        T, I = self.ctx.world_size * len(self.islands), len(self.islands)
+        self.generation = gen
+        self.evaluations = sum(int(st.get("evaluations", 0)) for r, st in saved.items()
+                               if r % self.ctx.world_size == self.ctx.rank)
+        for li, s in enumerate(self.islands):
+            g = self.ctx.rank * I + li
+            src = flat[g::T] if len(flat) >= T else [flat[g % len(flat)]]
+            self._load_island(s, src)
+        return True
+
+    @staticmethod
+    def _load_island(s: SimpleFunSearch, states: List[dict]) -> None:
+        pop, seen = [], set()
+        for ss in states:
+            for p in ss["population"]:
+                if p["code"] not in seen:
+                    seen.add(p["code"])
+                    pop.append((p["code"], float(p["score"])))
+        pop.sort(key=lambda x: x[1], reverse=True)
+        s.population = pop[:s.population_size]
+        s.generation = max(int(ss["generation"]) for ss in states)
+        best = max(states, key=lambda ss: float(ss["best_score"]))
+        s.best_policy, s.best_score = best["best_policy"], float(best["best_score"])
 
 
 def run_funsearch(config="configs/offline_islands.json", generations: Optional[int] = None, resume: bool = False,

@@ -63,7 +63,12 @@ def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = No
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     if not dist.is_initialized():
-        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+        kw = {}
+        if os.environ.get("FKS_DIST_TIMEOUT_S"):
+            # failure detection: a collective whose peer is gone raises after this long
+            import datetime
+            kw["timeout"] = datetime.timedelta(seconds=float(os.environ["FKS_DIST_TIMEOUT_S"]))
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
     _ctx = DistContext(rank=rank, world_size=world, local_rank=local, backend=backend, device=device)
     return _ctx
 
@@ -144,6 +149,27 @@ def all_reduce_sum(v: float) -> float:
     t = torch.tensor([float(v)], dtype=torch.float64, device=ctx.device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def degrade_to_local(reason: str = "") -> DistContext:
+    """Leave the process group after a failed collective and carry on as a
+    single-rank job (every collective helper then runs locally).  The rank id
+    is kept so this survivor keeps writing its own checkpoint file.  Used by
+    the island search so that losing one rank does not end the run (SURVEY
+    §5.3); the lost islands come back through `--resume` (see
+    `IslandFunSearch.load_elastic`)."""
+    global _ctx
+    ctx = context()
+    if ctx.distributed:
+        import torch.distributed as dist
+        try:
+            if dist.is_initialized():
+                dist.destroy_process_group()
+        except Exception:       # the group may already be broken; nothing left to release
+            pass
+    _ctx = DistContext(rank=ctx.rank, world_size=1, local_rank=ctx.local_rank, backend="none",
+                       device=ctx.device)
+    return _ctx
 
 
 def shutdown() -> None:

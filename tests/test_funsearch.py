@@ -198,3 +198,43 @@ def test_search_survives_injected_faults(tmp_path):
     assert score >= reference_scores()["best_fit"]
     logs = [json.loads(l) for l in open(tmp_path / "log.jsonl")]
     assert logs[-1]["generation"] == 3
+
+
+def _fake_island(codes_scores, gen):
+    return {"format": "fks-funsearch-checkpoint-v1", "generation": gen,
+            "population": [{"code": c, "score": s} for c, s in codes_scores],
+            "best_policy": codes_scores[0][0], "best_score": codes_scores[0][1], "evaluations": 0}
+
+
+def test_elastic_resume_reshards_islands(tmp_path):
+    """A checkpoint written by 2 ranks x 2 islands resumes on 1 rank with 1
+    island (populations merged) and with 8 islands (populations cloned)."""
+    from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
+    seeds = seed_policies()
+    ck = tmp_path / "ck"
+    ck.mkdir()
+    base = seeds["best_fit"]
+    for r in range(2):
+        isl = [_fake_island([(base + f"\n# r{r} i{i} a", 0.5 + 0.01 * (2 * r + i)),
+                             (base + f"\n# r{r} i{i} b", 0.1)], 40) for i in range(2)]
+        st = {"format": "fks-islands-checkpoint-v1", "generation": 40, "rank": r, "world_size": 2,
+              "evaluations": 100, "islands": isl}
+        (ck / f"islands_rank{r}.json").write_text(json.dumps(st))
+    # stale file from an older, larger run must be ignored
+    (ck / "islands_rank2.json").write_text(json.dumps(
+        {"format": "fks-islands-checkpoint-v1", "generation": 10, "rank": 2, "world_size": 4, "islands": []}))
+    cfg = _cfg(tmp_path)
+    cfg["funsearch"]["population_size"] = 20
+    cfg["islands"] = {"per_rank": 1, "migrate_every": 0}
+    one = IslandFunSearch(cfg)
+    assert one.load_elastic(str(ck))
+    assert one.generation == 40 and one.evaluations == 200
+    pop = one.islands[0].population
+    assert len(pop) == 8 and pop[0][1] == 0.53 and one.islands[0].best_score == 0.53
+    cfg["islands"]["per_rank"] = 8
+    many = IslandFunSearch(cfg)
+    assert many.load_elastic(str(ck))
+    assert [round(s.best_score, 2) for s in many.islands] == [0.5, 0.51, 0.52, 0.53] * 2
+    # a resumed run keeps evolving from there
+    code, score = many.run(generations=1, resume=False)
+    assert many.generation == 41 and score >= 0.53

@@ -125,3 +125,42 @@ def test_native_csv_loader_matches_python_parser():
                 assert np.array_equal(getattr(a.pods, name), getattr(b.pods, name)), name
     with pytest.raises(KeyError):
         p.load_workload("gpu_models_filtered.csv", "openb_pod_list_multigpu20.csv", native=True)
+
+
+def test_island_search_survives_rank_loss(tmp_path):
+    """Rank 1 disappears mid-run (gloo, 2 ranks): rank 0's next collective
+    fails, it logs a rank_failure record, checkpoints and finishes alone;
+    a later --resume on one process picks the run up from rank 0's file."""
+    ck = tmp_path / "ck"
+    cfg = {"llm": {"backend": "mutation", "seed": 3}, "safe_execution": {"timeout_seconds": 3},
+           "funsearch": {"population_size": 6, "generations": 4, "early_stop_threshold": 1.0, "elite_size": 3,
+                         "max_workers": 2, "policies_per_generation": 2},
+           "islands": {"per_rank": 1, "migrate_every": 1, "migrants": 1},
+           "device": {"kind": "cpu"}, "checkpoint": {"dir": str(ck), "every": 1}}
+    (tmp_path / "cfg.json").write_text(json.dumps(cfg))
+    script = tmp_path / "w.py"
+    script.write_text(
+        "import json, os, sys\n"
+        "from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch\n"
+        f"fs = IslandFunSearch({str(tmp_path / 'cfg.json')!r})\n"
+        "fs.initialize()\n"
+        "for g in range(4):\n"
+        "    if fs.ctx.rank == 1 and g == 2:\n"
+        "        sys.stdout.flush(); os._exit(0)\n"
+        "    fs.evolve()\n"
+        "code, score = fs.global_best()\n"
+        "print(json.dumps({'gen': fs.generation, 'world': fs.ctx.world_size, 'score': score,\n"
+        "                  'failures': [f['collective'] for f in fs.failures]}))\n")
+    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1", FKS_DIST_TIMEOUT_S="60")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(31000 + os.getpid() % 1000), str(script)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["gen"] == 4 and out["world"] == 1 and len(out["failures"]) == 1
+    assert out["score"] > 0.44
+    st = json.loads((ck / "islands_rank0.json").read_text())
+    assert st["generation"] == 4 and st["world_size"] == 1
+    from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
+    fs = IslandFunSearch(str(tmp_path / "cfg.json"))
+    assert fs.load_elastic(str(ck)) and fs.generation == 4
