@@ -164,3 +164,21 @@ def test_island_search_survives_rank_loss(tmp_path):
     from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
     fs = IslandFunSearch(str(tmp_path / "cfg.json"))
     assert fs.load_elastic(str(ck)) and fs.generation == 4
+
+
+def test_scaling_harness_cpu():
+    """bench.scaling drives bench.py at 1 and 2 ranks (gloo) and reports the
+    weak-scaling efficiency relative to N=1."""
+    from funsearch_kubernetes_simulator_amd.bench import scaling
+    rows = scaling.summarize({1: {"value": 10.0, "ms_per_step": 5.0}, 2: {"value": 18.0, "ms_per_step": 5.5},
+                              4: None})
+    assert rows[1]["efficiency"] == 0.9 and rows[2]["value"] is None
+    r = subprocess.run([sys.executable, "-m", "funsearch_kubernetes_simulator_amd.bench.scaling", "--gpus", "1,2",
+                        "--port", str(32000 + os.getpid() % 1000), "--", "--device", "cpu", "--steps", "1",
+                        "--warmup", "1", "--islands", "1", "--candidates", "4"],
+                       env=dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1"), capture_output=True, text=True,
+                       timeout=900, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-2000:]
+    summary = json.loads(r.stdout.strip().splitlines()[-1])["scaling"]
+    assert [s["n_gpus"] for s in summary] == [1, 2]
+    assert all(s["value"] > 0 for s in summary) and summary[0]["efficiency"] == 1.0
