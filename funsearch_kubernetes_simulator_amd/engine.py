@@ -159,6 +159,8 @@ class Evaluator:
             from .ops import hip_engine
             idx = device if isinstance(device, int) else int(os.environ.get("LOCAL_RANK", 0))
             available = hip_engine.device_available()
+            if available and not isinstance(device, int):
+                idx %= hip_engine.native().device_count()   # ranks > GPUs (gloo rehearsal) share the cards
             if not available and device != "auto":
                 raise RuntimeError("HIP device requested but none is visible")
             if available:

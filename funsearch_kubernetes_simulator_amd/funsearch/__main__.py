@@ -22,7 +22,8 @@ def main() -> None:
     ap.add_argument("--device", choices=["auto", "cpu", "gpu"])
     ap.add_argument("--resume", action="store_true")
     ap.add_argument("--checkpoint-dir")
-    ap.add_argument("--log")
+    ap.add_argument("--log", "--metrics-log", dest="log",
+                    help="JSONL metrics path (--metrics-log under torchrun, whose parser claims --log)")
     ap.add_argument("--save", help="write the top-5 JSON (reference schema) here")
     ap.add_argument("--device-min-batch", type=int,
                     help="smallest program batch sent to the device VM (smaller ones run on the CPU VM)")
