@@ -238,3 +238,26 @@ def test_elastic_resume_reshards_islands(tmp_path):
     # a resumed run keeps evolving from there
     code, score = many.run(generations=1, resume=False)
     assert many.generation == 41 and score >= 0.53
+
+
+def test_cli_elastic_resume_changes_island_count(tmp_path):
+    """CLI: a 2-island run, then `--resume --islands 3` on the same checkpoint
+    directory continues from its generation (islands re-sharded)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cfgp = tmp_path / "cfg.json"
+    cfgp.write_text(json.dumps(_cfg(tmp_path)))
+    base = [sys.executable, "-m", "funsearch_kubernetes_simulator_amd.funsearch", "--config", str(cfgp),
+            "--device", "cpu", "--checkpoint-dir", str(tmp_path / "ck"), "--metrics-log", str(tmp_path / "m.jsonl")]
+    env = dict(os.environ, PYTHONPATH=repo, OMP_NUM_THREADS="2")
+    r1 = subprocess.run(base + ["--islands", "2", "--generations", "2"], env=env, capture_output=True, text=True,
+                        timeout=600)
+    assert r1.returncode == 0, r1.stderr[-2000:]
+    r2 = subprocess.run(base + ["--islands", "3", "--generations", "1", "--resume"], env=env, capture_output=True,
+                        text=True, timeout=600)
+    assert r2.returncode == 0, r2.stderr[-2000:]
+    out = json.loads([l for l in r2.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["generations"] == 3 and out["islands_per_rank"] == 3
+    assert out["best_score"] >= reference_scores()["best_fit"]
+    assert len(json.loads((tmp_path / "ck" / "islands_rank0.json").read_text())["islands"]) == 3
