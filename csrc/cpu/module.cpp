@@ -95,6 +95,36 @@ void fill_row(double* row, const SimResult& r) {
 }
 
 
+// Scorer calling a natively compiled program (policy/native_codegen.py built
+// for the host with g++, ops/jit.py compile_host_module): same ABI as the
+// device path (csrc/hip/jit_abi.h ProgFn), one call per node.
+typedef int64_t (*HostProgFn)(int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t,
+                              int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t,
+                              int32_t, int32_t, const int64_t*, int32_t, int32_t, int32_t, int64_t, int32_t,
+                              const int64_t*);
+struct NativeHostScorer {
+  HostProgFn fn;
+  const int64_t* kc;
+  const std::vector<int64_t>* gmem8;   // [node][8]
+  int32_t exc = EXC_NONE;
+  ScoreOut operator()(const ScoreCtx& c, int n) {
+    ScoreOut o;
+    const Workload& w = c.w;
+    const int g0 = w.gpu_start[n], ng = w.gpu_start[n + 1] - g0;
+    if (ng > 8) { o.exc = EXC_UNSUPPORTED; return o; }
+    int32_t gl[8] = {0}, gt[8] = {0};
+    for (int j = 0; j < ng; ++j) { gl[j] = c.s.gmilli_left[g0 + j]; gt[j] = w.gmilli_total[g0 + j]; }
+    const int64_t r = fn((int32_t)c.s.cpu_left[n], (int32_t)w.cpu_total[n], (int32_t)c.s.mem_left[n],
+                         (int32_t)w.mem_total[n], c.s.gpu_left[n], w.ngpus[n], gl[0], gl[1], gl[2], gl[3], gl[4],
+                         gl[5], gl[6], gl[7], gt[0], gt[1], gt[2], gt[3], gt[4], gt[5], gt[6], gt[7],
+                         gmem8->data() + (size_t)n * 8, (int32_t)w.pcpu[c.pod], (int32_t)w.pmem[c.pod],
+                         w.pgmilli[c.pod] | (w.pngpu[c.pod] << 16), c.pod_ctime, (int32_t)w.pdur[c.pod], kc);
+    if (r < 0) { o.exc = (int32_t)(-r); exc = o.exc; return o; }
+    o.v = Num::I(r);
+    return o;
+  }
+};
+
 }  // namespace
 
 template <class T>
@@ -236,6 +266,43 @@ PYBIND11_MODULE(_fks_cpu, m) {
     return out;
   }, py::arg("workload"), py::arg("codes"), py::arg("fconsts"), py::arg("iconsts"), py::arg("ctags"),
      py::arg("options") = py::dict(), py::arg("threads") = 1);
+
+  m.def("simulate_native_batch", [](const Workload& w, std::vector<uint64_t> fns,
+                                    py::array_t<int64_t, py::array::c_style | py::array::forcecast> kc,
+                                    py::array_t<int32_t, py::array::c_style | py::array::forcecast> koff,
+                                    py::dict opts, int threads) {
+    const int64_t P = (int64_t)fns.size();
+    if ((int64_t)koff.size() != P) throw std::invalid_argument("koff must have one entry per program");
+    for (int n = 0; n < w.n_nodes; ++n) {
+      const int64_t vals[4] = {w.cpu_total[n], w.cpu_left0[n], w.mem_total[n], w.mem_left0[n]};
+      for (int64_t v : vals)
+        if (v > INT32_MAX || v < -(int64_t)INT32_MAX) throw std::invalid_argument("node resources outside int32");
+    }
+    for (int i = 0; i < w.n_pods; ++i)
+      if (w.pgmilli[i] >= (1 << 16) || w.pngpu[i] >= (1 << 8) || w.pcpu[i] > INT32_MAX || w.pmem[i] > INT32_MAX ||
+          w.pdur[i] > INT32_MAX)
+        throw std::invalid_argument("pod request outside the native ABI's packing");
+    std::vector<int64_t> gmem8((size_t)w.n_nodes * 8, 0);
+    for (int n = 0; n < w.n_nodes; ++n)
+      for (int j = 0; j < std::min(8, w.gpu_start[n + 1] - w.gpu_start[n]); ++j)
+        gmem8[(size_t)n * 8 + j] = w.gmem_total[w.gpu_start[n] + j];
+    SimOptions o = make_options(opts);
+    py::array_t<double> out({P, (int64_t)kCols});
+    double* op = out.mutable_data();
+    const int64_t* kp = kc.data();
+    const int32_t* ko = koff.data();
+    {
+      py::gil_scoped_release rel;
+      parallel_for(P, threads, [&](int64_t i) {
+        NativeHostScorer sc{reinterpret_cast<HostProgFn>(fns[i]), kp + ko[i], &gmem8};
+        SimResult r = simulate(w, sc, o);
+        if (r.exc == EXC_NONE && sc.exc) r.exc = sc.exc;
+        fill_row(op + i * kCols, r);
+      });
+    }
+    return out;
+  }, py::arg("workload"), py::arg("fns"), py::arg("kc"), py::arg("koff"), py::arg("options") = py::dict(),
+     py::arg("threads") = 1);
 
   m.def("score_program_once", [](py::bytes code, std::vector<double> fconst, std::vector<int64_t> iconst,
                                  std::vector<uint8_t> ctag, py::dict pod, py::dict node, std::vector<int64_t> gpu_left,

@@ -12,11 +12,7 @@
 // against glibc (tests/test_dd_math.py).
 #pragma once
 
-#ifndef __HIPCC_RTC__   // hiprtc (policy JIT) provides these itself
-#include <hip/hip_runtime.h>
-#include <math.h>
-#include <stdint.h>
-#endif
+#include "jit_env.h"
 
 namespace fksd {
 

@@ -101,7 +101,7 @@ struct HostBuf {
 struct Slot {
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
-  DevBuf res, tab, fam, w, code, meta, kpay, ktag, gheap, prof, wc, queue;
+  DevBuf res, tab, fam, w, code, meta, kpay, ktag, gheap, prof, wc, queue, kc;
   HostBuf h_in, h_tab, h_wc;
   int P = 0;
   int fam_spec = -1;    // family shared by the whole staged batch, or -1
@@ -109,7 +109,7 @@ struct Slot {
   bool busy = false;
   roctx_range_id_t range = 0;   // roctx range spanning submit -> wait (rocprofv3 --marker-trace)
   void release() {
-    for (DevBuf* b : {&res, &tab, &fam, &w, &code, &meta, &kpay, &ktag, &gheap, &prof, &wc, &queue}) b->release();
+    for (DevBuf* b : {&res, &tab, &fam, &w, &code, &meta, &kpay, &ktag, &gheap, &prof, &wc, &queue, &kc}) b->release();
     h_in.release();
     h_tab.release();
     h_wc.release();
@@ -274,6 +274,70 @@ class DeviceEngine {
     }
   }
 
+  // Natively compiled programs (policy/native_codegen.py + ops/jit.py): fn[p]
+  // is the device address of policy p's scorer inside a loaded JIT module,
+  // kc the concatenated constant blocks, koff[p] where policy p's starts.
+  void submit_native(int slot, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> fn,
+                     py::array_t<int64_t, py::array::c_style | py::array::forcecast> kc,
+                     py::array_t<int32_t, py::array::c_style | py::array::forcecast> koff) {
+    Slot& s = idle_slot(slot);
+    const int P = (int)fn.size();
+    if (P < 1) throw std::invalid_argument("empty batch");
+    if ((int)koff.size() != P) throw std::invalid_argument("koff must have one entry per policy");
+    for (int i = 0; i < P; ++i) {
+      if (fn.at(i) == 0) throw std::invalid_argument("null program pointer");
+      if (koff.at(i) < 0 || koff.at(i) >= (int64_t)kc.size()) throw std::invalid_argument("koff out of range");
+    }
+    HIP_OK(hipSetDevice(device_));
+    s.range = roctxRangeStartA("fks.batch.native");
+    HIP_OK(hipStreamSynchronize(s.stream));   // the previous batch no longer reads the staging
+    ensure_batch(s, P);
+    s.fam_spec = -1;
+    const size_t fb = (size_t)P * 8, ob = (size_t)P * 4, kb = (size_t)kc.size() * 8;
+    s.h_in.reserve(fb + ob + 64);
+    std::memcpy(s.h_in.as<char>(), fn.data(), fb);       // read by the kernel through the mapping
+    std::memcpy(s.h_in.as<char>() + fb, koff.data(), ob);
+    s.kc.reserve(kb + 16);
+    s.h_wc.reserve(sizeof(DevWorkload));
+    HIP_OK(hipMemcpyAsync(s.kc.p, kc.data(), kb, hipMemcpyHostToDevice, s.stream));
+    HIP_OK(hipStreamSynchronize(s.stream));   // kc is pageable: finish the copy while it is alive
+    {
+      py::gil_scoped_release rel;
+      const bool g = use_gheap_native(P);
+      const DevWorkload Wl = launch_workload(g, 0, false);
+      const size_t lds = lds_bytes(g, Wl.heap_top, 0);
+      if (lds > kMaxLds) throw std::invalid_argument("replay layout exceeds the 160 KiB LDS");
+      uint64_t* gh = g ? gheap_for(s, P) : nullptr;
+      const fksk::NativeArgs a{Wl, upload_workload(s, Wl), s.h_in.dev<const uint64_t>(), s.kc.as<const int64_t>(),
+                               reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + fb), s.res.as<DevResult>(), gh};
+      if (npass_ == 1) HIP_OK(fksk::launch_native_np1(g, P, lds, s.stream, a));
+      else if (npass_ == 2) HIP_OK(fksk::launch_native_np2(g, P, lds, s.stream, a));
+      else HIP_OK(fksk::launch_native_np4(g, P, lds, s.stream, a));
+      finish(s);
+    }
+  }
+
+  py::array_t<double> evaluate_native(py::array_t<uint64_t, py::array::c_style | py::array::forcecast> fn,
+                                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> kc,
+                                      py::array_t<int32_t, py::array::c_style | py::array::forcecast> koff) {
+    submit_native(0, fn, kc, koff);
+    return wait(0);
+  }
+
+  // device addresses of the native programs' runtime library
+  py::array_t<uint64_t> native_rt_table() {
+    HIP_OK(hipSetDevice(device_));
+    Slot& s = *slots_[0];
+    uint64_t* d = nullptr;
+    HIP_OK(hipMalloc(&d, 4 * 8));
+    HIP_OK(fksk::native_rt_table(d, s.stream));
+    py::array_t<uint64_t> out(4);
+    HIP_OK(hipMemcpyAsync(out.mutable_data(), d, 4 * 8, hipMemcpyDeviceToHost, s.stream));
+    HIP_OK(hipStreamSynchronize(s.stream));
+    (void)hipFree(d);
+    return out;
+  }
+
   bool ready(int slot) {
     Slot& s = slot_at(slot);
     if (!s.busy) return true;
@@ -416,6 +480,8 @@ class DeviceEngine {
     HIP_OK(fksk::set_vm_attrs_np1(mx)); HIP_OK(fksk::set_vm_attrs_np2(mx)); HIP_OK(fksk::set_vm_attrs_np4(mx));
     HIP_OK(fksk::set_prof_attrs(mx));
     HIP_OK(fksk::set_rows_attrs(mx));
+    HIP_OK(fksk::set_native_attrs_np1(mx)); HIP_OK(fksk::set_native_attrs_np2(mx));
+    HIP_OK(fksk::set_native_attrs_np4(mx));
   }
 
   // 4-policies-per-wave row kernel: clusters of <= 16 nodes, exact repush
@@ -461,6 +527,11 @@ class DeviceEngine {
     const size_t lds = rows_lds_bytes(W_.n_pods, T);
     return std::min<int>(fksk::rows_waves_per_cu(fam, lds), (int)(kMaxLds / ((lds + 2047) & ~size_t(2047))));
   }
+
+  // native-program kernels allocate 128 VGPRs (the JIT register floor): 2
+  // waves per SIMD with the HBM heap, so the LDS heap (2 per CU) wins only for
+  // batches that fit it
+  bool use_gheap_native(int P) const { return use_gheap(P); }
 
   bool use_gheap(int P) const {
     if (!lds_heap_ok_ || lds_bytes(false, 0, 0) > kMaxLds) return true;

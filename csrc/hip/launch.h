@@ -38,6 +38,18 @@ struct VmArgs {
   uint64_t* prof;
 };
 
+// Native programs (FKS_KIND 4): fn[p] = device address of policy p's
+// JIT-compiled scorer (jit_abi.h ProgFn), kc + koff[p] its constant block.
+struct NativeArgs {
+  DevWorkload W;
+  const DevWorkload* Wc;
+  const uint64_t* fn;     // [P] function pointers (pinned host memory, device-mapped)
+  const int64_t* kc;      // concatenated constant blocks
+  const int32_t* koff;    // [P] offsets into kc
+  DevResult* out;
+  uint64_t* gheap;
+};
+
 // One set of launchers per NPASS (1, 2, 4), named *_np<NPASS>.
 // fam_spec >= 0: every policy of the batch has that family (specialised
 // kernel); -1: mixed batch.
@@ -46,7 +58,9 @@ struct VmArgs {
                                   const BuiltinArgs& a);                                              \
   hipError_t launch_vm_np##N(bool gheap, int P, size_t lds, hipStream_t s, const VmArgs& a);          \
   hipError_t set_builtin_attrs_np##N(int max_lds);                                                    \
-  hipError_t set_vm_attrs_np##N(int max_lds);
+  hipError_t set_vm_attrs_np##N(int max_lds);                                                         \
+  hipError_t launch_native_np##N(bool gheap, int P, size_t lds, hipStream_t s, const NativeArgs& a);  \
+  hipError_t set_native_attrs_np##N(int max_lds);
 FKS_DECLARE_NPASS(1)
 FKS_DECLARE_NPASS(2)
 FKS_DECLARE_NPASS(4)
@@ -64,6 +78,9 @@ hipError_t launch_builtin_rows_prof(int fam_spec, int P, int waves, uint32_t* qu
 // resident row-kernel waves per CU for a family's instance at `lds` bytes (-1: error)
 int rows_waves_per_cu(int fam_spec, size_t lds);
 hipError_t set_rows_attrs(int max_lds);
+
+// addresses of the native programs' runtime library (fks_rt_binop, fks_rt_unop, register floor)
+hipError_t native_rt_table(uint64_t* dev_out, hipStream_t s);
 
 // phase-profiled variants (NPASS = 1)
 hipError_t launch_builtin_prof(bool gheap, int P, size_t lds, hipStream_t s, const BuiltinArgs& a);

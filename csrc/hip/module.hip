@@ -22,6 +22,7 @@
 #include "replay_rows.hip.h"
 #include "scorers.hip.h"
 #include "vm_dev.hip.h"
+#include "jit_abi.h"
 
 namespace py = pybind11;
 using namespace fksd;
@@ -226,6 +227,54 @@ py::array_t<float> mfma_probe(int device) {
   return out;
 }
 
+// A loaded JIT code object of natively compiled programs (ops/jit.py).
+// Load: hipModuleLoadData; the module's `fks_rt_table` global receives the
+// runtime-library addresses; `fks_jit_table` reports the program addresses.
+class JitModule {
+ public:
+  JitModule(py::bytes image, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> rt, int n_programs,
+            int device)
+      : device_(device), n_(n_programs) {
+    if (n_programs < 1) throw std::invalid_argument("empty JIT module");
+    const std::string img = image;
+    HIP_OK(hipSetDevice(device_));
+    HIP_OK(hipModuleLoadData(&mod_, img.data()));
+    hipDeviceptr_t g = nullptr;
+    size_t gbytes = 0;
+    HIP_OK(hipModuleGetGlobal(&g, &gbytes, mod_, "fks_rt_table"));
+    if (gbytes < (size_t)rt.size() * 8) throw std::runtime_error("fks_rt_table too small");
+    HIP_OK(hipMemcpyHtoD(g, const_cast<uint64_t*>(rt.data()), (size_t)rt.size() * 8));
+    hipFunction_t f;
+    HIP_OK(hipModuleGetFunction(&f, mod_, "fks_jit_table"));
+    uint64_t* d = nullptr;
+    HIP_OK(hipMalloc(&d, (size_t)n_ * 8));
+    void* args[] = {&d};
+    HIP_OK(hipModuleLaunchKernel(f, 1, 1, 1, 1, 1, 1, 0, nullptr, args, nullptr));
+    ptrs_.resize(n_);
+    HIP_OK(hipMemcpy(ptrs_.data(), d, (size_t)n_ * 8, hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    for (uint64_t p : ptrs_)
+      if (p == 0) throw std::runtime_error("JIT module reported a null program address");
+  }
+  ~JitModule() {
+    if (mod_) {
+      (void)hipSetDevice(device_);
+      (void)hipDeviceSynchronize();   // no launch may still call into the module
+      (void)hipModuleUnload(mod_);
+    }
+  }
+  py::array_t<uint64_t> pointers() const {
+    py::array_t<uint64_t> out(n_);
+    std::memcpy(out.mutable_data(), ptrs_.data(), (size_t)n_ * 8);
+    return out;
+  }
+
+ private:
+  int device_ = 0, n_ = 0;
+  hipModule_t mod_ = nullptr;
+  std::vector<uint64_t> ptrs_;
+};
+
 int device_count() {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -259,7 +308,16 @@ PYBIND11_MODULE(_fks_hip, m) {
       .def("would_use_rows", &DeviceEngine::would_use_rows)
       .def("profile_rows", &DeviceEngine::profile_rows)
       .def("synchronize", &DeviceEngine::synchronize)
-      .def("info", &DeviceEngine::info);
+      .def("info", &DeviceEngine::info)
+      .def("submit_native", &DeviceEngine::submit_native)
+      .def("evaluate_native", &DeviceEngine::evaluate_native)
+      .def("native_rt_table", &DeviceEngine::native_rt_table);
+  py::class_<JitModule>(m, "JitModule")
+      .def(py::init<py::bytes, py::array_t<uint64_t, py::array::c_style | py::array::forcecast>, int, int>(),
+           py::arg("image"), py::arg("rt"), py::arg("n_programs"), py::arg("device") = 0)
+      .def("pointers", &JitModule::pointers);
+  m.attr("JIT_VGPRS") = kJitVgprs;
+  m.attr("JIT_SGPRS") = kJitSgprs;
   m.attr("WEIGHTS_PER_POLICY") = kWeights;
   // host builds of the device math, for differential tests against glibc
   m.def("dd_pow", [](double x, double y) { double o = 0; int s = fksd::dd_pow(x, y, o); return py::make_tuple(s, o); });

@@ -26,6 +26,7 @@
 #pragma once
 
 #include "device_common.h"
+#include "exc_codes.h"
 #include "heap_wave.h"
 
 namespace fksd {
@@ -33,10 +34,6 @@ namespace fksd {
 constexpr int kGmax = 8;        // GPUs per node held in registers
 constexpr int kFresh = 0, kRetry = 1, kDelete = 2;
 
-enum ExcCode : int32_t {
-  EXC_NONE = 0, EXC_ZERO_DIVISION = 1, EXC_VALUE = 2, EXC_OVERFLOW = 3, EXC_TYPE = 4,
-  EXC_INDEX = 5, EXC_ALLOC = 6, EXC_NAME = 7, EXC_UNSUPPORTED = 100, EXC_BUDGET = 101, EXC_INVARIANT = 102,
-};
 
 struct DevWorkload {
   int32_t n_nodes, n_pods, n_classes, n_fire;

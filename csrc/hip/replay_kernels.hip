@@ -5,6 +5,8 @@
 //   FKS_KIND 1 -> bytecode-VM kernels for FKS_NPASS
 //   FKS_KIND 2 -> phase-profiled diagnostics kernels (NPASS = 1)
 //   FKS_KIND 3 -> row kernels (4 policies per wave, <= 16 nodes; replay_rows.hip.h)
+//   FKS_KIND 4 -> native-program kernels (JIT-compiled scorers called through
+//                 function pointers; jit_abi.h) for FKS_NPASS
 // Each unit defines the matching launchers of launch.h.
 #include <hip/hip_runtime.h>
 
@@ -13,6 +15,7 @@
 #include "scorers.hip.h"
 #include "vm_dev.hip.h"
 #include "replay_rows.hip.h"
+#include "jit_abi.h"
 
 #ifndef FKS_KIND
 #define FKS_KIND 0
@@ -200,6 +203,65 @@ void k_replay_rows_prof(fksk::BuiltinArgs a, int P, uint32_t* queue, uint32_t qb
 }
 #endif
 
+
+#if FKS_KIND == 4
+// Scorer of natively compiled programs: one indirect call per node pass to the
+// policy's JIT function (wave-uniform pointer -> a plain s_swappc).
+struct NativeScorerDev {
+  ProgFn fn;
+  const int64_t* gmem;   // [node][kGmax] GPU memory MiB
+  const int64_t* kc;     // the policy's [budget, constants...]
+  template <int NPASS>
+  __device__ int64_t score(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, int& exc) {
+    const int node = ps * kWave + lane_id();
+    const int32_t* gl = nr.gml[ps];
+    const int32_t* gt = nr.gmt[ps];
+    const int64_t r = fn(nr.cpu_left[ps], nr.cpu_total[ps], nr.mem_left[ps], nr.mem_total[ps], nr.gpu_left[ps],
+                         nr.ngpus[ps], gl[0], gl[1], gl[2], gl[3], gl[4], gl[5], gl[6], gl[7], gt[0], gt[1], gt[2], gt[3],
+                         gt[4], gt[5], gt[6], gt[7], gmem + (size_t)node * kGmax, pod.cpu, pod.mem,
+                         pod.gmilli | (pod.ngpu << 16), pod.ctime, pod.dur, kc);
+    if (r < 0) { exc = (int)(-r); return 0; }
+    return r;
+  }
+};
+
+// Register floor: an address-taken function touching v127 / s101 raises this
+// unit's amdgpu.max_num_vgpr / max_num_sgpr, and with them the allocation of
+// every kernel here that makes an indirect call, to what JIT-compiled
+// programs may use (kJitVgprs / kJitSgprs, checked by ops/jit.py).
+__device__ __noinline__ int64_t fks_reg_floor(int64_t a) {
+  asm volatile("" ::: "v127", "s101");
+  return a;
+}
+
+// Runtime library of native programs (jit_abi.h rt_binop / rt_unop): the
+// exact float //, %, **, math.log / exp / sqrt / pow of the device VM.
+extern "C" __device__ __noinline__ Ret2 fks_rt_binop(int op, int64_t ab, int32_t afl, int64_t bb, int32_t bfl) {
+  return d_binop_s(op, ab, afl, bb, bfl);
+}
+extern "C" __device__ __noinline__ Ret2 fks_rt_unop(int op, int64_t ab, int32_t afl) { return d_unop_s(op, ab, afl); }
+
+__global__ void k_native_rt_table(uint64_t* out) {
+  if (threadIdx.x == 0) {
+    out[0] = (uint64_t)&fks_rt_binop;
+    out[1] = (uint64_t)&fks_rt_unop;
+    out[2] = (uint64_t)&fks_reg_floor;
+    out[3] = 0;
+  }
+}
+
+template <int NPASS, bool GHEAP>
+__global__ __launch_bounds__(64, GHEAP ? 2 : 1) void k_replay_native(fksk::NativeArgs a) {
+  const int p = blockIdx.x;
+  const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
+  NativeScorerDev sc;
+  sc.fn = reinterpret_cast<ProgFn>(uniu64(a.fn[p]));
+  sc.gmem = a.W.gmem_total;
+  sc.kc = reinterpret_cast<const int64_t*>(uniu64(reinterpret_cast<uint64_t>(a.kc + a.koff[p])));
+  replay_one<NPASS>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p);
+}
+#endif
+
 }  // namespace
 
 namespace fksk {
@@ -304,6 +366,25 @@ hipError_t set_rows_attrs(int mx) {
     if (r != hipSuccess) e = r;
   return e;
 }
+#endif
+
+
+#if FKS_KIND == 4
+hipError_t FKS_CAT(launch_native_np, FKS_NPASS)(bool gheap, int P, size_t lds, hipStream_t s, const NativeArgs& a) {
+  if (gheap) hipLaunchKernelGGL((k_replay_native<FKS_NPASS, true>), dim3(P), dim3(64), lds, s, a);
+  else hipLaunchKernelGGL((k_replay_native<FKS_NPASS, false>), dim3(P), dim3(64), lds, s, a);
+  return hipGetLastError();
+}
+hipError_t FKS_CAT(set_native_attrs_np, FKS_NPASS)(int mx) {
+  const hipError_t e = raise_lds(&k_replay_native<FKS_NPASS, true>, mx);
+  return e != hipSuccess ? e : raise_lds(&k_replay_native<FKS_NPASS, false>, mx);
+}
+#if FKS_NPASS == 1
+hipError_t native_rt_table(uint64_t* dev_out, hipStream_t s) {
+  hipLaunchKernelGGL(k_native_rt_table, dim3(1), dim3(64), 0, s, dev_out);
+  return hipGetLastError();
+}
+#endif
 #endif
 
 }  // namespace fksk

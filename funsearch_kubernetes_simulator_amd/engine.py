@@ -4,8 +4,11 @@ Routing per program (every path yields the reference's score bit-for-bit):
 
 1. compile to bytecode (`policy.compiler`); programs outside the native
    subset go straight to the object engine (CPython ``exec``, step 4);
-2. MI355X (`ops.hip_engine`): one k_replay wave per program, all programs of
-   a call in one launch;
+2. MI355X (`ops.hip_engine`): natively compiled programs first
+   (`policy.native_codegen` -> `ops.jit`, one k_replay_native wave per program,
+   any batch size; compiled shapes are cached), then the device bytecode VM for
+   what the native backend declines, when the batch is large enough to fill
+   the chip;
 3. native CPU VM (`ops.cpu_engine`): for no-GPU hosts, for programs the device
    reports as EXC_UNSUPPORTED (bigint / complex / trig / near-tie math) or
    EXC_BUDGET (per-call instruction budget), and for results whose exact-mean
@@ -57,8 +60,7 @@ class EvalResult:
 def _row_to_result(row: np.ndarray, engine: str) -> EvalResult:
     exc = int(row[COLS["exc"]])
     if exc:
-        return EvalResult(0.0 if exc not in (Exc.UNSUPPORTED, Exc.BUDGET) else 0.0, exc, engine,
-                          n_events=int(row[COLS["n_events"]]))
+        return EvalResult(0.0, exc, engine, n_events=int(row[COLS["n_events"]]))
     res = EvaluationResults(
         avg_cpu_utilization=float(row[COLS["avg_cpu"]]),
         avg_memory_utilization=float(row[COLS["avg_mem"]]),
@@ -149,6 +151,8 @@ class Evaluator:
         # below this many programs a batch runs faster on the CPU VM (one replay per
         # core, ~0.1 s each) than as a handful of latency-bound device waves
         self.device_min_batch = int(self.options.pop("device_min_batch", 128))
+        # natively compiled programs on the device (any batch size)
+        self.native = bool(self.options.pop("native", True))
         # fault-injection hook: fail this fraction of program
         # evaluations as if the replay had raised -> score 0, like the reference
         self.fault_rate = float(self.options.pop("fault_rate", 0.0) or 0.0)
@@ -169,7 +173,8 @@ class Evaluator:
                 except hip_engine.UnsupportedWorkload:
                     if device != "auto":
                         raise
-        self.stats = {"device": 0, "cpu_vm": 0, "object": 0, "compile_errors": 0}
+        self.stats = {"device": 0, "device_native": 0, "cpu_vm": 0, "object": 0, "compile_errors": 0,
+                      "jit_s": 0.0, "jit_shapes": 0}
         self._done: Dict[int, np.ndarray] = {}   # CPU stand-in for in-flight slots
 
     @property
@@ -215,10 +220,13 @@ class Evaluator:
             if prog is None:
                 self.stats["compile_errors"] += 1
             compiled.append(prog)
-        # 1) device
+        # 1) device: native code, then the bytecode VM
         pending = [i for i, p in enumerate(compiled) if p is not None]
         if self.device is not None:
             dev_idx = [i for i in pending if compiled[i].device_ok]
+            if dev_idx and self.native:
+                self._absorb_native(dev_idx, compiled, out, 0)
+            dev_idx = [i for i in dev_idx if out[i] is None]
             if len(dev_idx) >= self.device_min_batch:
                 tab = self.device.evaluate_programs([compiled[i] for i in dev_idx])
                 for row, i in zip(tab, dev_idx):
@@ -259,6 +267,17 @@ class Evaluator:
                     out[i] = EvalResult(0.0, int(Exc.VALUE), "fault-injection")
                     self.stats["faults"] = self.stats.get("faults", 0) + 1
         return out  # type: ignore[return-value]
+
+    def _absorb_native(self, idx, compiled, out, slot: int) -> None:
+        batch = self.device.submit_native(slot, [compiled[i] for i in idx])
+        self.stats["jit_s"] += batch.compile_s
+        self.stats["jit_shapes"] += batch.compiled
+        tab = self.device.wait(slot)
+        for row, i in zip(tab, idx):
+            if int(row[COLS["exc"]]) in (Exc.UNSUPPORTED, Exc.BUDGET) or row[COLS["inexact"]]:
+                continue
+            out[i] = _row_to_result(row, "hip-native")
+            self.stats["device_native"] += 1
 
     def _object_engine_ok(self) -> bool:
         # the object engine implements only the reference's semantics

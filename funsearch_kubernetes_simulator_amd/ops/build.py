@@ -70,7 +70,7 @@ def build_cpu(force: bool = False) -> Path:
 #: instances compile in parallel.
 HIP_UNITS = [("module", "module.hip", []), ("screen", "screen.hip", [])] + [
     (f"replay_k{kind}_np{npass}", "replay_kernels.hip", [f"-DFKS_KIND={kind}", f"-DFKS_NPASS={npass}"])
-    for kind, npasses in ((0, (1, 2, 4)), (1, (1, 2, 4)), (2, (1,)), (3, (1,))) for npass in npasses]
+    for kind, npasses in ((0, (1, 2, 4)), (1, (1, 2, 4)), (2, (1,)), (3, (1,)), (4, (1, 2, 4))) for npass in npasses]
 
 
 def _hip_flags() -> List[str]:

@@ -122,3 +122,39 @@ def simulate_program_batch(w: Workload, progs: Sequence[CompiledPolicy],
                                            [p.fconst for p in progs], [p.iconst for p in progs],
                                            [p.ctag for p in progs], (options or SimOptions()).as_dict(),
                                            threads)
+
+
+# ---------------------------------------------------------------------------- native programs on the CPU
+_host_libs: dict = {}
+
+
+def host_native_library(progs: Sequence[CompiledPolicy], workdir: Optional[str] = None):
+    """g++ build of the programs' native code (policy/native_codegen.py, the
+    same C++ the device JIT compiles) loaded with ctypes: (library, addresses)."""
+    import ctypes
+    import hashlib
+    import tempfile
+    from . import jit
+    from ..policy.native_codegen import module_source
+    key = hashlib.sha1(module_source(progs, host=True).encode()).hexdigest()
+    if key not in _host_libs:
+        d = workdir or tempfile.mkdtemp(prefix="fks_hostjit_")
+        path = jit.compile_host_module(progs, os.path.join(d, f"m_{key[:12]}.so"))
+        lib = ctypes.CDLL(path)
+        n = ctypes.c_int.in_dll(lib, "fks_host_count").value
+        table = (ctypes.c_void_p * n).in_dll(lib, "fks_host_table")
+        _host_libs[key] = (lib, [int(table[i]) for i in range(n)])
+    return _host_libs[key]
+
+
+def simulate_native_batch(w: Workload, progs: Sequence[CompiledPolicy], options: Optional[SimOptions] = None,
+                          threads: int = 0) -> np.ndarray:
+    """Replays with host-compiled native programs: [P, 13] like the VM batch."""
+    from ..policy.native_codegen import constant_block
+    threads = threads or default_threads()
+    opts = options or SimOptions()
+    _, addrs = host_native_library(progs)
+    blocks = [constant_block(p, opts.budget if opts.budget > 0 else DEFAULT_CALL_BUDGET) for p in progs]
+    koff = np.cumsum([0] + [len(b) for b in blocks[:-1]]).astype(np.int32)
+    return native().simulate_native_batch(native_workload(w), addrs, np.concatenate(blocks), koff, opts.as_dict(),
+                                          threads)

@@ -205,8 +205,37 @@ class DeviceEvaluator:
         self._eng.set_options(options)
         self.options = options
 
+        self._jit = None
+        self._native_post: Dict[int, Tuple[int, np.ndarray]] = {}   # slot -> (P, native row indices)
+
     def info(self) -> dict:
         return dict(self._eng.info())
+
+    # -- natively compiled programs (policy/native_codegen.py, ops/jit.py) ------------------
+    @property
+    def native_compiler(self):
+        if self._jit is None:
+            from .jit import NativeCompiler
+            self._jit = NativeCompiler(self._eng, self.device, budget=int(self.options.get("budget") or DEFAULT_CALL_BUDGET))
+        return self._jit
+
+    def submit_native(self, slot: int, progs: Sequence[CompiledPolicy]):
+        """Compile (shape-cached) and launch one k_replay_native wave per program on
+        `slot`.  Programs the native backend cannot take (codegen / register limits)
+        get an EXC_UNSUPPORTED row from `wait`, so callers fall back per program.
+        Returns the `NativeBatch` (compile time, cache hits, reasons)."""
+        batch = self.native_compiler.prepare(progs)
+        idx = np.flatnonzero(batch.ok)
+        self._native_post[slot] = (len(progs), idx)
+        if idx.size:
+            self._eng.submit_native(slot, batch.fn[idx], batch.kc, batch.koff[idx])
+        return batch
+
+    def evaluate_native(self, progs: Sequence[CompiledPolicy]) -> np.ndarray:
+        if not progs:
+            return np.zeros((0, len(RESULT_COLUMNS)))
+        self.submit_native(0, progs)
+        return self.wait(0)
 
     def set_options(self, **opts) -> None:
         if "snapshot_interval" in opts and opts["snapshot_interval"] != self.options["snapshot_interval"]:
@@ -243,12 +272,23 @@ class DeviceEvaluator:
     def submit_programs(self, slot: int, progs: Sequence[CompiledPolicy]) -> None:
         self._eng.submit_programs(slot, *pack_programs(progs), max(p.nregs for p in progs))
 
-    def ready(self, slot: int) -> bool:
-        return self._eng.ready(slot)
-
     def wait(self, slot: int) -> np.ndarray:
         """[P, 13] result table of the batch in flight on `slot`."""
-        return self._eng.wait(slot)
+        post = self._native_post.pop(slot, None)
+        if post is None:
+            return self._eng.wait(slot)
+        P, idx = post
+        out = np.zeros((P, len(RESULT_COLUMNS)))
+        out[:, 10] = 100.0   # EXC_UNSUPPORTED: not native -> the caller's next engine
+        if idx.size:
+            out[idx] = self._eng.wait(slot)
+        return out
+
+    def ready(self, slot: int) -> bool:
+        post = self._native_post.get(slot)
+        if post is not None and post[1].size == 0:
+            return True
+        return self._eng.ready(slot)
 
     def evaluate_programs(self, progs: Sequence[CompiledPolicy]) -> np.ndarray:
         if not progs:

@@ -1,0 +1,282 @@
+"""Run-time compiler of policy programs for the MI355X (native program backend).
+
+Pipeline per batch of new program *shapes* (bytecode + constant tags; the
+constants themselves are data, `policy.native_codegen`):
+
+  native_codegen.module_source  ->  clang -O3 -emit-llvm (gfx950, device
+  only, no HIP headers, no device libraries)  ->  ``"amdgpu-agpr-alloc"="0"``
+  on every function  ->  llc -O3  ->  resource check from the assembly's
+  per-function ``.set <fn>.num_vgpr / numbered_sgpr / private_seg_size``
+  symbols  ->  llvm-mc + ld.lld  ->  code object  ->
+  ``_fks_hip.JitModule`` (hipModuleLoadData; the module's ``fks_rt_table``
+  gets the extension's runtime-library addresses; ``fks_jit_table`` reports
+  every program's device address).
+
+The replay kernel (`k_replay_native`, csrc/hip/replay_kernels.hip) calls a
+program through its address with an ordinary indirect call, so a compile never
+touches the replay loop.  The caller allocates `JIT_VGPRS` / `JIT_SGPRS`
+registers (its register floor); a program whose own use exceeds them, or whose
+stack frame would not fit the dynamic stack, is reported unsupported and
+evaluated by the VM / CPU engines instead.
+
+Compiles of independent module chunks run in parallel subprocesses (the
+clang processes release the GIL), and every compiled shape is cached for the
+life of the process, so re-evaluating a program -- or any program that differs
+from a compiled one only in its numeric constants -- costs no compile at all.
+"""
+
+from __future__ import annotations
+
+import math
+import os
+import re
+import subprocess
+import tempfile
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .._paths import CSRC_DIR
+from ..policy.compiler import CompiledPolicy
+from ..policy.native_codegen import CodegenError, constant_block, module_source, shape_key
+
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+CLANG = os.path.join(ROCM, "lib", "llvm", "bin", "clang")
+LLD = os.path.join(ROCM, "lib", "llvm", "bin", "ld.lld")
+LLC = os.path.join(ROCM, "lib", "llvm", "bin", "llc")
+LLVM_MC = os.path.join(ROCM, "lib", "llvm", "bin", "llvm-mc")
+_ATTR_RE = re.compile(r"^(attributes #\d+ = \{)", re.M)
+ARCH = os.environ.get("FKS_OFFLOAD_ARCH", "gfx950")
+JIT_INCLUDE = str(CSRC_DIR / "hip")
+DEVICE_FLAGS = ["-x", "hip", "--offload-device-only", "-nogpulib", "-nogpuinc", "-O3", f"--offload-arch={ARCH}",
+                "-std=c++17", "-DFKS_JIT", "-ffp-contract=off", "-fno-fast-math", "-Wno-unused-label",
+                "-Wno-tautological-compare", f"-I{JIT_INCLUDE}"]
+#: the runtime library's worst frame (fks_rt_binop/unop, measured from the
+#: extension's assembly: <= 48 B) plus the replay kernel's call-site spills
+RT_FRAME_BYTES = 256
+STACK_LIMIT_BYTES = 1024   # HIP's default per-lane stack for dynamic-stack kernels
+
+
+class JitError(RuntimeError):
+    """The toolchain failed on a module (a bug, not an unsupported program)."""
+
+
+@dataclass
+class Resources:
+    vgprs: int = 0
+    agprs: int = 0
+    sgprs: int = 0
+    private: int = 0
+
+    def fits(self, vgpr_cap: int, sgpr_cap: int) -> Optional[str]:
+        if self.vgprs > vgpr_cap:
+            return f"{self.vgprs} VGPRs > {vgpr_cap}"
+        if self.agprs:
+            return f"uses {self.agprs} AGPRs"
+        if self.sgprs > sgpr_cap:
+            return f"{self.sgprs} SGPRs > {sgpr_cap}"
+        if self.private + RT_FRAME_BYTES > STACK_LIMIT_BYTES:
+            return f"{self.private} B stack frame"
+        return None
+
+
+_SET_RE = re.compile(r"^\s*\.set\s+(?:\.L)?(fks_prog_\d+)\.(num_vgpr|num_agpr|numbered_sgpr|private_seg_size),\s*(.+)$")
+
+
+def _first_int(expr: str) -> int:
+    """Own count of a resource symbol: ``max(52, amdgpu.max_num_vgpr)`` -> 52."""
+    m = re.search(r"-?\d+", expr)
+    return int(m.group(0)) if m else 0
+
+
+def function_resources(asm: str) -> Dict[str, Resources]:
+    out: Dict[str, Resources] = {}
+    for line in asm.splitlines():
+        m = _SET_RE.match(line)
+        if not m:
+            continue
+        r = out.setdefault(m.group(1), Resources())
+        v = _first_int(m.group(3))
+        key = m.group(2)
+        if key == "num_vgpr":
+            r.vgprs = v
+        elif key == "num_agpr":
+            r.agprs = v
+        elif key == "numbered_sgpr":
+            r.sgprs = v
+        else:
+            r.private = v
+    return out
+
+
+@dataclass
+class CompiledModule:
+    image: bytes
+    n: int
+    resources: List[Optional[Resources]]
+    compile_s: float
+    handle: object = None            # _fks_hip.JitModule once loaded
+    pointers: Optional[np.ndarray] = None
+
+
+def _run(cmd: List[str], what: str) -> None:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise JitError(f"{what} failed ({r.returncode}): {r.stderr[-4000:]}")
+
+
+def compile_device_module(progs: Sequence[CompiledPolicy], workdir: Optional[str] = None) -> CompiledModule:
+    """gfx950 code object holding ``fks_prog_<i>`` for every program."""
+    t0 = time.perf_counter()
+    src = module_source(progs, with_probes=False)
+    with tempfile.TemporaryDirectory(prefix="fksjit_", dir=workdir) as d:
+        cpp, ll, asm, obj, co = (os.path.join(d, n) for n in ("m.hip", "m.ll", "m.s", "m.o", "m.co"))
+        with open(cpp, "w") as f:
+            f.write(src)
+        _run([CLANG, *DEVICE_FLAGS, "-S", "-emit-llvm", cpp, "-o", ll], "clang -emit-llvm")
+        # No accumulation registers anywhere in JIT code: the calling replay
+        # kernel's AGPRs sit above its VGPRs, and a function that makes calls
+        # would otherwise get a 64 VGPR + 64 AGPR split instead of 128 VGPRs.
+        with open(ll) as f:
+            ir = _ATTR_RE.sub(r'\1 "amdgpu-agpr-alloc"="0"', f.read())
+        with open(ll, "w") as f:
+            f.write(ir)
+        _run([LLC, "-mtriple=amdgcn-amd-amdhsa", f"-mcpu={ARCH}", "-O3", ll, "-o", asm], "llc")
+        with open(asm) as f:
+            text = f.read()
+        _run([LLVM_MC, "-triple=amdgcn-amd-amdhsa", f"-mcpu={ARCH}", "-filetype=obj", asm, "-o", obj], "llvm-mc")
+        _run([LLD, "-shared", "--no-undefined", obj, "-o", co], "ld.lld")
+        with open(co, "rb") as f:
+            image = f.read()
+    res = function_resources(text)
+    return CompiledModule(image, len(progs), [res.get(f"fks_prog_{i}") for i in range(len(progs))],
+                          time.perf_counter() - t0)
+
+
+def compile_host_module(progs: Sequence[CompiledPolicy], path: str) -> str:
+    """The same programs built for the host with g++ (``FKS_HOST_JIT``):
+    exports ``fks_host_table`` / ``fks_host_count``.  Used by the codegen
+    tests (CPU replays through the oracle engine) and as a CPU-native path."""
+    src = module_source(progs, host=True)
+    cpp = path + ".cpp"
+    with open(cpp, "w") as f:
+        f.write(src)
+    _run([os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-DFKS_HOST_JIT", f"-I{JIT_INCLUDE}", "-shared", "-fPIC",
+          "-ffp-contract=off", "-fno-fast-math", "-Wno-unused-label", "-x", "c++", cpp, "-o", path], "g++")
+    return path
+
+
+# ---------------------------------------------------------------------------- device cache
+@dataclass
+class NativeBatch:
+    """Per-policy launch data of one batch (programs in input order)."""
+    fn: np.ndarray                   # uint64 [P] device addresses (0: not native)
+    kc: np.ndarray                   # int64 concatenated constant blocks
+    koff: np.ndarray                 # int32 [P]
+    ok: np.ndarray                   # bool [P]
+    reasons: Dict[int, str] = field(default_factory=dict)
+    compile_s: float = 0.0           # wall time spent compiling for this batch
+    compiled: int = 0                # new shapes compiled for this batch
+
+
+class NativeCompiler:
+    """Shape cache + parallel compiler + loader for one HIP device."""
+
+    def __init__(self, engine, device: int = 0, workers: int = 0, budget: int = 1 << 22, max_chunk: int = 16):
+        from . import hip_engine
+        self._hip = hip_engine.native()
+        self._engine = engine            # _fks_hip.DeviceEngine (for the runtime table)
+        self.device = device
+        self.workers = workers or _default_workers()
+        self.budget = int(budget)
+        self.max_chunk = max_chunk
+        self._rt = np.asarray(engine.native_rt_table(), dtype=np.uint64)
+        self.vgpr_cap = int(self._hip.JIT_VGPRS)
+        self.sgpr_cap = int(self._hip.JIT_SGPRS)
+        self._shapes: Dict[str, Tuple[int, int]] = {}   # shape -> (module index, program index)
+        self._bad: Dict[str, str] = {}                  # shape -> reason it is not native
+        self._modules: List[CompiledModule] = []
+        self._lock = threading.Lock()
+        self.stats = {"modules": 0, "shapes": 0, "compile_s": 0.0, "rejected": 0, "hits": 0}
+
+    def prepare(self, progs: Sequence[CompiledPolicy]) -> NativeBatch:
+        keys = [shape_key(p) for p in progs]
+        new: Dict[str, CompiledPolicy] = {}
+        for k, p in zip(keys, progs):
+            if k not in self._shapes and k not in self._bad and k not in new:
+                new[k] = p
+        t0 = time.perf_counter()
+        if new:
+            self._compile_shapes(new)
+        dt = time.perf_counter() - t0
+        P = len(progs)
+        fn = np.zeros(P, dtype=np.uint64)
+        ok = np.zeros(P, dtype=bool)
+        koff = np.zeros(P, dtype=np.int32)
+        blocks, pos, reasons = [], 0, {}
+        for i, (k, p) in enumerate(zip(keys, progs)):
+            kb = constant_block(p, self.budget)
+            koff[i] = pos
+            blocks.append(kb)
+            pos += len(kb)
+            if k in self._shapes:
+                mi, pi_ = self._shapes[k]
+                fn[i] = self._modules[mi].pointers[pi_]
+                ok[i] = True
+            else:
+                reasons[i] = self._bad.get(k, "not compiled")
+        self.stats["hits"] += P - len(new)
+        return NativeBatch(fn, np.concatenate(blocks) if blocks else np.zeros(1, np.int64), koff, ok, reasons, dt,
+                           len(new))
+
+    def _compile_shapes(self, new: Dict[str, CompiledPolicy]) -> None:
+        items = list(new.items())
+        # code generation first (cheap, in-process): shapes it cannot lower are rejected
+        good = []
+        for k, p in items:
+            try:
+                module_source([p], with_probes=False)
+                good.append((k, p))
+            except CodegenError as exc:
+                self._bad[k] = f"codegen: {exc}"
+                self.stats["rejected"] += 1
+        if not good:
+            return
+        n_chunks = max(1, min(self.workers, len(good)))
+        size = max(1, min(self.max_chunk, math.ceil(len(good) / n_chunks)))
+        chunks = [good[i:i + size] for i in range(0, len(good), size)]
+        with ThreadPoolExecutor(max_workers=min(self.workers, len(chunks))) as ex:
+            mods = list(ex.map(lambda ch: compile_device_module([p for _, p in ch]), chunks))
+        for ch, mod in zip(chunks, mods):
+            self.stats["compile_s"] += mod.compile_s
+            mod.handle = self._hip.JitModule(mod.image, self._rt, mod.n, self.device)
+            mod.pointers = np.asarray(mod.handle.pointers(), dtype=np.uint64)
+            mi = len(self._modules)
+            self._modules.append(mod)
+            self.stats["modules"] += 1
+            for j, (k, _) in enumerate(ch):
+                res = mod.resources[j]
+                why = "no resource record" if res is None else res.fits(self.vgpr_cap, self.sgpr_cap)
+                if why:
+                    self._bad[k] = why
+                    self.stats["rejected"] += 1
+                else:
+                    self._shapes[k] = (mi, j)
+                    self.stats["shapes"] += 1
+
+
+def _default_workers() -> int:
+    env = os.environ.get("FKS_JIT_WORKERS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    from .cpu_engine import default_threads
+    return max(1, min(16, default_threads()))
+
+
+__all__ = ["CompiledModule", "JitError", "NativeBatch", "NativeCompiler", "Resources", "compile_device_module",
+           "compile_host_module", "function_resources"]
+

@@ -9,29 +9,13 @@ from funsearch_kubernetes_simulator_amd.ops import cpu_engine as ce
 from funsearch_kubernetes_simulator_amd.policy.bytecode import Exc
 from funsearch_kubernetes_simulator_amd.policy.compiler import CompileError, compile_policy
 
-from test_compiler import SNIPPETS
+from program_corpus import programs as corpus_programs
 
 pytestmark = pytest.mark.gpu
 
 
 def _programs():
-    codes = list(reference_policies().values()) + list(seed_policies().values())
-    rng = np.random.default_rng(9)
-    codes += [fam.to_program("feature_linear", w) for w in fam.sample_feature_linear(6, rng)]
-    codes += [fam.to_program("random_linear", w) for w in fam.sample_random_linear(4, rng)]
-    for s in SNIPPETS:
-        body = s if "return" in s else s + "\n    return 1"
-        codes.append("def priority_function(pod, node):\n    if (pod.cpu_milli > node.cpu_milli_left or "
-                     "pod.memory_mib > node.memory_mib_left or pod.num_gpu > node.gpu_left):\n        return 0\n"
-                     "    if pod.num_gpu > 0 and sum(1 for g in node.gpus if g.gpu_milli_left >= pod.gpu_milli) "
-                     "< pod.num_gpu:\n        return 0\n    " + body + "\n")
-    progs = []
-    for c in codes:
-        try:
-            progs.append(compile_policy(c))
-        except CompileError:
-            pass
-    return progs
+    return corpus_programs()
 
 
 @pytest.mark.parametrize("mode", ["lds", "hbm"])
