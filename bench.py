@@ -66,6 +66,9 @@ def main() -> None:
     ap.add_argument("--sync-islands", action="store_true",
                     help="one launch per generation for all islands (default: one HIP stream per island)")
     ap.add_argument("--save-best", default="", help="write the champion program (reference results-JSON schema)")
+    ap.add_argument("--programs", type=int, default=64,
+                    help="after the timed region: evaluate this many FunSearch candidate programs (offline-mutation "
+                         "children) through the native program backend and report them as `program_path` (0: skip)")
     args = ap.parse_args()
 
     from funsearch_kubernetes_simulator_amd.parallel import dist
@@ -95,6 +98,11 @@ def main() -> None:
                    n_slots=max(1, args.islands))
     if args.device == "gpu" and ev.device is None:
         raise SystemExit("no HIP device visible")
+    if args.device == "gpu" and ctx.backend == "nccl":
+        # the RCCL collective buffers and the replay engine must live on the same card
+        import torch
+        assert ctx.device.index == device == ev.device.device == torch.cuda.current_device(), \
+            (ctx.device, device, ev.device.device, torch.cuda.current_device())
     islands = make_islands(args.islands, args.family, args.candidates, args.elite,
                            seed=args.seed + 104729 * ctx.rank)
 
@@ -185,6 +193,14 @@ def main() -> None:
     elapsed = dist.all_reduce_max(time.perf_counter() - t0)
     events_total = dist.all_reduce_sum(events[0])
 
+    program_path = None
+    if args.programs > 0 and ev.device is not None:
+        # the program-for-program comparison with the reference's eval path (outside the timed region)
+        from funsearch_kubernetes_simulator_amd.bench.programs import measure_native, mutation_children
+        program_path = measure_native(ev.device, mutation_children(args.programs, seed=args.seed + ctx.rank))
+        program_path["vs_baseline"] = round(program_path["evals_per_s_incl_jit"] / BASELINE_EVALS_PER_S, 2)
+        program_path["engine"] = "hip-native (JIT-compiled programs, k_replay_native)"
+
     per_step = args.islands * args.candidates
     total = per_step * args.steps * ctx.world_size
     value = total / elapsed
@@ -218,8 +234,11 @@ def main() -> None:
                 "model": f"{args.family} policy family, exact replay (reference-bit-identical scores)",
                 "global_batch": per_step * ctx.world_size,
                 "seq_len": int(workload.pods.n_pods),
-                "parallelism": f"islands: {args.islands}/GPU x {ctx.world_size} GPU(s), RCCL all-gather "
-                               f"migration every {args.migrate_every} gens",
+                "parallelism": f"islands: {args.islands}/GPU x {ctx.world_size} rank(s), "
+                               + (f"{'RCCL' if ctx.backend == 'nccl' else ctx.backend} all-gather migration every "
+                                  f"{args.migrate_every} gens" if ctx.distributed else "single rank (no collectives)"),
+                "dist_backend": ctx.backend,
+                "world_size": ctx.world_size,
                 "candidates_per_island": args.candidates,
                 "backend": ev.backend,
                 "heap_mode": args.heap_mode,
@@ -232,6 +251,10 @@ def main() -> None:
                          "gpu_milli_util": row[COLS["avg_gpu_milli"]], "frag": row[COLS["frag"]]},
             "reference_champion": {"score": 0.49013357497851473, "cpu_util": 0.459, "mem_util": 0.261,
                                    "gpu_count_util": 0.734, "frag": 0.033},
+            "vs_baseline_note": "value = parametric-family evals/s (BASELINE config 2: random-weight candidates) "
+                                "divided by the reference's PROGRAM evals/s (15.84, 8 CPU workers); program_path "
+                                "is the program-for-program comparison",
+            "program_path": program_path,
         }
         if args.save_best:
             k = {"random_linear": 4, "feature_linear": fam.N_FEATURES}.get(args.family, fam.N_COMPOSITE)

@@ -1,0 +1,65 @@
+"""Program-path throughput: FunSearch candidate *programs* (not parametric
+family members) evaluated exactly, as the evolution loop produces them.
+
+`mutation_children` draws offline-mutation children (funsearch/llm.py
+`MutationClient`, the LLM stand-in of the config-3 runs) of the reference and
+seed programs; `measure_native` times them through the MI355X native backend
+(JIT compile + k_replay_native) -- the number to compare with the reference's
+program evals/s (15.84), next to the parametric headline."""
+
+from __future__ import annotations
+
+import random
+import time
+from typing import List
+
+from ..funsearch.llm import MutationClient
+from ..models.library import reference_policies, seed_policies
+from ..policy.compiler import CompiledPolicy, CompileError, compile_policy
+from ..policy.template import PolicyTemplate
+
+
+def mutation_children(n: int, seed: int = 0, device_only: bool = True) -> List[CompiledPolicy]:
+    client = MutationClient(seed)
+    parents = list(reference_policies().values()) + list(seed_policies().values())
+    out: List[CompiledPolicy] = []
+    seen = set()
+    rng = random.Random(seed)
+    tries = 0
+    while len(out) < n and tries < 50 * n:
+        tries += 1
+        pa = rng.sample(parents, 2)
+        prompt = PolicyTemplate.create_prompt_for_llm([(pa[0], 0.45), (pa[1], 0.44)], "feedback")
+        resp = client.chat.completions.create(model="m", messages=[{"role": "user", "content": prompt}])
+        code = PolicyTemplate.fill_template(resp.choices[0].message.content)
+        if code in seen:
+            continue
+        try:
+            p = compile_policy(code)
+        except CompileError:
+            continue
+        if device_only and not p.device_ok:
+            continue
+        seen.add(code)
+        out.append(p)
+        if rng.random() < 0.3:
+            parents.append(code)
+    return out
+
+
+def measure_native(dev, progs: List[CompiledPolicy]) -> dict:
+    """Evaluate `progs` natively twice: the first pass pays the JIT for every
+    new shape, the second finds them all cached (pure device time)."""
+    t0 = time.perf_counter()
+    batch = dev.submit_native(0, progs)
+    t1 = time.perf_counter()
+    tab = dev.wait(0)
+    t2 = time.perf_counter()
+    dev.submit_native(0, progs)
+    tab2 = dev.wait(0)
+    t3 = time.perf_counter()
+    n = len(progs)
+    return {"programs": n, "native": int(batch.ok.sum()), "new_shapes": int(batch.compiled),
+            "jit_s": round(t1 - t0, 3), "device_s": round(t2 - t1, 3),
+            "evals_per_s_incl_jit": round(n / (t2 - t0), 1), "evals_per_s_cached": round(n / (t3 - t2), 1),
+            "events": int(tab[:, 8].sum()), "repeat_identical": bool((tab == tab2).all())}

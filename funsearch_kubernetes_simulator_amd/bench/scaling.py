@@ -54,8 +54,10 @@ def summarize(results: dict) -> List[dict]:
             rows.append({"n_gpus": n, "value": None, "ms_per_step": None, "efficiency": None})
             continue
         eff = rec["value"] / (n * base["value"]) if base else None
+        cfg = rec.get("config", {})
         rows.append({"n_gpus": n, "value": rec["value"], "ms_per_step": rec["ms_per_step"],
-                     "efficiency": None if eff is None else round(eff, 4)})
+                     "efficiency": None if eff is None else round(eff, 4),
+                     "dist_backend": cfg.get("dist_backend"), "world_size": cfg.get("world_size")})
     return rows
 
 

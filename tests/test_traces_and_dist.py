@@ -127,10 +127,7 @@ def test_native_csv_loader_matches_python_parser():
         p.load_workload("gpu_models_filtered.csv", "openb_pod_list_multigpu20.csv", native=True)
 
 
-def test_island_search_survives_rank_loss(tmp_path):
-    """Rank 1 disappears mid-run (gloo, 2 ranks): rank 0's next collective
-    fails, it logs a rank_failure record, checkpoints and finishes alone;
-    a later --resume on one process picks the run up from rank 0's file."""
+def _rank_loss_config(tmp_path):
     ck = tmp_path / "ck"
     cfg = {"llm": {"backend": "mutation", "seed": 3}, "safe_execution": {"timeout_seconds": 3},
            "funsearch": {"population_size": 6, "generations": 4, "early_stop_threshold": 1.0, "elite_size": 3,
@@ -138,25 +135,41 @@ def test_island_search_survives_rank_loss(tmp_path):
            "islands": {"per_rank": 1, "migrate_every": 1, "migrants": 1},
            "device": {"kind": "cpu"}, "checkpoint": {"dir": str(ck), "every": 1}}
     (tmp_path / "cfg.json").write_text(json.dumps(cfg))
+    return ck
+
+
+def test_island_search_survives_rank_crash(tmp_path):
+    """Rank 1 is SIGKILLed mid-run (gloo, 2 ranks started directly with the
+    env:// rendezvous -- no torchrun agent, which would tear the whole group
+    down on a crash): rank 0's next collective fails, it logs a rank_failure
+    record, checkpoints and finishes alone; a later --resume on one process
+    picks the run up from rank 0's file."""
+    ck = _rank_loss_config(tmp_path)
     script = tmp_path / "w.py"
     script.write_text(
-        "import json, os, sys\n"
+        "import json, os, signal, sys\n"
         "from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch\n"
         f"fs = IslandFunSearch({str(tmp_path / 'cfg.json')!r})\n"
         "fs.initialize()\n"
         "for g in range(4):\n"
         "    if fs.ctx.rank == 1 and g == 2:\n"
-        "        sys.stdout.flush(); os._exit(0)\n"
+        "        sys.stdout.flush(); os.kill(os.getpid(), signal.SIGKILL)   # a real crash\n"
         "    fs.evolve()\n"
         "code, score = fs.global_best()\n"
         "print(json.dumps({'gen': fs.generation, 'world': fs.ctx.world_size, 'score': score,\n"
         "                  'failures': [f['collective'] for f in fs.failures]}))\n")
-    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1", FKS_DIST_TIMEOUT_S="60")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr", "127.0.0.1", "--master-port", str(31000 + os.getpid() % 1000), str(script)]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stderr[-3000:]
-    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    port = str(31000 + os.getpid() % 1000)
+    procs = []
+    for rank in (0, 1):
+        env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1", FKS_DIST_TIMEOUT_S="60", RANK=str(rank),
+                   LOCAL_RANK=str(rank), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    out0, err0 = procs[0].communicate(timeout=600)
+    procs[1].communicate(timeout=60)
+    assert procs[1].returncode == -9                       # killed by the signal, not a clean exit
+    assert procs[0].returncode == 0, err0[-3000:]
+    out = json.loads([l for l in out0.splitlines() if l.startswith("{")][-1])
     assert out["gen"] == 4 and out["world"] == 1 and len(out["failures"]) == 1
     assert out["score"] > 0.44
     st = json.loads((ck / "islands_rank0.json").read_text())
@@ -164,6 +177,39 @@ def test_island_search_survives_rank_loss(tmp_path):
     from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
     fs = IslandFunSearch(str(tmp_path / "cfg.json"))
     assert fs.load_elastic(str(ck)) and fs.generation == 4
+
+
+def test_torchrun_restart_resumes_after_rank_crash(tmp_path):
+    """Under torchrun a crashing rank (non-zero exit) makes the agent stop the
+    whole group, so in-process survival cannot happen there; the reachable
+    recovery is ``--max-restarts`` + elastic resume: the restarted group
+    reloads the per-rank checkpoints and finishes the run."""
+    ck = _rank_loss_config(tmp_path)
+    script = tmp_path / "w.py"
+    script.write_text(
+        "import json, os, sys\n"
+        "from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch\n"
+        f"fs = IslandFunSearch({str(tmp_path / 'cfg.json')!r})\n"
+        f"if not fs.load_elastic({str(ck)!r}):\n"
+        "    fs.initialize()\n"
+        "first = os.environ.get('TORCHELASTIC_RESTART_COUNT', '0') == '0'\n"
+        "while fs.generation < 4:\n"
+        "    if first and fs.ctx.rank == 1 and fs.generation == 2:\n"
+        "        sys.stdout.flush(); os._exit(3)   # crash on the first attempt only\n"
+        "    fs.evolve()\n"
+        "code, score = fs.global_best()\n"
+        "print(json.dumps({'gen': fs.generation, 'world': fs.ctx.world_size, 'score': score,\n"
+        "                  'restart': os.environ.get('TORCHELASTIC_RESTART_COUNT')}))\n")
+    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1", FKS_DIST_TIMEOUT_S="60")
+    # dynamic (c10d) rendezvous: every restart round re-forms the group on a fresh store prefix
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--max-restarts=1",
+           "--rdzv-backend=c10d", f"--rdzv-endpoint=127.0.0.1:{33000 + os.getpid() % 1000}", str(script)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    import re
+    outs = [json.loads(m) for m in re.findall(r"\{[^{}]*\}", r.stdout)]   # the two ranks' lines may interleave
+    assert outs and all(o["gen"] == 4 and o["world"] == 2 and o["restart"] == "1" for o in outs)
+    assert max(o["score"] for o in outs) > 0.44
 
 
 def test_scaling_harness_cpu():

@@ -12,7 +12,6 @@ evals/s on the same programs, and a bit-exactness check of every row.
 import argparse
 import json
 import os
-import random
 import sys
 import time
 
@@ -20,37 +19,13 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+from funsearch_kubernetes_simulator_amd.bench.programs import mutation_children  # noqa: E402
 from funsearch_kubernetes_simulator_amd.core import load_default_workload  # noqa: E402
-from funsearch_kubernetes_simulator_amd.funsearch.llm import MutationClient  # noqa: E402
-from funsearch_kubernetes_simulator_amd.models.library import reference_policies, seed_policies  # noqa: E402
 from funsearch_kubernetes_simulator_amd.ops import cpu_engine as ce  # noqa: E402
-from funsearch_kubernetes_simulator_amd.policy.compiler import CompileError, compile_policy  # noqa: E402
-from funsearch_kubernetes_simulator_amd.policy.template import PolicyTemplate  # noqa: E402
 
 
 def children(n, seed):
-    client = MutationClient(seed)
-    parents = list(reference_policies().values()) + list(seed_policies().values())
-    out, seen = [], set()
-    rng = random.Random(seed)
-    while len(out) < n:
-        pa = rng.sample(parents, 2)
-        prompt = PolicyTemplate.create_prompt_for_llm([(pa[0], 0.45), (pa[1], 0.44)], "feedback")
-        body = client.chat.completions.create(model="m", messages=[{"role": "user", "content": prompt}]).choices[0].message.content
-        code = PolicyTemplate.fill_template(body)
-        if code in seen:
-            continue
-        try:
-            p = compile_policy(code)
-        except CompileError:
-            continue
-        if not p.device_ok:
-            continue
-        seen.add(code)
-        out.append(p)
-        if rng.random() < 0.3:
-            parents.append(code)
-    return out
+    return mutation_children(n, seed)
 
 
 def main():
