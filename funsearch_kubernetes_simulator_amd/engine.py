@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import copy
 import os
+import time
 from concurrent.futures import ProcessPoolExecutor
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
@@ -197,9 +198,6 @@ class Evaluator:
         else:
             self._done[slot] = self.evaluate_family(family, weights)
 
-    def ready(self, slot: int) -> bool:
-        return self.device.ready(slot) if self.device is not None else True
-
     def wait(self, slot: int) -> np.ndarray:
         return self.device.wait(slot) if self.device is not None else self._done.pop(slot)
 
@@ -212,19 +210,29 @@ class Evaluator:
 
     # -- programs ---------------------------------------------------------------------
     def evaluate_programs(self, codes: Sequence[str]) -> List[EvalResult]:
-        n = len(codes)
-        out: List[Optional[EvalResult]] = [None] * n
         compiled: List[Optional[CompiledPolicy]] = []
         for c in codes:
             prog, err = try_compile(c)
             if prog is None:
                 self.stats["compile_errors"] += 1
             compiled.append(prog)
+        out = self._evaluate_compiled(list(codes), compiled, native=self.native)
+        if self.fault_rate > 0:
+            for i in range(len(out)):
+                if self._fault_rng.random() < self.fault_rate:
+                    out[i] = EvalResult(0.0, int(Exc.VALUE), "fault-injection")
+                    self.stats["faults"] = self.stats.get("faults", 0) + 1
+        return out
+
+    def _evaluate_compiled(self, codes: Sequence[str], compiled: List[Optional[CompiledPolicy]],
+                           native: bool) -> List[EvalResult]:
+        n = len(codes)
+        out: List[Optional[EvalResult]] = [None] * n
         # 1) device: native code, then the bytecode VM
         pending = [i for i, p in enumerate(compiled) if p is not None]
         if self.device is not None:
             dev_idx = [i for i in pending if compiled[i].device_ok]
-            if dev_idx and self.native:
+            if dev_idx and native:
                 self._absorb_native(dev_idx, compiled, out, 0)
             dev_idx = [i for i in dev_idx if out[i] is None]
             if len(dev_idx) >= self.device_min_batch:
@@ -261,6 +269,59 @@ class Evaluator:
             for i, r in zip(rest, results):
                 out[i] = r
                 self.stats["object"] += 1
+        return out  # type: ignore[return-value]
+
+    # -- asynchronous program batches (pipelined islands) ------------------------------
+    def submit_programs(self, codes: Sequence[str], slot: int) -> "PendingPrograms":
+        """Start evaluating `codes` on device slot `slot` (its own HIP stream):
+        compiles to bytecode and, on a device, JIT-compiles the native shapes and
+        launches them; returns at once.  `ready` / `collect` finish the batch
+        (programs the native backend declines run on the next engine at collect
+        time).  Without a device everything happens at collect time."""
+        pend = PendingPrograms(list(codes), slot)
+        pend.compiled = []
+        for c in pend.codes:
+            prog, _ = try_compile(c)
+            if prog is None:
+                self.stats["compile_errors"] += 1
+            pend.compiled.append(prog)
+        if self.device is not None and self.native:
+            idx = [i for i, p in enumerate(pend.compiled) if p is not None and p.device_ok]
+            if idx:
+                t0 = time.perf_counter()
+                batch = self.device.submit_native(slot, [pend.compiled[i] for i in idx])
+                pend.jit_s = batch.compile_s
+                pend.new_shapes = batch.compiled
+                pend.native_idx = idx
+                pend.t_launch = time.perf_counter()
+                self.stats["jit_s"] += batch.compile_s
+                self.stats["jit_shapes"] += batch.compiled
+                pend.submit_s = pend.t_launch - t0
+        return pend
+
+    def ready(self, pend) -> bool:
+        """Slot index (family batches) or `PendingPrograms`: finished?"""
+        if isinstance(pend, int):
+            return self.device.ready(pend) if self.device is not None else True
+        return not pend.native_idx or self.device.ready(pend.slot)
+
+    def collect(self, pend: "PendingPrograms") -> List[EvalResult]:
+        n = len(pend.codes)
+        out: List[Optional[EvalResult]] = [None] * n
+        if pend.native_idx:
+            tab = self.device.wait(pend.slot)
+            pend.t_done = time.perf_counter()
+            for row, i in zip(tab, pend.native_idx):
+                if int(row[COLS["exc"]]) in (Exc.UNSUPPORTED, Exc.BUDGET) or row[COLS["inexact"]]:
+                    continue
+                out[i] = _row_to_result(row, "hip-native")
+                self.stats["device_native"] += 1
+        rest = [i for i in range(n) if out[i] is None]
+        if rest:
+            sub = self._evaluate_compiled([pend.codes[i] for i in rest], [pend.compiled[i] for i in rest],
+                                          native=False)
+            for i, r in zip(rest, sub):
+                out[i] = r
         if self.fault_rate > 0:
             for i in range(n):
                 if self._fault_rng.random() < self.fault_rate:
@@ -287,6 +348,20 @@ class Evaluator:
 
     def scores(self, codes: Sequence[str]) -> List[float]:
         return [r.score for r in self.evaluate_programs(codes)]
+
+
+@dataclass
+class PendingPrograms:
+    """A program batch in flight on one device slot (`Evaluator.submit_programs`)."""
+    codes: List[str]
+    slot: int
+    compiled: List[Optional[CompiledPolicy]] = field(default_factory=list)
+    native_idx: List[int] = field(default_factory=list)
+    jit_s: float = 0.0
+    submit_s: float = 0.0
+    new_shapes: int = 0
+    t_launch: float = 0.0
+    t_done: float = 0.0
 
 
 _default: Dict[str, Evaluator] = {}

@@ -54,6 +54,10 @@ class IslandFunSearch:
         self.migrate_every = int(isl.get("migrate_every", 50))
         self.n_migrants = int(isl.get("migrants", 2))
         self.elastic = bool(isl.get("elastic", True))
+        # islands step independently (LLM / JIT / device stages overlap across islands)
+        self.pipeline = bool(isl.get("pipeline", False))
+        self.generation_base = 0
+        self._last_migration = 0
         self.failures: List[dict] = []
         dev = (self.config.get("device") or {}).get("kind", "auto")
         if dev == "auto" and self.ctx.backend == "nccl":
@@ -197,6 +201,171 @@ class IslandFunSearch:
                         s.best_score, s.best_policy = score, code
             s.population = sorted(s.population, key=lambda x: x[1], reverse=True)[:s.population_size]
 
+    # -- pipelined generations ---------------------------------------
+    def _plan(self, s: SimpleFunSearch):
+        s.population.sort(key=lambda x: x[1], reverse=True)
+        elites = s.population[:s.elite_size]
+        n_new = max(0, min(s.policies_per_generation, s.population_size - len(elites)))
+        return elites, n_new
+
+    def _merge(self, s: SimpleFunSearch, elites, children: List[str], results) -> None:
+        new = []
+        for code, res in zip(children, results):
+            if s._is_too_similar(code, res.score):
+                continue
+            new.append((code, res.score))
+            if res.score > s.best_score:
+                s.best_score, s.best_policy = res.score, code
+        s.population = sorted(elites + new, key=lambda x: x[1], reverse=True)[:s.population_size]
+
+    def run_pipelined(self, generations: int, threshold: float) -> None:
+        """Every island runs its own generation loop -- LLM requests (thread
+        pool), JIT compile + device launch on the island's own HIP stream,
+        merge -- so one island's LLM round trips and compiles overlap the other
+        islands' device replays instead of the whole rank waiting on each stage
+        in turn.  Each island's generation g+1 still samples from its own
+        generation-g population (per-island semantics of `evolve`); islands
+        meet only at migration points and at the end.  The JSONL log gets one
+        ``island_generation`` record per island step (llm_s / jit_s / eval_s
+        wall intervals) and one ``generation`` record per completed global
+        generation (with the device-busy fraction of the wall time)."""
+        k = len(self.islands)
+        stop = [False]
+        target = self.generation + generations
+        gen = [self.generation] * k
+        phase = ["idle"] * k
+        fut: List[object] = [None] * k
+        plan: List[object] = [None] * k
+        stamp = [dict() for _ in range(k)]
+        done_children = {}
+        workers = max(2, min(64, sum(s.max_workers for s in self.islands) + k))
+        busy_since = [None]
+        busy_total = [0.0]
+        t_start = time.time()
+        inflight = [False] * k
+        global_rec = {}   # generation -> partial aggregate
+
+        def set_busy():
+            now = time.time()
+            any_on = any(inflight)
+            if any_on and busy_since[0] is None:
+                busy_since[0] = now
+            elif not any_on and busy_since[0] is not None:
+                busy_total[0] += now - busy_since[0]
+                busy_since[0] = None
+
+        def gen_children(i):
+            s = self.islands[i]
+            elites, n_new = plan[i]
+            if not elites or n_new == 0:
+                return []
+            with concurrent.futures.ThreadPoolExecutor(max_workers=max(1, min(n_new, s.max_workers))) as ex:
+                outs = list(ex.map(lambda j: s._generate_single_policy(j, elites, FEEDBACK), range(n_new)))
+            return [code for _, code in outs if code]
+
+        def launch(i, children):
+            return self.evaluator.submit_programs(children, slot=i % max(1, self._n_slots()))
+
+        with concurrent.futures.ThreadPoolExecutor(max_workers=workers) as pool:
+            while True:
+                progressed = False
+                at_barrier = self.migrate_every and all(
+                    phase[i] == "idle" and gen[i] % self.migrate_every == 0 and gen[i] > self.generation_base
+                    for i in range(k)) and len(set(gen)) == 1 and gen[0] != self._last_migration
+                if at_barrier:
+                    with roctx_range(f"funsearch.migrate gen {gen[0]}"):
+                        self._collective("migrate", self.migrate, None)
+                    self._last_migration = gen[0]
+                for i in range(k):
+                    s = self.islands[i]
+                    if phase[i] == "idle":
+                        if gen[i] >= target or stop[0]:
+                            continue
+                        if (self.migrate_every and gen[i] % self.migrate_every == 0 and gen[i] > self.generation_base
+                                and gen[i] != self._last_migration):
+                            continue   # wait for the others at the migration point
+                        s.generation += 1
+                        plan[i] = self._plan(s)
+                        stamp[i] = {"t0": time.time()}
+                        fut[i] = pool.submit(gen_children, i)
+                        phase[i] = "llm"
+                        progressed = True
+                    elif phase[i] == "llm" and fut[i].done():
+                        children = fut[i].result()
+                        stamp[i]["t_llm"] = time.time()
+                        done_children[i] = children
+                        fut[i] = pool.submit(launch, i, children)
+                        phase[i] = "launch"
+                        progressed = True
+                    elif phase[i] == "launch" and fut[i].done():
+                        fut[i] = fut[i].result()        # PendingPrograms
+                        stamp[i]["t_launch"] = time.time()
+                        inflight[i] = bool(fut[i].native_idx)
+                        set_busy()
+                        phase[i] = "eval"
+                        progressed = True
+                    elif phase[i] == "eval" and self.evaluator.ready(fut[i]):
+                        pend = fut[i]
+                        results = self.evaluator.collect(pend)
+                        inflight[i] = False
+                        set_busy()
+                        t_end = time.time()
+                        children = done_children.pop(i)
+                        self._merge(s, plan[i][0], children, results)
+                        self.evaluations += len(children)
+                        gen[i] += 1
+                        st = stamp[i]
+                        rec = dict(kind="island_generation", rank=self.ctx.rank, island=i, generation=gen[i],
+                                   children=len(children), best=round(s.best_score, 6),
+                                   llm_s=round(st["t_llm"] - st["t0"], 4), jit_s=round(pend.jit_s, 4),
+                                   eval_s=round(t_end - st["t_launch"], 4), wall_s=round(t_end - st["t0"], 4),
+                                   new_shapes=pend.new_shapes, t0=round(st["t0"] - t_start, 4),
+                                   t_end=round(t_end - t_start, 4))
+                        self.log.write(**rec)
+                        agg = global_rec.setdefault(gen[i], {"children": 0, "islands": 0, "llm_s": 0.0, "jit_s": 0.0,
+                                                             "eval_s": 0.0, "t0": st["t0"]})
+                        agg["children"] += len(children)
+                        agg["islands"] += 1
+                        agg["llm_s"] += rec["llm_s"]
+                        agg["jit_s"] += rec["jit_s"]
+                        agg["eval_s"] += rec["eval_s"]
+                        agg["t0"] = min(agg["t0"], st["t0"])
+                        if agg["islands"] == k:
+                            self._finish_generation(gen[i], global_rec.pop(gen[i]), busy_total, busy_since,
+                                                    t_start, threshold, stop)
+                        phase[i] = "idle"
+                        progressed = True
+                if all(phase[i] == "idle" and (gen[i] >= target or stop[0]) for i in range(k)):
+                    break
+                if not progressed:
+                    time.sleep(0.0005)
+
+    def _n_slots(self) -> int:
+        dev = getattr(self.evaluator, "device", None)
+        return dev.n_slots if dev is not None else max(1, len(self.islands))
+
+    def _finish_generation(self, g: int, agg: dict, busy_total, busy_since, t_start: float, threshold: float,
+                           stop) -> None:
+        self.generation = g
+        best_local = self.best[1]
+        best_global = self._collective("all_reduce_max", lambda: dist.all_reduce_max(best_local), best_local)
+        now = time.time()
+        busy = busy_total[0] + (now - busy_since[0] if busy_since[0] is not None else 0.0)
+        wall = now - agg["t0"]
+        rec = dict(kind="generation", rank=self.ctx.rank, generation=g, best=best_local, best_global=best_global,
+                   children=agg["children"], islands=[round(s.best_score, 6) for s in self.islands],
+                   llm_s=round(agg["llm_s"], 4), jit_s=round(agg["jit_s"], 4), eval_s=round(agg["eval_s"], 4),
+                   wall_s=round(wall, 4), pipelined=True,
+                   device_busy=round(busy / max(1e-9, now - t_start), 4),
+                   evals_per_s=round(self.evaluations / max(1e-9, now - t_start), 2))
+        self.log.write(**rec)
+        if self.verbose and self.ctx.is_main:
+            print(json.dumps(rec), flush=True)
+        if self.ck_dir and self.ck_every and g % self.ck_every == 0:
+            self.save_checkpoint()
+        if best_global >= threshold:
+            stop[0] = True
+
     def run(self, generations: Optional[int] = None, resume: bool = False) -> Tuple[Optional[str], float]:
         if resume and self.ck_dir:
             self.load_elastic(self.ck_dir)
@@ -204,6 +373,11 @@ class IslandFunSearch:
         generations = generations or self.islands[0].max_generations
         threshold = self.islands[0].early_stop_threshold
         start = self.generation
+        if self.pipeline:
+            self.generation_base = start
+            self._last_migration = start
+            self.run_pipelined(generations, threshold)
+            return self.global_best()
         while self.generation - start < generations:
             rec = self.evolve()
             if self.verbose and self.ctx.is_main:

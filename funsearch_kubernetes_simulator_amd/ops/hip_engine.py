@@ -231,6 +231,14 @@ class DeviceEvaluator:
             self._eng.submit_native(slot, batch.fn[idx], batch.kc, batch.koff[idx])
         return batch
 
+    def profile_native(self, progs: Sequence[CompiledPolicy]):
+        """s_memtime phase-profiled native launch: (table [P, 13], cycles [P, 8] by
+        PHASES + ("pop_loads",)); programs must all be native-compilable."""
+        batch = self.native_compiler.prepare(progs)
+        if not batch.ok.all():
+            raise ValueError(f"not native: {batch.reasons}")
+        return self._eng.profile_native(batch.fn, batch.kc, batch.koff)
+
     def evaluate_native(self, progs: Sequence[CompiledPolicy]) -> np.ndarray:
         if not progs:
             return np.zeros((0, len(RESULT_COLUMNS)))

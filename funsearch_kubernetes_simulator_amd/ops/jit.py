@@ -201,37 +201,63 @@ class NativeCompiler:
         self._bad: Dict[str, str] = {}                  # shape -> reason it is not native
         self._modules: List[CompiledModule] = []
         self._lock = threading.Lock()
+        self._inflight: Dict[str, threading.Event] = {}
+        self._procs = threading.BoundedSemaphore(self.workers)
         self.stats = {"modules": 0, "shapes": 0, "compile_s": 0.0, "rejected": 0, "hits": 0}
 
     def prepare(self, progs: Sequence[CompiledPolicy]) -> NativeBatch:
+        """Compile every shape of `progs` not compiled yet (thread-safe: islands
+        call this concurrently; a shape another thread is compiling is waited
+        for, not compiled twice) and build the batch's launch data."""
         keys = [shape_key(p) for p in progs]
-        new: Dict[str, CompiledPolicy] = {}
-        for k, p in zip(keys, progs):
-            if k not in self._shapes and k not in self._bad and k not in new:
-                new[k] = p
+        mine: Dict[str, CompiledPolicy] = {}
+        others = []
+        with self._lock:
+            for k, p in zip(keys, progs):
+                if k in self._shapes or k in self._bad or k in mine:
+                    continue
+                ev = self._inflight.get(k)
+                if ev is not None:
+                    others.append(ev)
+                else:
+                    mine[k] = p
+            for k in mine:
+                self._inflight[k] = threading.Event()
         t0 = time.perf_counter()
-        if new:
-            self._compile_shapes(new)
+        try:
+            if mine:
+                self._compile_shapes(mine)
+        finally:
+            with self._lock:
+                for k in mine:
+                    self._inflight.pop(k).set()
+        for ev in others:
+            ev.wait()
         dt = time.perf_counter() - t0
         P = len(progs)
         fn = np.zeros(P, dtype=np.uint64)
         ok = np.zeros(P, dtype=bool)
         koff = np.zeros(P, dtype=np.int32)
         blocks, pos, reasons = [], 0, {}
-        for i, (k, p) in enumerate(zip(keys, progs)):
-            kb = constant_block(p, self.budget)
-            koff[i] = pos
-            blocks.append(kb)
-            pos += len(kb)
-            if k in self._shapes:
-                mi, pi_ = self._shapes[k]
-                fn[i] = self._modules[mi].pointers[pi_]
-                ok[i] = True
-            else:
-                reasons[i] = self._bad.get(k, "not compiled")
-        self.stats["hits"] += P - len(new)
+        with self._lock:
+            for i, (k, p) in enumerate(zip(keys, progs)):
+                kb = constant_block(p, self.budget)
+                koff[i] = pos
+                blocks.append(kb)
+                pos += len(kb)
+                if k in self._shapes:
+                    mi, pi_ = self._shapes[k]
+                    fn[i] = self._modules[mi].pointers[pi_]
+                    ok[i] = True
+                else:
+                    reasons[i] = self._bad.get(k, "not compiled")
+            self.stats["hits"] += P - len(mine)
         return NativeBatch(fn, np.concatenate(blocks) if blocks else np.zeros(1, np.int64), koff, ok, reasons, dt,
-                           len(new))
+                           len(mine))
+
+    def _compile_one(self, chunk) -> CompiledModule:
+        with self._procs:   # bounds concurrent toolchain processes across all callers
+            return compile_device_module([p for _, p in chunk])
 
     def _compile_shapes(self, new: Dict[str, CompiledPolicy]) -> None:
         items = list(new.items())
@@ -242,31 +268,33 @@ class NativeCompiler:
                 module_source([p], with_probes=False)
                 good.append((k, p))
             except CodegenError as exc:
-                self._bad[k] = f"codegen: {exc}"
-                self.stats["rejected"] += 1
+                with self._lock:
+                    self._bad[k] = f"codegen: {exc}"
+                    self.stats["rejected"] += 1
         if not good:
             return
         n_chunks = max(1, min(self.workers, len(good)))
         size = max(1, min(self.max_chunk, math.ceil(len(good) / n_chunks)))
         chunks = [good[i:i + size] for i in range(0, len(good), size)]
         with ThreadPoolExecutor(max_workers=min(self.workers, len(chunks))) as ex:
-            mods = list(ex.map(lambda ch: compile_device_module([p for _, p in ch]), chunks))
+            mods = list(ex.map(self._compile_one, chunks))
         for ch, mod in zip(chunks, mods):
-            self.stats["compile_s"] += mod.compile_s
             mod.handle = self._hip.JitModule(mod.image, self._rt, mod.n, self.device)
             mod.pointers = np.asarray(mod.handle.pointers(), dtype=np.uint64)
-            mi = len(self._modules)
-            self._modules.append(mod)
-            self.stats["modules"] += 1
-            for j, (k, _) in enumerate(ch):
-                res = mod.resources[j]
-                why = "no resource record" if res is None else res.fits(self.vgpr_cap, self.sgpr_cap)
-                if why:
-                    self._bad[k] = why
-                    self.stats["rejected"] += 1
-                else:
-                    self._shapes[k] = (mi, j)
-                    self.stats["shapes"] += 1
+            with self._lock:
+                self.stats["compile_s"] += mod.compile_s
+                mi = len(self._modules)
+                self._modules.append(mod)
+                self.stats["modules"] += 1
+                for j, (k, _) in enumerate(ch):
+                    res = mod.resources[j]
+                    why = "no resource record" if res is None else res.fits(self.vgpr_cap, self.sgpr_cap)
+                    if why:
+                        self._bad[k] = why
+                        self.stats["rejected"] += 1
+                    else:
+                        self._shapes[k] = (mi, j)
+                        self.stats["shapes"] += 1
 
 
 def _default_workers() -> int:

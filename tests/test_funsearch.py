@@ -261,3 +261,40 @@ def test_cli_elastic_resume_changes_island_count(tmp_path):
     assert out["generations"] == 3 and out["islands_per_rank"] == 3
     assert out["best_score"] >= reference_scores()["best_fit"]
     assert len(json.loads((tmp_path / "ck" / "islands_rank0.json").read_text())["islands"]) == 3
+
+
+def test_pipelined_islands_match_lockstep_with_one_worker(tmp_path):
+    """Pipelined islands (each island steps on its own; LLM / JIT / device
+    stages overlap across islands) keep every island's per-generation
+    semantics: with one LLM worker (deterministic request order) and one
+    island the populations equal the lock-step `evolve` loop's."""
+    from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
+    pops = []
+    for pipe in (False, True):
+        cfg = _cfg(tmp_path, max_workers=1)
+        cfg["islands"] = {"per_rank": 1, "migrate_every": 0, "migrants": 1, "pipeline": pipe}
+        cfg["log_path"] = str(tmp_path / f"log{int(pipe)}.jsonl")
+        cfg["checkpoint"] = {}
+        fs = IslandFunSearch(cfg)
+        fs.run(3)
+        assert fs.generation == 3
+        pops.append([(c, s) for c, s in fs.islands[0].population])
+    assert pops[0] == pops[1]
+    recs = [json.loads(l) for l in open(tmp_path / "log1.jsonl")]
+    kinds = {r["kind"] for r in recs}
+    assert {"island_generation", "generation"} <= kinds
+    g = [r for r in recs if r["kind"] == "generation"]
+    assert [r["generation"] for r in g] == [1, 2, 3] and all("device_busy" in r for r in g)
+
+
+def test_pipelined_islands_migrate_at_barrier(tmp_path):
+    from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
+    cfg = _cfg(tmp_path)
+    cfg["islands"] = {"per_rank": 3, "migrate_every": 2, "migrants": 1, "pipeline": True}
+    cfg["checkpoint"] = {"dir": str(tmp_path / "ck"), "every": 2}
+    fs = IslandFunSearch(cfg)
+    code, score = fs.run(4)
+    assert fs.generation == 4 and score >= reference_scores()["best_fit"]
+    recs = [json.loads(l) for l in open(tmp_path / "log.jsonl")]
+    assert len([r for r in recs if r["kind"] == "island_generation"]) == 12
+    assert (tmp_path / "ck" / "islands_rank0.json").exists()

@@ -1,0 +1,45 @@
+"""s_memtime phase split of the native-program replay kernel (latency regime:
+a few dozen programs, one wave each).  Prints cycles per event by phase.
+
+    python tools/native_phase.py --programs 48
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from funsearch_kubernetes_simulator_amd.bench.programs import mutation_children  # noqa: E402
+from funsearch_kubernetes_simulator_amd.core import load_default_workload  # noqa: E402
+from funsearch_kubernetes_simulator_amd.models.library import reference_policies  # noqa: E402
+from funsearch_kubernetes_simulator_amd.policy.compiler import compile_policy  # noqa: E402
+
+PH = ("pop", "delete", "score", "fail", "commit", "eval", "pop_loads")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--programs", type=int, default=48)
+    ap.add_argument("--heap-mode", default="lds")
+    a = ap.parse_args()
+    from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
+    dev = he.DeviceEvaluator(load_default_workload(), options={"heap_mode": a.heap_mode})
+    sets = {"first_fit": [compile_policy(reference_policies()["first_fit"])],
+            "funsearch_4901": [compile_policy(reference_policies()["funsearch_4901"])],
+            "children": mutation_children(a.programs, 0)}
+    for name, progs in sets.items():
+        dev.profile_native(progs)   # compile + warm
+        tab, prof = dev.profile_native(progs)
+        ev = float(tab[:, 8].sum())
+        tot = prof[:, :7].sum()
+        print(json.dumps({"set": name, "P": len(progs), "events": int(ev),
+                          "cycles_per_event": round(float(tot) / ev, 1),
+                          "phases_per_event": {PH[i]: round(float(prof[:, i].sum()) / ev, 1) for i in range(7)}}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
