@@ -271,6 +271,30 @@ class Evaluator:
                 self.stats["object"] += 1
         return out  # type: ignore[return-value]
 
+    def score_compiled(self, progs: Sequence[CompiledPolicy], slot: int = 0) -> np.ndarray:
+        """Scores of already-compiled programs (e.g. constant variants of one
+        shape, funsearch/polish.py): one native device launch when a device is
+        attached (programs it declines fall back to the CPU VM), else the CPU VM."""
+        out = np.zeros(len(progs))
+        rest = list(range(len(progs)))
+        if self.device is not None and self.native and progs:
+            self.device.submit_native(slot, progs)
+            tab = self.device.wait(slot)
+            ok = (tab[:, COLS["exc"]] != Exc.UNSUPPORTED) & (tab[:, COLS["exc"]] != Exc.BUDGET) \
+                & (tab[:, COLS["inexact"]] == 0)
+            out[ok] = tab[ok, COLS["score"]]
+            rest = [i for i in range(len(progs)) if not ok[i]]
+            self.stats["device_native"] += int(ok.sum())
+        if rest:
+            from .ops import cpu_engine
+            tab = cpu_engine.simulate_program_batch(self.workload, [progs[i] for i in rest],
+                                                    cpu_engine.SimOptions(**self._cpu_opts()), self.cpu_threads)
+            for row, i in zip(tab, rest):
+                exc = int(row[COLS["exc"]])
+                out[i] = 0.0 if exc else row[COLS["score"]]
+            self.stats["cpu_vm"] += len(rest)
+        return out
+
     # -- asynchronous program batches (pipelined islands) ------------------------------
     def submit_programs(self, codes: Sequence[str], slot: int) -> "PendingPrograms":
         """Start evaluating `codes` on device slot `slot` (its own HIP stream):

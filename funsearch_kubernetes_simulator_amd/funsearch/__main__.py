@@ -52,7 +52,8 @@ def main() -> None:
         if a.save:
             best_isl.save_top_policies(5, a.save)
         print(json.dumps({"best_score": score, "generations": run.generation, "evaluations": run.evaluations,
-                          "ranks": run.ctx.world_size, "islands_per_rank": run.n_islands}))
+                          "ranks": run.ctx.world_size, "islands_per_rank": run.n_islands,
+                          "engine_stats": run.evaluator.stats}))
     dist.shutdown()
 
 

@@ -54,6 +54,12 @@ class IslandFunSearch:
         self.migrate_every = int(isl.get("migrate_every", 50))
         self.n_migrants = int(isl.get("migrants", 2))
         self.elastic = bool(isl.get("elastic", True))
+        # constant polish of island champions on the device (funsearch/polish.py)
+        pol = self.config.get("polish") or {}
+        self.polish_every = int(pol.get("every", 0))
+        self.polish_variants = int(pol.get("variants", 1024))
+        self.polish_rounds = int(pol.get("rounds", 3))
+        self._polished = set()
         # islands step independently (LLM / JIT / device stages overlap across islands)
         self.pipeline = bool(isl.get("pipeline", False))
         self.generation_base = 0
@@ -71,7 +77,8 @@ class IslandFunSearch:
             opts["fault_seed"] = int(fi.get("seed", 0))
         if fi.get("llm_failure_rate"):
             self.config.setdefault("llm", {})["fault_rate"] = float(fi["llm_failure_rate"])
-        self.evaluator = evaluator or Evaluator(device=dev, options=opts)
+        # one HIP stream (slot) per island, so pipelined islands never share one
+        self.evaluator = evaluator or Evaluator(device=dev, options=opts, n_slots=max(4, self.n_islands))
         llm_cfg = dict(self.config.get("llm") or {})
         base_seed = int(llm_cfg.get("seed", 0)) + 1000003 * self.ctx.rank
         self.islands: List[SimpleFunSearch] = []
@@ -141,6 +148,8 @@ class IslandFunSearch:
                 if res.score > s.best_score:
                     s.best_score, s.best_policy = res.score, code
             s.population = sorted(elites + new, key=lambda x: x[1], reverse=True)[:s.population_size]
+        for i in range(len(self.islands)):
+            self.maybe_polish(i)
         if self.migrate_every and self.generation % self.migrate_every == 0:
             with roctx_range(f"funsearch.migrate gen {self.generation}"):
                 self._collective("migrate", self.migrate, None)
@@ -217,6 +226,39 @@ class IslandFunSearch:
             if res.score > s.best_score:
                 s.best_score, s.best_policy = res.score, code
         s.population = sorted(elites + new, key=lambda x: x[1], reverse=True)[:s.population_size]
+
+    def maybe_polish(self, i: int) -> Optional[dict]:
+        """Every ``polish.every`` generations: tune the numeric literals of island
+        i's best program with one batched device search (thousands of constant
+        settings, one JIT compile), re-score the rewritten text through the normal
+        evaluation path, and put it into the population if it is better."""
+        s = self.islands[i]
+        if not self.polish_every or s.generation % self.polish_every or not s.population:
+            return None
+        code, score = max(s.population, key=lambda x: x[1])
+        if code in self._polished:
+            return None
+        self._polished.add(code)
+        from .polish import polish
+        slot = i % max(1, self._n_slots())
+        t0 = time.time()
+        res = polish(lambda progs: self.evaluator.score_compiled(progs, slot), code, base_score=score,
+                     variants=self.polish_variants, rounds=self.polish_rounds,
+                     seed=hash((self.ctx.rank, i, s.generation)) & 0xFFFF)
+        rec = dict(kind="polish", rank=self.ctx.rank, island=i, generation=s.generation, base=score,
+                   polished=res.score, evaluated=res.evaluated, seconds=round(time.time() - t0, 3))
+        if res.improved:
+            exact = self.evaluator.evaluate_programs([res.code])[0]   # the rewritten TEXT, normal path
+            rec["rescored"] = exact.score
+            if exact.score > score and res.code not in {c for c, _ in s.population}:
+                s.population = sorted(s.population + [(res.code, exact.score)], key=lambda x: x[1],
+                                      reverse=True)[:s.population_size]
+                if exact.score > s.best_score:
+                    s.best_score, s.best_policy = exact.score, res.code
+                self._polished.add(res.code)
+        self.evaluations += res.evaluated
+        self.log.write(**rec)
+        return rec
 
     def run_pipelined(self, generations: int, threshold: float) -> None:
         """Every island runs its own generation loop -- LLM requests (thread
@@ -314,6 +356,7 @@ class IslandFunSearch:
                         self._merge(s, plan[i][0], children, results)
                         self.evaluations += len(children)
                         gen[i] += 1
+                        self.maybe_polish(i)
                         st = stamp[i]
                         rec = dict(kind="island_generation", rank=self.ctx.rank, island=i, generation=gen[i],
                                    children=len(children), best=round(s.best_score, 6),
@@ -357,7 +400,9 @@ class IslandFunSearch:
                    llm_s=round(agg["llm_s"], 4), jit_s=round(agg["jit_s"], 4), eval_s=round(agg["eval_s"], 4),
                    wall_s=round(wall, 4), pipelined=True,
                    device_busy=round(busy / max(1e-9, now - t_start), 4),
-                   evals_per_s=round(self.evaluations / max(1e-9, now - t_start), 2))
+                   evals_per_s=round(self.evaluations / max(1e-9, now - t_start), 2),
+                   engines={k: v for k, v in self.evaluator.stats.items() if k in
+                            ("device_native", "device", "cpu_vm", "object", "compile_errors", "jit_shapes")})
         self.log.write(**rec)
         if self.verbose and self.ctx.is_main:
             print(json.dumps(rec), flush=True)

@@ -76,6 +76,8 @@ class CompiledPolicy:
     nregs: int
     source: str
     features: frozenset = field(default_factory=frozenset)
+    #: numeric source literals: (pool index, line, col, end line, end col)
+    literals: list = field(default_factory=list)
 
     @property
     def n_insns(self) -> int:
@@ -106,6 +108,7 @@ class Compiler:
         self.source = source
         self.code: List[list] = []         # [op, d, a, b, imm]
         self.consts: Dict[Tuple[int, object], int] = {}
+        self.literals: List[Tuple[int, int, int, int, int]] = []   # (pool index, line, col, end line, end col)
         self.fconst: List[float] = []
         self.iconst: List[int] = []
         self.ctag: List[int] = []
@@ -143,7 +146,23 @@ class Compiler:
     def patch(self, at: int, target: int) -> None:
         self.code[at][4] = target
 
-    def const(self, value) -> int:
+    def const(self, value, literal: Optional[ast.Constant] = None) -> int:
+        """Pool index of a constant.  Compiler-made constants are shared by
+        value; every numeric *literal of the source* gets a pool entry of its own
+        (recorded in `literals` with its source span), so the constants a
+        program author wrote can be changed as data -- one compiled shape, many
+        weight settings (funsearch/polish.py) -- without touching the loop
+        counters and flags the compiler itself emits."""
+        if literal is not None and isinstance(value, (int, float)) and not isinstance(value, bool):
+            if isinstance(value, int) and not INT64_MIN <= value <= INT64_MAX:
+                raise CompileError("integer constant outside int64")
+            idx = len(self.ctag)
+            fl = isinstance(value, float)
+            self.ctag.append(TAG_FLOAT if fl else TAG_INT)
+            self.fconst.append(float(value) if fl else 0.0)
+            self.iconst.append(0 if fl else value)
+            self.literals.append((idx, literal.lineno, literal.col_offset, literal.end_lineno, literal.end_col_offset))
+            return idx
         if isinstance(value, bool):
             value = int(value)
         if isinstance(value, int):
@@ -161,9 +180,9 @@ class Compiler:
             self.iconst.append(value if key[0] == TAG_INT else 0)
         return self.consts[key]
 
-    def load_const(self, value, into: Optional[Val] = None) -> Val:
+    def load_const(self, value, into: Optional[Val] = None, literal: Optional[ast.Constant] = None) -> Val:
         v = into or self.tmp()
-        self.emit(Op.CONST, v.reg, imm=self.const(value))
+        self.emit(Op.CONST, v.reg, imm=self.const(value, literal))
         return v
 
     def raise_(self, exc: Exc) -> None:
@@ -211,7 +230,7 @@ class Compiler:
         self._renumber_registers()
         nregs = max((c[1] for c in self.code if c[1] != NO_REG), default=0) + 1
         return CompiledPolicy(b"".join(pack_insn(*c) for c in self.code), self.fconst, self.iconst,
-                              self.ctag, nregs, self.source, frozenset(self.features))
+                              self.ctag, nregs, self.source, frozenset(self.features), list(self.literals))
 
     #: ops whose `imm` field names a register (or NO_REG)
     _IMM_REG_OPS = (Op.GLIST_SLICE, Op.GLIST_INSERT)
@@ -786,7 +805,7 @@ class Compiler:
 
     def e_Constant(self, e: ast.Constant) -> Val:
         if isinstance(e.value, (bool, int, float)):
-            return self.load_const(e.value)
+            return self.load_const(e.value, literal=e)
         raise CompileError(f"unsupported constant {e.value!r}")
 
     def e_Name(self, e: ast.Name) -> Val:

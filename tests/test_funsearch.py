@@ -298,3 +298,21 @@ def test_pipelined_islands_migrate_at_barrier(tmp_path):
     recs = [json.loads(l) for l in open(tmp_path / "log.jsonl")]
     assert len([r for r in recs if r["kind"] == "island_generation"]) == 12
     assert (tmp_path / "ck" / "islands_rank0.json").exists()
+
+
+def test_islands_with_constant_polish(tmp_path):
+    """polish.every: island champions get a batched constant search; the
+    rewritten program enters the population only with its exact re-score."""
+    from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
+    cfg = _cfg(tmp_path)
+    cfg["islands"] = {"per_rank": 2, "migrate_every": 0, "migrants": 1, "pipeline": True}
+    cfg["polish"] = {"every": 1, "variants": 6, "rounds": 1}
+    cfg["checkpoint"] = {}
+    fs = IslandFunSearch(cfg)
+    fs.run(2)
+    recs = [json.loads(l) for l in open(tmp_path / "log.jsonl")]
+    pol = [r for r in recs if r["kind"] == "polish"]
+    assert pol and all(r["evaluated"] >= 6 for r in pol)
+    for r in pol:
+        if "rescored" in r:
+            assert r["rescored"] == r["polished"]
