@@ -209,14 +209,15 @@ class Evaluator:
         return opts
 
     # -- programs ---------------------------------------------------------------------
-    def evaluate_programs(self, codes: Sequence[str]) -> List[EvalResult]:
+    def evaluate_programs(self, codes: Sequence[str], slot: int = 0) -> List[EvalResult]:
+        """Scores of program texts (synchronous; device work on HIP slot `slot`)."""
         compiled: List[Optional[CompiledPolicy]] = []
         for c in codes:
             prog, err = try_compile(c)
             if prog is None:
                 self.stats["compile_errors"] += 1
             compiled.append(prog)
-        out = self._evaluate_compiled(list(codes), compiled, native=self.native)
+        out = self._evaluate_compiled(list(codes), compiled, native=self.native, slot=slot)
         if self.fault_rate > 0:
             for i in range(len(out)):
                 if self._fault_rng.random() < self.fault_rate:
@@ -225,7 +226,7 @@ class Evaluator:
         return out
 
     def _evaluate_compiled(self, codes: Sequence[str], compiled: List[Optional[CompiledPolicy]],
-                           native: bool) -> List[EvalResult]:
+                           native: bool, slot: int = 0) -> List[EvalResult]:
         n = len(codes)
         out: List[Optional[EvalResult]] = [None] * n
         # 1) device: native code, then the bytecode VM
@@ -233,7 +234,7 @@ class Evaluator:
         if self.device is not None:
             dev_idx = [i for i in pending if compiled[i].device_ok]
             if dev_idx and native:
-                self._absorb_native(dev_idx, compiled, out, 0)
+                self._absorb_native(dev_idx, compiled, out, slot)
             dev_idx = [i for i in dev_idx if out[i] is None]
             if len(dev_idx) >= self.device_min_batch:
                 tab = self.device.evaluate_programs([compiled[i] for i in dev_idx])

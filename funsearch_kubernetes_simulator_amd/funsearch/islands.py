@@ -248,7 +248,7 @@ class IslandFunSearch:
         rec = dict(kind="polish", rank=self.ctx.rank, island=i, generation=s.generation, base=score,
                    polished=res.score, evaluated=res.evaluated, seconds=round(time.time() - t0, 3))
         if res.improved:
-            exact = self.evaluator.evaluate_programs([res.code])[0]   # the rewritten TEXT, normal path
+            exact = self.evaluator.evaluate_programs([res.code], slot=slot)[0]   # the rewritten TEXT, normal path
             rec["rescored"] = exact.score
             if exact.score > score and res.code not in {c for c, _ in s.population}:
                 s.population = sorted(s.population + [(res.code, exact.score)], key=lambda x: x[1],
