@@ -100,7 +100,7 @@ void fill_row(double* row, const SimResult& r) {
 // device path (csrc/hip/jit_abi.h ProgFn), one call per node.
 typedef int64_t (*HostProgFn)(int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t,
                               int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t,
-                              int32_t, int32_t, const int64_t*, int32_t, int32_t, int32_t, int64_t, int32_t,
+                              int32_t, const int64_t*, int32_t, int32_t, int32_t, int64_t, int32_t,
                               const int64_t*);
 struct NativeHostScorer {
   HostProgFn fn;
@@ -115,7 +115,8 @@ struct NativeHostScorer {
     int32_t gl[8] = {0}, gt[8] = {0};
     for (int j = 0; j < ng; ++j) { gl[j] = c.s.gmilli_left[g0 + j]; gt[j] = w.gmilli_total[g0 + j]; }
     const int64_t r = fn((int32_t)c.s.cpu_left[n], (int32_t)w.cpu_total[n], (int32_t)c.s.mem_left[n],
-                         (int32_t)w.mem_total[n], c.s.gpu_left[n], w.ngpus[n], gl[0], gl[1], gl[2], gl[3], gl[4],
+                         (int32_t)w.mem_total[n],
+                         (int32_t)(((uint32_t)c.s.gpu_left[n] & 0xFFFFu) | ((uint32_t)w.ngpus[n] << 16)), gl[0], gl[1], gl[2], gl[3], gl[4],
                          gl[5], gl[6], gl[7], gt[0], gt[1], gt[2], gt[3], gt[4], gt[5], gt[6], gt[7],
                          gmem8->data() + (size_t)n * 8, (int32_t)w.pcpu[c.pod], (int32_t)w.pmem[c.pod],
                          w.pgmilli[c.pod] | (w.pngpu[c.pod] << 16), c.pod_ctime, (int32_t)w.pdur[c.pod], kc);

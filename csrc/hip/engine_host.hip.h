@@ -213,6 +213,11 @@ class DeviceEngine {
       if (m == "on" && !rows_ok_) throw std::invalid_argument("row kernel needs <= 16 nodes, <= 64 gpu_milli classes");
       row_mode_ = m;
     }
+    if (o.contains("native_rows")) {
+      const int r = o["native_rows"].cast<int>();
+      if (r < 0 || r > kRowsPerWave) throw std::invalid_argument("native_rows must be in [0, 4]");
+      native_rows_opt_ = r;
+    }
     if (o.contains("row_heap_top")) row_top_opt_ = o["row_heap_top"].cast<int>();   // -1: auto
     if (o.contains("row_wave_share")) {
       const double f = o["row_wave_share"].cast<double>();
@@ -280,6 +285,27 @@ class DeviceEngine {
   void submit_native(int slot, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> fn,
                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> kc,
                      py::array_t<int32_t, py::array::c_style | py::array::forcecast> koff) {
+    submit_native_impl(slot, fn, kc, koff, false);
+  }
+
+  // native programs on the s_memtime-profiled row kernel: (result table, [waves, 8] phase cycles)
+  py::tuple profile_native(py::array_t<uint64_t, py::array::c_style | py::array::forcecast> fn,
+                           py::array_t<int64_t, py::array::c_style | py::array::forcecast> kc,
+                           py::array_t<int32_t, py::array::c_style | py::array::forcecast> koff) {
+    if (!use_rows((int)fn.size())) throw std::invalid_argument("native profiling runs on the row kernel (<= 16 nodes)");
+    submit_native_impl(0, fn, kc, koff, true);
+    Slot& s = *slots_[0];
+    const int waves = last_native_waves_;
+    py::array_t<uint64_t> prof({(py::ssize_t)waves, (py::ssize_t)8});
+    HIP_OK(hipMemcpyAsync(prof.mutable_data(), s.prof.p, (size_t)waves * 64, hipMemcpyDeviceToHost, s.stream));
+    py::array_t<double> tab = wait(0);
+    HIP_OK(hipStreamSynchronize(s.stream));
+    return py::make_tuple(tab, prof);
+  }
+
+  void submit_native_impl(int slot, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> fn,
+                          py::array_t<int64_t, py::array::c_style | py::array::forcecast> kc,
+                          py::array_t<int32_t, py::array::c_style | py::array::forcecast> koff, bool profiled) {
     Slot& s = idle_slot(slot);
     const int P = (int)fn.size();
     if (P < 1) throw std::invalid_argument("empty batch");
@@ -303,6 +329,11 @@ class DeviceEngine {
     HIP_OK(hipStreamSynchronize(s.stream));   // kc is pageable: finish the copy while it is alive
     {
       py::gil_scoped_release rel;
+      if (use_rows(P)) {
+        launch_rows_native(s, P, fb, profiled);
+        finish(s);
+        return;
+      }
       const bool g = use_gheap_native(P);
       const DevWorkload Wl = launch_workload(g, 0, false);
       const size_t lds = lds_bytes(g, Wl.heap_top, 0);
@@ -450,6 +481,8 @@ class DeviceEngine {
     d["row_heap_top"] = row_top();
     d["row_waves_per_cu"] = row_layout(FAM_COMPOSITE_LINEAR).second;
     d["row_wave_share"] = row_share_;
+    d["native_rows_last"] = last_native_rows_;
+    d["native_waves_last"] = last_native_waves_;
     return d;
   }
 
@@ -482,6 +515,7 @@ class DeviceEngine {
     HIP_OK(fksk::set_rows_attrs(mx));
     HIP_OK(fksk::set_native_attrs_np1(mx)); HIP_OK(fksk::set_native_attrs_np2(mx));
     HIP_OK(fksk::set_native_attrs_np4(mx));
+    HIP_OK(fksk::set_native_rows_attrs(mx));
   }
 
   // 4-policies-per-wave row kernel: clusters of <= 16 nodes, exact repush
@@ -682,6 +716,40 @@ class DeviceEngine {
     return waves;
   }
 
+  // Native programs on the row kernel.  LLM-sized batches (up to two waves per
+  // CU) run one program per wave with the whole heap in LDS -- the replay is
+  // latency-bound there, and a lone row has no other row's divergence in its
+  // event loop; larger batches pack four programs per wave.
+  void launch_rows_native(Slot& s, int P, size_t fn_bytes, bool profiled = false) {
+    const int ra = native_rows_opt_ > 0 ? native_rows_opt_ : (P <= 2 * num_cus_ ? 1 : kRowsPerWave);
+    DevWorkload Wl = W_;
+    const int entries = row_heap_entries(W_.n_pods);
+    // largest heap top (2^k - 1 slots, at most the whole heap) that keeps two waves per CU
+    int T = 1;
+    while (T < entries - 1 && rows_lds_bytes(W_.n_pods, 2 * T + 1, ra) <= kMaxLds / 2) T = 2 * T + 1;
+    Wl.heap_top = T;
+    const size_t lds = rows_lds_bytes(W_.n_pods, T, ra) + (profiled ? kRowProfBytes : 0);
+    if (lds > kMaxLds) throw std::invalid_argument("native row kernel layout exceeds the 160 KiB LDS");
+    const int per_cu = std::max(1, std::min(fksk::native_rows_waves_per_cu(lds), (int)(kMaxLds / ((lds + 2047) & ~size_t(2047)))));
+    const int cap = std::max(1, (int)(row_share_ * per_cu * num_cus_));
+    const int waves = std::max(1, std::min((P + ra - 1) / ra, cap));
+    s.gheap.reserve((size_t)entries * 8 * (size_t)waves * kRowsPerWave);
+    if (s.queue.p == nullptr) {
+      s.queue.reserve(64);
+      HIP_OK(hipMemsetAsync(s.queue.p, 0, 64, s.stream));
+      s.qbase = 0;
+    }
+    if (profiled) s.prof.reserve((size_t)waves * 64);
+    const fksk::BuiltinArgs a{Wl, upload_workload(s, Wl), nullptr, nullptr, nullptr, s.res.as<DevResult>(),
+                              s.gheap.as<uint64_t>(), profiled ? s.prof.as<uint64_t>() : nullptr};
+    const RowNativeArgs nat{s.h_in.dev<const uint64_t>(), s.kc.as<const int64_t>(),
+                            reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + fn_bytes)};
+    HIP_OK(fksk::launch_native_rows(P, waves, ra, s.queue.as<uint32_t>(), s.qbase, lds, s.stream, a, nat));
+    s.qbase += (uint32_t)P + (uint32_t)waves * (uint32_t)ra;   // every active row makes one final, empty claim
+    last_native_rows_ = ra;
+    last_native_waves_ = waves;
+  }
+
   void launch_vm(Slot& s, int nregs) {
     const int P = s.P;
     const bool g = use_gheap(P);
@@ -728,6 +796,8 @@ class DeviceEngine {
   std::string row_mode_ = "auto";
   int row_top_opt_ = -1;
   double row_share_ = 1.0;
+  int native_rows_opt_ = 0;    // rows per wave for native programs (0: auto)
+  int last_native_rows_ = 0, last_native_waves_ = 0;
   mutable std::vector<std::pair<int, int>> row_layout_cache_ = std::vector<std::pair<int, int>>(8, {0, 0});
   int num_cus_ = 0;
   std::string arch_;

@@ -22,8 +22,14 @@ constexpr int kJitSgprs = 102;   // numbered SGPRs the calling kernel allocates 
 
 // pod fields: p_gpu = gpu_milli | num_gpu << 16 (the device pod record's packing);
 // kc = [instruction budget, constant payloads...] of the policy (int64, float bits)
+// n_gpu_ng = (uint16)free GPUs | GPU count << 16: the argument list is 31
+// dwords, all in VGPRs (v31 holds the work-item ids; a 32nd dword would be
+// passed through scratch memory on every call)
+__device__ __forceinline__ int32_t pack_gpu_ng(int32_t gpu_left, int32_t ngpus) {
+  return (int32_t)(((uint32_t)gpu_left & 0xFFFFu) | ((uint32_t)ngpus << 16));
+}
 typedef int64_t (*ProgFn)(int32_t n_cpu_left, int32_t n_cpu_total, int32_t n_mem_left, int32_t n_mem_total,
-                          int32_t n_gpu_left, int32_t n_ngpus, int32_t gl0, int32_t gl1, int32_t gl2, int32_t gl3,
+                          int32_t n_gpu_ng, int32_t gl0, int32_t gl1, int32_t gl2, int32_t gl3,
                           int32_t gl4, int32_t gl5, int32_t gl6, int32_t gl7, int32_t gt0, int32_t gt1, int32_t gt2,
                           int32_t gt3, int32_t gt4, int32_t gt5, int32_t gt6, int32_t gt7, const int64_t* gmem,
                           int32_t p_cpu, int32_t p_mem, int32_t p_gpu, int64_t p_ctime, int32_t p_dur,

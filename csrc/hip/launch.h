@@ -9,6 +9,7 @@
 
 #include "replay.hip.h"
 #include "vm_dev.hip.h"
+#include "replay_rows.hip.h"
 
 namespace fksk {
 
@@ -78,6 +79,14 @@ hipError_t launch_builtin_rows_prof(int fam_spec, int P, int waves, uint32_t* qu
 // resident row-kernel waves per CU for a family's instance at `lds` bytes (-1: error)
 int rows_waves_per_cu(int fam_spec, size_t lds);
 hipError_t set_rows_attrs(int max_lds);
+
+// row kernel over natively compiled programs (fn / kc / koff as in NativeArgs);
+// rows_active rows per wave claim programs, so a launch makes P + rows_active * waves claims;
+// a.prof != nullptr: the s_memtime phase-profiled build ([waves, 8] cycles)
+hipError_t launch_native_rows(int P, int waves, int rows_active, uint32_t* queue, uint32_t qbase, size_t lds,
+                              hipStream_t s, const BuiltinArgs& a, const fksd::RowNativeArgs& nat);
+hipError_t set_native_rows_attrs(int max_lds);
+int native_rows_waves_per_cu(size_t lds);
 
 // addresses of the native programs' runtime library (fks_rt_binop, fks_rt_unop, register floor)
 hipError_t native_rt_table(uint64_t* dev_out, hipStream_t s);

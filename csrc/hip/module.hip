@@ -311,6 +311,7 @@ PYBIND11_MODULE(_fks_hip, m) {
       .def("info", &DeviceEngine::info)
       .def("submit_native", &DeviceEngine::submit_native)
       .def("evaluate_native", &DeviceEngine::evaluate_native)
+      .def("profile_native", &DeviceEngine::profile_native)
       .def("native_rt_table", &DeviceEngine::native_rt_table);
   py::class_<JitModule>(m, "JitModule")
       .def(py::init<py::bytes, py::array_t<uint64_t, py::array::c_style | py::array::forcecast>, int, int>(),

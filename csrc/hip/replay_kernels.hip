@@ -216,8 +216,8 @@ struct NativeScorerDev {
     const int node = ps * kWave + lane_id();
     const int32_t* gl = nr.gml[ps];
     const int32_t* gt = nr.gmt[ps];
-    const int64_t r = fn(nr.cpu_left[ps], nr.cpu_total[ps], nr.mem_left[ps], nr.mem_total[ps], nr.gpu_left[ps],
-                         nr.ngpus[ps], gl[0], gl[1], gl[2], gl[3], gl[4], gl[5], gl[6], gl[7], gt[0], gt[1], gt[2], gt[3],
+    const int64_t r = fn(nr.cpu_left[ps], nr.cpu_total[ps], nr.mem_left[ps], nr.mem_total[ps],
+                         pack_gpu_ng(nr.gpu_left[ps], nr.ngpus[ps]), gl[0], gl[1], gl[2], gl[3], gl[4], gl[5], gl[6], gl[7], gt[0], gt[1], gt[2], gt[3],
                          gt[4], gt[5], gt[6], gt[7], gmem + (size_t)node * kGmax, pod.cpu, pod.mem,
                          pod.gmilli | (pod.ngpu << 16), pod.ctime, pod.dur, kc);
     if (r < 0) { exc = (int)(-r); return 0; }
@@ -249,6 +249,22 @@ __global__ void k_native_rt_table(uint64_t* out) {
     out[3] = 0;
   }
 }
+
+#if FKS_NPASS == 1
+// Row kernel with natively compiled programs (replay_rows.hip.h, kFamNative):
+// clusters of <= 16 nodes; `rows_active` rows per wave claim programs (1 for
+// latency-bound LLM-sized batches, 4 for large ones).
+__global__ __launch_bounds__(64, 1) void k_replay_rows_native(fksk::BuiltinArgs a, RowNativeArgs nat, int P,
+                                                             uint32_t* queue, uint32_t qbase, int rows_active) {
+  replay_rows<kFamNative>(a.W, a.Wc, nullptr, nullptr, a.gheap, a.out, P, queue, qbase, nullptr, nat, rows_active);
+}
+// s_memtime phase-profiled build (diagnostics): a.prof = [waves, 8] cycles
+__global__ __launch_bounds__(64, 1) void k_replay_rows_native_prof(fksk::BuiltinArgs a, RowNativeArgs nat, int P,
+                                                                  uint32_t* queue, uint32_t qbase, int rows_active) {
+  replay_rows<kFamNative, RowProf>(a.W, a.Wc, nullptr, nullptr, a.gheap, a.out, P, queue, qbase, a.prof, nat,
+                                   rows_active);
+}
+#endif
 
 template <int NPASS, bool GHEAP>
 __global__ __launch_bounds__(64, GHEAP ? 2 : 1) void k_replay_native(fksk::NativeArgs a) {
@@ -380,6 +396,20 @@ hipError_t FKS_CAT(set_native_attrs_np, FKS_NPASS)(int mx) {
   return e != hipSuccess ? e : raise_lds(&k_replay_native<FKS_NPASS, false>, mx);
 }
 #if FKS_NPASS == 1
+hipError_t launch_native_rows(int P, int waves, int rows_active, uint32_t* queue, uint32_t qbase, size_t lds,
+                              hipStream_t st, const BuiltinArgs& a, const fksd::RowNativeArgs& nat) {
+  if (a.prof) hipLaunchKernelGGL(k_replay_rows_native_prof, dim3(waves), dim3(64), lds, st, a, nat, P, queue, qbase, rows_active);
+  else hipLaunchKernelGGL(k_replay_rows_native, dim3(waves), dim3(64), lds, st, a, nat, P, queue, qbase, rows_active);
+  return hipGetLastError();
+}
+hipError_t set_native_rows_attrs(int mx) {
+  const hipError_t e = raise_lds(&k_replay_rows_native, mx);
+  return e != hipSuccess ? e : raise_lds(&k_replay_rows_native_prof, mx);
+}
+int native_rows_waves_per_cu(size_t lds) {
+  int n = 0;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_replay_rows_native, 64, lds) == hipSuccess ? n : -1;
+}
 hipError_t native_rt_table(uint64_t* dev_out, hipStream_t s) {
   hipLaunchKernelGGL(k_native_rt_table, dim3(1), dim3(64), 0, s, dev_out);
   return hipGetLastError();

@@ -26,8 +26,18 @@
 
 #include "replay.hip.h"
 #include "scorers.hip.h"
+#include "jit_abi.h"
 
 namespace fksd {
+
+// FAM value of the native-program instance: every row calls its own
+// JIT-compiled scorer (jit_abi.h ProgFn) instead of a built-in family.
+constexpr int kFamNative = 100;
+struct RowNativeArgs {
+  const uint64_t* fn;     // [P] device addresses of the programs' scorers
+  const int64_t* kc;      // concatenated constant blocks
+  const int32_t* koff;    // [P] offset of policy p's block in kc
+};
 
 constexpr int kRow = 16;            // lanes per DPP row = max nodes per policy
 constexpr int kRowsPerWave = 4;
@@ -245,8 +255,8 @@ constexpr int kRowClassBytes = (kRow * kRowClassSlots * 4 + kRow * kNodeConsts *
 __host__ __device__ inline size_t rows_row_bytes(int n_pods, int T) {
   return (size_t)lds_delmap_words(n_pods) * 4 + (size_t)(T + 1) * 8;
 }
-__host__ __device__ inline size_t rows_lds_bytes(int n_pods, int T) {
-  return (size_t)kRowsPerWave * kWeights * 8 + kRowClassBytes + kRowsPerWave * rows_row_bytes(n_pods, T);
+__host__ __device__ inline size_t rows_lds_bytes(int n_pods, int T, int rows = kRowsPerWave) {
+  return (size_t)kRowsPerWave * kWeights * 8 + kRowClassBytes + (size_t)rows * rows_row_bytes(n_pods, T);
 }
 
 // Wave-level phase profiler for the row kernel (diagnostics build only): each
@@ -286,10 +296,17 @@ constexpr int kRowProfBytes = 128;
 // (device-mapped pinned host memory), gheap: [4 * gridDim.x,
 // row_heap_entries(N)] HBM heap slices (one per row slot), heap0p: the
 // initial heap shifted by one slot (address = slot + 1).
+//
+// FAM == kFamNative: natively compiled programs (`nat`), one per row; only
+// rows < rows_active claim policies, so small batches can run one program per
+// wave (the whole heap in LDS, no other row's divergence in the event loop).
 template <int FAM, class Prof = RowNoProf>
 __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const int32_t* fam, const double* weights,
                             uint64_t* gheap, DevResult* out, int P, uint32_t* queue, uint32_t qbase,
-                            uint64_t* prof_out = nullptr) {
+                            uint64_t* prof_out = nullptr, RowNativeArgs nat = RowNativeArgs{nullptr, nullptr, nullptr},
+                            int rows_active = kRowsPerWave) {
+  constexpr bool kNative = FAM == kFamNative;
+  const int ra = kNative ? rows_active : kRowsPerWave;
   // W: the kernel-argument copy, read once for the hot scalars below; every
   // other field is re-read where it is used through an opaque pointer to the
   // HBM copy (scalar loads), so the loop carries no spilled SGPR copies of it
@@ -349,6 +366,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
     // the counter is never reset: this launch's claims start at qbase (the
     // host adds every launch's P + rows claims), so no fill kernel has to
     // queue for a CU slot before the replay can start
+    if (kNative && row >= ra) return P;   // idle row: never claims
     const int c = jv == 0 ? (int)(__hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - qbase) : 0;
     return row_read(c, rbase, 0);
   };
@@ -372,11 +390,18 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
   double thr = 0.0;
   uint64_t hsh = 0;
   int32_t exc = EXC_NONE;
-  
+  ProgFn prog = nullptr;          // native: the row's scorer
+  const int64_t* kcp = nullptr;   // native: its constant block
+
   // start policy p on this row: weights, heap image, bitmap, node state, counters
   auto begin = [&]() {
-    wl[jv] = *global_ptr(&weights[(size_t)p * kWeights + jv]);
-    if (FAM < 0) family = *global_ptr(&fam[p]);
+    if constexpr (kNative) {
+      prog = reinterpret_cast<ProgFn>(*global_ptr(&nat.fn[p]));
+      kcp = nat.kc + *global_ptr(&nat.koff[p]);
+    } else {
+      wl[jv] = *global_ptr(&weights[(size_t)p * kWeights + jv]);
+      if (FAM < 0) family = *global_ptr(&fam[p]);
+    }
     const int words = row_heap_entries(N) / 2;   // 16-byte pairs of the shifted heap
     for (int i = jv; i < words; i += kRow) {
       const u64x2 v = heap_src[i];
@@ -413,7 +438,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
   };
 
   Prof prof;
-  prof.start(reinterpret_cast<FKS_LDS uint64_t*>(reinterpret_cast<FKS_LDS char*>(lds) + rows_lds_bytes(N, T)));
+  prof.start(reinterpret_cast<FKS_LDS uint64_t*>(reinterpret_cast<FKS_LDS char*>(lds) + rows_lds_bytes(N, T, ra)));
   bool have = p < P;
   if (have) begin();
   prof.mark(PH_EVAL);
@@ -459,7 +484,18 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
         load_consts();
         int lexc = EXC_NONE;
         int64_t s = 0;
-        if (node_valid && feasible<1>(0, nr, pod)) {
+        if constexpr (kNative) {
+          // the program holds the template's feasibility prologue itself
+          if (node_valid) {
+            const int32_t* gl = nr.gml[0];
+            const int32_t* gt = nr.gmt[0];
+            s = prog(nr.cpu_left[0], nr.cpu_total[0], nr.mem_left[0], nr.mem_total[0], pack_gpu_ng(nr.gpu_left[0], nr.ngpus[0]),
+                     gl[0], gl[1], gl[2], gl[3], gl[4], gl[5], gl[6], gl[7], gt[0], gt[1], gt[2], gt[3], gt[4], gt[5],
+                     gt[6], gt[7], cold()->gmem_total + (size_t)jv * kGmax, pod.cpu, pod.mem,
+                     pod.gmilli | (pod.ngpu << 16), pod.ctime, pod.dur, kcp);
+            if (s < 0) { lexc = (int)(-s); s = 0; }
+          }
+        } else if (node_valid && feasible<1>(0, nr, pod)) {
           // weights read from LDS where each term uses them (no 32-VGPR weight vector)
           const FKS_LDS double* wq = wl;
           s = BuiltinScorerDev<FAM>::template score_weights<1>(family, wq, 0, nr, pod, lexc);

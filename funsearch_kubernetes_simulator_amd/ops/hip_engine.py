@@ -232,8 +232,8 @@ class DeviceEvaluator:
         return batch
 
     def profile_native(self, progs: Sequence[CompiledPolicy]):
-        """s_memtime phase-profiled native launch: (table [P, 13], cycles [P, 8] by
-        PHASES + ("pop_loads",)); programs must all be native-compilable."""
+        """s_memtime phase-profiled native row-kernel launch: (table [P, 13], wave
+        cycles [waves, 8] by ROW_PHASES); programs must all be native-compilable."""
         batch = self.native_compiler.prepare(progs)
         if not batch.ok.all():
             raise ValueError(f"not native: {batch.reasons}")

@@ -49,8 +49,11 @@ from .bytecode import NO_REG, TAG_FLOAT, Op, unpack_code
 from .compiler import CompiledPolicy
 
 #: parameter list shared by every generated program (keep in sync with jit_abi.h ProgFn)
+#: (31 argument dwords: v0-v30 -- v31 carries the work-item ids, so a 32nd
+#: dword would travel through the stack, i.e. a scratch store + load per call;
+#: the node's free-GPU count and GPU count share one dword)
 PROG_PARAMS = ("int32_t n_cpu_left, int32_t n_cpu_total, int32_t n_mem_left, int32_t n_mem_total, "
-               "int32_t n_gpu_left, int32_t n_ngpus, "
+               "int32_t n_gpu_ng, "
                "int32_t gl0, int32_t gl1, int32_t gl2, int32_t gl3, int32_t gl4, int32_t gl5, int32_t gl6, "
                "int32_t gl7, int32_t gt0, int32_t gt1, int32_t gt2, int32_t gt3, int32_t gt4, int32_t gt5, "
                "int32_t gt6, int32_t gt7, const int64_t* gmem, "
@@ -259,6 +262,8 @@ def program_source(prog: CompiledPolicy, name: str, lift_consts: bool = True) ->
     w("  int exc_ = EXC_NONE;")
     w("  int64_t bud_ = kc[0];")
     w("  (void)bud_; (void)gmem;")
+    w("  const int32_t n_gpu_left = (int16_t)(n_gpu_ng & 0xFFFF), n_ngpus = n_gpu_ng >> 16;")
+    w("  (void)n_gpu_left; (void)n_ngpus;")
 
     def R(r: int) -> str:
         if r == NO_REG:

@@ -48,6 +48,27 @@ def test_native_equals_cpu_vm_full_trace(dev, default_workload):
     assert compared >= len(progs) - 4, skipped
 
 
+@pytest.mark.parametrize("layout", [{"native_rows": 1}, {"native_rows": 4}, {"row_kernel": "off"}],
+                         ids=["rows1", "rows4", "wave"])
+def test_native_kernel_layouts_agree(dev, default_workload, layout):
+    """Row kernel with one / four programs per wave and the one-wave-per-program
+    kernel: every row bit-identical to the CPU VM (score, means, counts, trace hash)."""
+    progs = programs()[:24]
+    vm = ce.simulate_program_batch(default_workload, progs, threads=16)
+    dev.set_options(**layout)
+    try:
+        nat = dev.evaluate_native(progs)
+        info = dev.info()
+    finally:
+        dev.set_options(native_rows=0, row_kernel="auto")
+    if "native_rows" in layout:
+        assert info["native_rows_last"] == layout["native_rows"], info
+    for i, p in enumerate(progs):
+        if int(nat[i, 10]) in (Exc.UNSUPPORTED, Exc.BUDGET) or int(vm[i, 10]) in (Exc.UNSUPPORTED, Exc.BUDGET):
+            continue
+        assert np.array_equal(nat[i], vm[i]), (layout, i, nat[i], vm[i])
+
+
 def test_shape_cache_reuses_compiled_code(dev):
     a = compile_policy("def priority_function(pod, node):\n    return 5000 - node.cpu_milli_left * 0.25\n")
     b = compile_policy("def priority_function(pod, node):\n    return 7000 - node.cpu_milli_left * 0.5\n")

@@ -1,5 +1,6 @@
-"""s_memtime phase split of the native-program replay kernel (latency regime:
-a few dozen programs, one wave each).  Prints cycles per event by phase.
+"""s_memtime phase split of the native-program row kernel (latency regime:
+a few dozen programs, one program per wave).  Prints wave cycles per event by
+phase (the profiled build is a diagnostics kernel: s_memtime itself adds cost).
 
     python tools/native_phase.py --programs 48
 """
@@ -17,16 +18,16 @@ from funsearch_kubernetes_simulator_amd.core import load_default_workload  # noq
 from funsearch_kubernetes_simulator_amd.models.library import reference_policies  # noqa: E402
 from funsearch_kubernetes_simulator_amd.policy.compiler import compile_policy  # noqa: E402
 
-PH = ("pop", "delete", "score", "fail", "commit", "eval", "pop_loads")
+PH = ("pop", "delete", "score", "fail", "commit", "eval", "next_policy")
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--programs", type=int, default=48)
-    ap.add_argument("--heap-mode", default="lds")
+    ap.add_argument("--rows", type=int, default=0, help="programs per wave (0: auto)")
     a = ap.parse_args()
     from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
-    dev = he.DeviceEvaluator(load_default_workload(), options={"heap_mode": a.heap_mode})
+    dev = he.DeviceEvaluator(load_default_workload(), options={"native_rows": a.rows})
     sets = {"first_fit": [compile_policy(reference_policies()["first_fit"])],
             "funsearch_4901": [compile_policy(reference_policies()["funsearch_4901"])],
             "children": mutation_children(a.programs, 0)}
