@@ -323,7 +323,7 @@ class DeviceEngine {
     s.h_in.reserve(fb + ob + 64);
     std::memcpy(s.h_in.as<char>(), fn.data(), fb);       // read by the kernel through the mapping
     std::memcpy(s.h_in.as<char>() + fb, koff.data(), ob);
-    s.kc.reserve(kb + 16);
+    s.kc.reserve(kb + (size_t)kKcLds * 8 + 16);   // the kernels copy kKcLds entries from every block start
     s.h_wc.reserve(sizeof(DevWorkload));
     HIP_OK(hipMemcpyAsync(s.kc.p, kc.data(), kb, hipMemcpyHostToDevice, s.stream));
     HIP_OK(hipStreamSynchronize(s.stream));   // kc is pageable: finish the copy while it is alive
@@ -335,8 +335,9 @@ class DeviceEngine {
         return;
       }
       const bool g = use_gheap_native(P);
-      const DevWorkload Wl = launch_workload(g, 0, false);
-      const size_t lds = lds_bytes(g, Wl.heap_top, 0);
+      // kKcLds / 64 VM-register rows of LDS hold the policy's constant block
+      const DevWorkload Wl = launch_workload(g, kKcLds / kWave, false);
+      const size_t lds = lds_bytes(g, Wl.heap_top, kKcLds / kWave);
       if (lds > kMaxLds) throw std::invalid_argument("replay layout exceeds the 160 KiB LDS");
       uint64_t* gh = g ? gheap_for(s, P) : nullptr;
       const fksk::NativeArgs a{Wl, upload_workload(s, Wl), s.h_in.dev<const uint64_t>(), s.kc.as<const int64_t>(),
@@ -565,7 +566,10 @@ class DeviceEngine {
   // native-program kernels allocate 128 VGPRs (the JIT register floor): 2
   // waves per SIMD with the HBM heap, so the LDS heap (2 per CU) wins only for
   // batches that fit it
-  bool use_gheap_native(int P) const { return use_gheap(P); }
+  bool use_gheap_native(int P) const {
+    if (lds_bytes(false, 0, kKcLds / kWave) > kMaxLds) return true;   // LDS heap + constant block
+    return use_gheap(P);
+  }
 
   bool use_gheap(int P) const {
     if (!lds_heap_ok_ || lds_bytes(false, 0, 0) > kMaxLds) return true;
@@ -726,9 +730,9 @@ class DeviceEngine {
     const int entries = row_heap_entries(W_.n_pods);
     // largest heap top (2^k - 1 slots, at most the whole heap) that keeps two waves per CU
     int T = 1;
-    while (T < entries - 1 && rows_lds_bytes(W_.n_pods, 2 * T + 1, ra) <= kMaxLds / 2) T = 2 * T + 1;
+    while (T < entries - 1 && rows_lds_bytes(W_.n_pods, 2 * T + 1, ra, true) <= kMaxLds / 2) T = 2 * T + 1;
     Wl.heap_top = T;
-    const size_t lds = rows_lds_bytes(W_.n_pods, T, ra) + (profiled ? kRowProfBytes : 0);
+    const size_t lds = rows_lds_bytes(W_.n_pods, T, ra, true) + (profiled ? kRowProfBytes : 0);
     if (lds > kMaxLds) throw std::invalid_argument("native row kernel layout exceeds the 160 KiB LDS");
     const int per_cu = std::max(1, std::min(fksk::native_rows_waves_per_cu(lds), (int)(kMaxLds / ((lds + 2047) & ~size_t(2047)))));
     const int cap = std::max(1, (int)(row_share_ * per_cu * num_cus_));

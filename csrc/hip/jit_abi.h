@@ -28,12 +28,22 @@ constexpr int kJitSgprs = 102;   // numbered SGPRs the calling kernel allocates 
 __device__ __forceinline__ int32_t pack_gpu_ng(int32_t gpu_left, int32_t ngpus) {
   return (int32_t)(((uint32_t)gpu_left & 0xFFFFu) | ((uint32_t)ngpus << 16));
 }
+// kc = the policy's constant block, copied into the calling wave's LDS when the
+// policy starts (a constant read is one ds_read_b64 instead of a dependent
+// global load on every use); a program may hold at most kKcLds entries
+// (native_codegen rejects larger blocks, which then run on the VM engines)
+constexpr int kKcLds = 256;
+#if defined(FKS_HOST_JIT)
+typedef const int64_t* KcPtr;
+#else
+typedef const __attribute__((address_space(3))) int64_t* KcPtr;
+#endif
 typedef int64_t (*ProgFn)(int32_t n_cpu_left, int32_t n_cpu_total, int32_t n_mem_left, int32_t n_mem_total,
                           int32_t n_gpu_ng, int32_t gl0, int32_t gl1, int32_t gl2, int32_t gl3,
                           int32_t gl4, int32_t gl5, int32_t gl6, int32_t gl7, int32_t gt0, int32_t gt1, int32_t gt2,
                           int32_t gt3, int32_t gt4, int32_t gt5, int32_t gt6, int32_t gt7, const int64_t* gmem,
                           int32_t p_cpu, int32_t p_mem, int32_t p_gpu, int64_t p_ctime, int32_t p_dur,
-                          const int64_t* kc);
+                          KcPtr kc);
 
 // ---- runtime library -------------------------------------------------------------
 // The float // and %, **, math.log / exp / sqrt / pow machinery (double-double

@@ -210,7 +210,7 @@ void k_replay_rows_prof(fksk::BuiltinArgs a, int P, uint32_t* queue, uint32_t qb
 struct NativeScorerDev {
   ProgFn fn;
   const int64_t* gmem;   // [node][kGmax] GPU memory MiB
-  const int64_t* kc;     // the policy's [budget, constants...]
+  KcPtr kc;              // the policy's [budget, constants...], staged in LDS
   template <int NPASS>
   __device__ int64_t score(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, int& exc) {
     const int node = ps * kWave + lane_id();
@@ -273,7 +273,13 @@ __global__ __launch_bounds__(64, GHEAP ? 2 : 1) void k_replay_native(fksk::Nativ
   NativeScorerDev sc;
   sc.fn = reinterpret_cast<ProgFn>(uniu64(a.fn[p]));
   sc.gmem = a.W.gmem_total;
-  sc.kc = reinterpret_cast<const int64_t*>(uniu64(reinterpret_cast<uint64_t>(a.kc + a.koff[p])));
+  // the constant block moves into the slot's register area (the host reserves
+  // kKcLds / 64 VM registers for it; the allocation is padded by kKcLds entries,
+  // so the fixed-size copy never reads past it)
+  const FKS_GLOBAL int64_t* ksrc = global_ptr(a.kc + a.koff[p]);
+  FKS_LDS int64_t* kl = reinterpret_cast<FKS_LDS int64_t*>(lds_ptr(s.vregs));
+  for (int i = lane_id(); i < kKcLds; i += kWave) kl[i] = ksrc[i];
+  sc.kc = kl;
   replay_one<NPASS>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p);
 }
 #endif

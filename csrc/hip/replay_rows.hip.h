@@ -255,8 +255,11 @@ constexpr int kRowClassBytes = (kRow * kRowClassSlots * 4 + kRow * kNodeConsts *
 __host__ __device__ inline size_t rows_row_bytes(int n_pods, int T) {
   return (size_t)lds_delmap_words(n_pods) * 4 + (size_t)(T + 1) * 8;
 }
-__host__ __device__ inline size_t rows_lds_bytes(int n_pods, int T, int rows = kRowsPerWave) {
-  return (size_t)kRowsPerWave * kWeights * 8 + kRowClassBytes + (size_t)rows * rows_row_bytes(n_pods, T);
+// native programs (kc = true) also stage each active row's constant block
+// (kKcLds int64) after the rows' heap areas
+__host__ __device__ inline size_t rows_lds_bytes(int n_pods, int T, int rows = kRowsPerWave, bool kc = false) {
+  return (size_t)kRowsPerWave * kWeights * 8 + kRowClassBytes + (size_t)rows * rows_row_bytes(n_pods, T) +
+         (kc ? (size_t)rows * kKcLds * 8 : 0);
 }
 
 // Wave-level phase profiler for the row kernel (diagnostics build only): each
@@ -391,13 +394,18 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
   uint64_t hsh = 0;
   int32_t exc = EXC_NONE;
   ProgFn prog = nullptr;          // native: the row's scorer
-  const int64_t* kcp = nullptr;   // native: its constant block
+  // native: its constant block, staged in LDS after the active rows' heap areas
+  FKS_LDS int64_t* kcp = reinterpret_cast<FKS_LDS int64_t*>(
+      reinterpret_cast<FKS_LDS char*>(lds + kRowsPerWave * kWeights) + kRowClassBytes +
+      (size_t)ra * rows_row_bytes(N, T)) + (size_t)row * kKcLds;
 
   // start policy p on this row: weights, heap image, bitmap, node state, counters
   auto begin = [&]() {
     if constexpr (kNative) {
       prog = reinterpret_cast<ProgFn>(*global_ptr(&nat.fn[p]));
-      kcp = nat.kc + *global_ptr(&nat.koff[p]);
+      // fixed-size copy: the host pads the kc allocation by kKcLds entries
+      const FKS_GLOBAL int64_t* ksrc = global_ptr(nat.kc + *global_ptr(&nat.koff[p]));
+      for (int i = jv; i < kKcLds; i += kRow) kcp[i] = ksrc[i];
     } else {
       wl[jv] = *global_ptr(&weights[(size_t)p * kWeights + jv]);
       if (FAM < 0) family = *global_ptr(&fam[p]);
@@ -438,7 +446,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
   };
 
   Prof prof;
-  prof.start(reinterpret_cast<FKS_LDS uint64_t*>(reinterpret_cast<FKS_LDS char*>(lds) + rows_lds_bytes(N, T, ra)));
+  prof.start(reinterpret_cast<FKS_LDS uint64_t*>(reinterpret_cast<FKS_LDS char*>(lds) + rows_lds_bytes(N, T, ra, kNative)));
   bool have = p < P;
   if (have) begin();
   prof.mark(PH_EVAL);

@@ -57,7 +57,9 @@ PROG_PARAMS = ("int32_t n_cpu_left, int32_t n_cpu_total, int32_t n_mem_left, int
                "int32_t gl0, int32_t gl1, int32_t gl2, int32_t gl3, int32_t gl4, int32_t gl5, int32_t gl6, "
                "int32_t gl7, int32_t gt0, int32_t gt1, int32_t gt2, int32_t gt3, int32_t gt4, int32_t gt5, "
                "int32_t gt6, int32_t gt7, const int64_t* gmem, "
-               "int32_t p_cpu, int32_t p_mem, int32_t p_gpu, int64_t p_ctime, int32_t p_dur, const int64_t* kc")
+               "int32_t p_cpu, int32_t p_mem, int32_t p_gpu, int64_t p_ctime, int32_t p_dur, KcPtr kc")
+#: constant-block entries the replay kernels stage in LDS per policy (jit_abi.h kKcLds)
+KC_LDS = 256
 
 I, F = 1, 2          # type lattice bits: may be int / may be float
 IF_ = I | F
@@ -232,6 +234,8 @@ def infer_types(code, flow, ctag) -> List[Dict[int, int]]:
 # ---------------------------------------------------------------------------- emission
 def program_source(prog: CompiledPolicy, name: str, lift_consts: bool = True) -> str:
     """C++ of one program: ``extern "C" int64_t name(PROG_PARAMS)``."""
+    if lift_consts and 1 + len(prog.ctag) > KC_LDS:
+        raise CodegenError(f"{len(prog.ctag)} constants > {KC_LDS - 1} (the LDS constant block)")
     code = unpack_code(prog.code)
     flow = _loop_structure(code)
     types = infer_types(code, flow, prog.ctag)
@@ -469,7 +473,7 @@ FKS_JIT_RT_TABLE_DEFINITION
 """
 
 #: argument list of a probe kernel's direct call (values from memory so nothing folds)
-_PROBE_ARGS = ", ".join([f"a[{k + 1}]" for k in range(22)] + ["g", "a[23]", "a[24]", "a[25]", "g[1]", "a[26]", "g"])
+_PROBE_ARGS = ", ".join([f"a[{k + 1}]" for k in range(22)] + ["g", "a[23]", "a[24]", "a[25]", "g[1]", "a[26]", "(KcPtr)g"])
 
 
 def module_source(progs: Sequence[CompiledPolicy], with_probes: bool = True, host: bool = False,

@@ -200,10 +200,10 @@ def test_torchrun_restart_resumes_after_rank_crash(tmp_path):
         "code, score = fs.global_best()\n"
         "print(json.dumps({'gen': fs.generation, 'world': fs.ctx.world_size, 'score': score,\n"
         "                  'restart': os.environ.get('TORCHELASTIC_RESTART_COUNT')}))\n")
-    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1", FKS_DIST_TIMEOUT_S="60")
+    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1", FKS_DIST_TIMEOUT_S="60", GLOO_SOCKET_IFNAME="lo")
     # dynamic (c10d) rendezvous: every restart round re-forms the group on a fresh store prefix
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--max-restarts=1",
-           "--rdzv-backend=c10d", f"--rdzv-endpoint=127.0.0.1:{33000 + os.getpid() % 1000}", str(script)]
+           "--rdzv-backend=c10d", "--local-addr=127.0.0.1", f"--rdzv-endpoint=127.0.0.1:{33000 + os.getpid() % 1000}", str(script)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]
     import re
