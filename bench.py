@@ -69,7 +69,16 @@ def main() -> None:
     ap.add_argument("--programs", type=int, default=64,
                     help="after the timed region: evaluate this many FunSearch candidate programs (offline-mutation "
                          "children) through the native program backend and report them as `program_path` (0: skip)")
+    ap.add_argument("--screen", type=int, default=1,
+                    help="MFMA pre-filter: propose K x --candidates per island generation, screen them with "
+                         "k_screen_linear (composite family), replay the best 1/K exactly (1: off)")
+    ap.add_argument("--screen-stride", type=int, default=4, help="screen on every k-th recorded state")
+    ap.add_argument("--time-budget", type=float, default=0.0,
+                    help="run generations until this many seconds have passed (instead of --steps); "
+                         "steps = generations completed")
     args = ap.parse_args()
+    if args.screen > 1 and args.family != "composite_linear":
+        raise SystemExit("--screen needs --family composite_linear (the screened feature basis)")
 
     from funsearch_kubernetes_simulator_amd.parallel import dist
     ctx = dist.init_distributed(use_gpu=args.device == "gpu")
@@ -105,6 +114,23 @@ def main() -> None:
             (ctx.device, device, ev.device.device, torch.cuda.current_device())
     islands = make_islands(args.islands, args.family, args.candidates, args.elite,
                            seed=args.seed + 104729 * ctx.rank)
+    screener = None
+    screen_stats = {"screened": 0, "screen_s": 0.0}
+    if args.screen > 1:
+        from funsearch_kubernetes_simulator_amd.ops.screening import Screener
+        screener = Screener(workload, device=device if args.device == "gpu" else "cpu",
+                            state_stride=args.screen_stride)
+
+    def propose(isl) -> np.ndarray:
+        if screener is None:
+            return isl.propose()
+        cand = isl.propose(args.screen * args.candidates)
+        t = time.perf_counter()
+        with roctx_range("bench.screen"):
+            keep = screener.select(cand, args.candidates)
+        screen_stats["screen_s"] += time.perf_counter() - t
+        screen_stats["screened"] += len(cand)
+        return cand[keep]
 
     def sync():
         if args.device == "gpu":
@@ -126,7 +152,7 @@ def main() -> None:
     def epoch_sync(gen0: int, n: int) -> None:
         """All islands in one launch per generation (--sync-islands)."""
         for gen in range(gen0, gen0 + n):
-            props = [isl.propose() for isl in islands]
+            props = [propose(isl) for isl in islands]
             tab = ev.evaluate_family(args.family, np.concatenate(props))
             off = 0
             for isl, p in zip(islands, props):
@@ -141,7 +167,7 @@ def main() -> None:
         props, gens, left = [None] * k, [gen0] * k, [n] * k
 
         def launch(i: int) -> None:
-            props[i] = islands[i].propose()
+            props[i] = propose(islands[i])
             ev.submit_family(i, args.family, props[i])
 
         for i in range(k):
@@ -187,8 +213,19 @@ def main() -> None:
     run(0, args.warmup)
     sync()
     events[0] = 0.0
+    screen_stats.update(screened=0, screen_s=0.0)
     t0 = time.perf_counter()
-    run(args.warmup, args.steps)
+    if args.time_budget > 0:
+        # whole migration epochs until the budget is spent (ranks agree on when to stop)
+        g, chunk = args.warmup, max(1, args.migrate_every or 5)
+        while True:
+            run(g, chunk)
+            g += chunk
+            if dist.all_reduce_max(time.perf_counter() - t0) >= args.time_budget:
+                break
+        args.steps = g - args.warmup
+    else:
+        run(args.warmup, args.steps)
     sync()
     elapsed = dist.all_reduce_max(time.perf_counter() - t0)
     events_total = dist.all_reduce_sum(events[0])
@@ -256,6 +293,15 @@ def main() -> None:
                                 "is the program-for-program comparison",
             "program_path": program_path,
         }
+        if screener is not None:
+            out["screen"] = {"k": args.screen, "state_stride": args.screen_stride, "states": screener.n_states,
+                             "kernel": "k_screen_linear (v_mfma_f32_32x32x2f32)",
+                             "screened_per_s": round(screen_stats["screened"] * ctx.world_size / elapsed, 1),
+                             "screen_s_rank0": round(screen_stats["screen_s"], 3),
+                             "note": "value counts exact replays only; each replayed candidate is the best 1/k "
+                                     "of k proposals by the MFMA surrogate"}
+        if args.time_budget > 0:
+            out["time_budget_s"] = args.time_budget
         if args.save_best:
             k = {"random_linear": 4, "feature_linear": fam.N_FEATURES}.get(args.family, fam.N_COMPOSITE)
             code = fam.to_program(args.family, wbest[:k])

@@ -103,6 +103,7 @@ struct Slot {
   hipEvent_t done = nullptr;
   DevBuf res, tab, fam, w, code, meta, kpay, ktag, gheap, prof, wc, queue, kc;
   HostBuf h_in, h_tab, h_wc;
+  bool fused_table = false;   // the launch wrote h_tab itself (row kernels)
   int P = 0;
   int fam_spec = -1;    // family shared by the whole staged batch, or -1
   uint32_t qbase = 0;   // row-kernel queue counter value at the next launch
@@ -706,14 +707,15 @@ class DeviceEngine {
     s.gheap.reserve((size_t)row_heap_entries(W_.n_pods) * 8 * (size_t)waves * kRowsPerWave);
     if (s.queue.p == nullptr) {   // zeroed once; launches then offset their claims
       s.queue.reserve(64);
-      HIP_OK(hipMemsetAsync(s.queue.p, 0, 64, s.stream));
+      zero_queue(s);
       s.qbase = 0;
     }
     if (profiled) s.prof.reserve((size_t)waves * 64);
     const size_t wb = (size_t)P * kWeights * 8;
     const fksk::BuiltinArgs a{Wl, upload_workload(s, Wl), reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + wb),
                               s.h_in.dev<double>(), s.w.as<double>(), s.res.as<DevResult>(), s.gheap.as<uint64_t>(),
-                              profiled ? s.prof.as<uint64_t>() : nullptr};
+                              profiled ? s.prof.as<uint64_t>() : nullptr, s.h_tab.dev<double>()};
+    s.fused_table = true;
     if (profiled) HIP_OK(fksk::launch_builtin_rows_prof(s.fam_spec, P, waves, s.queue.as<uint32_t>(), s.qbase, lds, s.stream, a));
     else HIP_OK(fksk::launch_builtin_rows(s.fam_spec, P, waves, s.queue.as<uint32_t>(), s.qbase, lds, s.stream, a));
     s.qbase += (uint32_t)P + (uint32_t)waves * kRowsPerWave;   // every row makes one final, empty claim
@@ -740,12 +742,13 @@ class DeviceEngine {
     s.gheap.reserve((size_t)entries * 8 * (size_t)waves * kRowsPerWave);
     if (s.queue.p == nullptr) {
       s.queue.reserve(64);
-      HIP_OK(hipMemsetAsync(s.queue.p, 0, 64, s.stream));
+      zero_queue(s);
       s.qbase = 0;
     }
     if (profiled) s.prof.reserve((size_t)waves * 64);
     const fksk::BuiltinArgs a{Wl, upload_workload(s, Wl), nullptr, nullptr, nullptr, s.res.as<DevResult>(),
-                              s.gheap.as<uint64_t>(), profiled ? s.prof.as<uint64_t>() : nullptr};
+                              s.gheap.as<uint64_t>(), profiled ? s.prof.as<uint64_t>() : nullptr, s.h_tab.dev<double>()};
+    s.fused_table = true;
     const RowNativeArgs nat{s.h_in.dev<const uint64_t>(), s.kc.as<const int64_t>(),
                             reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + fn_bytes)};
     HIP_OK(fksk::launch_native_rows(P, waves, ra, s.queue.as<uint32_t>(), s.qbase, lds, s.stream, a, nat));
@@ -767,6 +770,15 @@ class DeviceEngine {
     else HIP_OK(fksk::launch_vm_np4(g, P, lds, s.stream, a));
   }
 
+  // the persistent-queue counter starts at zero once per slot: a copy-engine
+  // transfer, not a fill kernel (a fill kernel would wait for a CU slot behind
+  // the other slots' persistent waves -- hundreds of ms in a profile)
+  static void zero_queue(Slot& s) {
+    static const uint64_t zeros[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    HIP_OK(hipMemcpyAsync(s.queue.p, zeros, 64, hipMemcpyHostToDevice, s.stream));
+    HIP_OK(hipStreamSynchronize(s.stream));
+  }
+
   // the launch's workload struct, also resident in HBM (the kernels' cold-field copy)
   const DevWorkload* upload_workload(Slot& s, const DevWorkload& Wl) {
     // the device copy is re-sent only when the launch configuration changes
@@ -783,8 +795,12 @@ class DeviceEngine {
   // k_eval_reduce, result table -> pinned host, completion event
   void finish(Slot& s) {
     const int P = s.P;
-    hipLaunchKernelGGL(k_eval_reduce, dim3((P + 63) / 64), dim3(64), 0, s.stream, s.res.as<DevResult>(),
-                       s.h_tab.dev<double>(), P);   // zero-copy into the pinned result table
+    // row kernels write the result table themselves (evaluator fused into the
+    // write-back); the wave kernels leave it to k_eval_reduce
+    if (!s.fused_table)
+      hipLaunchKernelGGL(k_eval_reduce, dim3((P + 63) / 64), dim3(64), 0, s.stream, s.res.as<DevResult>(),
+                         s.h_tab.dev<double>(), P);   // zero-copy into the pinned result table
+    s.fused_table = false;
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(s.done, s.stream));
     s.busy = true;

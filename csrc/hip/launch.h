@@ -26,6 +26,7 @@ struct BuiltinArgs {
   DevResult* out;
   uint64_t* gheap;        // HBM heap slices (GHEAP) or nullptr
   uint64_t* prof;         // [P, 8] phase cycles (profiling launches only)
+  double* table = nullptr;  // row kernels: [P, 13] result table written by the kernel (k_eval_reduce fused)
 };
 
 struct VmArgs {

@@ -191,7 +191,8 @@ __global__ FKS_VM_BOUNDS(GHEAP) void k_replay_vm_prof(fksk::VmArgs a) {
 #endif
 template <int FAM>
 __global__ __launch_bounds__(64, FAM < 0 ? 2 : (FAM == 3 || FAM == 4) ? FKS_ROW_HEAVY_WAVES : FKS_ROW_WAVES) void k_replay_rows(fksk::BuiltinArgs a, int P, uint32_t* queue, uint32_t qbase) {
-  replay_rows<FAM>(a.W, a.Wc, a.fam, a.weights, a.gheap, a.out, P, queue, qbase);
+  replay_rows<FAM>(a.W, a.Wc, a.fam, a.weights, a.gheap, a.out, P, queue, qbase, nullptr,
+                   RowNativeArgs{nullptr, nullptr, nullptr}, kRowsPerWave, a.table);
 }
 #endif
 
@@ -199,7 +200,8 @@ __global__ __launch_bounds__(64, FAM < 0 ? 2 : (FAM == 3 || FAM == 4) ? FKS_ROW_
 template <int FAM>
 __global__ __launch_bounds__(64, FAM < 0 ? 2 : (FAM == 3 || FAM == 4) ? FKS_ROW_HEAVY_WAVES : FKS_ROW_WAVES)
 void k_replay_rows_prof(fksk::BuiltinArgs a, int P, uint32_t* queue, uint32_t qbase) {
-  replay_rows<FAM, RowProf>(a.W, a.Wc, a.fam, a.weights, a.gheap, a.out, P, queue, qbase, a.prof);
+  replay_rows<FAM, RowProf>(a.W, a.Wc, a.fam, a.weights, a.gheap, a.out, P, queue, qbase, a.prof,
+                            RowNativeArgs{nullptr, nullptr, nullptr}, kRowsPerWave, a.table);
 }
 #endif
 
@@ -256,13 +258,14 @@ __global__ void k_native_rt_table(uint64_t* out) {
 // latency-bound LLM-sized batches, 4 for large ones).
 __global__ __launch_bounds__(64, 1) void k_replay_rows_native(fksk::BuiltinArgs a, RowNativeArgs nat, int P,
                                                              uint32_t* queue, uint32_t qbase, int rows_active) {
-  replay_rows<kFamNative>(a.W, a.Wc, nullptr, nullptr, a.gheap, a.out, P, queue, qbase, nullptr, nat, rows_active);
+  replay_rows<kFamNative>(a.W, a.Wc, nullptr, nullptr, a.gheap, a.out, P, queue, qbase, nullptr, nat, rows_active,
+                          a.table);
 }
 // s_memtime phase-profiled build (diagnostics): a.prof = [waves, 8] cycles
 __global__ __launch_bounds__(64, 1) void k_replay_rows_native_prof(fksk::BuiltinArgs a, RowNativeArgs nat, int P,
                                                                   uint32_t* queue, uint32_t qbase, int rows_active) {
   replay_rows<kFamNative, RowProf>(a.W, a.Wc, nullptr, nullptr, a.gheap, a.out, P, queue, qbase, a.prof, nat,
-                                   rows_active);
+                                   rows_active, a.table);
 }
 #endif
 

@@ -307,7 +307,7 @@ template <int FAM, class Prof = RowNoProf>
 __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const int32_t* fam, const double* weights,
                             uint64_t* gheap, DevResult* out, int P, uint32_t* queue, uint32_t qbase,
                             uint64_t* prof_out = nullptr, RowNativeArgs nat = RowNativeArgs{nullptr, nullptr, nullptr},
-                            int rows_active = kRowsPerWave) {
+                            int rows_active = kRowsPerWave, double* table = nullptr) {
   constexpr bool kNative = FAM == kFamNative;
   const int ra = kNative ? rows_active : kRowsPerWave;
   // W: the kernel-argument copy, read once for the hot scalars below; every
@@ -644,6 +644,44 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
       o->hash = hsh;
       o->exc = exc;
       o->inexact = inexact;
+    }
+    if (table) {
+      // the evaluator (k_eval_reduce's arithmetic, fused): lane k < 5 turns its
+      // own accumulator into the exact mean (its count is that accumulator's),
+      // the row gathers the five means, and lane c < 13 writes column c
+      double av = 0.0;
+      if (jv < 5 && acc.count > 0)
+        av = fixed_div_round_dev((i128)(((u128)acc.hi << 64) | acc.lo), (uint64_t)acc.count);
+      const uint64_t ab = (uint64_t)__double_as_longlong(av);
+      double avg[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        avg[k] = __longlong_as_double((long long)(((uint64_t)(uint32_t)row_read((int)(ab >> 32), rbase, k) << 32) |
+                                                  (uint32_t)row_read((int)(uint32_t)ab, rbase, k)));
+      double score = 0.0;
+      if (exc == EXC_NONE && n_snap > 0 && n_dropped == 0) {
+        const double overall = (avg[0] + avg[1] + avg[2] + avg[3]) / 4.0;
+        const double pen = avg[4] < 0.1 ? avg[4] : 0.1;
+        double sc = overall - pen;
+        sc = sc < 1.0 ? sc : 1.0;
+        score = sc > 0.0 ? sc : 0.0;
+      }
+      const bool ok = exc == EXC_NONE;   // an aborted replay reports only its exception class
+      double v = 0.0;
+      switch (jv) {
+        case 0: v = score; break;
+        case 1: case 2: case 3: case 4: case 5: v = avg[jv - 1]; break;
+        case 6: v = (double)n_snap; break;
+        case 7: v = (double)n_frag; break;
+        case 8: v = (double)processed; break;
+        case 9: v = (double)n_dropped; break;
+        case 10: v = (double)exc; break;
+        case 11: v = (double)inexact; break;
+        case 12: v = (double)(hsh >> 11); break;
+        default: break;
+      }
+      if (!ok && jv != 10) v = 0.0;
+      if (jv < 13) table[(size_t)p * 13 + jv] = v;
     }
     p = claim();
     have = p < P;

@@ -50,7 +50,7 @@ class ParamIsland:
         i = int(np.argmax(self.elite_scores))
         return self.elites[i], float(self.elite_scores[i])
 
-    def propose(self) -> np.ndarray:
+    def propose(self, n: Optional[int] = None) -> np.ndarray:
         """A generation of candidates, longest predicted replay first.
 
         The device drains a batch through a persistent queue in index order,
@@ -58,7 +58,7 @@ class ParamIsland:
         scheduling) keeps the rows of a wave finishing close together.  A
         mutant is predicted to replay as many events as its parent, a
         crossover as its longer parent; fresh samples (unknown) go first."""
-        n = self.n_candidates
+        n = self.n_candidates if n is None else int(n)
         if len(self.elites) == 0:
             return self.sampler(n, self.rng)
         n_fresh = max(1, int(n * self.fresh_fraction))

@@ -189,28 +189,54 @@ def screen_numpy(X, Wt, R, Rfail, Np: int, chunk: int = 256) -> np.ndarray:
 
 
 class Screener:
-    """Surrogate fitness of composite-family candidates on one recorded trajectory."""
+    """Surrogate fitness of composite-family candidates on one recorded trajectory.
 
-    def __init__(self, w: Workload, reference_weights=None, kind: str = "myopic", device="auto"):
+    ``state_stride`` keeps every k-th recorded state (the surrogate is a sum
+    over states, so a subsample ranks candidates almost identically at 1/k of
+    the MFMA work).  On a HIP device the features / rewards are uploaded once
+    (``_fks_hip.ScreenDevice``) and every `score` call moves only the
+    candidates' weights and their fitness."""
+
+    def __init__(self, w: Workload, reference_weights=None, kind: str = "myopic", device="auto",
+                 state_stride: int = 1):
         self.workload = w
-        self.states = record_states(w, "composite_linear", reference_weights)
+        st = record_states(w, "composite_linear", reference_weights)
+        if state_stride > 1:
+            keep = np.arange(0, st.n_states, int(state_stride))
+            st = RecordedStates(st.pod[keep], st.decision[keep], st.cpu_left[keep], st.mem_left[keep],
+                                st.gpu_left[keep], st.gml[keep])
+        self.states = st
         self.Np = _pad_nodes(w.cluster.n_nodes)
         self.X = composite_features(w, self.states)
         self.R, self.Rfail = rewards(w, self.states, kind)
         self.device = None
+        self._dev = None
         if device != "cpu":
             from . import hip_engine
             if hip_engine.device_available():
                 self.device = 0 if device == "auto" else int(device)
+                self._dev = hip_engine.native().ScreenDevice(self.X, self.R, self.Rfail, self.Np, self.device)
             elif device not in ("auto",):
                 raise RuntimeError("HIP device requested but none is visible")
+
+    @property
+    def n_states(self) -> int:
+        return self.states.n_states
 
     def score(self, weights: np.ndarray) -> np.ndarray:
         P = np.atleast_2d(weights).shape[0]
         Wt = weights_matrix(weights)
-        if self.device is not None:
-            from .hip_engine import native
-            fit = native().screen_linear(self.X, Wt, self.R, self.Rfail, self.Np, self.device)
+        if self._dev is not None:
+            fit = self._dev.score(Wt)
         else:
             fit = screen_numpy(self.X, Wt, self.R, self.Rfail, self.Np)
         return np.asarray(fit[:P], dtype=np.float64)
+
+    def select(self, weights: np.ndarray, keep: int) -> np.ndarray:
+        """Indices of the `keep` best-screened candidates, in their input order
+        (the proposer's longest-replay-first order survives the filter)."""
+        fit = self.score(weights)
+        if keep >= len(fit):
+            return np.arange(len(fit))
+        top = np.argpartition(-fit, keep - 1)[:keep]
+        return np.sort(top)
