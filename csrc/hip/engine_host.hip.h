@@ -25,6 +25,8 @@
 #include <pybind11/pybind11.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -751,6 +753,9 @@ class DeviceEngine {
     s.fused_table = true;
     const RowNativeArgs nat{s.h_in.dev<const uint64_t>(), s.kc.as<const int64_t>(),
                             reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + fn_bytes)};
+    if (std::getenv("FKS_DEBUG_LAUNCH"))
+      std::fprintf(stderr, "[fks] native rows: P=%d rows=%d waves=%d T=%d lds=%zu qbase=%u stream=%p\n", P, ra, waves, T,
+                   lds, s.qbase, (void*)s.stream);
     HIP_OK(fksk::launch_native_rows(P, waves, ra, s.queue.as<uint32_t>(), s.qbase, lds, s.stream, a, nat));
     s.qbase += (uint32_t)P + (uint32_t)waves * (uint32_t)ra;   // every active row makes one final, empty claim
     last_native_rows_ = ra;

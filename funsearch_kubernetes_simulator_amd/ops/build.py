@@ -105,10 +105,21 @@ def build_hip(force: bool = False, jobs: int = 0) -> Path:
     return target
 
 
+def _report(target: Path, before: float) -> None:
+    """One line per extension: compiled now, or reused (its sources are older)."""
+    after = target.stat().st_mtime if target.exists() else -1.0
+    state = "compiled" if after != before else "up to date (sources older than the .so), reused"
+    print(f"[fks build] {target.name}: {state}", flush=True)
+
+
 def build_all(force: bool = False) -> None:
-    build_cpu(force)
+    targets = [(build_cpu, NATIVE_DIR / f"_fks_cpu{_ext_suffix()}")]
     if (CSRC_DIR / "hip" / "module.hip").exists():
-        build_hip(force)
+        targets.append((build_hip, NATIVE_DIR / f"_fks_hip{_ext_suffix()}"))
+    for fn, target in targets:
+        before = target.stat().st_mtime if target.exists() else -1.0
+        fn(force)
+        _report(target, before)
 
 
 if __name__ == "__main__":

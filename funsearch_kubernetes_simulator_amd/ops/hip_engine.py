@@ -16,6 +16,8 @@ from __future__ import annotations
 import heapq
 import math
 import os
+import threading
+import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -206,6 +208,7 @@ class DeviceEvaluator:
         self.options = options
 
         self._jit = None
+        self._jit_lock = threading.Lock()
         self._native_post: Dict[int, Tuple[int, np.ndarray]] = {}   # slot -> (P, native row indices)
 
     def info(self) -> dict:
@@ -214,9 +217,16 @@ class DeviceEvaluator:
     # -- natively compiled programs (policy/native_codegen.py, ops/jit.py) ------------------
     @property
     def native_compiler(self):
+        # Created once, under a lock: island threads submit their first batches
+        # concurrently, and a second compiler instance would replace the first
+        # one -- whose JIT modules (hipModuleUnload on collection) the first
+        # thread's kernels are still executing.
         if self._jit is None:
-            from .jit import NativeCompiler
-            self._jit = NativeCompiler(self._eng, self.device, budget=int(self.options.get("budget") or DEFAULT_CALL_BUDGET))
+            with self._jit_lock:
+                if self._jit is None:
+                    from .jit import NativeCompiler
+                    self._jit = NativeCompiler(self._eng, self.device,
+                                               budget=int(self.options.get("budget") or DEFAULT_CALL_BUDGET))
         return self._jit
 
     def submit_native(self, slot: int, progs: Sequence[CompiledPolicy]):
@@ -226,6 +236,13 @@ class DeviceEvaluator:
         Returns the `NativeBatch` (compile time, cache hits, reasons)."""
         batch = self.native_compiler.prepare(progs)
         idx = np.flatnonzero(batch.ok)
+        dump = os.environ.get("FKS_DUMP_BATCHES")
+        if dump and idx.size:
+            # diagnostics: every native launch's program texts, written before the launch
+            import json
+            with open(dump, "a") as f:
+                f.write(json.dumps({"slot": slot, "t": time.time(), "P": int(idx.size),
+                                    "codes": [progs[i].source for i in idx]}) + "\n")
         self._native_post[slot] = (len(progs), idx)
         if idx.size:
             self._eng.submit_native(slot, batch.fn[idx], batch.kc, batch.koff[idx])

@@ -114,6 +114,27 @@ def test_scaled_synthetic_256_nodes_matches_cpu():
         assert np.array_equal(gpu, cpu), family
 
 
+def test_config5_full_shape_matches_cpu():
+    """BASELINE config 5 at its full shape (65,536 pods / 256 nodes: NPASS = 4,
+    HBM heaps of 64k entries): device == CPU oracle for built-in, linear-family
+    and natively compiled reference programs."""
+    from funsearch_kubernetes_simulator_amd.core import synthetic_workload
+    from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
+    w = synthetic_workload(n_nodes=256, n_pods=65536, seed=0)
+    dev = he.DeviceEvaluator(w)
+    assert dev.info()["npass"] == 4
+    for family in ("first_fit", "best_fit", "composite_linear"):
+        W = fam.SAMPLERS[family](8, np.random.default_rng(11)) if family in fam.SAMPLERS else None
+        gpu = dev.evaluate_builtin(family, W, n=8)
+        cpu = ce.simulate_builtin_batch(w, family, fam.pad_weights(W) if W is not None else np.zeros((8, 16)))
+        assert np.array_equal(gpu, cpu), family
+        assert np.all(gpu[:, 8] > 65536)   # every pod replayed (creations + deletions + retries)
+    from funsearch_kubernetes_simulator_amd.models.library import reference_policies
+    from funsearch_kubernetes_simulator_amd.policy.compiler import compile_policy
+    progs = [compile_policy(c) for c in reference_policies().values()]
+    assert np.array_equal(dev.evaluate_native(progs), ce.simulate_program_batch(w, progs))
+
+
 # ---- row kernel: 4 policies per wave (clusters of <= 16 nodes) --------------------------
 
 def test_row_kernel_is_default_for_16_nodes(dev):

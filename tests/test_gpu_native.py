@@ -100,3 +100,39 @@ def test_engine_routes_small_batches_to_native(default_workload):
     assert [r.engine for r in res] == ["hip-native"] * 3
     ref = reference_scores()
     assert [r.score for r in res] == [ref[k] for k in list(reference_policies())[:3]]
+
+
+def test_concurrent_first_submits_share_one_compiler(default_workload):
+    """Island threads start their first native batches at the same moment on a
+    fresh evaluator (a resumed run evaluates nothing before them): they must
+    share one JIT compiler -- a second instance would replace the first and
+    unload the modules the first thread's kernels are running (a device fault
+    at the first launch of every resumed config-3 run, before the fix)."""
+    import threading
+    from funsearch_kubernetes_simulator_amd.bench.programs import mutation_children
+    from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
+    dev = he.DeviceEvaluator(default_workload, n_slots=4)
+    batches = [mutation_children(6, seed=40 + k) for k in range(4)]
+    barrier = threading.Barrier(4)
+    compilers, out, errs = [None] * 4, [None] * 4, []
+
+    def run(k):
+        try:
+            barrier.wait()
+            dev.submit_native(k, batches[k])
+            compilers[k] = dev.native_compiler
+            out[k] = dev.wait(k)
+        except Exception as exc:   # surfaced below
+            errs.append(repr(exc))
+
+    threads = [threading.Thread(target=run, args=(k,)) for k in range(4)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errs, errs
+    assert all(c is compilers[0] for c in compilers)
+    for k in range(4):
+        ok = out[k][:, 10] != Exc.UNSUPPORTED
+        cpu = ce.simulate_program_batch(default_workload, batches[k])
+        assert np.array_equal(out[k][ok], cpu[ok])
