@@ -56,6 +56,8 @@ def main() -> None:
     ap.add_argument("--migrants", type=int, default=8)
     ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"])
     ap.add_argument("--heap-mode", default="auto", choices=["auto", "lds", "hbm"])
+    ap.add_argument("--heap-top", type=int, default=-1,
+                    help="wave kernel (> 16 nodes): heap slots kept in LDS per policy (2^k - 1; -1: auto)")
     ap.add_argument("--row-wave-share", type=float, default=1.0,
                     help="fraction of the chip's resident waves one island launch takes (row kernel)")
     ap.add_argument("--seed", type=int, default=1234)
@@ -102,8 +104,10 @@ def main() -> None:
     else:
         device = "cpu"
     # the per-event trace hash only serves cross-engine equality tests: off here
-    ev = Evaluator(workload, device=device, options={"heap_mode": args.heap_mode, "trace_hash": False,
-                                                     "row_wave_share": args.row_wave_share},
+    opts = {"heap_mode": args.heap_mode, "trace_hash": False, "row_wave_share": args.row_wave_share}
+    if args.heap_top >= 0:
+        opts["heap_top"] = args.heap_top
+    ev = Evaluator(workload, device=device, options=opts,
                    n_slots=max(1, args.islands))
     if args.device == "gpu" and ev.device is None:
         raise SystemExit("no HIP device visible")
