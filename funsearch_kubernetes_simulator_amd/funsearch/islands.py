@@ -59,6 +59,10 @@ class IslandFunSearch:
         self.polish_every = int(pol.get("every", 0))
         self.polish_variants = int(pol.get("variants", 1024))
         self.polish_rounds = int(pol.get("rounds", 3))
+        # repeat: polish the island champion at every due generation with fresh
+        # random variants, even when it has been polished before (a (1 + lambda)
+        # strategy over its constants that keeps running on the device)
+        self.polish_repeat = bool(pol.get("repeat", False))
         self._polished = set()
         # islands step independently (LLM / JIT / device stages overlap across islands)
         self.pipeline = bool(isl.get("pipeline", False))
@@ -227,17 +231,24 @@ class IslandFunSearch:
                 s.best_score, s.best_policy = res.score, code
         s.population = sorted(elites + new, key=lambda x: x[1], reverse=True)[:s.population_size]
 
-    def maybe_polish(self, i: int) -> Optional[dict]:
+    def polish_due(self, i: int) -> bool:
+        s = self.islands[i]
+        if not self.polish_every or s.generation % self.polish_every or not s.population:
+            return False
+        code, _ = max(s.population, key=lambda x: x[1])
+        return self.polish_repeat or code not in self._polished
+
+    def maybe_polish(self, i: int, log: bool = True) -> Optional[dict]:
         """Every ``polish.every`` generations: tune the numeric literals of island
         i's best program with one batched device search (thousands of constant
         settings, one JIT compile), re-score the rewritten text through the normal
-        evaluation path, and put it into the population if it is better."""
+        evaluation path, and put it into the population if it is better.  Runs
+        on the island's own HIP slot (the pipelined loop calls it from a worker
+        thread, so the other islands keep stepping meanwhile)."""
+        if not self.polish_due(i):
+            return None
         s = self.islands[i]
-        if not self.polish_every or s.generation % self.polish_every or not s.population:
-            return None
         code, score = max(s.population, key=lambda x: x[1])
-        if code in self._polished:
-            return None
         self._polished.add(code)
         from .polish import polish
         slot = i % max(1, self._n_slots())
@@ -257,7 +268,8 @@ class IslandFunSearch:
                     s.best_score, s.best_policy = exact.score, res.code
                 self._polished.add(res.code)
         self.evaluations += res.evaluated
-        self.log.write(**rec)
+        if log:
+            self.log.write(**rec)
         return rec
 
     def run_pipelined(self, generations: int, threshold: float) -> None:
@@ -356,7 +368,6 @@ class IslandFunSearch:
                         self._merge(s, plan[i][0], children, results)
                         self.evaluations += len(children)
                         gen[i] += 1
-                        self.maybe_polish(i)
                         st = stamp[i]
                         rec = dict(kind="island_generation", rank=self.ctx.rank, island=i, generation=gen[i],
                                    children=len(children), best=round(s.best_score, 6),
@@ -376,6 +387,22 @@ class IslandFunSearch:
                         if agg["islands"] == k:
                             self._finish_generation(gen[i], global_rec.pop(gen[i]), busy_total, busy_since,
                                                     t_start, threshold, stop)
+                        if self.polish_due(i):
+                            # constant polish on the island's slot, in a worker: the
+                            # other islands keep stepping; this island resumes after it
+                            fut[i] = pool.submit(self.maybe_polish, i, False)
+                            inflight[i] = True
+                            set_busy()
+                            phase[i] = "polish"
+                        else:
+                            phase[i] = "idle"
+                        progressed = True
+                    elif phase[i] == "polish" and fut[i].done():
+                        rec = fut[i].result()
+                        if rec:
+                            self.log.write(**rec)
+                        inflight[i] = False
+                        set_busy()
                         phase[i] = "idle"
                         progressed = True
                 if all(phase[i] == "idle" and (gen[i] >= target or stop[0]) for i in range(k)):

@@ -316,3 +316,23 @@ def test_islands_with_constant_polish(tmp_path):
     for r in pol:
         if "rescored" in r:
             assert r["rescored"] == r["polished"]
+
+
+def test_pipelined_polish_repeats_and_runs_in_the_island_pipeline(tmp_path):
+    """polish.repeat: the champion is polished again at every due generation
+    (fresh random variants), asynchronously inside the island's own pipeline
+    step: every island still completes every generation, the polish records
+    land in the log, and the evaluation count includes the variants."""
+    from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
+    cfg = _cfg(tmp_path)
+    cfg["islands"] = {"per_rank": 2, "migrate_every": 2, "migrants": 1, "pipeline": True}
+    cfg["polish"] = {"every": 1, "variants": 4, "rounds": 1, "repeat": True}
+    cfg["checkpoint"] = {}
+    fs = IslandFunSearch(cfg)
+    fs.run(3)
+    assert fs.generation == 3
+    recs = [json.loads(l) for l in open(tmp_path / "log.jsonl")]
+    pol = [r for r in recs if r["kind"] == "polish"]
+    assert len(pol) == 6                        # 2 islands x 3 generations, champions repeated
+    assert len([r for r in recs if r["kind"] == "island_generation"]) == 6
+    assert fs.evaluations >= sum(r["evaluated"] for r in pol)

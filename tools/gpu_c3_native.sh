@@ -4,11 +4,13 @@
 set -o pipefail
 export PYTHONPATH=$PWD
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+CFG=${CFG:-configs/config3_native.json}
+RUN=${RUN:-runs/config3_native}
 mkdir -p gpurun_out/c3n
-cp runs/config3_native/islands_rank0.json runs/config3_native/metrics.jsonl gpurun_out/c3n/ 2>/dev/null
+cp $RUN/islands_rank0.json $RUN/metrics.jsonl gpurun_out/c3n/ 2>/dev/null
 G=${G:-100}
 T=${T:-1100}
-timeout -k 10 $T python -u -m funsearch_kubernetes_simulator_amd.funsearch --config configs/config3_native.json \
+timeout -k 10 $T python -u -m funsearch_kubernetes_simulator_amd.funsearch --config $CFG \
   --generations $G --resume --checkpoint-dir gpurun_out/c3n --log gpurun_out/c3n/metrics.jsonl \
   --save gpurun_out/c3n/top5.json > gpurun_out/c3n/run.log 2>&1
 rc=$?
