@@ -36,10 +36,11 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu", action="store_true", help="also time the CPU VM on the same programs")
     ap.add_argument("--single", type=int, default=0, help="also time K programs one per launch (replay latency)")
+    ap.add_argument("--options", default="{}", help="DeviceEvaluator options (JSON), e.g. '{\"row_kernel\": \"off\"}'")
     a = ap.parse_args()
     from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
     w = load_default_workload()
-    dev = he.DeviceEvaluator(w)
+    dev = he.DeviceEvaluator(w, options=json.loads(a.options))
     threads = a.threads or ce.default_threads()
     progs = children(a.batch * a.batches, a.seed)
     # warm the compiler / module loader (first hipModuleLoadData, clang page-in)
