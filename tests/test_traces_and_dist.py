@@ -228,3 +228,16 @@ def test_scaling_harness_cpu():
     summary = json.loads(r.stdout.strip().splitlines()[-1])["scaling"]
     assert [s["n_gpus"] for s in summary] == [1, 2]
     assert all(s["value"] > 0 for s in summary) and summary[0]["efficiency"] == 1.0
+
+
+def test_config4_launcher_two_gloo_ranks(tmp_path):
+    """tools/run_config4.sh (BASELINE config 4: one island per rank, RCCL elite
+    migration, torchrun --max-restarts + --resume) rehearsed with 2 gloo ranks."""
+    env = dict(os.environ, NPROC="2", GENS="2", RUN_DIR=str(tmp_path / "c4"), FKS_DIST_BACKEND="gloo",
+               PORT=str(34000 + os.getpid() % 1000), OMP_NUM_THREADS="1", GLOO_SOCKET_IFNAME="lo")
+    r = subprocess.run(["bash", os.path.join(REPO, "tools", "run_config4.sh")], env=env, capture_output=True,
+                       text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["ranks"] == 2 and out["islands_per_rank"] == 1 and out["generations"] == 2
+    assert (tmp_path / "c4" / "metrics.rank1.jsonl").exists()
