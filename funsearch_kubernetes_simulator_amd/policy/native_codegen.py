@@ -87,10 +87,75 @@ class CodegenError(ValueError):
     """The bytecode has a shape the native backend does not lower."""
 
 
+def _literal_slots(prog: CompiledPolicy) -> set:
+    """Pool entries that hold source literals (the data of a shape); the rest
+    are compiler-generated (loop start / step, ...) and fixed by the code."""
+    return {int(lit[0]) for lit in getattr(prog, "literals", ()) or ()}
+
+
+def _all_list_at(code, flow) -> List[set]:
+    """Must-analysis over the bytecode CFG: for every pc, the registers that hold
+    ``node.gpus`` unchanged on every path reaching it (defined by GLIST_ALL, or a
+    MOV of such a register, and not overwritten since).  For those lists an
+    element is its own index and the length is the GPU count, so ``for g in
+    node.gpus`` loops index the GPU fields with the (wave-uniform) loop counter
+    instead of unpacking the 4-bit list."""
+    n = len(code)
+    succ: List[List[int]] = []
+    for pc, (op, d, a, b, imm) in enumerate(code):
+        if op == Op.IF:
+            nxt = [pc + 1, imm + 1]
+        elif op in (Op.ELSE, Op.LOOP_NEXT):
+            nxt = [imm]
+        elif op == Op.LOOP_TEST:
+            nxt = [pc + 1, imm]
+        elif op == Op.BREAK:
+            nxt = [flow["break"][pc]]
+        elif op == Op.CONTINUE:
+            nxt = [flow["continue"][pc]]
+        elif op in (Op.RET, Op.RAISE, Op.END):
+            nxt = []
+        else:
+            nxt = [pc + 1]
+        succ.append([x for x in nxt if 0 <= x < n])
+    TOP = None   # "every register" (not yet reached)
+    state_in: List[object] = [TOP] * n
+    state_in[0] = frozenset()
+    work = [0]
+    while work:
+        pc = work.pop()
+        cur = state_in[pc]
+        op, d, a, b, imm = code[pc]
+        out = set(cur)
+        if d != NO_REG:
+            if op == Op.GLIST_ALL or (op == Op.MOV and a in cur):
+                out.add(d)
+            else:
+                out.discard(d)
+        out = frozenset(out)
+        for t in succ[pc]:
+            old = state_in[t]
+            new = out if old is TOP else (old & out)
+            if new != old:
+                state_in[t] = new
+                work.append(t)
+    return [set() if x is TOP else set(x) for x in state_in]
+
+
+def _inline_constants(prog: CompiledPolicy) -> List[Tuple[int, int, float, int]]:
+    lits = _literal_slots(prog)
+    return [(k, int(prog.ctag[k]), float(prog.fconst[k]), int(prog.iconst[k])) for k in range(len(prog.ctag))
+            if k not in lits]
+
+
 def shape_key(prog: CompiledPolicy) -> str:
-    """Programs with equal keys share one compiled function (constants are data)."""
+    """Programs with equal keys share one compiled function: source literals are
+    data (read from the constant block), so programs that differ only in them
+    share a shape; compiler-generated constants are immediates in the code and
+    part of the key."""
     h = hashlib.sha1(prog.code)
     h.update(bytes(prog.ctag))
+    h.update(repr(_inline_constants(prog)).encode())
     return h.hexdigest()
 
 
@@ -237,7 +302,9 @@ def program_source(prog: CompiledPolicy, name: str, lift_consts: bool = True) ->
     if lift_consts and 1 + len(prog.ctag) > KC_LDS:
         raise CodegenError(f"{len(prog.ctag)} constants > {KC_LDS - 1} (the LDS constant block)")
     code = unpack_code(prog.code)
+    literal_slots = _literal_slots(prog)
     flow = _loop_structure(code)
+    all_lists_at = _all_list_at(code, flow)
     types = infer_types(code, flow, prog.ctag)
     regs = set()
     for op, d, a, b, imm in code:
@@ -313,7 +380,9 @@ def program_source(prog: CompiledPolicy, name: str, lift_consts: bool = True) ->
             continue
         if op == Op.CONST:
             fl = prog.ctag[imm] == TAG_FLOAT
-            if lift_consts:
+            # source literals come from the constant block; compiler-generated
+            # constants (loop start / step, ...) are immediates the optimiser sees
+            if lift_consts and imm in literal_slots:
                 w(f"  {R(d)} = PyN{{kc[{1 + imm}], {'true' if fl else 'false'}}};")
             elif fl:
                 bits = struct.unpack("<q", struct.pack("<d", prog.fconst[imm]))[0]
@@ -339,9 +408,16 @@ def program_source(prog: CompiledPolicy, name: str, lift_consts: bool = True) ->
         elif op == Op.GLIST_ALL:
             w(f"  {R(d)} = pi(glist_all(n_ngpus));")
         elif op == Op.GLIST_LEN:
-            w(f"  {R(d)} = pi({R(a)}.b & 0xF);")
+            if a in all_lists_at[pc]:
+                w(f"  {R(d)} = pi((int64_t)n_ngpus);")
+            else:
+                w(f"  {R(d)} = pi({R(a)}.b & 0xF);")
         elif op == Op.GLIST_GET:
-            w(f"  {{ const int e_ = glist_get({R(a)}, {R(b)}, {R(d)}); if (e_) {RAISE('e_')} }}")
+            if a in all_lists_at[pc]:   # node.gpus[i] is GPU i (glist_get's checks, no unpacking)
+                w(f"  if ({R(b)}.fl) {RAISE('EXC_TYPE')} else {{ const int64_t k_ = {R(b)}.b < 0 ? {R(b)}.b + n_ngpus : "
+                  f"{R(b)}.b; if (k_ < 0 || k_ >= n_ngpus) {RAISE('EXC_INDEX')} else {R(d)} = pi(k_); }}")
+            else:
+                w(f"  {{ const int e_ = glist_get({R(a)}, {R(b)}, {R(d)}); if (e_) {RAISE('e_')} }}")
         elif op == Op.GLIST_SLICE:
             lo = R(b) if b != NO_REG else "pi(0)"
             hi = R(imm) if imm != NO_REG else "pi(0)"

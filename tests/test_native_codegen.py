@@ -58,3 +58,23 @@ def test_module_source_compiles_for_host(tmp_path):
     assert (tmp_path / "m.so").exists()
     src = module_source(progs)
     assert "fks_jit_table" in src and src.count("extern \"C\" __device__ __noinline__ int64_t fks_prog_") == 8
+
+
+def test_node_gpus_index_specialisation_matches_vm(default_workload):
+    """`for g in node.gpus` / `node.gpus[i]` on an unmodified GPU list are lowered
+    to direct GPU indices (no 4-bit list unpacking): negative indices, index
+    errors, len() and lists rebuilt in a branch must behave exactly as the VM."""
+    srcs = [
+        "def priority_function(pod, node):\n    return len(node.gpus) * 10 + node.gpus[-1].gpu_milli_left if node.gpus else 1\n",
+        "def priority_function(pod, node):\n    gs = node.gpus\n    s = 0\n    for i in range(len(gs)):\n"
+        "        s += gs[i].gpu_milli_left * (i + 1)\n    return s\n",
+        "def priority_function(pod, node):\n    return node.gpus[3].gpu_milli_left + 1\n",        # IndexError on small nodes
+        "def priority_function(pod, node):\n    gs = node.gpus\n    if pod.num_gpu > 1:\n        gs = gs[1:]\n"
+        "    t = 0\n    for g in gs:\n        t += g.gpu_milli_left\n    return t + len(gs)\n",
+        "def priority_function(pod, node):\n    best = 0\n    for g in node.gpus:\n        for h in node.gpus:\n"
+        "            best = max(best, g.gpu_milli_left - h.gpu_milli_left)\n    return best + 1\n",
+    ]
+    progs = [compile_policy(s) for s in srcs]
+    nat = ce.simulate_native_batch(default_workload, progs, threads=4)
+    vm = ce.simulate_program_batch(default_workload, progs, threads=4)
+    assert np.array_equal(nat, vm)
