@@ -81,8 +81,11 @@ class IslandFunSearch:
             opts["fault_seed"] = int(fi.get("seed", 0))
         if fi.get("llm_failure_rate"):
             self.config.setdefault("llm", {})["fault_rate"] = float(fi["llm_failure_rate"])
-        # one HIP stream (slot) per island, so pipelined islands never share one
-        self.evaluator = evaluator or Evaluator(device=dev, options=opts, n_slots=max(4, self.n_islands))
+        # one HIP stream (slot) per island, so pipelined islands never share one,
+        # plus one for the family coupler (funsearch/coupling.py)
+        cpl = dict(self.config.get("coupling") or {})
+        self.evaluator = evaluator or Evaluator(device=dev, options=opts,
+                                                n_slots=max(4, self.n_islands) + (1 if cpl.get("every") else 0))
         llm_cfg = dict(self.config.get("llm") or {})
         base_seed = int(llm_cfg.get("seed", 0)) + 1000003 * self.ctx.rank
         self.islands: List[SimpleFunSearch] = []
@@ -106,6 +109,11 @@ class IslandFunSearch:
         ck = self.config.get("checkpoint") or {}
         self.ck_dir = ck.get("dir")
         self.ck_every = int(ck.get("every", 0))
+        self.coupler = None
+        if cpl.get("every"):
+            from .coupling import FamilyCoupler
+            self.coupler = FamilyCoupler(self.evaluator, cpl, slot=self._n_slots() - 1,
+                                         seed=int(cpl.get("seed", 0)) + 7907 * self.ctx.rank)
 
     # -- helpers --------------------------------------------------------------------------
     @property
@@ -154,6 +162,9 @@ class IslandFunSearch:
             s.population = sorted(elites + new, key=lambda x: x[1], reverse=True)[:s.population_size]
         for i in range(len(self.islands)):
             self.maybe_polish(i)
+        if self.coupler is not None and self.coupler.due(self.generation):
+            for rec in self.run_coupling():
+                self.inject_coupled(rec)
         if self.migrate_every and self.generation % self.migrate_every == 0:
             with roctx_range(f"funsearch.migrate gen {self.generation}"):
                 self._collective("migrate", self.migrate, None)
@@ -231,6 +242,42 @@ class IslandFunSearch:
                 s.best_score, s.best_policy = res.score, code
         s.population = sorted(elites + new, key=lambda x: x[1], reverse=True)[:s.population_size]
 
+    # -- family coupling (funsearch/coupling.py) -----------------------------------------------
+    def run_coupling(self) -> List[dict]:
+        """One coupler round: family search on the device, champion rendered as
+        program text and re-scored exactly.  Safe to run in a worker thread
+        (touches no island population)."""
+        with roctx_range(f"funsearch.coupling round {self.coupler.rounds}"):
+            return self.coupler.round()
+
+    def inject_coupled(self, rec: dict, idle: Optional[List[int]] = None) -> Optional[int]:
+        """Put a coupled family champion into the island with the lowest best
+        score (among `idle`); returns the island index, or None if every
+        candidate island already holds the program or would drop it."""
+        cand = list(range(len(self.islands))) if idle is None else list(idle)
+        if not cand:
+            return None
+        i = min(cand, key=lambda k: self.islands[k].best_score)
+        s = self.islands[i]
+        code, score = rec["code"], float(rec["score"])
+        known = {c for c, _ in s.population}
+        accepted = code not in known and (len(s.population) < s.population_size
+                                          or score > min(sc for _, sc in s.population))
+        if accepted:
+            s.population = sorted(s.population + [(code, score)], key=lambda x: x[1],
+                                  reverse=True)[:s.population_size]
+            if score > s.best_score:
+                s.best_score, s.best_policy = score, code
+        self.evaluations += 1
+        self.log.write(kind="coupling", rank=self.ctx.rank, island=i, generation=s.generation,
+                       family=rec["family"], family_score=rec["family_score"], score=score,
+                       accepted=accepted, coupler_rounds=self.coupler.rounds,
+                       coupler_evaluated=self.coupler.evaluated, coupler_s=round(self.coupler.seconds, 3))
+        if self.verbose and self.ctx.is_main:
+            print(json.dumps(dict(kind="coupling", island=i, family=rec["family"], score=score,
+                                  accepted=accepted)), flush=True)
+        return i if accepted else None
+
     def polish_due(self, i: int) -> bool:
         s = self.islands[i]
         if not self.polish_every or s.generation % self.polish_every or not s.population:
@@ -298,6 +345,7 @@ class IslandFunSearch:
         t_start = time.time()
         inflight = [False] * k
         global_rec = {}   # generation -> partial aggregate
+        cpl = {"fut": None, "inbox": [], "last": self.generation}
 
         def set_busy():
             now = time.time()
@@ -330,6 +378,22 @@ class IslandFunSearch:
                     with roctx_range(f"funsearch.migrate gen {gen[0]}"):
                         self._collective("migrate", self.migrate, None)
                     self._last_migration = gen[0]
+                if self.coupler is not None:
+                    # the family coupler runs on its own slot in a worker; its
+                    # champions wait in an inbox until an island is idle
+                    if cpl["fut"] is not None and cpl["fut"].done():
+                        cpl["inbox"].extend(cpl["fut"].result())
+                        cpl["fut"] = None
+                        progressed = True
+                    g_min = min(gen)
+                    if (cpl["fut"] is None and g_min > cpl["last"] and self.coupler.due(g_min)
+                            and g_min < target and not stop[0]):
+                        cpl["last"] = g_min
+                        cpl["fut"] = pool.submit(self.run_coupling)
+                    idle = [j for j in range(k) if phase[j] == "idle"]
+                    while cpl["inbox"] and idle:
+                        self.inject_coupled(cpl["inbox"].pop(0), idle)
+                        progressed = True
                 for i in range(k):
                     s = self.islands[i]
                     if phase[i] == "idle":
@@ -405,7 +469,8 @@ class IslandFunSearch:
                         set_busy()
                         phase[i] = "idle"
                         progressed = True
-                if all(phase[i] == "idle" and (gen[i] >= target or stop[0]) for i in range(k)):
+                if (all(phase[i] == "idle" and (gen[i] >= target or stop[0]) for i in range(k))
+                        and cpl["fut"] is None and not cpl["inbox"]):
                     break
                 if not progressed:
                     time.sleep(0.0005)
@@ -474,6 +539,8 @@ class IslandFunSearch:
         state = {"format": "fks-islands-checkpoint-v1", "generation": self.generation,
                  "rank": self.ctx.rank, "world_size": self.ctx.world_size,
                  "evaluations": self.evaluations, "islands": [s.state_dict() for s in self.islands]}
+        if self.coupler is not None:
+            state["coupling"] = self.coupler.state_dict()
         tmp = path + ".tmp"
         with open(tmp, "w") as fh:
             json.dump(state, fh)
@@ -491,7 +558,8 @@ class IslandFunSearch:
             s.generation = int(ss["generation"])
             s.population = [(p["code"], float(p["score"])) for p in ss["population"]]
             s.best_policy, s.best_score = ss["best_policy"], float(ss["best_score"])
-
+        if self.coupler is not None and st.get("coupling"):
+            self.coupler.load_state_dict(st["coupling"])
 
     def load_elastic(self, ck_dir: str) -> bool:
         """Resume from the newest complete checkpoint set in `ck_dir`, whatever
@@ -518,6 +586,9 @@ class IslandFunSearch:
         gen, ws = max(complete or sets)
         saved = sets[(gen, ws)]
         own = saved.get(self.ctx.rank)
+        cst = (own or saved[min(saved)]).get("coupling")
+        if self.coupler is not None and cst:
+            self.coupler.load_state_dict(cst)
         if ws == self.ctx.world_size and own is not None and len(own["islands"]) == len(self.islands):
             self.generation = gen
             self.evaluations = int(own.get("evaluations", 0))

@@ -336,3 +336,37 @@ def test_pipelined_polish_repeats_and_runs_in_the_island_pipeline(tmp_path):
     assert len(pol) == 6                        # 2 islands x 3 generations, champions repeated
     assert len([r for r in recs if r["kind"] == "island_generation"]) == 6
     assert fs.evaluations >= sum(r["evaluated"] for r in pol)
+
+
+@pytest.mark.parametrize("pipe", [False, True])
+def test_family_coupling_feeds_program_islands(tmp_path, pipe):
+    """coupling.every: a parametric family search (the reference's
+    `_create_random_policy` family) runs beside the program islands; its
+    champion is rendered as program text, re-scored through the normal program
+    path (bit-identical to the family score) and injected into the island with
+    the lowest best score; the coupler's state survives a checkpoint."""
+    from funsearch_kubernetes_simulator_amd.engine import Evaluator
+    from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
+    cfg = _cfg(tmp_path)
+    cfg["islands"] = {"per_rank": 2, "migrate_every": 0, "migrants": 1, "pipeline": pipe}
+    cfg["coupling"] = {"every": 1, "generations": 1, "candidates": 24, "elite": 4,
+                       "families": ["random_linear"]}
+    cfg["checkpoint"] = {"dir": str(tmp_path / "ck"), "every": 1}
+    fs = IslandFunSearch(cfg)
+    fs.run(2)
+    recs = [json.loads(l) for l in open(tmp_path / "log.jsonl")]
+    cp = [r for r in recs if r["kind"] == "coupling"]
+    assert cp and all(r["family"] == "random_linear" for r in cp)
+    assert all(r["score"] == r["family_score"] for r in cp)    # program text == family member, exactly
+    assert fs.coupler.rounds >= 1 and fs.coupler.evaluated >= 24
+    acc = [r for r in cp if r["accepted"]]
+    if acc:
+        pops = {c for s in fs.islands for c, _ in s.population}
+        assert any("node.cpu_milli_left *" in c for c in pops)
+    # checkpoint round trip of the coupler state
+    fs.save_checkpoint()
+    fs2 = IslandFunSearch(cfg, evaluator=Evaluator(device="cpu"))
+    assert fs2.load_elastic(str(tmp_path / "ck"))
+    isl1, isl2 = fs.coupler.islands["random_linear"], fs2.coupler.islands["random_linear"]
+    assert fs2.coupler.rounds == fs.coupler.rounds
+    assert (isl1.elite_scores == isl2.elite_scores).all() and (isl1.elites == isl2.elites).all()
