@@ -79,12 +79,18 @@ __host__ __device__ inline int lds_vreg_offset(int n_pods) {
   return lds_heap_entries(n_pods) + lds_delmap_words(n_pods) / 2;
 }
 
-// Per-lane view of node state handed to a scorer.
+// Per-lane view of node state handed to a scorer.  A node's GPUs are one
+// model (one CSV row per node in the trace format), so their milli totals are
+// one value per node (`gmt1`; the host checks it): 1 register per node slot
+// instead of kGmax -- 28 VGPRs on 256-node clusters, the difference between 2
+// and 3 waves per SIMD there.  gt(ps, j) is the per-GPU view (0 past ngpus,
+// like the zero padding of the host table).
 template <int NPASS>
 struct NodeRegs {
   int32_t cpu_left[NPASS], mem_left[NPASS], gpu_left[NPASS];
   int32_t cpu_total[NPASS], mem_total[NPASS], ngpus[NPASS];
-  int32_t gml[NPASS][kGmax], gmt[NPASS][kGmax];
+  int32_t gml[NPASS][kGmax], gmt1[NPASS];
+  __device__ __forceinline__ int32_t gt(int ps, int j) const { return j < ngpus[ps] ? gmt1[ps] : 0; }
 };
 
 struct PodView {
@@ -204,7 +210,7 @@ __device__ bool invariants_hold(const DevWorkload& W, const WaveHeap& heap, int 
 #pragma unroll
     for (int j = 0; j < kGmax; ++j)
       if (j < nr.ngpus[ps]) {
-        const int32_t l = nr.gml[ps][j], t = nr.gmt[ps][j];
+        const int32_t l = nr.gml[ps][j], t = nr.gt(ps, j);
         bad |= l < 0 || l > t || row[3 + j] + l != t;
       }
   }
@@ -254,10 +260,8 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
     nr.mem_total[ps] = W.mem_total[node];
     nr.ngpus[ps] = W.ngpus[node];
 #pragma unroll
-    for (int j = 0; j < kGmax; ++j) {
-      nr.gml[ps][j] = W.gml_left0[node * kGmax + j];
-      nr.gmt[ps][j] = W.gml_total[node * kGmax + j];
-    }
+    for (int j = 0; j < kGmax; ++j) nr.gml[ps][j] = W.gml_left0[node * kGmax + j];
+    nr.gmt1[ps] = W.gml_total[node * kGmax];
   }
   // waiting histogram over gpu_milli classes: class k -> lane k%64, slot k/64
   constexpr int KP = 4;  // up to 256 classes

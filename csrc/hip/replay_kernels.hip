@@ -101,11 +101,14 @@ hipError_t raise_lds(T* f, int max_lds) {
 #ifndef FKS_LIGHT_WAVES
 #define FKS_LIGHT_WAVES 4   // first-fit / best-fit / random_linear (build-time knob for A/B runs)
 #endif
+#ifndef FKS_NP4_WAVES
+#define FKS_NP4_WAVES 3     // 256-node clusters (config 5): one GPU-milli total per node keeps them <= 168 VGPRs
+#endif
 #ifndef FKS_HEAVY_WAVES
 #define FKS_HEAVY_WAVES 3   // feature / composite families and mixed batches
 #endif
 #define FKS_FAM_BOUNDS(G, F, NP)                                               \
-  __launch_bounds__(64, !(G) ? 1 : (NP) >= 4 ? 2 : (NP) == 2 ? 3              \
+  __launch_bounds__(64, !(G) ? 1 : (NP) >= 4 ? FKS_NP4_WAVES : (NP) == 2 ? 3   \
                            : (((F) == 3 || (F) == 4 || (F) < 0) ? FKS_HEAVY_WAVES : FKS_LIGHT_WAVES))
 template <int NPASS, bool GHEAP, int FAM>
 __global__ FKS_FAM_BOUNDS(GHEAP, FAM, NPASS) void k_replay_builtin(fksk::BuiltinArgs a) {
@@ -217,7 +220,9 @@ struct NativeScorerDev {
   __device__ int64_t score(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, int& exc) {
     const int node = ps * kWave + lane_id();
     const int32_t* gl = nr.gml[ps];
-    const int32_t* gt = nr.gmt[ps];
+    int32_t gt[kGmax];
+#pragma unroll
+    for (int g = 0; g < kGmax; ++g) gt[g] = nr.gt(ps, g);
     const int64_t r = fn(nr.cpu_left[ps], nr.cpu_total[ps], nr.mem_left[ps], nr.mem_total[ps],
                          pack_gpu_ng(nr.gpu_left[ps], nr.ngpus[ps]), gl[0], gl[1], gl[2], gl[3], gl[4], gl[5], gl[6], gl[7], gt[0], gt[1], gt[2], gt[3],
                          gt[4], gt[5], gt[6], gt[7], gmem + (size_t)node * kGmax, pod.cpu, pod.mem,

@@ -382,8 +382,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
     nr.cpu_total[0] = e[0];
     nr.mem_total[0] = e[1];
     nr.ngpus[0] = e[2];
-#pragma unroll
-    for (int g = 0; g < kGmax; ++g) nr.gmt[0][g] = e[3 + g];
+    nr.gmt1[0] = e[3];
   };
   int32_t wcnt[kRowClassSlots];
   int32_t used_cpu = 0, used_mem = 0, used_gcnt = 0, used_gml = 0;   // host: totals < 2^31
@@ -496,7 +495,9 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
           // the program holds the template's feasibility prologue itself
           if (node_valid) {
             const int32_t* gl = nr.gml[0];
-            const int32_t* gt = nr.gmt[0];
+            int32_t gt[kGmax];
+#pragma unroll
+            for (int g = 0; g < kGmax; ++g) gt[g] = nr.gt(0, g);
             s = prog(nr.cpu_left[0], nr.cpu_total[0], nr.mem_left[0], nr.mem_total[0], pack_gpu_ng(nr.gpu_left[0], nr.ngpus[0]),
                      gl[0], gl[1], gl[2], gl[3], gl[4], gl[5], gl[6], gl[7], gt[0], gt[1], gt[2], gt[3], gt[4], gt[5],
                      gt[6], gt[7], cold()->gmem_total + (size_t)jv * kGmax, pod.cpu, pod.mem,

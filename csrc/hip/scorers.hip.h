@@ -134,7 +134,7 @@ struct BuiltinScorerDev {
       if (j < ng) {
         const int32_t l = nr.gml[ps][j];
         free_m += l;
-        idle += (l == nr.gmt[ps][j]);
+        idle += (l == nr.gt(ps, j));
         gmax = (j == 0 || l > gmax) ? l : gmax;
         gmin = (j == 0 || l < gmin) ? l : gmin;
         if (gpod && l >= pod.gmilli && (best < 0 || l - pod.gmilli < best)) best = l - pod.gmilli;
@@ -142,7 +142,7 @@ struct BuiltinScorerDev {
     }
     double gpu_u = 0.0;
     if (gpod) {
-      const int64_t cap = (int64_t)nr.gpu_left[ps] * nr.gmt[ps][0];
+      const int64_t cap = (int64_t)nr.gpu_left[ps] * nr.gt(ps, 0);
       gpu_u = (double)(cap - free_m) / (double)(cap > 1 ? cap : 1);   // cap is int64
     }
     double s = 0.0;
@@ -191,8 +191,8 @@ struct BuiltinScorerDev {
       if (j < ng) {
         const int32_t l = nr.gml[ps][j];
         free_m += l;
-        idle += (l == nr.gmt[ps][j]);
-        part += (0 < l && l < nr.gmt[ps][j]);
+        idle += (l == nr.gt(ps, j));
+        part += (0 < l && l < nr.gt(ps, j));
         if (pod.ngpu > 0 && l >= pod.gmilli && (best < 0 || l - pod.gmilli < best)) best = l - pod.gmilli;
       }
     }

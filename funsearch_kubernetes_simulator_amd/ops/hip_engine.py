@@ -97,6 +97,12 @@ def prepare_device_workload(w: Workload, snapshot_interval: float = 0.05) -> Dic
         raise UnsupportedWorkload(f"more than {GMAX} GPUs on a node")
     if c.gpu_milli_total.size and (c.gpu_milli_total.max() >= 2 ** 20 or c.gpu_milli_total.min() < 0):
         raise UnsupportedWorkload("GPU milli totals outside [0, 2^20) (32-bit per-node sums on device)")
+    if c.gpu_milli_total.size:
+        # the kernels hold one GPU milli total per node (NodeRegs::gmt1)
+        owner = np.repeat(np.arange(N), np.diff(c.gpu_start))
+        first = c.gpu_milli_total[c.gpu_start[owner]]
+        if not np.array_equal(first, c.gpu_milli_total):
+            raise UnsupportedWorkload("GPUs of one node with different milli totals")
     if len(np.unique(p.pod_rank)) != P:
         raise UnsupportedWorkload("duplicate pod ids")
     if P >= 2 ** 20:

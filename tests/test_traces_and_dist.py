@@ -241,3 +241,18 @@ def test_config4_launcher_two_gloo_ranks(tmp_path):
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["ranks"] == 2 and out["islands_per_rank"] == 1 and out["generations"] == 2
     assert (tmp_path / "c4" / "metrics.rank1.jsonl").exists()
+
+
+def test_device_workload_requires_one_gpu_model_per_node(default_workload):
+    """The kernels keep one GPU-milli total per node (NodeRegs::gmt1): a node
+    whose GPUs differ is rejected up front (UnsupportedWorkload -> CPU
+    engines), never replayed with a wrong total."""
+    import copy
+    from funsearch_kubernetes_simulator_amd.ops.hip_engine import UnsupportedWorkload, prepare_device_workload
+    prepare_device_workload(default_workload)            # OpenB: one model per node
+    w = copy.deepcopy(default_workload)
+    a, b = int(w.cluster.gpu_start[0]), int(w.cluster.gpu_start[1])
+    assert b - a >= 2
+    w.cluster.gpu_milli_total[a + 1] = 500
+    with pytest.raises(UnsupportedWorkload, match="milli totals"):
+        prepare_device_workload(w)
