@@ -1,15 +1,21 @@
-// Correctly rounded exp / log / pow for the device interpreter.
+// Correctly rounded exp / log / pow for the device (VM runtime and the
+// native programs' rt_binop / rt_unop).
 //
-// CPython delegates `**`, math.exp, math.log and math.pow to glibc, whose
-// results are correctly rounded except in rare hard cases.  The device
-// evaluates the same functions in double-double arithmetic (~2^-100
-// relative error) and rounds once, so it returns the correctly rounded
-// double; results that land within 2^-90 of a rounding midpoint (the exact
-// tie cases, e.g. small integer powers) are reported as `defer` and the
-// policy is re-run on the host, where glibc decides.
+// CPython delegates `**`, math.exp, math.log and math.pow to glibc.  The
+// device evaluates them in double-double arithmetic (~2^-100 relative error)
+// and rounds once, so it returns the correctly rounded double; results that
+// land within 2^-84..2^-90 of a rounding midpoint (exact ties such as small
+// integer powers) are reported as `defer` and the policy is re-run on the
+// host, where glibc decides.
 //
-// __host__ __device__ so the identical code is unit-tested on the host
-// against glibc (tests/test_dd_math.py).
+// Measured (csrc/tools/dd_math_check.cpp, tests/test_dd_math.py): glibc's pow
+// and exp are NOT correctly rounded (<= 0.52 ULP), so ~0.08% of calls differ
+// from CPython by one ULP (log: a few per million); in every such case the
+// device holds the correctly rounded value.  A one-ULP difference only
+// matters if it moves a node's int(score) across an integer or flips a
+// comparison between values within one ULP of each other.
+//
+// __host__ __device__ so the identical code is checked on the host.
 #pragma once
 
 #include "jit_env.h"
@@ -52,29 +58,41 @@ __host__ __device__ inline dd dd_mul_d(dd a, double b) {
 }
 __host__ __device__ inline dd dd_ldexp(dd a, int e) { return {ldexp(a.hi, e), ldexp(a.lo, e)}; }
 
+// 1/n! as double-doubles, n = 2..7 (the terms of e^r - 1 that need ~106 bits)
+struct DdConst { double hi, lo; };
+#define FKS_INV_FACT_DD                                                   \
+  {{0.5, 0.0}, {0.16666666666666666, 9.25185853854297e-18},               \
+   {0.041666666666666664, 2.3129646346357427e-18},                        \
+   {0.008333333333333333, 1.1564823173178714e-19},                        \
+   {0.001388888888888889, -5.300543954373577e-20},                        \
+   {0.0001984126984126984, 1.7209558293420705e-22}}
+
 // exp of a double-double argument; |a| <= 700 required (caller checks).
+// a = k ln2 + 32 r, |r| <= ln2 / 64; e^r - 1 by a degree-12 polynomial whose
+// terms r^8..r^12 (< 2^-68 of the sum) are summed in double and r^2..r^7 in
+// double-double Horner steps with exact 1/n! constants (no divisions); then
+// five squarings (1+s)^32 and the 2^k scale.  Relative error ~2^-100 (the
+// rounding check of dd_round keeps a 2^-84 margin for pow, 2^-90 for exp/log).
 __host__ __device__ inline dd dd_exp(dd a) {
   const dd ln2 = {6.931471805599452862e-01, 2.319046813846299558e-17};
-  const double k = nearbyint(a.hi / ln2.hi);
+  const double k = nearbyint(a.hi * 1.4426950408889634);
   dd r = dd_add(a, dd_mul_d({-ln2.hi, -ln2.lo}, k));
-  r = dd_ldexp(r, -10);  // |r| < 3.4e-4
-  // e^r - 1 by Taylor to r^11
-  dd term = r, s = r;
-  double inv = 1.0;
-  for (int n = 2; n <= 11; ++n) {
-    term = dd_mul(term, r);
-    inv = 1.0 / (double)n;
-    // term_n = term_{n-1} * r / n  (divide exactly by a small integer in dd)
-    dd q = {term.hi * inv, 0.0};
-    // refine q = term / n with one correction step
-    dd back = two_prod(q.hi, (double)n);
-    double rem = ((term.hi - back.hi) - back.lo + term.lo) / (double)n;
-    term = quick_two_sum(q.hi, rem);
-    s = dd_add(s, term);
-  }
-  (void)inv;
-  // (1+s)^(2^10): s <- 2s + s^2
-  for (int i = 0; i < 10; ++i) s = dd_add(dd_add(s, s), dd_mul(s, s));
+  r = dd_ldexp(r, -5);  // |r| < 0.0109
+  const double rh = r.hi;
+  // r^8 .. r^12 tail in double: ((((c12 r + c11) r + c10) r + c9) r + c8)
+  double q = 2.08767569878681e-09;
+  q = q * rh + 2.505210838544172e-08;
+  q = q * rh + 2.755731922398589e-07;
+  q = q * rh + 2.7557319223985893e-06;
+  q = q * rh + 2.48015873015873e-05;
+  const DdConst c[6] = FKS_INV_FACT_DD;
+  dd p = {q, 0.0};
+#pragma unroll
+  for (int n = 5; n >= 0; --n) p = dd_add(dd_mul(p, r), dd{c[n].hi, c[n].lo});
+  // p = 1/2 + r/6 + ... ; s = r + r^2 p = e^r - 1
+  dd s = dd_add(r, dd_mul(dd_mul(r, r), p));
+  // (1+s)^(2^5): s <- 2s + s^2
+  for (int i = 0; i < 5; ++i) s = dd_add(dd_ldexp(s, 1), dd_mul(s, s));
   dd res = dd_add({1.0, 0.0}, s);
   return dd_ldexp(res, (int)k);
 }
