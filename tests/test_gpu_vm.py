@@ -29,13 +29,14 @@ def test_device_vm_equals_cpu_vm(default_workload, mode):
     progs = _programs()
     gpu = dev.evaluate_programs(progs)
     cpu = ce.simulate_program_batch(sub, progs, threads=8)
-    compared = 0
+    deferred = []
     for i, p in enumerate(progs):
         if int(gpu[i, 10]) == Exc.UNSUPPORTED:
-            continue   # deferred to the host by design (trig, near-tie math, bigint)
+            deferred.append(i)   # deferred to the host by design (trig, near-tie math, bigint)
+            continue
         assert np.array_equal(gpu[i], cpu[i]), (i, p.source[-300:], gpu[i], cpu[i])
-        compared += 1
-    assert compared >= len(progs) - 6
+    # the deferred programs are named in the failure message (the engine re-runs them on the CPU VM)
+    assert len(deferred) <= 6, [(i, progs[i].source[-200:]) for i in deferred]
 
 
 def test_device_vm_runaway_program_drains(default_workload):
