@@ -216,6 +216,7 @@ class DeviceEngine {
       if (m == "on" && !rows_ok_) throw std::invalid_argument("row kernel needs <= 16 nodes, <= 64 gpu_milli classes");
       row_mode_ = m;
     }
+    if (o.contains("native_duo")) native_duo_ = o["native_duo"].cast<bool>();
     if (o.contains("native_rows")) {
       const int r = o["native_rows"].cast<int>();
       if (r < 0 || r > kRowsPerWave) throw std::invalid_argument("native_rows must be in [0, 4]");
@@ -520,6 +521,7 @@ class DeviceEngine {
     HIP_OK(fksk::set_native_attrs_np1(mx)); HIP_OK(fksk::set_native_attrs_np2(mx));
     HIP_OK(fksk::set_native_attrs_np4(mx));
     HIP_OK(fksk::set_native_rows_attrs(mx));
+    HIP_OK(fksk::set_native_duo_attrs(mx));
   }
 
   // 4-policies-per-wave row kernel: clusters of <= 16 nodes, exact repush
@@ -733,6 +735,26 @@ class DeviceEngine {
     const int ra = native_rows_opt_ > 0 ? native_rows_opt_ : (P <= 2 * num_cus_ ? 1 : kRowsPerWave);
     DevWorkload Wl = W_;
     const int entries = row_heap_entries(W_.n_pods);
+    if (ra == 1 && native_duo_ && !profiled) {
+      // latency regime: two waves per program (heap wave + scoring wave, replay_duo.hip.h)
+      int T = 1;
+      while (T < entries - 1 && duo_lds_bytes(W_.n_pods, 2 * T + 1) <= kMaxLds / 2) T = 2 * T + 1;
+      Wl.heap_top = T;
+      const size_t lds = duo_lds_bytes(W_.n_pods, T);
+      if (lds > kMaxLds) throw std::invalid_argument("native duo layout exceeds the 160 KiB LDS");
+      s.gheap.reserve((size_t)entries * 8 * (size_t)P);
+      const fksk::BuiltinArgs a{Wl, upload_workload(s, Wl), nullptr, nullptr, nullptr, s.res.as<DevResult>(),
+                                s.gheap.as<uint64_t>(), nullptr, s.h_tab.dev<double>()};
+      s.fused_table = true;
+      const RowNativeArgs nat{s.h_in.dev<const uint64_t>(), s.kc.as<const int64_t>(),
+                              reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + fn_bytes)};
+      if (std::getenv("FKS_DEBUG_LAUNCH"))
+        std::fprintf(stderr, "[fks] native duo: P=%d T=%d lds=%zu stream=%p\n", P, T, lds, (void*)s.stream);
+      HIP_OK(fksk::launch_native_duo(P, lds, s.stream, a, nat));
+      last_native_rows_ = 0;   // 0: the two-wave kernel
+      last_native_waves_ = 2 * P;
+      return;
+    }
     // largest heap top (2^k - 1 slots, at most the whole heap) that keeps two waves per CU
     int T = 1;
     while (T < entries - 1 && rows_lds_bytes(W_.n_pods, 2 * T + 1, ra, true) <= kMaxLds / 2) T = 2 * T + 1;
@@ -822,6 +844,7 @@ class DeviceEngine {
   std::string row_mode_ = "auto";
   int row_top_opt_ = -1;
   double row_share_ = 1.0;
+  bool native_duo_ = true;     // two-wave kernel for one-program-per-wave batches
   int native_rows_opt_ = 0;    // rows per wave for native programs (0: auto)
   int last_native_rows_ = 0, last_native_waves_ = 0;
   mutable std::vector<std::pair<int, int>> row_layout_cache_ = std::vector<std::pair<int, int>>(8, {0, 0});

@@ -20,6 +20,7 @@
 #include "launch.h"
 #include "replay.hip.h"
 #include "replay_rows.hip.h"
+#include "replay_duo.hip.h"
 #include "scorers.hip.h"
 #include "vm_dev.hip.h"
 #include "jit_abi.h"

@@ -1,0 +1,444 @@
+// k_replay_native_duo: one natively compiled program per workgroup of TWO
+// waves that split a replay's dependency chain (latency regime: LLM-sized
+// batches of a few dozen programs on <= 16 nodes).
+//
+// In the one-program-per-wave row kernel every event runs pop -> sift of the
+// heap's last entry -> score -> commit -> push back to back on one wave,
+// although the sift and the scoring are independent (s_memtime split:
+// ~3.2k cycles of pop/sift, 2.9k-9.2k of scoring per event).  Here
+//   * wave H owns the CPython heap (LDS top + HBM tail, RowHeap) and its
+//     deletion bitmap: it pops an event, publishes the key in an LDS ring,
+//     then sifts; a DELETION needs nothing back, so H runs ahead through
+//     deletions (bounded by the ring); for a creation it waits for S's
+//     verdict and pushes (the deletion entry of a placement, or -- after
+//     computing the first-deletion repush time itself -- the re-queued pod);
+//   * wave S owns the node registers, the waiting-class histogram, the
+//     utilisation totals, the exact accumulators and the program: it replays
+//     the events in order (node updates, scoring through the JIT function
+//     pointer, argmax, GPU pick, snapshot schedule) and answers creations.
+// The two waves of a workgroup are co-resident, and each waits on the other
+// through LDS counters with release/acquire ordering and a bounded spin (a
+// lost partner ends the replay with EXC_INVARIANT instead of hanging).
+// Event order, heap operations and arithmetic are exactly those of
+// replay_rows (bit-identical results; tests/test_gpu_native.py).
+#pragma once
+
+#include "replay_rows.hip.h"
+
+namespace fksd {
+
+constexpr int kDuoRing = 64;                  // events H may run ahead of S
+constexpr uint32_t kDuoSpinCap = 1u << 26;    // polls before a wait is declared lost
+enum DuoReply : int32_t { DUO_NONE = 0, DUO_PLACED = 1, DUO_FAIL = 2, DUO_ABORT = 3 };
+
+struct DuoBox {
+  uint64_t ev[kDuoRing];   // popped keys, ring (H -> S)
+  uint64_t item;           // S -> H: heap entry to push after a placement
+  uint32_t head;           // events published by H
+  uint32_t tail;           // events consumed by S
+  uint32_t rseq;           // creations answered by S (the event index + 1)
+  int32_t code;            // DuoReply of the last answer
+  uint32_t term;           // H: no more events
+  int32_t h_exc, n_repush, n_dropped;
+};
+__host__ __device__ inline size_t duo_lds_bytes(int n_pods, int T) {
+  return rows_lds_bytes(n_pods, T, 1, true) + ((sizeof(DuoBox) + 15) & ~size_t(15));
+}
+
+__device__ __forceinline__ uint32_t duo_ld(FKS_LDS uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void duo_st(FKS_LDS uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64_t* gheap, DevResult* out,
+                           RowNativeArgs nat, double* table) {
+  auto cold = [&]() {
+    const DevWorkload* g = reinterpret_cast<const DevWorkload*>(uniu64(reinterpret_cast<uint64_t>(Wdev)));
+    asm volatile("" : "+s"(g));
+    return const_ptr(g);
+  };
+  extern __shared__ uint64_t lds_raw[];
+  const int lane = lane_id();
+  const int wave = (int)(threadIdx.x >> 6);   // 0: H (heap), 1: S (scoring)
+  const int p = blockIdx.x;
+  const int N = W.n_pods;
+  const int T = W.heap_top;
+  const int lb = W.low_bits, nb = W.node_bits, rb = W.rank_bits;
+  const int tshift = rb + lb;
+  const uint64_t time_max = (W.time_bits >= 63) ? ~0ull : ((1ull << W.time_bits) - 1);
+  int jv = lane & 15;
+  const bool node_valid = jv < W.n_nodes;
+
+  // LDS: [weights area (unused) | class values | node constants | bitmap | heap top | constant block | box]
+  FKS_LDS uint64_t* lds = lds_ptr(lds_raw);
+  FKS_LDS int32_t* cls_lds = reinterpret_cast<FKS_LDS int32_t*>(lds + kRowsPerWave * kWeights);
+  FKS_LDS char* rowbase = reinterpret_cast<FKS_LDS char*>(lds + kRowsPerWave * kWeights) + kRowClassBytes;
+  FKS_LDS int32_t* ntab = cls_lds + kRow * kRowClassSlots;
+  FKS_LDS int64_t* kcp = reinterpret_cast<FKS_LDS int64_t*>(rowbase + rows_row_bytes(N, T));
+  FKS_LDS DuoBox* box = reinterpret_cast<FKS_LDS DuoBox*>(reinterpret_cast<FKS_LDS char*>(lds) + rows_lds_bytes(N, T, 1, true));
+
+  if (wave == 0) {
+    if (lane < W.n_classes) cls_lds[lane] = *global_ptr(&W.class_value[lane]);
+    if (lane < kRow) {
+      ntab[lane * kNodeConsts + 0] = W.cpu_total[lane];
+      ntab[lane * kNodeConsts + 1] = W.mem_total[lane];
+      ntab[lane * kNodeConsts + 2] = W.ngpus[lane];
+#pragma unroll
+      for (int g = 0; g < kGmax; ++g) ntab[lane * kNodeConsts + 3 + g] = W.gml_total[lane * kGmax + g];
+    }
+    if (lane == 0) {
+      box->item = 0; box->head = 0; box->tail = 0; box->rseq = 0; box->code = DUO_NONE; box->term = 0;
+      box->h_exc = EXC_NONE; box->n_repush = 0; box->n_dropped = 0;
+    }
+  } else {
+    const FKS_GLOBAL int64_t* ksrc = global_ptr(nat.kc + *global_ptr(&nat.koff[p]));
+    for (int i = lane; i < kKcLds; i += kWave) kcp[i] = ksrc[i];
+  }
+  __syncthreads();
+  if (lane >= kRow) return;   // rows 1-3 of both waves take no part (no barrier follows)
+
+  if (wave == 0) {
+    // ================= H: the heap
+    RowHeap heap;
+    heap.delmap = reinterpret_cast<FKS_LDS uint32_t*>(rowbase);
+    heap.top = reinterpret_cast<FKS_LDS uint64_t*>(rowbase + (size_t)lds_delmap_words(N) * 4);
+    heap.h = global_ptr(gheap + (size_t)p * row_heap_entries(N));
+    heap.T = T;
+    heap.lb = lb;
+    heap.j = jv;
+    heap.rbase = 0;
+    heap.anc = heap.dir = 0;
+    for (int x = jv; x > 0 && x < 15; x = (x - 1) >> 1) {
+      const int a = (x - 1) >> 1;
+      heap.anc |= 1u << a;
+      if ((x & 1) == 0) heap.dir |= 1u << a;
+    }
+    const FKS_GLOBAL u64x2* heap_src = reinterpret_cast<const FKS_GLOBAL u64x2*>(global_ptr(W.heap0p));
+    for (int i = jv; i < row_heap_entries(N) / 2; i += kRow) {
+      const u64x2 v = heap_src[i];
+      if (2 * i < T + 1) *reinterpret_cast<FKS_LDS u64x2*>(heap.top + 2 * i) = v;
+      else *reinterpret_cast<FKS_GLOBAL u64x2*>(heap.h + 2 * i) = v;
+    }
+    for (int i = jv; i < lds_delmap_words(N); i += kRow) heap.delmap[i] = 0u;
+    __builtin_amdgcn_s_waitcnt(0);
+    int n = N, n_repush = 0, n_dropped = 0;
+    int32_t hexc = EXC_NONE;
+    uint32_t k = 0;
+    while (n > 0) {
+      asm volatile("" : "+v"(jv));
+      heap.j = jv;
+      const uint64_t top = heap.ld(0);
+      const uint64_t last = heap.ld(n - 1);
+      --n;
+      // a free ring slot (S consumes in order)
+      uint32_t spins = 0;
+      while (k - duo_ld(&box->tail) >= (uint32_t)kDuoRing) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > kDuoSpinCap) { hexc = EXC_INVARIANT; break; }
+      }
+      if (hexc != EXC_NONE) break;
+      if (jv == 0) box->ev[k % kDuoRing] = top;
+      if (jv == 0) duo_st(&box->head, k + 1);
+      if (n > 0) heap.pop_reinsert(n, last);
+      if ((int)(top & 3) != kDelete) {
+        spins = 0;
+        while (duo_ld(&box->rseq) != k + 1) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > kDuoSpinCap) { hexc = EXC_INVARIANT; break; }
+        }
+        if (hexc != EXC_NONE) break;
+        const int code = box->code;
+        if (code == DUO_ABORT) break;   // S holds the exception
+        uint64_t item = box->item;
+        if (code == DUO_FAIL) {
+          item = 0;
+          const int rank = (int)((top >> lb) & ((1ull << rb) - 1));
+          const int f = heap.first_deletion(n);
+          if (f >= 0) {
+            const uint64_t nt = (heap.ld(f) >> tshift) + 1;
+            if (nt > time_max) { hexc = EXC_UNSUPPORTED; break; }
+            item = (nt << tshift) | ((uint64_t)rank << lb) | kRetry;
+            ++n_repush;
+          } else {
+            ++n_dropped;
+          }
+        }
+        if (item != 0) {
+          heap.push(n, item);
+          ++n;
+        }
+      }
+      ++k;
+    }
+    if (jv == 0) {
+      box->h_exc = hexc;
+      box->n_repush = n_repush;
+      box->n_dropped = n_dropped;
+      duo_st(&box->term, 1u);
+    }
+    return;
+  }
+
+  // ================= S: nodes, program, evaluator
+  const ProgFn prog = reinterpret_cast<ProgFn>(*global_ptr(&nat.fn[p]));
+  NodeRegs<1> nr;
+  {
+    const FKS_CONST DevWorkload* Wb = cold();
+    nr.cpu_left[0] = Wb->cpu_left0[jv];
+    nr.mem_left[0] = Wb->mem_left0[jv];
+    nr.gpu_left[0] = Wb->gpu_left0[jv];
+#pragma unroll
+    for (int g = 0; g < kGmax; ++g) nr.gml[0][g] = Wb->gml_left0[jv * kGmax + g];
+  }
+  int32_t wcnt[kRowClassSlots];
+#pragma unroll
+  for (int sl = 0; sl < kRowClassSlots; ++sl) wcnt[sl] = 0;
+  int32_t used_cpu = (int32_t)cold()->used_cpu0, used_mem = (int32_t)cold()->used_mem0;
+  int32_t used_gcnt = (int32_t)cold()->used_gcnt0, used_gml = (int32_t)cold()->used_gmilli0;
+  RowAcc acc;
+  acc.init();
+  int32_t processed = 0, next_fire = INT32_MAX;
+  int ksnap = 0;
+  double thr = cold()->thr_after_fire;
+  if (cold()->n_fire > 0) {
+    next_fire = (int32_t)*global_ptr(&cold()->snap_fire[0]);
+  } else {
+    int32_t c = 1;
+    while ((double)c / (double)N < thr) ++c;
+    next_fire = c;
+  }
+  uint64_t hsh = 0xcbf29ce484222325ull;
+  int32_t exc = EXC_NONE;
+  auto reply = [&](int code, uint64_t item, uint32_t k) {
+    if (jv == 0) {
+      box->item = item;
+      box->code = code;
+      duo_st(&box->rseq, k + 1);
+    }
+  };
+  uint32_t k = 0;
+  for (;;) {
+    asm volatile("" : "+v"(jv));
+    // next event, or the end of the replay
+    uint32_t spins = 0;
+    bool have = false;
+    for (;;) {
+      if (duo_ld(&box->head) > k) { have = true; break; }
+      if (duo_ld(&box->term)) { have = duo_ld(&box->head) > k; break; }
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > kDuoSpinCap) { exc = EXC_INVARIANT; break; }
+    }
+    if (!have) break;
+    const uint64_t top = box->ev[k % kDuoRing];
+    if (jv == 0) duo_st(&box->tail, k + 1);
+    const int rank = (int)((top >> lb) & ((1ull << rb) - 1));
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const v4i precv = *reinterpret_cast<const FKS_GLOBAL v4i*>(global_ptr(&W.pod[rank]));
+    const int kind = (int)(top & 3);
+    const int64_t t = (int64_t)(top >> tshift);
+    PodView pod;
+    pod.cpu = precv.x; pod.mem = precv.y; pod.dur = precv.z;
+    pod.gmilli = precv.w & 0xFFFF; pod.ngpu = (precv.w >> 16) & 0xFF; pod.cls = (precv.w >> 24) & 0xFF;
+    pod.ctime = t; pod.rank = rank;
+
+    if (kind == kDelete) {
+      const int node = (int)((top >> 2) & ((1u << nb) - 1));
+      const int mask = (int)((top >> (2 + nb)) & 0xFF);
+      if (jv == node) {
+        nr.cpu_left[0] += pod.cpu;
+        nr.mem_left[0] += pod.mem;
+        nr.gpu_left[0] += pod.ngpu;
+#pragma unroll
+        for (int g = 0; g < kGmax; ++g)
+          if ((mask >> g) & 1) nr.gml[0][g] += pod.gmilli;
+      }
+      used_cpu -= pod.cpu; used_mem -= pod.mem; used_gcnt -= pod.ngpu;
+      used_gml -= pod.gmilli * __popc(mask);
+      if (cold()->trace_hash) hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 1, (uint64_t)t);
+    } else {
+      {
+        const FKS_LDS int32_t* e = ntab + jv * kNodeConsts;
+        nr.cpu_total[0] = e[0];
+        nr.mem_total[0] = e[1];
+        nr.ngpus[0] = e[2];
+        nr.gmt1[0] = e[3];
+      }
+      int lexc = EXC_NONE;
+      int64_t s = 0;
+      if (node_valid) {
+        const int32_t* gl = nr.gml[0];
+        int32_t gt[kGmax];
+#pragma unroll
+        for (int g = 0; g < kGmax; ++g) gt[g] = nr.gt(0, g);
+        s = prog(nr.cpu_left[0], nr.cpu_total[0], nr.mem_left[0], nr.mem_total[0], pack_gpu_ng(nr.gpu_left[0], nr.ngpus[0]),
+                 gl[0], gl[1], gl[2], gl[3], gl[4], gl[5], gl[6], gl[7], gt[0], gt[1], gt[2], gt[3], gt[4], gt[5],
+                 gt[6], gt[7], cold()->gmem_total + (size_t)jv * kGmax, pod.cpu, pod.mem,
+                 pod.gmilli | (pod.ngpu << 16), pod.ctime, pod.dur, kcp);
+        if (s < 0) { lexc = (int)(-s); s = 0; }
+      }
+      const uint32_t bad = row_ballot(lexc != EXC_NONE, 0);
+      if (bad) {
+        exc = row_read(lexc, 0, __ffs(bad) - 1);
+        reply(DUO_ABORT, 0, k);
+        break;
+      }
+      const int64_t m = (int64_t)row_max_u64((uint64_t)s);
+      const int best_node = m > 0 ? __ffs(row_ballot(s == m, 0)) - 1 : -1;
+      if (best_node < 0) {
+        // failed placement: S keeps the metrics, H computes the repush
+        if (kind == kFresh && pod.ngpu > 0) {
+#pragma unroll
+          for (int sl = 0; sl < kRowClassSlots; ++sl)
+            if (sl == (pod.cls >> 4) && jv == (pod.cls & 15)) wcnt[sl] += 1;
+        }
+        reply(DUO_FAIL, 0, k);   // H's first-deletion scan overlaps the fragmentation sum
+        double frag = 0.0;
+        int mcls = -1;
+#pragma unroll
+        for (int sl = 0; sl < kRowClassSlots; ++sl) {
+          const uint32_t b = row_ballot(wcnt[sl] > 0, 0);
+          if (mcls < 0 && b) mcls = sl * kRow + __ffs(b) - 1;
+        }
+        if (mcls >= 0) {
+          const int mv = cls_lds[mcls];
+          int64_t stranded = 0;
+#pragma unroll
+          for (int g = 0; g < kGmax; ++g) {
+            const int l = nr.gml[0][g];
+            if (g < nr.ngpus[0] && 0 < l && l < mv) stranded += l;
+          }
+          stranded = row_sum_i64(node_valid ? stranded : 0);
+          const int64_t tg = cold()->tot_gmilli;
+          frag = tg > 0 ? (double)stranded / (double)tg : 0.0;
+        }
+        acc.add(4, frag, jv);
+        if (cold()->trace_hash) hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 2, (uint64_t)t);
+      } else {
+        int gmask = 0, ok = 1;
+        if (pod.ngpu > 0) {
+          int myok = 1;
+          const int mymask = pick_gpus<1>(nr, 0, pod.gmilli, pod.ngpu, cold()->first_fit_alloc != 0, myok);
+          const int packed = row_read(mymask | (myok << 8), 0, best_node);
+          gmask = packed & 0xFF;
+          ok = packed >> 8;
+        }
+        if (!ok) { exc = EXC_ALLOC; reply(DUO_ABORT, 0, k); break; }
+        const uint64_t dt = (uint64_t)(t + pod.dur);
+        if (t + pod.dur < 0 || dt > time_max) { exc = EXC_UNSUPPORTED; reply(DUO_ABORT, 0, k); break; }
+        // answer first: H's push runs while S commits
+        reply(DUO_PLACED, (dt << tshift) | ((uint64_t)rank << lb) | ((uint64_t)gmask << (2 + nb)) |
+                              ((uint64_t)best_node << 2) | kDelete, k);
+        if (jv == best_node) {
+          nr.cpu_left[0] -= pod.cpu;
+          nr.mem_left[0] -= pod.mem;
+          nr.gpu_left[0] -= pod.ngpu;
+#pragma unroll
+          for (int g = 0; g < kGmax; ++g)
+            if ((gmask >> g) & 1) nr.gml[0][g] -= pod.gmilli;
+        }
+        used_cpu += pod.cpu; used_mem += pod.mem; used_gcnt += pod.ngpu;
+        used_gml += pod.gmilli * __popc(gmask);
+        if (kind == kRetry && pod.ngpu > 0) {
+#pragma unroll
+          for (int sl = 0; sl < kRowClassSlots; ++sl)
+            if (sl == (pod.cls >> 4) && jv == (pod.cls & 15)) wcnt[sl] -= 1;
+        }
+        if (cold()->trace_hash)
+          hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2), ((uint64_t)t << 8) ^ (uint64_t)best_node);
+      }
+    }
+    // evaluator hook (host-precomputed snapshot schedule), as in replay_rows
+    ++processed;
+    if (processed >= next_fire) {
+      const FKS_CONST DevWorkload* Ws = cold();
+      const double r0 = Ws->tot_cpu > 0 ? (double)used_cpu / (double)Ws->tot_cpu : 0.0;
+      const double r1 = Ws->tot_mem > 0 ? (double)used_mem / (double)Ws->tot_mem : 0.0;
+      const double r2 = Ws->tot_gcnt > 0 ? (double)used_gcnt / (double)Ws->tot_gcnt : 0.0;
+      const double r3 = Ws->tot_gmilli > 0 ? (double)used_gml / (double)Ws->tot_gmilli : 0.0;
+      acc.add(0, r0, jv); acc.add(1, r1, jv); acc.add(2, r2, jv); acc.add(3, r3, jv);
+      ++ksnap;
+      if (ksnap < Ws->n_fire) {
+        next_fire = (int32_t)*global_ptr(&Ws->snap_fire[ksnap]);
+      } else {
+        if (ksnap > Ws->n_fire) thr += Ws->snapshot_interval;
+        int32_t c = processed + 1;
+        while ((double)c / (double)N < thr) ++c;
+        next_fire = c;
+      }
+    }
+    ++k;
+  }
+  // wait for H to finish (it may still be pushing / scanning), then take its counters
+  {
+    uint32_t spins = 0;
+    while (!duo_ld(&box->term)) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > kDuoSpinCap) { exc = exc != EXC_NONE ? exc : EXC_INVARIANT; break; }
+    }
+  }
+  if (exc == EXC_NONE && box->h_exc != EXC_NONE) {
+    exc = box->h_exc;
+    --processed;   // H aborted on this event (repush time overflow) before it counted
+  }
+  const int n_repush = box->n_repush, n_dropped = box->n_dropped;
+
+  // ---------------- result (replay_rows' write-back, fused evaluator)
+  const int64_t n_snap = row_read(acc.count, 0, 0);
+  const int64_t n_frag = row_read(acc.count, 0, 4);
+  const int inexact = row_ballot(jv < 5 && acc.inexact != 0, 0) != 0;
+  DevResult* o = out + p;
+  if (jv < 5) {
+    o->acc_lo[jv] = acc.lo;
+    o->acc_hi[jv] = acc.hi;
+  }
+  if (jv == 0) {
+    o->n_events = processed;
+    o->n_snap = n_snap;
+    o->n_frag = n_frag;
+    o->n_unplaced = n_dropped;
+    o->n_repush = n_repush;
+    o->max_nodes = 0;
+    o->hash = hsh;
+    o->exc = exc;
+    o->inexact = inexact;
+  }
+  if (table) {
+    double av = 0.0;
+    if (jv < 5 && acc.count > 0)
+      av = fixed_div_round_dev((i128)(((u128)acc.hi << 64) | acc.lo), (uint64_t)acc.count);
+    const uint64_t ab = (uint64_t)__double_as_longlong(av);
+    double avg[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+      avg[q] = __longlong_as_double((long long)(((uint64_t)(uint32_t)row_read((int)(ab >> 32), 0, q) << 32) |
+                                                (uint32_t)row_read((int)(uint32_t)ab, 0, q)));
+    double score = 0.0;
+    if (exc == EXC_NONE && n_snap > 0 && n_dropped == 0) {
+      const double overall = (avg[0] + avg[1] + avg[2] + avg[3]) / 4.0;
+      const double pen = avg[4] < 0.1 ? avg[4] : 0.1;
+      double sc = overall - pen;
+      sc = sc < 1.0 ? sc : 1.0;
+      score = sc > 0.0 ? sc : 0.0;
+    }
+    const bool ok = exc == EXC_NONE;
+    double v = 0.0;
+    switch (jv) {
+      case 0: v = score; break;
+      case 1: case 2: case 3: case 4: case 5: v = avg[jv - 1]; break;
+      case 6: v = (double)n_snap; break;
+      case 7: v = (double)n_frag; break;
+      case 8: v = (double)processed; break;
+      case 9: v = (double)n_dropped; break;
+      case 10: v = (double)exc; break;
+      case 11: v = (double)inexact; break;
+      case 12: v = (double)(hsh >> 11); break;
+      default: break;
+    }
+    if (!ok && jv != 10) v = 0.0;
+    if (jv < 13) table[(size_t)p * 13 + jv] = v;
+  }
+}
+
+}  // namespace fksd

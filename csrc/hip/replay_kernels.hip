@@ -15,6 +15,7 @@
 #include "scorers.hip.h"
 #include "vm_dev.hip.h"
 #include "replay_rows.hip.h"
+#include "replay_duo.hip.h"
 #include "jit_abi.h"
 
 #ifndef FKS_KIND
@@ -272,6 +273,10 @@ __global__ __launch_bounds__(64, 1) void k_replay_rows_native_prof(fksk::Builtin
   replay_rows<kFamNative, RowProf>(a.W, a.Wc, nullptr, nullptr, a.gheap, a.out, P, queue, qbase, a.prof, nat,
                                    rows_active, a.table);
 }
+// Two waves per program (wave 0: heap, wave 1: scoring; replay_duo.hip.h).
+__global__ __launch_bounds__(128, 1) void k_replay_native_duo(fksk::BuiltinArgs a, RowNativeArgs nat) {
+  replay_duo(a.W, a.Wc, a.gheap, a.out, nat, a.table);
+}
 #endif
 
 template <int NPASS, bool GHEAP>
@@ -420,6 +425,11 @@ hipError_t set_native_rows_attrs(int mx) {
   const hipError_t e = raise_lds(&k_replay_rows_native, mx);
   return e != hipSuccess ? e : raise_lds(&k_replay_rows_native_prof, mx);
 }
+hipError_t launch_native_duo(int P, size_t lds, hipStream_t st, const BuiltinArgs& a, const fksd::RowNativeArgs& nat) {
+  hipLaunchKernelGGL(k_replay_native_duo, dim3(P), dim3(128), lds, st, a, nat);
+  return hipGetLastError();
+}
+hipError_t set_native_duo_attrs(int mx) { return raise_lds(&k_replay_native_duo, mx); }
 int native_rows_waves_per_cu(size_t lds) {
   int n = 0;
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_replay_rows_native, 64, lds) == hipSuccess ? n : -1;

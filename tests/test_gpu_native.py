@@ -48,11 +48,13 @@ def test_native_equals_cpu_vm_full_trace(dev, default_workload):
     assert compared >= len(progs) - 4, skipped
 
 
-@pytest.mark.parametrize("layout", [{"native_rows": 1}, {"native_rows": 4}, {"row_kernel": "off"}],
-                         ids=["rows1", "rows4", "wave"])
+@pytest.mark.parametrize("layout", [{"native_rows": 1, "native_duo": False}, {"native_rows": 1, "native_duo": True},
+                                    {"native_rows": 4}, {"row_kernel": "off"}],
+                         ids=["rows1", "duo", "rows4", "wave"])
 def test_native_kernel_layouts_agree(dev, default_workload, layout):
-    """Row kernel with one / four programs per wave and the one-wave-per-program
-    kernel: every row bit-identical to the CPU VM (score, means, counts, trace hash)."""
+    """Row kernel with one / four programs per wave, the two-wave (heap wave +
+    scoring wave) kernel and the one-wave-per-program kernel: every row
+    bit-identical to the CPU VM (score, means, counts, trace hash)."""
     progs = programs()[:24]
     vm = ce.simulate_program_batch(default_workload, progs, threads=16)
     dev.set_options(**layout)
@@ -60,9 +62,10 @@ def test_native_kernel_layouts_agree(dev, default_workload, layout):
         nat = dev.evaluate_native(progs)
         info = dev.info()
     finally:
-        dev.set_options(native_rows=0, row_kernel="auto")
+        dev.set_options(native_rows=0, row_kernel="auto", native_duo=True)
     if "native_rows" in layout:
-        assert info["native_rows_last"] == layout["native_rows"], info
+        want = 0 if layout.get("native_duo") else layout["native_rows"]   # 0: the two-wave kernel
+        assert info["native_rows_last"] == want, info
     for i, p in enumerate(progs):
         if int(nat[i, 10]) in (Exc.UNSUPPORTED, Exc.BUDGET) or int(vm[i, 10]) in (Exc.UNSUPPORTED, Exc.BUDGET):
             continue
