@@ -24,8 +24,10 @@ exception class it was; `EvalResult.engine` which engine produced it.
 
 from __future__ import annotations
 
+import atexit
 import copy
 import os
+import threading
 import time
 from concurrent.futures import ProcessPoolExecutor
 from dataclasses import dataclass, field
@@ -157,6 +159,12 @@ class Evaluator:
         # fault-injection hook: fail this fraction of program
         # evaluations as if the replay had raised -> score 0, like the reference
         self.fault_rate = float(self.options.pop("fault_rate", 0.0) or 0.0)
+        # bytecode compiles of program batches in worker processes: the compiler is
+        # pure Python (~4 ms per program), and pipelined islands otherwise queue on
+        # the GIL for it (0: in-process)
+        self.compile_workers = int(self.options.pop("compile_workers", 0) or 0)
+        self._compile_pool = None
+        self._compile_lock = threading.Lock()
         self._fault_rng = np.random.default_rng(int(self.options.pop("fault_seed", 0)))
         self.device = None
         want_gpu = device not in ("cpu", None)
@@ -209,14 +217,32 @@ class Evaluator:
         return opts
 
     # -- programs ---------------------------------------------------------------------
-    def evaluate_programs(self, codes: Sequence[str], slot: int = 0) -> List[EvalResult]:
-        """Scores of program texts (synchronous; device work on HIP slot `slot`)."""
-        compiled: List[Optional[CompiledPolicy]] = []
-        for c in codes:
-            prog, err = try_compile(c)
+    def compile_batch(self, codes: Sequence[str]) -> List[Optional[CompiledPolicy]]:
+        """Bytecode for every program text (None: rejected), in worker processes
+        when ``compile_workers`` > 0 and the batch has more than one program."""
+        codes = list(codes)
+        if self.compile_workers > 0 and len(codes) > 1:
+            with self._compile_lock:
+                if self._compile_pool is None:
+                    import multiprocessing
+                    # spawn: the workers never inherit the parent's HIP state
+                    self._compile_pool = ProcessPoolExecutor(max_workers=self.compile_workers,
+                                                             mp_context=multiprocessing.get_context("spawn"))
+                    atexit.register(self._compile_pool.shutdown, wait=False, cancel_futures=True)
+            chunk = max(1, len(codes) // (2 * self.compile_workers))
+            results = list(self._compile_pool.map(try_compile, codes, chunksize=chunk))
+        else:
+            results = [try_compile(c) for c in codes]
+        out = []
+        for prog, _ in results:
             if prog is None:
                 self.stats["compile_errors"] += 1
-            compiled.append(prog)
+            out.append(prog)
+        return out
+
+    def evaluate_programs(self, codes: Sequence[str], slot: int = 0) -> List[EvalResult]:
+        """Scores of program texts (synchronous; device work on HIP slot `slot`)."""
+        compiled = self.compile_batch(codes)
         out = self._evaluate_compiled(list(codes), compiled, native=self.native, slot=slot)
         if self.fault_rate > 0:
             for i in range(len(out)):
@@ -304,12 +330,7 @@ class Evaluator:
         (programs the native backend declines run on the next engine at collect
         time).  Without a device everything happens at collect time."""
         pend = PendingPrograms(list(codes), slot)
-        pend.compiled = []
-        for c in pend.codes:
-            prog, _ = try_compile(c)
-            if prog is None:
-                self.stats["compile_errors"] += 1
-            pend.compiled.append(prog)
+        pend.compiled = self.compile_batch(pend.codes)
         if self.device is not None and self.native:
             idx = [i for i, p in enumerate(pend.compiled) if p is not None and p.device_ok]
             if idx:

@@ -75,6 +75,8 @@ class IslandFunSearch:
         opts = {}
         if "min_batch" in (self.config.get("device") or {}):
             opts["device_min_batch"] = int(self.config["device"]["min_batch"])
+        if "compile_workers" in (self.config.get("device") or {}):
+            opts["compile_workers"] = int(self.config["device"]["compile_workers"])
         fi = self.config.get("fault_injection") or {}
         if fi.get("eval_failure_rate"):
             opts["fault_rate"] = float(fi["eval_failure_rate"])

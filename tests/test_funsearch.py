@@ -370,3 +370,22 @@ def test_family_coupling_feeds_program_islands(tmp_path, pipe):
     isl1, isl2 = fs.coupler.islands["random_linear"], fs2.coupler.islands["random_linear"]
     assert fs2.coupler.rounds == fs.coupler.rounds
     assert (isl1.elite_scores == isl2.elite_scores).all() and (isl1.elites == isl2.elites).all()
+
+
+def test_compile_workers_give_identical_results(default_workload):
+    """device.compile_workers: bytecode compiles of a batch run in spawned
+    worker processes (off the GIL of pipelined islands); same programs, same
+    scores, rejected programs still counted."""
+    from funsearch_kubernetes_simulator_amd.bench.programs import mutation_children
+    from funsearch_kubernetes_simulator_amd.core.arrays import Workload
+    from funsearch_kubernetes_simulator_amd.engine import Evaluator
+    import numpy as np
+    sub = Workload(default_workload.cluster, default_workload.pods.subset(np.arange(0, 400)))
+    codes = [p.source for p in mutation_children(6, seed=11)] + ["def priority_function(pod, node):\n    import os\n"]
+    a = Evaluator(sub, device="cpu")
+    b = Evaluator(sub, device="cpu", options={"compile_workers": 2})
+    ca, cb = a.compile_batch(codes), b.compile_batch(codes)
+    assert [p is None for p in ca] == [p is None for p in cb] and cb[-1] is None
+    assert all(x.code == y.code and x.source == y.source for x, y in zip(ca, cb) if x is not None)
+    assert [r.score for r in a.evaluate_programs(codes)] == [r.score for r in b.evaluate_programs(codes)]
+    assert b.stats["compile_errors"] == 2
