@@ -240,7 +240,7 @@ def main() -> None:
         from funsearch_kubernetes_simulator_amd.bench.programs import measure_native, mutation_children
         program_path = measure_native(ev.device, mutation_children(args.programs, seed=args.seed + ctx.rank))
         program_path["vs_baseline"] = round(program_path["evals_per_s_incl_jit"] / BASELINE_EVALS_PER_S, 2)
-        program_path["engine"] = "hip-native (JIT-compiled programs, k_replay_native)"
+        program_path["engine"] = "hip-native (JIT-compiled programs called from a precompiled replay kernel)"
 
     per_step = args.islands * args.candidates
     total = per_step * args.steps * ctx.world_size

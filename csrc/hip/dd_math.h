@@ -46,6 +46,13 @@ __host__ __device__ inline dd dd_add(dd a, dd b) {
   s.lo += t.lo;
   return quick_two_sum(s.hi, s.lo);
 }
+// a + b where the two do not cancel (same sign, or |b| far below |a|): one
+// two_sum plus the low parts (~2^-104 relative, the cancellation-free case of dd_add)
+__host__ __device__ inline dd dd_add_nc(dd a, dd b) {
+  dd s = two_sum(a.hi, b.hi);
+  s.lo += a.lo + b.lo;
+  return quick_two_sum(s.hi, s.lo);
+}
 __host__ __device__ inline dd dd_mul(dd a, dd b) {
   dd p = two_prod(a.hi, b.hi);
   p.lo += a.hi * b.lo + a.lo * b.hi;
@@ -87,13 +94,15 @@ __host__ __device__ inline dd dd_exp(dd a) {
   q = q * rh + 2.48015873015873e-05;
   const DdConst c[6] = FKS_INV_FACT_DD;
   dd p = {q, 0.0};
+  // no step below cancels (|p r| <= 0.02 |c_n|, |r^2 p| <= 0.006 |r|, |s^2| <= 0.006 |2 s|,
+  // |s| < 0.35 in 1 + s), so the short double-double add is exact enough
 #pragma unroll
-  for (int n = 5; n >= 0; --n) p = dd_add(dd_mul(p, r), dd{c[n].hi, c[n].lo});
+  for (int n = 5; n >= 0; --n) p = dd_add_nc(dd{c[n].hi, c[n].lo}, dd_mul(p, r));
   // p = 1/2 + r/6 + ... ; s = r + r^2 p = e^r - 1
-  dd s = dd_add(r, dd_mul(dd_mul(r, r), p));
+  dd s = dd_add_nc(r, dd_mul(dd_mul(r, r), p));
   // (1+s)^(2^5): s <- 2s + s^2
-  for (int i = 0; i < 5; ++i) s = dd_add(dd_ldexp(s, 1), dd_mul(s, s));
-  dd res = dd_add({1.0, 0.0}, s);
+  for (int i = 0; i < 5; ++i) s = dd_add_nc(dd_ldexp(s, 1), dd_mul(s, s));
+  dd res = dd_add_nc({1.0, 0.0}, s);
   return dd_ldexp(res, (int)k);
 }
 

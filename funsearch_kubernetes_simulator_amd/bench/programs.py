@@ -59,7 +59,11 @@ def measure_native(dev, progs: List[CompiledPolicy]) -> dict:
     tab2 = dev.wait(0)
     t3 = time.perf_counter()
     n = len(progs)
-    return {"programs": n, "native": int(batch.ok.sum()), "new_shapes": int(batch.compiled),
+    info = dev.info()
+    kernel = ({0: "k_replay_native_duo (two waves per program)"}.get(info.get("native_rows_last"),
+              f"k_replay_rows_native ({info.get('native_rows_last')} per wave)")
+              if info.get("native_waves_last") else "k_replay_native")
+    return {"programs": n, "kernel": kernel, "native": int(batch.ok.sum()), "new_shapes": int(batch.compiled),
             "jit_s": round(t1 - t0, 3), "device_s": round(t2 - t1, 3),
             "evals_per_s_incl_jit": round(n / (t2 - t0), 1), "evals_per_s_cached": round(n / (t3 - t2), 1),
             "events": int(tab[:, 8].sum()), "repeat_identical": bool((tab == tab2).all())}
