@@ -597,7 +597,7 @@ class DeviceEngine {
     const int entries = (int)(heap_bytes_ / 8);
     if (heap_top_opt_ >= 0) return std::min(heap_top_opt_, entries);
     // (NPASS 4: 3 waves/SIMD, FKS_NP4_WAVES; NPASS 2: 3)
-    const size_t per_cu = vm ? kVmPoliciesPerCu : (npass_ >= 4 ? 12 : npass_ == 2 ? 12 : kPoliciesPerCu);
+    const size_t per_cu = vm ? kVmPoliciesPerCu : (npass_ >= 4 ? 4 * FKS_NP4_WAVES : npass_ == 2 ? 12 : kPoliciesPerCu);
     const size_t budget = kMaxLds / per_cu;
     const size_t fixed = delmap_bytes_ + (size_t)nregs * 64 * 8 + (size_t)(W_.inv_words + kWeightWords) * 8;
     int T = 0;

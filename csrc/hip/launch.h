@@ -11,6 +11,12 @@
 #include "vm_dev.hip.h"
 #include "replay_rows.hip.h"
 
+// waves per SIMD of the 256-node (NPASS 4) wave kernels; the host sizes their
+// LDS share to match (build knob for A/B runs)
+#ifndef FKS_NP4_WAVES
+#define FKS_NP4_WAVES 3     // one GPU-milli total per node keeps them <= 168 VGPRs
+#endif
+
 namespace fksk {
 
 using fksd::DevProgramTable;

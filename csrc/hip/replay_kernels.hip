@@ -102,9 +102,6 @@ hipError_t raise_lds(T* f, int max_lds) {
 #ifndef FKS_LIGHT_WAVES
 #define FKS_LIGHT_WAVES 4   // first-fit / best-fit / random_linear (build-time knob for A/B runs)
 #endif
-#ifndef FKS_NP4_WAVES
-#define FKS_NP4_WAVES 3     // 256-node clusters (config 5): one GPU-milli total per node keeps them <= 168 VGPRs
-#endif
 #ifndef FKS_HEAVY_WAVES
 #define FKS_HEAVY_WAVES 3   // feature / composite families and mixed batches
 #endif
