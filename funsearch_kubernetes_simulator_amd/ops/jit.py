@@ -52,7 +52,10 @@ LLVM_MC = os.path.join(ROCM, "lib", "llvm", "bin", "llvm-mc")
 _ATTR_RE = re.compile(r"^(attributes #\d+ = \{)", re.M)
 ARCH = os.environ.get("FKS_OFFLOAD_ARCH", "gfx950")
 JIT_INCLUDE = str(CSRC_DIR / "hip")
-DEVICE_FLAGS = ["-x", "hip", "--offload-device-only", "-nogpulib", "-nogpuinc", "-O3", f"--offload-arch={ARCH}",
+#: clang's optimisation level for generated programs (llc always runs -O3);
+#: FKS_JIT_OPT overrides it for A/B runs
+JIT_CLANG_OPT = os.environ.get("FKS_JIT_OPT", "-O3")
+DEVICE_FLAGS = ["-x", "hip", "--offload-device-only", "-nogpulib", "-nogpuinc", JIT_CLANG_OPT, f"--offload-arch={ARCH}",
                 "-std=c++17", "-DFKS_JIT", "-ffp-contract=off", "-fno-fast-math", "-Wno-unused-label",
                 "-Wno-tautological-compare", f"-I{JIT_INCLUDE}"]
 #: the runtime library's worst frame (fks_rt_binop/unop, measured from the
