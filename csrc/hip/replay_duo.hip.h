@@ -52,6 +52,59 @@ __device__ __forceinline__ void duo_st(FKS_LDS uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// CPython heappop's re-insertion of `last` at the root of a heap of n >= 1
+// items, walked by a whole wave: lane j < 63 is node j (BFS order) of the
+// 6-level subtree under the path end and holds that node's child pair, so a
+// round descends six levels (the 16-lane RowHeap::pop_reinsert: four) -- the
+// 8k-entry heap of the OpenB trace in two rounds instead of three.  anc / dir:
+// BFS indices of node j's ancestors in the subtree / of those stepping right.
+// Same moves and stores as RowHeap::pop_reinsert (bit-identical heap arrays).
+__device__ void pop_reinsert64(const RowHeap& hp, int n, uint64_t last, int j, uint64_t anc, uint64_t dir) {
+  const int k = 31 - __clz(j + 1);   // depth of node j in the subtree
+  const int ki = j - ((1 << k) - 1);
+  constexpr int kRounds = 4;          // 24 levels (host guarantees n < 2^20)
+  int pos = 0, target = -1;
+#pragma unroll
+  for (int rd = 0; rd < kRounds; ++rd) {
+    if (2 * pos + 1 >= n) break;     // pos is a leaf
+    const int q = ((pos + 1) << k) - 1 + ki;
+    const int c = 2 * q + 1;
+    const bool valid = j < 63 && c < n;
+    uint64_t vl = ~0ull, vr = ~0ull;
+    if (valid) {
+      const u64x2 pr = hp.ld_pair(c);
+      vl = pr.x;
+      vr = pr.y;
+    }
+    const bool go_r = valid && (c + 1 < n) && !(vl < vr);
+    const uint64_t m = ballot(go_r);
+    const uint64_t ex = ballot(valid);
+    const bool on = valid && (ex & anc) == anc && ((m ^ dir) & anc) == 0;
+    const uint64_t onm = ballot(on);
+    const int jd = 63 - __clzll((long long)onm);   // deepest path parent
+    const int kd = 31 - __clz(jd + 1);
+    const int taken = kd + 1;                       // levels descended this round
+    const int qd = ((pos + 1) << kd) - 1 + (jd - ((1 << kd) - 1));
+    const int next = 2 * qd + 1 + (int)((m >> jd) & 1);
+    const uint64_t v = go_r ? vr : vl;
+    const uint64_t g = ballot(on && last < v);
+    const int jl = g ? __ffsll((long long)g) - 1 : 64;
+    if (on && j < jl) {   // moves up one level
+      hp.st(q, v);
+      hp.mark(q, v);
+    }
+    if (g) {
+      const int kk = 31 - __clz(jl + 1);
+      target = ((pos + 1) << kk) - 1 + (jl - ((1 << kk) - 1));
+      break;
+    }
+    pos = next;
+    if (taken < 6) break;   // reached a leaf
+  }
+  if (target < 0) target = pos;
+  if (j == 0) { hp.st(target, last); hp.mark(target, last); }
+}
+
 __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64_t* gheap, DevResult* out,
                            RowNativeArgs nat, double* table) {
   auto cold = [&]() {
@@ -97,7 +150,10 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
     for (int i = lane; i < kKcLds; i += kWave) kcp[i] = ksrc[i];
   }
   __syncthreads();
-  if (lane >= kRow) return;   // rows 1-3 of both waves take no part (no barrier follows)
+  // H uses all 64 lanes for the pop's subtree walk (its 16-lane heap routines
+  // run duplicated on the other rows: same values, same stores); rows 1-3 of S
+  // take no part (no barrier follows)
+  if (wave == 1 && lane >= kRow) return;
 
   if (wave == 0) {
     // ================= H: the heap
@@ -109,19 +165,20 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
     heap.lb = lb;
     heap.j = jv;
     heap.rbase = 0;
-    heap.anc = heap.dir = 0;
-    for (int x = jv; x > 0 && x < 15; x = (x - 1) >> 1) {
+    heap.anc = heap.dir = 0;   // (RowHeap::pop_reinsert is not used here)
+    uint64_t anc64 = 0, dir64 = 0;
+    for (int x = lane; x > 0 && x < 63; x = (x - 1) >> 1) {
       const int a = (x - 1) >> 1;
-      heap.anc |= 1u << a;
-      if ((x & 1) == 0) heap.dir |= 1u << a;
+      anc64 |= 1ull << a;
+      if ((x & 1) == 0) dir64 |= 1ull << a;   // even BFS index = right child
     }
     const FKS_GLOBAL u64x2* heap_src = reinterpret_cast<const FKS_GLOBAL u64x2*>(global_ptr(W.heap0p));
-    for (int i = jv; i < row_heap_entries(N) / 2; i += kRow) {
+    for (int i = lane; i < row_heap_entries(N) / 2; i += kWave) {
       const u64x2 v = heap_src[i];
       if (2 * i < T + 1) *reinterpret_cast<FKS_LDS u64x2*>(heap.top + 2 * i) = v;
       else *reinterpret_cast<FKS_GLOBAL u64x2*>(heap.h + 2 * i) = v;
     }
-    for (int i = jv; i < lds_delmap_words(N); i += kRow) heap.delmap[i] = 0u;
+    for (int i = lane; i < lds_delmap_words(N); i += kWave) heap.delmap[i] = 0u;
     __builtin_amdgcn_s_waitcnt(0);
     int n = N, n_repush = 0, n_dropped = 0;
     int32_t hexc = EXC_NONE;
@@ -139,9 +196,9 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
         if (++spins > kDuoSpinCap) { hexc = EXC_INVARIANT; break; }
       }
       if (hexc != EXC_NONE) break;
-      if (jv == 0) box->ev[k % kDuoRing] = top;
-      if (jv == 0) duo_st(&box->head, k + 1);
-      if (n > 0) heap.pop_reinsert(n, last);
+      if (lane == 0) box->ev[k % kDuoRing] = top;
+      if (lane == 0) duo_st(&box->head, k + 1);
+      if (n > 0) pop_reinsert64(heap, n, last, lane, anc64, dir64);
       if ((int)(top & 3) != kDelete) {
         spins = 0;
         while (duo_ld(&box->rseq) != k + 1) {
@@ -172,7 +229,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
       }
       ++k;
     }
-    if (jv == 0) {
+    if (lane == 0) {
       box->h_exc = hexc;
       box->n_repush = n_repush;
       box->n_dropped = n_dropped;
