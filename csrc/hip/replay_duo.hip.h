@@ -28,6 +28,9 @@
 namespace fksd {
 
 constexpr int kDuoRing = 64;                  // events H may run ahead of S
+#ifndef FKS_DUO_SLEEP
+#define FKS_DUO_SLEEP 1                       // s_sleep argument of a poll (0: busy poll)
+#endif
 constexpr uint32_t kDuoSpinCap = 1u << 26;    // polls before a wait is declared lost
 enum DuoReply : int32_t { DUO_NONE = 0, DUO_PLACED = 1, DUO_FAIL = 2, DUO_ABORT = 3 };
 
@@ -192,7 +195,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
       // a free ring slot (S consumes in order)
       uint32_t spins = 0;
       while (k - duo_ld(&box->tail) >= (uint32_t)kDuoRing) {
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(FKS_DUO_SLEEP);
         if (++spins > kDuoSpinCap) { hexc = EXC_INVARIANT; break; }
       }
       if (hexc != EXC_NONE) break;
@@ -202,7 +205,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
       if ((int)(top & 3) != kDelete) {
         spins = 0;
         while (duo_ld(&box->rseq) != k + 1) {
-          __builtin_amdgcn_s_sleep(1);
+          __builtin_amdgcn_s_sleep(FKS_DUO_SLEEP);
           if (++spins > kDuoSpinCap) { hexc = EXC_INVARIANT; break; }
         }
         if (hexc != EXC_NONE) break;
@@ -284,7 +287,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
     for (;;) {
       if (duo_ld(&box->head) > k) { have = true; break; }
       if (duo_ld(&box->term)) { have = duo_ld(&box->head) > k; break; }
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(FKS_DUO_SLEEP);
       if (++spins > kDuoSpinCap) { exc = EXC_INVARIANT; break; }
     }
     if (!have) break;
@@ -431,7 +434,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
   {
     uint32_t spins = 0;
     while (!duo_ld(&box->term)) {
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(FKS_DUO_SLEEP);
       if (++spins > kDuoSpinCap) { exc = exc != EXC_NONE ? exc : EXC_INVARIANT; break; }
     }
   }
