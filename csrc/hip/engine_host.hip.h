@@ -735,7 +735,7 @@ class DeviceEngine {
     const int ra = native_rows_opt_ > 0 ? native_rows_opt_ : (P <= 2 * num_cus_ ? 1 : kRowsPerWave);
     DevWorkload Wl = W_;
     const int entries = row_heap_entries(W_.n_pods);
-    if (ra == 1 && native_duo_ && !profiled) {
+    if (ra == 1 && native_duo_) {
       // latency regime: two waves per program (heap wave + scoring wave, replay_duo.hip.h)
       int T = 1;
       while (T < entries - 1 && duo_lds_bytes(W_.n_pods, 2 * T + 1) <= kMaxLds / 2) T = 2 * T + 1;
@@ -743,8 +743,10 @@ class DeviceEngine {
       const size_t lds = duo_lds_bytes(W_.n_pods, T);
       if (lds > kMaxLds) throw std::invalid_argument("native duo layout exceeds the 160 KiB LDS");
       s.gheap.reserve((size_t)entries * 8 * (size_t)P);
+      if (profiled) s.prof.reserve((size_t)P * 128);
       const fksk::BuiltinArgs a{Wl, upload_workload(s, Wl), nullptr, nullptr, nullptr, s.res.as<DevResult>(),
-                                s.gheap.as<uint64_t>(), nullptr, s.h_tab.dev<double>()};
+                                s.gheap.as<uint64_t>(), profiled ? s.prof.as<uint64_t>() : nullptr,
+                                s.h_tab.dev<double>()};
       s.fused_table = true;
       const RowNativeArgs nat{s.h_in.dev<const uint64_t>(), s.kc.as<const int64_t>(),
                               reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + fn_bytes)};

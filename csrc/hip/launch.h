@@ -93,7 +93,8 @@ hipError_t set_rows_attrs(int max_lds);
 hipError_t launch_native_rows(int P, int waves, int rows_active, uint32_t* queue, uint32_t qbase, size_t lds,
                               hipStream_t s, const BuiltinArgs& a, const fksd::RowNativeArgs& nat);
 hipError_t set_native_rows_attrs(int max_lds);
-// two-wave native replay (replay_duo.hip.h): one program per 128-thread workgroup
+// two-wave native replay (replay_duo.hip.h): one program per 128-thread workgroup;
+// a.prof != nullptr: the s_memtime phase-profiled build ([P, 2, 8] cycles)
 hipError_t launch_native_duo(int P, size_t lds, hipStream_t stream, const BuiltinArgs& a,
                              const fksd::RowNativeArgs& nat);
 hipError_t set_native_duo_attrs(int max_lds);

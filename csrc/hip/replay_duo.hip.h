@@ -108,8 +108,31 @@ __device__ void pop_reinsert64(const RowHeap& hp, int n, uint64_t last, int j, u
   if (j == 0) { hp.st(target, last); hp.mark(target, last); }
 }
 
+// PROF: s_memtime phase split (diagnostics build), per wave into
+// prof_out[16 * blockIdx.x + 8 * wave + phase] (H: pop, ring, sift, wait, push;
+// S: wait, pod, score, verdict, delete, eval)
+template <bool PROF = false>
 __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64_t* gheap, DevResult* out,
-                           RowNativeArgs nat, double* table) {
+                           RowNativeArgs nat, double* table, uint64_t* prof_out = nullptr) {
+  uint64_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t plast = 0;
+  auto mark = [&](int ph) {
+    if constexpr (PROF) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      pacc[ph] += now - plast;
+      plast = now;
+    }
+  };
+  auto flush = [&](int wv) {
+    if constexpr (PROF) {
+      if (lane_id() < 8) {
+        uint64_t v = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v = lane_id() == i ? pacc[i] : v;
+        prof_out[16 * (size_t)blockIdx.x + 8 * wv + lane_id()] = v;
+      }
+    }
+  };
   auto cold = [&]() {
     const DevWorkload* g = reinterpret_cast<const DevWorkload*>(uniu64(reinterpret_cast<uint64_t>(Wdev)));
     asm volatile("" : "+s"(g));
@@ -186,12 +209,14 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
     int n = N, n_repush = 0, n_dropped = 0;
     int32_t hexc = EXC_NONE;
     uint32_t k = 0;
+    if constexpr (PROF) plast = __builtin_amdgcn_s_memtime();
     while (n > 0) {
       asm volatile("" : "+v"(jv));
       heap.j = jv;
       const uint64_t top = heap.ld(0);
       const uint64_t last = heap.ld(n - 1);
       --n;
+      mark(0);
       // a free ring slot (S consumes in order)
       uint32_t spins = 0;
       while (k - duo_ld(&box->tail) >= (uint32_t)kDuoRing) {
@@ -201,7 +226,9 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
       if (hexc != EXC_NONE) break;
       if (lane == 0) box->ev[k % kDuoRing] = top;
       if (lane == 0) duo_st(&box->head, k + 1);
+      mark(1);
       if (n > 0) pop_reinsert64(heap, n, last, lane, anc64, dir64);
+      mark(2);
       if ((int)(top & 3) != kDelete) {
         spins = 0;
         while (duo_ld(&box->rseq) != k + 1) {
@@ -209,6 +236,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
           if (++spins > kDuoSpinCap) { hexc = EXC_INVARIANT; break; }
         }
         if (hexc != EXC_NONE) break;
+        mark(3);
         const int code = box->code;
         if (code == DUO_ABORT) break;   // S holds the exception
         uint64_t item = box->item;
@@ -229,9 +257,11 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
           heap.push(n, item);
           ++n;
         }
+        mark(4);
       }
       ++k;
     }
+    flush(0);
     if (lane == 0) {
       box->h_exc = hexc;
       box->n_repush = n_repush;
@@ -279,6 +309,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
     }
   };
   uint32_t k = 0;
+  if constexpr (PROF) plast = __builtin_amdgcn_s_memtime();
   for (;;) {
     asm volatile("" : "+v"(jv));
     // next event, or the end of the replay
@@ -291,6 +322,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
       if (++spins > kDuoSpinCap) { exc = EXC_INVARIANT; break; }
     }
     if (!have) break;
+    mark(0);
     const uint64_t top = box->ev[k % kDuoRing];
     if (jv == 0) duo_st(&box->tail, k + 1);
     const int rank = (int)((top >> lb) & ((1ull << rb) - 1));
@@ -302,6 +334,8 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
     pod.cpu = precv.x; pod.mem = precv.y; pod.dur = precv.z;
     pod.gmilli = precv.w & 0xFFFF; pod.ngpu = (precv.w >> 16) & 0xFF; pod.cls = (precv.w >> 24) & 0xFF;
     pod.ctime = t; pod.rank = rank;
+    if constexpr (PROF) __builtin_amdgcn_s_waitcnt(0);
+    mark(1);
 
     if (kind == kDelete) {
       const int node = (int)((top >> 2) & ((1u << nb) - 1));
@@ -317,6 +351,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
       used_cpu -= pod.cpu; used_mem -= pod.mem; used_gcnt -= pod.ngpu;
       used_gml -= pod.gmilli * __popc(mask);
       if (cold()->trace_hash) hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 1, (uint64_t)t);
+      mark(4);
     } else {
       {
         const FKS_LDS int32_t* e = ntab + jv * kNodeConsts;
@@ -346,6 +381,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
       }
       const int64_t m = (int64_t)row_max_u64((uint64_t)s);
       const int best_node = m > 0 ? __ffs(row_ballot(s == m, 0)) - 1 : -1;
+      mark(2);
       if (best_node < 0) {
         // failed placement: S keeps the metrics, H computes the repush
         if (kind == kFresh && pod.ngpu > 0) {
@@ -408,6 +444,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
         if (cold()->trace_hash)
           hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2), ((uint64_t)t << 8) ^ (uint64_t)best_node);
       }
+      mark(3);
     }
     // evaluator hook (host-precomputed snapshot schedule), as in replay_rows
     ++processed;
@@ -428,8 +465,10 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
         next_fire = c;
       }
     }
+    mark(5);
     ++k;
   }
+  flush(1);
   // wait for H to finish (it may still be pushing / scanning), then take its counters
   {
     uint32_t spins = 0;

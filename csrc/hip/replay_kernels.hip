@@ -272,7 +272,11 @@ __global__ __launch_bounds__(64, 1) void k_replay_rows_native_prof(fksk::Builtin
 }
 // Two waves per program (wave 0: heap, wave 1: scoring; replay_duo.hip.h).
 __global__ __launch_bounds__(128, 1) void k_replay_native_duo(fksk::BuiltinArgs a, RowNativeArgs nat) {
-  replay_duo(a.W, a.Wc, a.gheap, a.out, nat, a.table);
+  replay_duo<false>(a.W, a.Wc, a.gheap, a.out, nat, a.table);
+}
+// s_memtime-profiled build (diagnostics): a.prof = [blocks, 2 waves, 8] cycles
+__global__ __launch_bounds__(128, 1) void k_replay_native_duo_prof(fksk::BuiltinArgs a, RowNativeArgs nat) {
+  replay_duo<true>(a.W, a.Wc, a.gheap, a.out, nat, a.table, a.prof);
 }
 #endif
 
@@ -423,10 +427,14 @@ hipError_t set_native_rows_attrs(int mx) {
   return e != hipSuccess ? e : raise_lds(&k_replay_rows_native_prof, mx);
 }
 hipError_t launch_native_duo(int P, size_t lds, hipStream_t st, const BuiltinArgs& a, const fksd::RowNativeArgs& nat) {
-  hipLaunchKernelGGL(k_replay_native_duo, dim3(P), dim3(128), lds, st, a, nat);
+  if (a.prof) hipLaunchKernelGGL(k_replay_native_duo_prof, dim3(P), dim3(128), lds, st, a, nat);
+  else hipLaunchKernelGGL(k_replay_native_duo, dim3(P), dim3(128), lds, st, a, nat);
   return hipGetLastError();
 }
-hipError_t set_native_duo_attrs(int mx) { return raise_lds(&k_replay_native_duo, mx); }
+hipError_t set_native_duo_attrs(int mx) {
+  const hipError_t e = raise_lds(&k_replay_native_duo, mx);
+  return e != hipSuccess ? e : raise_lds(&k_replay_native_duo_prof, mx);
+}
 int native_rows_waves_per_cu(size_t lds) {
   int n = 0;
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_replay_rows_native, 64, lds) == hipSuccess ? n : -1;

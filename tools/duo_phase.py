@@ -1,0 +1,50 @@
+"""s_memtime phase split of the two-wave native kernel (replay_duo.hip.h):
+cycles per event of the heap wave (pop, ring, sift, wait, push) and of the
+scoring wave (wait, pod, score, verdict, delete, eval), one program per
+workgroup.  The profiled build adds its own cost (s_memtime, a wait on the pod
+record load).
+
+    python tools/duo_phase.py --programs 48
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from funsearch_kubernetes_simulator_amd.bench.programs import mutation_children  # noqa: E402
+from funsearch_kubernetes_simulator_amd.core import load_default_workload  # noqa: E402
+from funsearch_kubernetes_simulator_amd.models.library import reference_policies  # noqa: E402
+from funsearch_kubernetes_simulator_amd.policy.compiler import compile_policy  # noqa: E402
+
+H = ("pop", "ring", "sift", "wait", "push")
+S = ("wait", "pod", "score", "verdict", "delete", "eval")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--programs", type=int, default=48)
+    a = ap.parse_args()
+    from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
+    dev = he.DeviceEvaluator(load_default_workload(), options={"native_rows": 1, "native_duo": True})
+    sets = {"first_fit": [compile_policy(reference_policies()["first_fit"])],
+            "funsearch_4901": [compile_policy(reference_policies()["funsearch_4901"])],
+            "children": mutation_children(a.programs, 0)}
+    for name, progs in sets.items():
+        dev.profile_native(progs)   # compile + warm
+        tab, prof = dev.profile_native(progs)
+        prof = prof.reshape(len(progs), 2, 8)
+        ev = float(tab[:, 8].sum())
+        rec = {"set": name, "P": len(progs), "events": int(ev),
+               "heap_wave": {H[i]: round(float(prof[:, 0, i].sum()) / ev, 1) for i in range(len(H))},
+               "score_wave": {S[i]: round(float(prof[:, 1, i].sum()) / ev, 1) for i in range(len(S))}}
+        rec["heap_total"] = round(sum(rec["heap_wave"].values()), 1)
+        rec["score_total"] = round(sum(rec["score_wave"].values()), 1)
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
