@@ -208,29 +208,41 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
     __builtin_amdgcn_s_waitcnt(0);
     int n = N, n_repush = 0, n_dropped = 0;
     int32_t hexc = EXC_NONE;
-    uint32_t k = 0;
+    uint32_t k = 0, tail_seen = 0;
+    // publish event k (a free ring slot first: S consumes in order; the
+    // consumer count is re-read only when the last value seen says the ring
+    // may be full)
+    auto publish = [&](uint64_t key) -> bool {
+      uint32_t spins = 0;
+      while (k - tail_seen >= (uint32_t)kDuoRing) {
+        tail_seen = duo_ld(&box->tail);
+        if (k - tail_seen < (uint32_t)kDuoRing) break;
+        __builtin_amdgcn_s_sleep(FKS_DUO_SLEEP);
+        if (++spins > kDuoSpinCap) { hexc = EXC_INVARIANT; return false; }
+      }
+      if (lane == 0) box->ev[k % kDuoRing] = key;
+      if (lane == 0) duo_st(&box->head, k + 1);
+      return true;
+    };
+    bool published = false;   // event k already published (the previous push's forecast)
+    uint64_t top = 0;
     if constexpr (PROF) plast = __builtin_amdgcn_s_memtime();
     while (n > 0) {
       asm volatile("" : "+v"(jv));
       heap.j = jv;
-      const uint64_t top = heap.ld(0);
+      if (!published) {
+        top = heap.ld(0);
+        mark(0);
+        if (!publish(top)) break;   // published before `last` is even read
+      }
+      published = false;
       const uint64_t last = heap.ld(n - 1);
       --n;
-      mark(0);
-      // a free ring slot (S consumes in order)
-      uint32_t spins = 0;
-      while (k - duo_ld(&box->tail) >= (uint32_t)kDuoRing) {
-        __builtin_amdgcn_s_sleep(FKS_DUO_SLEEP);
-        if (++spins > kDuoSpinCap) { hexc = EXC_INVARIANT; break; }
-      }
-      if (hexc != EXC_NONE) break;
-      if (lane == 0) box->ev[k % kDuoRing] = top;
-      if (lane == 0) duo_st(&box->head, k + 1);
       mark(1);
       if (n > 0) pop_reinsert64(heap, n, last, lane, anc64, dir64);
       mark(2);
       if ((int)(top & 3) != kDelete) {
-        spins = 0;
+        uint32_t spins = 0;
         while (duo_ld(&box->rseq) != k + 1) {
           __builtin_amdgcn_s_sleep(FKS_DUO_SLEEP);
           if (++spins > kDuoSpinCap) { hexc = EXC_INVARIANT; break; }
@@ -254,8 +266,18 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
           }
         }
         if (item != 0) {
+          // the next pop returns min(root, item) (keys are unique): publish it
+          // before the push itself, so S starts the next event meanwhile
+          const uint64_t root = n > 0 ? heap.ld(0) : ~0ull;
+          const uint64_t next = item < root ? item : root;
+          ++k;
+          if (!publish(next)) break;
+          published = true;
+          top = next;
           heap.push(n, item);
           ++n;
+          mark(4);
+          continue;
         }
         mark(4);
       }
