@@ -314,6 +314,11 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
   int32_t processed = 0, next_fire = INT32_MAX;
   int ksnap = 0;
   double thr = cold()->thr_after_fire;
+  // per-event flags / pointers of the scoring path, read once (the scoring wave
+  // carries far fewer live values than the row kernel, so they stay in SGPRs)
+  const bool trace_hash = cold()->trace_hash != 0;
+  const bool first_fit_alloc = cold()->first_fit_alloc != 0;
+  const int64_t* gmem_node = cold()->gmem_total + (size_t)jv * kGmax;
   if (cold()->n_fire > 0) {
     next_fire = (int32_t)*global_ptr(&cold()->snap_fire[0]);
   } else {
@@ -372,7 +377,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
       }
       used_cpu -= pod.cpu; used_mem -= pod.mem; used_gcnt -= pod.ngpu;
       used_gml -= pod.gmilli * __popc(mask);
-      if (cold()->trace_hash) hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 1, (uint64_t)t);
+      if (trace_hash) hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 1, (uint64_t)t);
       mark(4);
     } else {
       {
@@ -391,7 +396,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
         for (int g = 0; g < kGmax; ++g) gt[g] = nr.gt(0, g);
         s = prog(nr.cpu_left[0], nr.cpu_total[0], nr.mem_left[0], nr.mem_total[0], pack_gpu_ng(nr.gpu_left[0], nr.ngpus[0]),
                  gl[0], gl[1], gl[2], gl[3], gl[4], gl[5], gl[6], gl[7], gt[0], gt[1], gt[2], gt[3], gt[4], gt[5],
-                 gt[6], gt[7], cold()->gmem_total + (size_t)jv * kGmax, pod.cpu, pod.mem,
+                 gt[6], gt[7], gmem_node, pod.cpu, pod.mem,
                  pod.gmilli | (pod.ngpu << 16), pod.ctime, pod.dur, kcp);
         if (s < 0) { lexc = (int)(-s); s = 0; }
       }
@@ -432,12 +437,12 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
           frag = tg > 0 ? (double)stranded / (double)tg : 0.0;
         }
         acc.add(4, frag, jv);
-        if (cold()->trace_hash) hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 2, (uint64_t)t);
+        if (trace_hash) hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 2, (uint64_t)t);
       } else {
         int gmask = 0, ok = 1;
         if (pod.ngpu > 0) {
           int myok = 1;
-          const int mymask = pick_gpus<1>(nr, 0, pod.gmilli, pod.ngpu, cold()->first_fit_alloc != 0, myok);
+          const int mymask = pick_gpus<1>(nr, 0, pod.gmilli, pod.ngpu, first_fit_alloc, myok);
           const int packed = row_read(mymask | (myok << 8), 0, best_node);
           gmask = packed & 0xFF;
           ok = packed >> 8;
@@ -463,7 +468,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
           for (int sl = 0; sl < kRowClassSlots; ++sl)
             if (sl == (pod.cls >> 4) && jv == (pod.cls & 15)) wcnt[sl] -= 1;
         }
-        if (cold()->trace_hash)
+        if (trace_hash)
           hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2), ((uint64_t)t << 8) ^ (uint64_t)best_node);
       }
       mark(3);
