@@ -13,6 +13,7 @@
 #include "seqmatch.hpp"
 #include "trace_io.hpp"
 #include "vm_cpu.hpp"
+#include "../jit/gcn_api.hpp"
 
 namespace py = pybind11;
 using namespace fks;
@@ -324,6 +325,80 @@ PYBIND11_MODULE(_fks_cpu, m) {
   m.def("exact_mean", [](std::vector<double> xs) {
     FixedAcc a; for (double x : xs) a.add(x);
     return py::make_tuple(fixed_mean(a), a.inexact);
+  });
+
+  // ---- baseline program JIT (csrc/jit): bytecode -> gfx950 machine code
+  m.def("gcn_compile", [](py::bytes code, py::array_t<uint8_t, py::array::c_style | py::array::forcecast> ctag,
+                          py::array_t<uint8_t, py::array::c_style | py::array::forcecast> is_lit,
+                          py::array_t<int64_t, py::array::c_style | py::array::forcecast> iconst,
+                          py::array_t<double, py::array::c_style | py::array::forcecast> fconst) {
+    const std::string c = code;
+    gcnapi::ProgramDesc p;
+    p.code = reinterpret_cast<const uint8_t*>(c.data());
+    p.code_bytes = c.size();
+    p.ctag = ctag.data(); p.is_lit = is_lit.data(); p.iconst = iconst.data(); p.fconst = fconst.data();
+    p.n_const = (size_t)ctag.size();
+    if ((size_t)is_lit.size() != p.n_const || (size_t)iconst.size() != p.n_const || (size_t)fconst.size() != p.n_const)
+      throw std::invalid_argument("constant arrays differ in length");
+    gcnapi::Result r;
+    {
+      py::gil_scoped_release rel;
+      r = gcnapi::compile(p);
+    }
+    py::dict out;
+    out["ok"] = r.ok;
+    out["reason"] = r.reason;
+    out["words"] = np_of(r.words);
+    out["relocs"] = np_of(r.relocs);
+    out["n_insns"] = r.n_insns; out["vgprs"] = r.vgprs; out["sgprs"] = r.sgprs; out["calls"] = r.calls;
+    out["vregs"] = r.vregs; out["tagged"] = r.tagged; out["mir"] = r.mir;
+    return out;
+  }, py::arg("code"), py::arg("ctag"), py::arg("is_lit"), py::arg("iconst"), py::arg("fconst"));
+  m.def("gcn_listing", [](py::bytes code, std::vector<uint8_t> ctag, std::vector<uint8_t> is_lit,
+                          std::vector<int64_t> iconst, std::vector<double> fconst) {
+    const std::string c = code;
+    gcnapi::ProgramDesc p;
+    p.code = reinterpret_cast<const uint8_t*>(c.data());
+    p.code_bytes = c.size();
+    p.ctag = ctag.data(); p.is_lit = is_lit.data(); p.iconst = iconst.data(); p.fconst = fconst.data();
+    p.n_const = ctag.size();
+    return gcnapi::listing(p);
+  });
+  m.def("gcn_emu_event", [](py::bytes code, std::vector<uint8_t> ctag, std::vector<uint8_t> is_lit,
+                            std::vector<int64_t> iconst, std::vector<double> fconst, std::vector<int64_t> kc,
+                            std::vector<int64_t> node, std::vector<int32_t> gl, std::vector<int32_t> gt,
+                            std::vector<int64_t> gmem, std::vector<int64_t> pod) {
+    const std::string c = code;
+    gcnapi::ProgramDesc p;
+    p.code = reinterpret_cast<const uint8_t*>(c.data());
+    p.code_bytes = c.size();
+    p.ctag = ctag.data(); p.is_lit = is_lit.data(); p.iconst = iconst.data(); p.fconst = fconst.data();
+    p.n_const = ctag.size();
+    return gcnapi::emu_event(p, kc, node, gl, gt, gmem, pod);
+  });
+  m.def("gcn_emu_batch", [](const Workload& w, std::vector<py::bytes> codes, std::vector<std::vector<uint8_t>> ctags,
+                            std::vector<std::vector<uint8_t>> lits, std::vector<std::vector<int64_t>> iconsts,
+                            std::vector<std::vector<double>> fconsts, std::vector<std::vector<int64_t>> kcs,
+                            py::dict opts, int threads) {
+    const size_t P = codes.size();
+    std::vector<std::string> cs(P);
+    std::vector<gcnapi::ProgramDesc> ps(P);
+    for (size_t i = 0; i < P; ++i) {
+      cs[i] = codes[i];
+      ps[i].code = reinterpret_cast<const uint8_t*>(cs[i].data());
+      ps[i].code_bytes = cs[i].size();
+      ps[i].ctag = ctags[i].data(); ps[i].is_lit = lits[i].data(); ps[i].iconst = iconsts[i].data();
+      ps[i].fconst = fconsts[i].data(); ps[i].n_const = ctags[i].size();
+    }
+    SimOptions o = make_options(opts);
+    std::vector<SimResult> rs;
+    {
+      py::gil_scoped_release rel;
+      rs = gcnapi::emu_simulate_batch(w, ps, kcs, o, threads);
+    }
+    py::array_t<double> out({(int64_t)P, (int64_t)kCols});
+    for (size_t i = 0; i < P; ++i) fill_row(out.mutable_data() + i * kCols, rs[i]);
+    return out;
   });
   m.attr("RESULT_COLUMNS") = py::make_tuple("score", "avg_cpu", "avg_mem", "avg_gpu_count", "avg_gpu_milli",
                                             "frag", "n_snapshots", "n_frag_events", "n_events", "n_unplaced",

@@ -1,0 +1,1358 @@
+// Baseline program JIT: policy bytecode -> gfx950 machine instructions.
+//
+// The LLVM path (policy/native_codegen.py -> ops/jit.py) produces tight code
+// but costs ~140 ms of clang + llc per program, which is more than a whole
+// replay of a new LLM program is worth.  This generator lowers the same
+// bytecode (ISA: csrc/include/fks/bytecode.hpp) directly, in tens of
+// microseconds, to a function with the same ABI (jit_abi.h ProgFn): it is
+// called from the precompiled replay kernels with the node in v0-v22, the pod
+// in v23-v28 and the LDS constant block in v29, and returns
+// int(max(0, priority)) or -exception in v[0:1].
+//
+// Design (SIMT over nodes, like the VMs):
+//  * static types from the same forward analysis as native_codegen.py: most
+//    operations are emitted for int64 or f64 operands; genuinely mixed
+//    operands call the precompiled runtime (rt_binop / rt_unop, d_binop_impl
+//    semantics) or use tag bits kept per lane in one VGPR;
+//  * registers: virtual registers get even-aligned VGPR pairs by liveness
+//    (interference colouring); only caller-saved registers are used, so the
+//    function needs no prologue saves; pod fields are wave-uniform and live
+//    in SGPR pairs;
+//  * control flow: structured, with EXEC masks -- IF saves EXEC, ELSE switches
+//    to the saved complement, ENDIF restores EXEC minus the lanes that left
+//    (returned / raised / broke / continued); loops keep their entry mask, a
+//    break mask and a continue mask, and every back edge charges the per-call
+//    iteration budget (EXC_BUDGET), so every loop ends;
+//  * exceptions are "soft" per lane, exactly as the C++ codegen: the first
+//    exception is kept, the lane keeps running until the next RET / back edge;
+//  * anything the baseline tier does not lower (an unknown opcode, register
+//    pressure) throws CodegenError and the program goes to the LLVM tier or
+//    the VMs.
+#pragma once
+
+#include <array>
+#include <map>
+#include <set>
+#include <stdexcept>
+#include <vector>
+
+#include "fks/bytecode.hpp"
+#include "fks/types.hpp"
+#include "gcn_lower.hpp"
+
+namespace fks {
+namespace gcn {
+
+class CodegenError : public std::runtime_error {
+ public:
+  using std::runtime_error::runtime_error;
+};
+
+enum : uint8_t { TY_I = 1, TY_F = 2, TY_IF = 3 };
+
+struct ProgIn {
+  const Insn* code = nullptr;
+  int n = 0;
+  const uint8_t* ctag = nullptr;
+  const uint8_t* is_lit = nullptr;   // constant slot read from the kc block at run time
+  const int64_t* iconst = nullptr;
+  const double* fconst = nullptr;
+  int n_const = 0;
+};
+
+struct GenStats {
+  int vregs = 0, vgprs_used = 0, sgprs_used = 0, calls = 0, tagged = 0;
+};
+
+class Codegen {
+ public:
+  explicit Codegen(const ProgIn& p) : P_(p), n_(p.n) {}
+
+  Func run(GenStats* st = nullptr) {
+    if (n_ <= 0) throw CodegenError("empty program");
+    if (P_.n_const + 1 > 256) throw CodegenError("constant block larger than the LDS staging area");
+    analyse_flow();
+    infer_types();
+    liveness();
+    simt_liveness();
+    layout_registers();
+    emit_all();
+    if (st) {
+      st->vregs = n_vregs_;
+      st->calls = (int)F_.calls.size();
+      st->tagged = n_tagged_;
+      st->vgprs_used = max_vgpr_ + 1;
+      st->sgprs_used = max_sgpr_ + 1;
+    }
+    return F_;
+  }
+
+ private:
+  const ProgIn& P_;
+  int n_;
+  Func F_;
+  // ---- flow
+  std::vector<int> brk_t_, cont_t_;
+  std::vector<std::array<int, 2>> succ_;
+  // ---- types: per pc entry state
+  std::vector<std::array<uint8_t, kMaxRegs>> ty_;
+  std::vector<char> reached_;
+  // ---- liveness (per lane: register allocation) and SIMT liveness (spills)
+  std::vector<uint64_t> live_in_, live_out_;
+  std::vector<uint64_t> slive_out_;
+  // ---- registers
+  int n_vregs_ = 0, n_tagged_ = 0;
+  std::array<int, kMaxRegs> base_{};      // VGPR pair base per virtual register (-1 unused)
+  std::array<int, kMaxRegs> tagbit_{};    // tag bit index (-1: untagged)
+  uint64_t tagged_ = 0;
+  bool use_node_ = false, use_gl_ = false, use_gmem_ = false, use_kc_ = false, has_loop_ = false;
+  std::array<int, 6> pod_s_{};            // SGPR pair per pod field (-1 unused)
+  int v_exc_ = -1, v_bud_ = -1, v_out_ = -1, v_spill_ = -1;
+  int v_tag_[2] = {-1, -1};
+  int T_[3] = {-1, -1, -1};               // temp VGPR pairs
+  int s_entry_ = -1, s_dead_ = -1, ST_[3] = {-1, -1, -1}, S_LIT_ = -1;
+  std::vector<int> free_spairs_;
+  std::vector<int> ctl_spairs_;           // SGPR pairs held by open control frames
+  int max_vgpr_ = 0, max_sgpr_ = 0;
+
+  struct Frame {
+    bool loop;
+    int pc;
+    int s_save = -1, s_else = -1;         // IF
+    int s_entry = -1, s_brk = -1, s_cont = -1;   // LOOP
+    int l_exit = -1, l_head = -1;
+  };
+  std::vector<Frame> frames_;
+  std::map<int, int> label_at_pc_;        // pc -> label placed before its code
+
+  // ============================================================ analysis
+  static bool defines(uint8_t op) {
+    switch (op) {
+      case OP_NOP: case OP_IF: case OP_ELSE: case OP_ENDIF: case OP_LOOP_BEGIN: case OP_LOOP_TEST:
+      case OP_LOOP_CONT: case OP_LOOP_NEXT: case OP_LOOP_EXIT: case OP_BREAK: case OP_CONTINUE: case OP_RET:
+      case OP_RAISE: case OP_END:
+        return false;
+      default:
+        return true;
+    }
+  }
+  uint64_t uses(int pc) const {
+    const Insn& in = P_.code[pc];
+    uint64_t u = 0;
+    if (in.op == OP_LOOP_BEGIN || in.op == OP_LOOP_EXIT || in.op == OP_CONST || in.op == OP_POD ||
+        in.op == OP_NODE || in.op == OP_RAISE)
+      return 0;
+    if (in.a != kNoReg) u |= 1ull << in.a;
+    if (in.b != kNoReg) u |= 1ull << in.b;
+    if ((in.op == OP_GLIST_SLICE || in.op == OP_GLIST_INSERT) && in.imm != kNoReg) u |= 1ull << in.imm;
+    return u;
+  }
+  uint64_t defs(int pc) const {
+    const Insn& in = P_.code[pc];
+    return (defines(in.op) && in.d != kNoReg) ? (1ull << in.d) : 0ull;
+  }
+
+  void analyse_flow() {
+    brk_t_.assign(n_, -1);
+    cont_t_.assign(n_, -1);
+    std::vector<int> stack;
+    std::map<int, int> exit_of;
+    std::map<int, std::vector<int>> conts;
+    std::map<int, int> pend_b, pend_c;
+    for (int pc = 0; pc < n_; ++pc) {
+      const Insn& in = P_.code[pc];
+      if (in.a != kNoReg && in.a >= kMaxRegs) throw CodegenError("register out of range");
+      if (in.op == OP_LOOP_BEGIN) { stack.push_back(pc); conts[pc]; }
+      else if (in.op == OP_LOOP_EXIT) {
+        if (stack.empty()) throw CodegenError("LOOP_EXIT without LOOP_BEGIN");
+        exit_of[stack.back()] = pc;
+        stack.pop_back();
+      } else if (in.op == OP_LOOP_CONT) {
+        if (stack.empty()) throw CodegenError("LOOP_CONT outside a loop");
+        conts[stack.back()].push_back(pc);
+      } else if (in.op == OP_BREAK || in.op == OP_CONTINUE) {
+        if (stack.empty()) throw CodegenError("BREAK / CONTINUE outside a loop");
+        (in.op == OP_BREAK ? pend_b : pend_c)[pc] = stack.back();
+      }
+    }
+    if (!stack.empty()) throw CodegenError("unterminated loop");
+    for (auto& kv : pend_b) brk_t_[kv.first] = exit_of[kv.second];
+    for (auto& kv : pend_c) {
+      int t = -1;
+      for (int c : conts[kv.second])
+        if (c > kv.first) { t = c; break; }
+      if (t < 0) throw CodegenError("CONTINUE without a following LOOP_CONT");
+      cont_t_[kv.first] = t;
+    }
+    succ_.assign(n_, {-1, -1});
+    for (int pc = 0; pc < n_; ++pc) {
+      const Insn& in = P_.code[pc];
+      std::array<int, 2> sc{-1, -1};
+      switch (in.op) {
+        case OP_IF: sc = {pc + 1, in.imm + 1}; break;
+        case OP_ELSE: case OP_LOOP_NEXT: sc = {in.imm, -1}; break;
+        case OP_LOOP_TEST: sc = {pc + 1, in.imm}; break;
+        case OP_BREAK: sc = {brk_t_[pc], -1}; break;
+        case OP_CONTINUE: sc = {cont_t_[pc], -1}; break;
+        case OP_RET: case OP_RAISE: case OP_END: break;
+        default: sc = {pc + 1, -1};
+      }
+      for (int t : sc)
+        if (t != -1 && (t < 0 || t >= n_)) throw CodegenError("jump target out of range");
+      succ_[pc] = sc;
+    }
+  }
+
+  static uint8_t result_type(uint8_t op, uint8_t ta, uint8_t tb, uint8_t ct) {
+    switch (op) {
+      case OP_CONST: return ct;
+      case OP_MOV: case OP_POS: return ta;
+      case OP_POD: case OP_NODE: case OP_GPU: case OP_GLIST_ALL: case OP_GLIST_LEN: case OP_GLIST_GET:
+      case OP_GLIST_SLICE: case OP_GLIST_NEW: case OP_GLIST_APPEND: case OP_GLIST_INSERT: case OP_NOT:
+      case OP_TRUTH: case OP_ISINT: case OP_LT: case OP_LE: case OP_GT: case OP_GE: case OP_EQ: case OP_NE:
+      case OP_INT: case OP_ROUND: case OP_LOOP_BEGIN:
+        return TY_I;
+      case OP_TDIV: case OP_FLOAT: case OP_SQRT: case OP_LOG: case OP_LOGB: case OP_EXP: case OP_MPOW:
+      case OP_SIN: case OP_COS: case OP_TAN:
+        return TY_F;
+      case OP_ADD: case OP_SUB: case OP_MUL: case OP_FDIV: case OP_MOD:
+        return (uint8_t)(((ta & TY_I) && (tb & TY_I) ? TY_I : 0) | ((ta & TY_F) || (tb & TY_F) ? TY_F : 0));
+      case OP_POW:
+        return (uint8_t)(((ta & TY_I) && (tb & TY_I) ? TY_IF : 0) | ((ta & TY_F) || (tb & TY_F) ? TY_F : 0));
+      case OP_NEG: case OP_ABS: return ta;
+      case OP_MIN2: case OP_MAX2: return (uint8_t)(ta | tb);
+      default: return 0;
+    }
+  }
+
+  void infer_types() {
+    ty_.assign(n_, {});
+    reached_.assign(n_, 0);
+    for (auto& a : ty_) a.fill(TY_I);
+    reached_[0] = 1;
+    std::vector<int> work{0};
+    std::vector<char> on(n_, 0);
+    on[0] = 1;
+    while (!work.empty()) {
+      const int pc = work.back();
+      work.pop_back();
+      on[pc] = 0;
+      const Insn& in = P_.code[pc];
+      std::array<uint8_t, kMaxRegs> out = ty_[pc];
+      if (in.d != kNoReg && defines(in.op)) {
+        uint8_t ct = 0;
+        if (in.op == OP_CONST) {
+          if (in.imm < 0 || in.imm >= P_.n_const) throw CodegenError("constant index out of range");
+          ct = P_.ctag[in.imm] == TAG_FLOAT ? TY_F : TY_I;
+        }
+        const uint8_t ta = in.a != kNoReg ? ty_[pc][in.a] : TY_I;
+        const uint8_t tb = in.b != kNoReg ? ty_[pc][in.b] : TY_I;
+        uint8_t t = result_type(in.op, ta, tb, ct);
+        if (t == 0) t = TY_IF;
+        out[in.d] = t;
+      }
+      for (int s : succ_[pc]) {
+        if (s < 0) continue;
+        bool changed = false;
+        if (!reached_[s]) {
+          reached_[s] = 1;
+          ty_[s] = out;
+          changed = true;
+        } else {
+          for (int r = 0; r < kMaxRegs; ++r) {
+            const uint8_t u = (uint8_t)(ty_[s][r] | out[r]);
+            if (u != ty_[s][r]) { ty_[s][r] = u; changed = true; }
+          }
+        }
+        if (changed && !on[s]) { on[s] = 1; work.push_back(s); }
+      }
+    }
+  }
+
+  void liveness() {
+    live_in_.assign(n_, 0);
+    live_out_.assign(n_, 0);
+    bool changed = true;
+    while (changed) {
+      changed = false;
+      for (int pc = n_ - 1; pc >= 0; --pc) {
+        uint64_t out = 0;
+        for (int s : succ_[pc])
+          if (s >= 0) out |= live_in_[s];
+        const uint64_t in = uses(pc) | (out & ~defs(pc));
+        if (out != live_out_[pc] || in != live_in_[pc]) {
+          live_out_[pc] = out;
+          live_in_[pc] = in;
+          changed = true;
+        }
+      }
+    }
+  }
+
+  // SIMT liveness: what ANY lane may still read.  The wave walks structured
+  // code linearly (then-branch, then else-branch; code after a break or a
+  // return still runs for the other lanes), so a register the suspended lanes
+  // need later is live here even if no path of the active lanes reads it.
+  // A runtime call clobbers every lane of the caller-saved registers, so its
+  // spill set comes from this relation.
+  void simt_liveness() {
+    std::vector<uint64_t> in(n_, 0);
+    slive_out_.assign(n_, 0);
+    bool changed = true;
+    while (changed) {
+      changed = false;
+      for (int pc = n_ - 1; pc >= 0; --pc) {
+        const Insn& ins = P_.code[pc];
+        uint64_t out = 0;
+        if (ins.op != OP_END && pc + 1 < n_) out |= in[pc + 1];
+        int t = -1;
+        if (ins.op == OP_IF || ins.op == OP_ELSE || ins.op == OP_LOOP_TEST || ins.op == OP_LOOP_NEXT) t = ins.imm;
+        if (t >= 0 && t < n_) out |= in[t];
+        const uint64_t li = uses(pc) | (out & ~defs(pc));
+        if (out != slive_out_[pc] || li != in[pc]) {
+          slive_out_[pc] = out;
+          in[pc] = li;
+          changed = true;
+        }
+      }
+    }
+  }
+
+  // ============================================================ registers
+  void layout_registers() {
+    uint64_t used = 0;
+    for (int pc = 0; pc < n_; ++pc) {
+      const Insn& in = P_.code[pc];
+      used |= uses(pc) | defs(pc);
+      if (in.op == OP_NODE) use_node_ = true;
+      if (in.op == OP_GLIST_ALL || in.op == OP_GLIST_LEN) use_node_ = true;
+      if (in.op == OP_GPU) {
+        if (in.imm == 0 || in.imm == 1) use_gl_ = true;
+        else use_gmem_ = true;
+      }
+      if (in.op == OP_CONST && P_.is_lit[in.imm]) use_kc_ = true;
+      if (in.op == OP_LOOP_BEGIN) has_loop_ = true;
+      if (in.op == OP_POD) {
+        const int f = (in.imm >= 0 && in.imm <= 5) ? in.imm : 5;
+        pod_s_[f] = 1;
+      }
+    }
+    // tagged registers: read somewhere while their type is mixed
+    for (int pc = 0; pc < n_; ++pc) {
+      if (!reached_[pc]) continue;
+      const uint64_t u = uses(pc);
+      for (int r = 0; r < kMaxRegs; ++r)
+        if ((u >> r & 1) && ty_[pc][r] == TY_IF) tagged_ |= 1ull << r;
+    }
+    // interference
+    std::vector<uint64_t> adj(kMaxRegs, 0);
+    auto clique = [&](uint64_t set) {
+      for (int r = 0; r < kMaxRegs; ++r)
+        if (set >> r & 1) adj[r] |= set & ~(1ull << r);
+    };
+    clique(live_in_[0]);
+    for (int pc = 0; pc < n_; ++pc) {
+      clique(live_in_[pc]);
+      const uint64_t d = defs(pc);
+      if (d) {
+        const int r = __builtin_ctzll(d);
+        adj[r] |= live_out_[pc] & ~d;
+        for (int q = 0; q < kMaxRegs; ++q)
+          if (live_out_[pc] >> q & 1 && q != r) adj[q] |= d;
+      }
+    }
+    // VGPR pools (caller-saved only; v0-v22 and v29 are the node arguments / kc)
+    std::vector<int> pairs = {24, 26, 30, 32, 34, 36, 38, 48, 50, 52, 54, 64, 66, 68, 70,
+                              80, 82, 84, 86, 96, 98, 100, 102, 112, 114, 116, 118};
+    std::vector<int> singles = {28};
+    if (!use_gl_) {
+      for (int b = 6; b <= 18; b += 2) pairs.push_back(b);
+      singles.push_back(5);
+      singles.push_back(20);
+    }
+    if (!use_gmem_) pairs.push_back(22);
+    else singles.push_back(23);
+    if (!use_node_ && !use_gl_ && !use_gmem_) {
+      // node fields unused: v0-v4 are free too (v0-v1 also carry the result)
+      pairs.push_back(2);
+      singles.push_back(4);
+    }
+    auto take_pair = [&]() {
+      if (pairs.empty()) throw CodegenError("out of VGPR pairs");
+      const int b = pairs.front();
+      pairs.erase(pairs.begin());
+      max_vgpr_ = std::max(max_vgpr_, b + 1);
+      return b;
+    };
+    auto take_single = [&]() {
+      if (singles.empty()) {
+        const int b = take_pair();
+        singles.push_back(b + 1);
+        return b;
+      }
+      const int s1 = singles.front();
+      singles.erase(singles.begin());
+      max_vgpr_ = std::max(max_vgpr_, s1);
+      return s1;
+    };
+    for (int i = 0; i < 4; ++i) F_.mr.x[i] = take_pair();
+    for (int i = 0; i < 3; ++i) T_[i] = take_pair();
+    v_out_ = take_pair();
+    v_exc_ = take_single();
+    if (has_loop_) v_bud_ = take_single();
+    n_tagged_ = __builtin_popcountll(tagged_);
+    tagbit_.fill(-1);
+    {
+      int k = 0;
+      for (int r = 0; r < kMaxRegs; ++r)
+        if (tagged_ >> r & 1) tagbit_[r] = k++;
+      if (k > 0) v_tag_[0] = take_single();
+      if (k > 32) v_tag_[1] = take_single();
+    }
+    v_spill_ = take_single();
+    // colour virtual registers (most-constrained first)
+    base_.fill(-1);
+    std::vector<int> order;
+    for (int r = 0; r < kMaxRegs; ++r)
+      if (used >> r & 1) order.push_back(r);
+    n_vregs_ = (int)order.size();
+    std::sort(order.begin(), order.end(),
+              [&](int a, int b) { return __builtin_popcountll(adj[a]) > __builtin_popcountll(adj[b]); });
+    std::vector<int> colour_base;   // colour -> VGPR pair
+    std::vector<int> colour(kMaxRegs, -1);
+    for (int r : order) {
+      std::vector<char> busy(colour_base.size(), 0);
+      for (int q = 0; q < kMaxRegs; ++q)
+        if ((adj[r] >> q & 1) && colour[q] >= 0) busy[(size_t)colour[q]] = 1;
+      int c = -1;
+      for (size_t k = 0; k < busy.size(); ++k)
+        if (!busy[k]) { c = (int)k; break; }
+      if (c < 0) {
+        colour_base.push_back(take_pair());
+        c = (int)colour_base.size() - 1;
+      }
+      colour[r] = c;
+      base_[r] = colour_base[(size_t)c];
+    }
+    // SGPR pairs: s[24:25] and s[28:29] are macro scratch; s30-s33 ABI; callee-saved ones untouched
+    free_spairs_ = {0, 2, 4, 6, 8, 10, 12, 14, 16, 18, 20, 22, 26, 40, 42, 44, 46, 56, 58, 60, 62, 72, 74, 76, 78,
+                    88, 90, 92, 94};
+    s_entry_ = take_spair();
+    s_dead_ = take_spair();
+    for (int i = 0; i < 3; ++i) ST_[i] = take_spair();
+    S_LIT_ = take_spair();
+    for (int f = 0; f < 6; ++f)
+      if (pod_s_[f] > 0) pod_s_[f] = take_spair();
+      else pod_s_[f] = -1;
+  }
+  int take_spair() {
+    if (free_spairs_.empty()) throw CodegenError("out of SGPR pairs");
+    const int b = free_spairs_.front();
+    free_spairs_.erase(free_spairs_.begin());
+    max_sgpr_ = std::max(max_sgpr_, b + 1);
+    return b;
+  }
+  void give_spair(int b) {
+    free_spairs_.insert(free_spairs_.begin(), b);
+  }
+
+  // ============================================================ emission helpers
+  void e(const MI& m) { F_.mi.push_back(m); }
+  uint16_t R(int r) const {
+    if (base_[r] < 0) throw CodegenError("register without a home");
+    return v(base_[r]);
+  }
+  uint16_t Rh(int r) const { return (uint16_t)(R(r) + 1); }
+  uint16_t T(int i) const { return v(T_[i]); }
+  uint16_t Th(int i) const { return v(T_[i] + 1); }
+  uint16_t X(int i) const { return v(F_.mr.x[i]); }
+  uint16_t ST(int i) const { return s(ST_[i]); }
+  uint16_t TAGV(int r) const { return v(v_tag_[tagbit_[r] >> 5]); }
+  int label() { return F_.new_label(); }
+  void place(int lab) { e(mkimm(LABEL, lab)); }
+  int label_for_pc(int pc) {
+    auto it = label_at_pc_.find(pc);
+    if (it != label_at_pc_.end()) return it->second;
+    const int l = label();
+    label_at_pc_[pc] = l;
+    return l;
+  }
+
+  // VOPC into an SGPR pair
+  void cmp(Opc op, uint16_t dst, uint16_t a, uint16_t b, uint8_t abs = 0) {
+    MI m = mk(op, NONE, a, b);
+    m.sd = dst;
+    m.abs = abs;
+    e(m);
+  }
+  void movk64(uint16_t dst_pair, uint64_t x) {   // SGPR pair constant
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t w = (uint32_t)(x >> (32 * h));
+      const uint16_t c = ic((int32_t)w);
+      if (c != NONE) e(mk(S_MOV_B32, (uint16_t)(dst_pair + h), c));
+      else e(mklit(S_MOV_B32, (uint16_t)(dst_pair + h), w));
+    }
+  }
+  void vmov32(uint16_t d, uint32_t x) {
+    const uint16_t c = ic((int32_t)x);
+    if (c != NONE) e(mk(V_MOV_B32, d, c));
+    else e(mklit(V_MOV_B32, d, x));
+  }
+  // exc = (exc == 0 && lanes(mask)) ? code : exc
+  void soft_raise(uint16_t mask, int code) {
+    cmp(V_CMP_EQ_U32, ST(2), ic(0), v(v_exc_));
+    e(mk(S_AND_B64, VCC, ST(2), mask));
+    if (ic(code) != NONE) e(mk(V_CNDMASK_B32, v(v_exc_), v(v_exc_), ic(code), VCC));
+    else {
+      vmov32(Th(2), (uint32_t)code);
+      e(mk(V_CNDMASK_B32, v(v_exc_), v(v_exc_), Th(2), VCC));
+    }
+  }
+  // same with the code in a VGPR
+  void soft_raise_v(uint16_t mask, uint16_t code_v) {
+    cmp(V_CMP_EQ_U32, ST(2), ic(0), v(v_exc_));
+    e(mk(S_AND_B64, VCC, ST(2), mask));
+    e(mk(V_CNDMASK_B32, v(v_exc_), v(v_exc_), code_v, VCC));
+  }
+  // lanes where register r holds a float -> SGPR pair
+  void tag_mask(int r, uint16_t dst) {
+    if (tagbit_[r] < 0) throw CodegenError("dynamic type of an untagged register");
+    e(mk(V_BFE_U32, Th(2), TAGV(r), ic(tagbit_[r] & 31), ic(1)));
+    cmp(V_CMP_NE_U32, dst, ic(0), Th(2));
+  }
+  // float flag of register r (type t at this pc) as an operand (inline 0 / 1 or a VGPR)
+  uint16_t flag_of(int r, uint8_t t, uint16_t tmpv) {
+    if (t == TY_I) return ic(0);
+    if (t == TY_F) return ic(1);
+    if (tagbit_[r] < 0) throw CodegenError("dynamic type of an untagged register");
+    e(mk(V_BFE_U32, tmpv, TAGV(r), ic(tagbit_[r] & 31), ic(1)));
+    return tmpv;
+  }
+  void set_tag_static(int r, bool fl) {
+    if (tagbit_[r] < 0) return;
+    const uint32_t bit = 1u << (tagbit_[r] & 31);
+    if (fl) {
+      if (ic(bit) != NONE) e(mk(V_OR_B32, TAGV(r), ic(bit), TAGV(r)));
+      else e(mklit(V_OR_B32, TAGV(r), bit, TAGV(r)));
+    } else {
+      e(mklit(V_AND_B32, TAGV(r), ~bit, TAGV(r)));
+    }
+  }
+  void set_tag_flag(int r, uint16_t flag_v) {   // flag_v: VGPR holding 0 / 1
+    if (tagbit_[r] < 0) return;
+    set_tag_static(r, false);
+    e(mk(V_LSHLREV_B32, Th(2), ic(tagbit_[r] & 31), flag_v));
+    e(mk(V_OR_B32, TAGV(r), TAGV(r), Th(2)));
+  }
+  void set_tag_mask(int r, uint16_t mask) {     // lanes of mask: float
+    if (tagbit_[r] < 0) return;
+    e(mk(V_CNDMASK_B32, Th(1), ic(0), ic(1), mask));
+    set_tag_flag(r, Th(1));
+  }
+  void copy_tag(int d, int a, uint8_t ta) {
+    if (tagbit_[d] < 0) return;
+    if (ta == TY_I) set_tag_static(d, false);
+    else if (ta == TY_F) set_tag_static(d, true);
+    else {
+      const uint16_t f = flag_of(a, ta, Th(1));
+      set_tag_flag(d, f);
+    }
+  }
+  // f64 value of register r (type t) -> operand code of a pair
+  uint16_t as_f64(int r, uint8_t t, int tmp) {
+    if (t == TY_F) return R(r);
+    e(mk(M_CVT_F64_I64, T(tmp), R(r)));
+    if (t == TY_I) return T(tmp);
+    tag_mask(r, ST(1));
+    e(mk(V_CNDMASK_B32, T(tmp), T(tmp), R(r), ST(1)));
+    e(mk(V_CNDMASK_B32, Th(tmp), Th(tmp), Rh(r), ST(1)));
+    return T(tmp);
+  }
+  // lanes (of `lanes_mask`) whose int64 operand (pair p) is outside [-2^53, 2^53] -> EXC_UNSUPPORTED
+  void check_exact_int(uint16_t p, uint16_t lanes_mask) {
+    e(mk(S_MOV_B32, s(S_LIT_), ic(0)));
+    e(mklit(S_MOV_B32, s(S_LIT_ + 1), 0x00200000u));
+    e(mk(V_LSHL_ADD_U64, T(0), p, ic(0), s(S_LIT_)));   // x + 2^53
+    e(mklit(S_MOV_B32, s(S_LIT_ + 1), 0x00400000u));
+    cmp(V_CMP_GT_U64, ST(1), T(0), s(S_LIT_));
+    if (lanes_mask != EXEC) e(mk(S_AND_B64, ST(1), ST(1), lanes_mask));
+    soft_raise(ST(1), EXC_UNSUPPORTED);
+  }
+  // SGPR pairs live across a runtime call
+  std::vector<int> live_sgprs() const {
+    std::vector<int> out = {30, 31, s_entry_, s_entry_ + 1, s_dead_, s_dead_ + 1};
+    for (int f = 0; f < 6; ++f)
+      if (pod_s_[f] >= 0) { out.push_back(pod_s_[f]); out.push_back(pod_s_[f] + 1); }
+    for (const Frame& fr : frames_)
+      for (int b : {fr.s_save, fr.s_else, fr.s_entry, fr.s_brk, fr.s_cont})
+        if (b >= 0) { out.push_back(b); out.push_back(b + 1); }
+    return out;
+  }
+  std::vector<int> live_vgprs(int pc, int d) const {
+    std::vector<int> out;
+    if (use_node_ || use_gl_ || use_gmem_)
+      for (int g = 0; g <= 4; ++g) out.push_back(g);
+    if (use_gl_)
+      for (int g = 5; g <= 20; ++g) out.push_back(g);
+    if (use_gmem_) { out.push_back(21); out.push_back(22); }
+    out.push_back(29);
+    out.push_back(v_exc_);
+    out.push_back(v_out_);
+    out.push_back(v_out_ + 1);
+    if (v_bud_ >= 0) out.push_back(v_bud_);
+    for (int t : v_tag_)
+      if (t >= 0) out.push_back(t);
+    // the destination is included: lanes outside EXEC keep its old value
+    const uint64_t live = slive_out_[pc] | live_out_[pc] | (d >= 0 ? (1ull << d) : 0ull);
+    std::set<int> bases;
+    for (int r = 0; r < kMaxRegs; ++r)
+      if ((live >> r & 1) && base_[r] >= 0) bases.insert(base_[r]);
+    for (int b : bases) { out.push_back(b); out.push_back(b + 1); }
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+    return out;
+  }
+  // d = rt_binop / rt_unop(op, a[, b]) with Python semantics for any operand types
+  void rtcall(int kind, int op, int pc, int d, int a, uint8_t ta, int b = -1, uint8_t tb = TY_I) {
+    e(mk(V_MOV_B64, X(0), R(a)));
+    CallInfo c;
+    c.kind = kind;
+    c.op = op;
+    c.a = X(0);
+    c.afl = flag_of(a, ta, X(3));
+    if (kind == 0) {
+      e(mk(V_MOV_B64, X(1), R(b)));
+      c.b = X(1);
+      c.bfl = flag_of(b, tb, (uint16_t)(X(3) + 1));
+    }
+    c.res = X(2);
+    c.resy = X(3);
+    c.spill_vgpr = v(v_spill_);
+    c.vgprs = live_vgprs(pc, d);
+    c.sgprs = live_sgprs();
+    if (c.sgprs.size() > 64) throw CodegenError("too many SGPRs live across a call");
+    MI m;
+    m.op = M_RTCALL;
+    m.ext = (int)F_.calls.size();
+    F_.calls.push_back(c);
+    e(m);
+    // exception code: fl | e << 8
+    e(mk(V_LSHRREV_B32, Th(0), ic(8), X(3)));
+    cmp(V_CMP_NE_U32, ST(0), ic(0), Th(0));
+    soft_raise_v(ST(0), Th(0));
+    e(mk(V_MOV_B64, R(d), X(2)));
+    if (tagbit_[d] >= 0) {
+      e(mk(V_AND_B32, T(0), ic(1), X(3)));
+      set_tag_flag(d, T(0));
+    }
+  }
+
+  Frame* innermost_loop() {
+    for (auto it = frames_.rbegin(); it != frames_.rend(); ++it)
+      if (it->loop) return &*it;
+    return nullptr;
+  }
+  // EXEC = base & ~(lanes that left the construct)
+  void restore_exec(uint16_t base) {
+    e(mk(S_ANDN2_B64, EXEC, base, s(s_dead_)));
+    if (Frame* l = innermost_loop()) {
+      e(mk(S_ANDN2_B64, EXEC, EXEC, s(l->s_brk)));
+      e(mk(S_ANDN2_B64, EXEC, EXEC, s(l->s_cont)));
+    }
+  }
+  // lanes of EXEC leave the function here
+  void leave_function() {
+    e(mk(S_OR_B64, s(s_dead_), s(s_dead_), EXEC));
+    e(mk(S_MOV_B64, EXEC, ic(0)));
+  }
+  // truth(r) -> SGPR pair
+  void truth(int r, uint8_t t, uint16_t dst) {
+    if (t == TY_I) { cmp(V_CMP_NE_I64, dst, ic(0), R(r)); return; }
+    if (t == TY_F) { cmp(V_CMP_NEQ_F64, dst, ic(0), R(r)); return; }
+    tag_mask(r, ST(1));
+    cmp(V_CMP_NE_I64, dst, ic(0), R(r));
+    cmp(V_CMP_NEQ_F64, ST(2), ic(0), R(r));
+    e(mk(S_AND_B64, ST(2), ST(2), ST(1)));
+    e(mk(S_ANDN2_B64, dst, dst, ST(1)));
+    e(mk(S_OR_B64, dst, dst, ST(2)));
+  }
+  void set_bool(int d, uint16_t mask) {   // d = int(mask)
+    e(mk(V_CNDMASK_B32, R(d), ic(0), ic(1), mask));
+    e(mk(V_MOV_B32, Rh(d), ic(0)));
+    set_tag_static(d, false);
+  }
+
+  // ============================================================ per-op lowering
+  void emit_all() {
+    // prologue
+    e(mkimm(S_WAITCNT, 0));
+    e(mk(S_MOV_B64, s(s_entry_), EXEC));
+    e(mk(S_MOV_B64, s(s_dead_), ic(0)));
+    static const int pod_arg[6] = {23, 24, 25, 25, 26, 28};
+    for (int f = 0; f < 6; ++f) {
+      const int sp = pod_s_[f];
+      if (sp < 0) continue;
+      e(mk(V_READFIRSTLANE_B32, s(sp), v(pod_arg[f])));
+      switch (f) {
+        case 0: case 1: case 5: e(mk(S_ASHR_I32, s(sp + 1), s(sp), ic(31))); break;
+        case 2: e(mk(S_LSHR_B32, s(sp), s(sp), ic(16))); e(mk(S_MOV_B32, s(sp + 1), ic(0))); break;
+        case 3: e(mklit(S_AND_B32, s(sp), 0xFFFFu, s(sp))); e(mk(S_MOV_B32, s(sp + 1), ic(0))); break;
+        case 4: e(mk(V_READFIRSTLANE_B32, s(sp + 1), v(27))); break;
+      }
+    }
+    e(mk(V_MOV_B32, v(v_exc_), ic(0)));
+    e(mk(V_MOV_B64, v(v_out_), ic(0)));
+    for (int t : v_tag_)
+      if (t >= 0) e(mk(V_MOV_B32, v(t), ic(0)));
+    if (v_bud_ >= 0) {
+      MI ld = mk(DS_READ_B64, T(0), v(29));
+      ld.imm = 0;
+      e(ld);
+      e(mkimm(S_WAITCNT, 0xC07F));
+      e(mk(V_MOV_B32, v(v_bud_), T(0)));
+    }
+    for (int r = 0; r < kMaxRegs; ++r)
+      if ((live_in_[0] >> r & 1) && base_[r] >= 0) e(mk(V_MOV_B64, R(r), ic(0)));
+    const int l_end = label();
+    for (int pc = 0; pc < n_; ++pc) {
+      auto it = label_at_pc_.find(pc);
+      if (it != label_at_pc_.end() && P_.code[pc].op != OP_ENDIF && P_.code[pc].op != OP_ELSE &&
+          P_.code[pc].op != OP_LOOP_EXIT)
+        place(it->second);
+      // unreached code is skipped, but structural ops still open / close
+      // their EXEC frames (an ENDIF after a then-branch that always returns
+      // is unreached by flow, yet the IF branches to it)
+      if (!reached_[pc] && !structural(P_.code[pc].op)) continue;
+      emit_op(pc);
+    }
+    if (!frames_.empty()) throw CodegenError("unbalanced control flow");
+    // epilogue: v[0:1] = exc ? -exc : out
+    place(l_end);
+    e(mk(S_MOV_B64, EXEC, s(s_entry_)));
+    cmp(V_CMP_NE_U32, ST(0), ic(0), v(v_exc_));
+    e(mk(V_SUB_U32, T(0), ic(0), v(v_exc_)));
+    e(mk(V_CNDMASK_B32, v(0), v(v_out_), T(0), ST(0)));
+    e(mk(V_CNDMASK_B32, v(1), v(v_out_ + 1), ic(-1), ST(0)));
+    e(mk(S_SETPC_B64, NONE, s(30)));
+  }
+
+  void emit_op(int pc) {
+    const Insn& in = P_.code[pc];
+    const auto& st = ty_[pc];
+    const uint8_t ta = in.a != kNoReg ? st[in.a] : TY_I;
+    const uint8_t tb = in.b != kNoReg ? st[in.b] : TY_I;
+    const int d = in.d, a = in.a, b = in.b;
+    switch (in.op) {
+      case OP_NOP: break;
+      case OP_CONST: {
+        const int k = in.imm;
+        const bool fl = P_.ctag[k] == TAG_FLOAT;
+        if (P_.is_lit[k]) {
+          MI ld = mk(DS_READ_B64, R(d), v(29));
+          ld.imm = 8 * (1 + k);
+          e(ld);
+          e(mkimm(S_WAITCNT, 0xC07F));
+        } else {
+          uint64_t bits;
+          if (fl) std::memcpy(&bits, &P_.fconst[k], 8);
+          else bits = (uint64_t)P_.iconst[k];
+          vmov32(R(d), (uint32_t)bits);
+          vmov32(Rh(d), (uint32_t)(bits >> 32));
+        }
+        set_tag_static(d, fl);
+        break;
+      }
+      case OP_MOV: case OP_POS:
+        if (base_[d] != base_[a]) e(mk(V_MOV_B64, R(d), R(a)));
+        copy_tag(d, a, ta);
+        break;
+      case OP_POD: {
+        const int f = (in.imm >= 0 && in.imm <= 5) ? in.imm : 5;
+        e(mk(V_MOV_B64, R(d), s(pod_s_[f])));
+        set_tag_static(d, false);
+        break;
+      }
+      case OP_NODE: {
+        const int f = (in.imm >= 0 && in.imm <= 5) ? in.imm : 5;
+        if (f <= 3) {
+          e(mk(V_MOV_B32, R(d), v(f)));
+          e(mk(V_ASHRREV_I32, Rh(d), ic(31), v(f)));
+        } else if (f == 4) {
+          e(mk(V_BFE_I32, R(d), v(4), ic(0), ic(16)));
+          e(mk(V_ASHRREV_I32, Rh(d), ic(31), R(d)));
+        } else {
+          e(mk(V_LSHRREV_B32, R(d), ic(16), v(4)));
+          e(mk(V_MOV_B32, Rh(d), ic(0)));
+        }
+        set_tag_static(d, false);
+        break;
+      }
+      case OP_GPU: emit_gpu(in, ta); break;
+      case OP_GLIST_ALL:
+        e(mk(V_LSHRREV_B32, T(1), ic(16), v(4)));                 // n
+        e(mk(V_LSHLREV_B32, Th(1), ic(2), T(1)));                 // 4n
+        e(mk(V_LSHLREV_B64, T(0), Th(1), ic(1)));                 // 1 << 4n (64-bit)
+        e(mk(V_LSHL_ADD_U64, T(0), T(0), ic(0), ic(-1)));         // - 1
+        e(mklit(V_AND_B32, T(0), 0x76543210u, T(0)));
+        e(mk(V_LSHLREV_B32, R(d), ic(4), T(0)));
+        e(mk(V_OR_B32, R(d), R(d), T(1)));
+        e(mk(V_LSHRREV_B32, Rh(d), ic(28), T(0)));
+        set_tag_static(d, false);
+        break;
+      case OP_GLIST_LEN:
+        e(mk(V_AND_B32, R(d), ic(15), R(a)));
+        e(mk(V_MOV_B32, Rh(d), ic(0)));
+        set_tag_static(d, false);
+        break;
+      case OP_GLIST_GET: emit_glist_get(in, tb); break;
+      case OP_GLIST_SLICE: emit_glist_slice(in, st); break;
+      case OP_GLIST_NEW:
+        e(mk(V_MOV_B64, R(d), ic(0)));
+        set_tag_static(d, false);
+        break;
+      case OP_GLIST_APPEND: emit_glist_append(in); break;
+      case OP_GLIST_INSERT: emit_glist_insert(in, st); break;
+      case OP_ADD: case OP_SUB: case OP_MUL:
+        if (ta == TY_IF || tb == TY_IF) { rtcall(0, in.op, pc, d, a, ta, b, tb); break; }
+        if (ta == TY_I && tb == TY_I) { emit_int_arith(in); break; }
+        {
+          const uint16_t fa = as_f64(a, ta, 0), fb = as_f64(b, tb, 1);
+          MI m = mk(in.op == OP_MUL ? V_MUL_F64 : V_ADD_F64, R(d), fa, fb);
+          if (in.op == OP_SUB) m.neg = 2;
+          e(m);
+          set_tag_static(d, true);
+        }
+        break;
+      case OP_TDIV:
+        if (ta == TY_IF || tb == TY_IF) { rtcall(0, in.op, pc, d, a, ta, b, tb); break; }
+        if (ta == TY_I && tb == TY_I) {
+          cmp(V_CMP_EQ_I64, ST(0), ic(0), R(b));
+          soft_raise(ST(0), EXC_ZERO_DIVISION);
+          check_exact_int(R(a), EXEC);
+          check_exact_int(R(b), EXEC);
+        }
+        {
+          const uint16_t fa = as_f64(a, ta, 0), fb = as_f64(b, tb, 1);
+          if (!(ta == TY_I && tb == TY_I)) {
+            cmp(V_CMP_EQ_F64, ST(0), ic(0), fb);
+            soft_raise(ST(0), EXC_ZERO_DIVISION);
+          }
+          e(mk(M_FDIV64, R(d), fa, fb));
+          set_tag_static(d, true);
+        }
+        break;
+      case OP_FDIV: case OP_MOD: case OP_POW: case OP_LOGB: case OP_MPOW:
+        rtcall(0, in.op, pc, d, a, ta, b, tb);
+        break;
+      case OP_SQRT: case OP_LOG: case OP_EXP: case OP_SIN: case OP_COS: case OP_TAN:
+        rtcall(1, in.op, pc, d, a, ta);
+        break;
+      case OP_NEG: case OP_ABS:
+        if (ta == TY_IF) { rtcall(1, in.op, pc, d, a, ta); break; }
+        if (ta == TY_F) {
+          if (base_[d] != base_[a]) e(mk(V_MOV_B32, R(d), R(a)));
+          if (in.op == OP_NEG) e(mklit(V_XOR_B32, Rh(d), 0x80000000u, Rh(a)));
+          else e(mklit(V_AND_B32, Rh(d), 0x7FFFFFFFu, Rh(a)));
+          set_tag_static(d, true);
+        } else {
+          movk64(s(S_LIT_), 0x8000000000000000ull);
+          cmp(V_CMP_EQ_I64, ST(0), R(a), s(S_LIT_));
+          soft_raise(ST(0), EXC_UNSUPPORTED);
+          MI lo = mk(V_SUB_CO_U32, T(0), ic(0), R(a)); lo.sd = ST(0); e(lo);
+          MI hi = mk(V_SUBB_CO_U32, Th(0), ic(0), Rh(a), ST(0)); hi.sd = ST(0); e(hi);
+          if (in.op == OP_NEG) {
+            e(mk(V_MOV_B64, R(d), T(0)));
+          } else {
+            cmp(V_CMP_LT_I32, ST(1), Rh(a), ic(0));
+            e(mk(V_CNDMASK_B32, R(d), R(a), T(0), ST(1)));
+            e(mk(V_CNDMASK_B32, Rh(d), Rh(a), Th(0), ST(1)));
+          }
+          set_tag_static(d, false);
+        }
+        break;
+      case OP_INT: case OP_ROUND:
+        if (ta == TY_IF) { rtcall(1, in.op, pc, d, a, ta); break; }
+        if (ta == TY_I) {
+          if (base_[d] != base_[a]) e(mk(V_MOV_B64, R(d), R(a)));
+          set_tag_static(d, false);
+          break;
+        }
+        {
+          uint16_t x = R(a);
+          if (in.op == OP_ROUND) { e(mk(V_RNDNE_F64, T(1), R(a))); x = T(1); }
+          cmp(V_CMP_CLASS_F64, ST(0), x, ic(3));
+          soft_raise(ST(0), EXC_VALUE);
+          e(mklit(S_MOV_B32, s(S_LIT_), 0x204u));
+          cmp(V_CMP_CLASS_F64, ST(0), x, s(S_LIT_));
+          soft_raise(ST(0), EXC_OVERFLOW);
+          e(mk(V_TRUNC_F64, T(0), x));
+          movk64(s(S_LIT_), 0x43E0000000000000ull);
+          cmp(V_CMP_GE_F64, ST(0), T(0), s(S_LIT_), 1);
+          soft_raise(ST(0), EXC_UNSUPPORTED);
+          e(mk(M_CVT_I64_F64, R(d), T(0)));
+          set_tag_static(d, false);
+        }
+        break;
+      case OP_FLOAT: {
+        const uint16_t f = as_f64(a, ta, 0);
+        if (f != R(d)) e(mk(V_MOV_B64, R(d), f));
+        set_tag_static(d, true);
+        break;
+      }
+      case OP_NOT: case OP_TRUTH:
+        truth(a, ta, ST(0));
+        if (in.op == OP_NOT) e(mk(S_ANDN2_B64, ST(0), EXEC, ST(0)));
+        set_bool(d, ST(0));
+        break;
+      case OP_ISINT:
+        if (ta == TY_IF) {
+          tag_mask(a, ST(0));
+          e(mk(S_ANDN2_B64, ST(0), EXEC, ST(0)));
+          set_bool(d, ST(0));
+        } else {
+          e(mk(V_MOV_B64, R(d), ic(ta == TY_I ? 1 : 0)));
+          set_tag_static(d, false);
+        }
+        break;
+      case OP_LT: case OP_LE: case OP_GT: case OP_GE: case OP_EQ: case OP_NE:
+        emit_compare(in.op, a, ta, b, tb, ST(0));
+        set_bool(d, ST(0));
+        break;
+      case OP_MIN2: case OP_MAX2: emit_minmax(in, ta, tb); break;
+      // ---- control flow
+      case OP_IF: {
+        Frame fr{};
+        fr.loop = false;
+        fr.pc = pc;
+        truth(a, ta, ST(0));
+        fr.s_save = take_spair();
+        const int t = in.imm;
+        if (t <= pc || t >= n_) throw CodegenError("bad IF target");
+        if (P_.code[t].op == OP_ELSE) {
+          fr.s_else = take_spair();
+          e(mk(S_ANDN2_B64, s(fr.s_else), EXEC, ST(0)));
+        } else if (P_.code[t].op != OP_ENDIF) {
+          throw CodegenError("IF target is neither ELSE nor ENDIF");
+        }
+        e(mk(S_AND_SAVEEXEC_B64, s(fr.s_save), ST(0)));
+        e(mkimm(S_CBRANCH_EXECZ, label_for_pc(t)));
+        frames_.push_back(fr);
+        break;
+      }
+      case OP_ELSE: {
+        if (frames_.empty() || frames_.back().loop || frames_.back().s_else < 0) throw CodegenError("stray ELSE");
+        place(label_for_pc(pc));
+        e(mk(S_MOV_B64, EXEC, s(frames_.back().s_else)));
+        e(mkimm(S_CBRANCH_EXECZ, label_for_pc(in.imm)));
+        break;
+      }
+      case OP_ENDIF: {
+        if (frames_.empty() || frames_.back().loop) throw CodegenError("stray ENDIF");
+        place(label_for_pc(pc));
+        Frame fr = frames_.back();
+        frames_.pop_back();
+        restore_exec(s(fr.s_save));
+        give_spair(fr.s_save);
+        if (fr.s_else >= 0) give_spair(fr.s_else);
+        break;
+      }
+      case OP_LOOP_BEGIN: {
+        Frame fr{};
+        fr.loop = true;
+        fr.pc = pc;
+        fr.s_entry = take_spair();
+        fr.s_brk = take_spair();
+        fr.s_cont = take_spair();
+        e(mk(S_MOV_B64, s(fr.s_entry), EXEC));
+        e(mk(S_MOV_B64, s(fr.s_brk), ic(0)));
+        e(mk(S_MOV_B64, s(fr.s_cont), ic(0)));
+        fr.l_head = label();
+        place(fr.l_head);
+        frames_.push_back(fr);
+        break;
+      }
+      case OP_LOOP_TEST: {
+        Frame* l = innermost_loop();
+        if (!l || frames_.back().pc != l->pc) throw CodegenError("LOOP_TEST not at loop level");
+        truth(a, ta, ST(0));
+        e(mk(S_AND_B64, EXEC, EXEC, ST(0)));
+        e(mkimm(S_CBRANCH_EXECZ, label_for_pc(in.imm)));
+        break;
+      }
+      case OP_LOOP_CONT: {
+        Frame* l = innermost_loop();
+        if (!l || frames_.back().pc != l->pc) throw CodegenError("LOOP_CONT not at loop level");
+        e(mk(S_OR_B64, EXEC, EXEC, s(l->s_cont)));
+        e(mk(S_MOV_B64, s(l->s_cont), ic(0)));
+        break;
+      }
+      case OP_LOOP_NEXT: {
+        Frame* l = innermost_loop();
+        if (!l || frames_.back().pc != l->pc) throw CodegenError("LOOP_NEXT not at loop level");
+        if (in.imm != l->pc + 1) throw CodegenError("loop back edge not to the loop head");
+        cmp(V_CMP_NE_U32, ST(0), ic(0), v(v_exc_));
+        e(mk(S_OR_B64, s(s_dead_), s(s_dead_), ST(0)));
+        e(mk(S_ANDN2_B64, EXEC, EXEC, ST(0)));
+        e(mk(V_SUB_U32, v(v_bud_), v(v_bud_), ic(1)));
+        cmp(V_CMP_LT_I32, ST(0), v(v_bud_), ic(0));
+        soft_raise(ST(0), EXC_BUDGET);
+        e(mk(S_OR_B64, s(s_dead_), s(s_dead_), ST(0)));
+        e(mk(S_ANDN2_B64, EXEC, EXEC, ST(0)));
+        e(mkimm(S_CBRANCH_EXECNZ, l->l_head));
+        if (pc + 1 >= n_ || P_.code[pc + 1].op != OP_LOOP_EXIT) e(mkimm(S_BRANCH, label_for_pc(l_exit_of(pc))));
+        break;
+      }
+      case OP_LOOP_EXIT: {
+        if (frames_.empty() || !frames_.back().loop) throw CodegenError("stray LOOP_EXIT");
+        place(label_for_pc(pc));
+        Frame fr = frames_.back();
+        frames_.pop_back();
+        e(mk(S_ANDN2_B64, EXEC, s(fr.s_entry), s(s_dead_)));
+        give_spair(fr.s_entry);
+        give_spair(fr.s_brk);
+        give_spair(fr.s_cont);
+        break;
+      }
+      case OP_BREAK: {
+        Frame* l = innermost_loop();
+        if (!l) throw CodegenError("BREAK outside a loop");
+        e(mk(S_OR_B64, s(l->s_brk), s(l->s_brk), EXEC));
+        e(mk(S_MOV_B64, EXEC, ic(0)));
+        break;
+      }
+      case OP_CONTINUE: {
+        Frame* l = innermost_loop();
+        if (!l) throw CodegenError("CONTINUE outside a loop");
+        e(mk(S_OR_B64, s(l->s_cont), s(l->s_cont), EXEC));
+        e(mk(S_MOV_B64, EXEC, ic(0)));
+        break;
+      }
+      case OP_RET:
+        emit_finish(a, ta);
+        leave_function();
+        break;
+      case OP_RAISE:
+        soft_raise(EXEC, in.imm);
+        leave_function();
+        break;
+      case OP_END:
+        soft_raise(EXEC, EXC_TYPE);
+        leave_function();
+        break;
+      default:
+        throw CodegenError("opcode " + std::to_string((int)in.op) + " has no baseline lowering");
+    }
+  }
+  static bool structural(uint8_t op) {
+    return op == OP_IF || op == OP_ELSE || op == OP_ENDIF || op == OP_LOOP_BEGIN || op == OP_LOOP_TEST ||
+           op == OP_LOOP_CONT || op == OP_LOOP_NEXT || op == OP_LOOP_EXIT;
+  }
+
+  int l_exit_of(int pc_next) const {
+    // the LOOP_EXIT that closes the loop whose LOOP_NEXT is at pc_next
+    int depth = 0;
+    for (int q = pc_next + 1; q < n_; ++q) {
+      if (P_.code[q].op == OP_LOOP_BEGIN) ++depth;
+      if (P_.code[q].op == OP_LOOP_EXIT) {
+        if (depth == 0) return q;
+        --depth;
+      }
+    }
+    throw CodegenError("loop without LOOP_EXIT");
+  }
+
+  // ---- int64 add / sub / mul with overflow -> EXC_UNSUPPORTED
+  void emit_int_arith(const Insn& in) {
+    const int d = in.d, a = in.a, b = in.b;
+    if (in.op == OP_MUL) {
+      // operands in int32 range multiply exactly with v_mad_i64_i32; anything
+      // wider is left to the next engine (EXC_UNSUPPORTED)
+      e(mk(V_ASHRREV_I32, T(1), ic(31), R(a)));
+      cmp(V_CMP_EQ_U32, ST(0), T(1), Rh(a));
+      e(mk(V_ASHRREV_I32, Th(1), ic(31), R(b)));
+      cmp(V_CMP_EQ_U32, ST(1), Th(1), Rh(b));
+      e(mk(S_AND_B64, ST(0), ST(0), ST(1)));
+      e(mk(S_ANDN2_B64, ST(1), EXEC, ST(0)));
+      soft_raise(ST(1), EXC_UNSUPPORTED);
+      e(mk3b(V_MAD_I64_I32, R(d), VCC, R(a), R(b), ic(0)));
+      set_tag_static(d, false);
+      return;
+    }
+    MI lo = mk(in.op == OP_ADD ? V_ADD_CO_U32 : V_SUB_CO_U32, T(0), R(a), R(b));
+    lo.sd = ST(0);
+    e(lo);
+    MI hi = mk(in.op == OP_ADD ? V_ADDC_CO_U32 : V_SUBB_CO_U32, Th(0), Rh(a), Rh(b), ST(0));
+    hi.sd = ST(0);
+    e(hi);
+    if (in.op == OP_ADD) {
+      e(mk(V_XOR_B32, T(1), Rh(a), Th(0)));
+      e(mk(V_XOR_B32, Th(1), Rh(b), Th(0)));
+    } else {
+      e(mk(V_XOR_B32, T(1), Rh(a), Rh(b)));
+      e(mk(V_XOR_B32, Th(1), Rh(a), Th(0)));
+    }
+    e(mk(V_AND_B32, T(1), T(1), Th(1)));
+    cmp(V_CMP_LT_I32, ST(1), T(1), ic(0));
+    soft_raise(ST(1), EXC_UNSUPPORTED);
+    e(mk(V_MOV_B64, R(d), T(0)));
+    set_tag_static(d, false);
+  }
+
+  // ---- node.gpus[j].field
+  void emit_gpu(const Insn& in, uint8_t ta) {
+    (void)ta;
+    const int d = in.d, a = in.a;
+    e(mk(V_AND_B32, T(1), ic(15), R(a)));   // j
+    if (in.imm == 0 || in.imm == 1) {
+      const int base = in.imm == 0 ? 5 : 13;
+      // select by the bits of j: 3 levels of v_cndmask
+      e(mk(V_AND_B32, Th(1), ic(1), T(1)));
+      cmp(V_CMP_NE_U32, ST(0), ic(0), Th(1));
+      e(mk(V_AND_B32, Th(1), ic(2), T(1)));
+      cmp(V_CMP_NE_U32, ST(1), ic(0), Th(1));
+      e(mk(V_AND_B32, Th(1), ic(4), T(1)));
+      cmp(V_CMP_NE_U32, ST(2), ic(0), Th(1));
+      e(mk(V_CNDMASK_B32, T(0), v(base + 0), v(base + 1), ST(0)));
+      e(mk(V_CNDMASK_B32, Th(0), v(base + 2), v(base + 3), ST(0)));
+      e(mk(V_CNDMASK_B32, T(2), v(base + 4), v(base + 5), ST(0)));
+      e(mk(V_CNDMASK_B32, Th(2), v(base + 6), v(base + 7), ST(0)));
+      e(mk(V_CNDMASK_B32, T(0), T(0), Th(0), ST(1)));
+      e(mk(V_CNDMASK_B32, T(2), T(2), Th(2), ST(1)));
+      e(mk(V_CNDMASK_B32, R(d), T(0), T(2), ST(2)));
+      e(mk(V_ASHRREV_I32, Rh(d), ic(31), R(d)));
+    } else {
+      // gmem[j]: 64-bit load from the node's row (v[21:22], 8 entries)
+      e(mk(V_LSHLREV_B32, Th(1), ic(3), T(1)));
+      MI lo = mk(V_ADD_CO_U32, T(0), v(21), Th(1)); lo.sd = ST(0); e(lo);
+      MI hi = mk(V_ADDC_CO_U32, Th(0), v(22), ic(0), ST(0)); hi.sd = ST(0); e(hi);
+      e(mk(GLOBAL_LOAD_DWORDX2, R(d), T(0)));
+      e(mkimm(S_WAITCNT, 0x0F70));
+    }
+    set_tag_static(d, false);
+  }
+
+  // ---- GPU lists (int64: bits 0-3 length, 4 bits per entry)
+  void emit_glist_get(const Insn& in, uint8_t tb) {
+    const int d = in.d, a = in.a, b = in.b;
+    // float index -> TypeError
+    if (tb == TY_F) soft_raise(EXEC, EXC_TYPE);
+    else if (tb == TY_IF) { tag_mask(b, ST(0)); soft_raise(ST(0), EXC_TYPE); }
+    e(mk(V_AND_B32, T(1), ic(15), R(a)));                    // n
+    e(mk(V_MOV_B32, Th(1), ic(0)));
+    // k = i < 0 ? i + n : i
+    e(mk(V_LSHL_ADD_U64, T(0), R(b), ic(0), T(1)));
+    cmp(V_CMP_LT_I64, ST(0), R(b), ic(0));
+    e(mk(V_CNDMASK_B32, T(0), R(b), T(0), ST(0)));
+    e(mk(V_CNDMASK_B32, Th(0), Rh(b), Th(0), ST(0)));
+    // k < 0 || k >= n -> IndexError
+    cmp(V_CMP_LT_I64, ST(0), T(0), ic(0));
+    cmp(V_CMP_GE_I64, ST(1), T(0), T(1));
+    e(mk(S_OR_B64, ST(0), ST(0), ST(1)));
+    soft_raise(ST(0), EXC_INDEX);   // a lane that raised TypeError above keeps it
+    // (lst >> (4 + 4k)) & 15
+    e(mk(V_LSHLREV_B32, Th(1), ic(2), T(0)));
+    e(mk(V_ADD_U32, Th(1), ic(4), Th(1)));
+    e(mk(V_LSHRREV_B64, T(2), Th(1), R(a)));
+    e(mk(V_AND_B32, R(d), ic(15), T(2)));
+    e(mk(V_MOV_B32, Rh(d), ic(0)));
+    set_tag_static(d, false);
+  }
+  // clamp a Python slice / insert position (int64 pair p) into [0, n] (n: VGPR) -> 32-bit VGPR out
+  void clamp_pos(uint16_t p, uint16_t nv, uint16_t out, uint16_t tmp_pair) {
+    // x < 0: x += n, then max(x, 0); x > n: n
+    e(mk(V_MOV_B32, (uint16_t)(tmp_pair + 1), ic(0)));
+    e(mk(V_MOV_B32, tmp_pair, nv));
+    e(mk(V_LSHL_ADD_U64, tmp_pair, p, ic(0), tmp_pair));       // x + n
+    cmp(V_CMP_LT_I64, ST(0), tmp_pair, ic(0));                  // x + n < 0
+    cmp(V_CMP_LT_I64, ST(1), p, ic(0));                         // x < 0
+    e(mk(V_CNDMASK_B32, out, tmp_pair, ic(0), ST(0)));           // max(x + n, 0)
+    e(mk(V_MOV_B32, tmp_pair, nv));
+    e(mk(V_MOV_B32, (uint16_t)(tmp_pair + 1), ic(0)));
+    cmp(V_CMP_GT_I64, ST(0), p, tmp_pair);                      // x > n
+    e(mk(V_CNDMASK_B32, (uint16_t)(tmp_pair + 1), p, nv, ST(0))); // min(x, n) (low word)
+    e(mk(V_CNDMASK_B32, out, (uint16_t)(tmp_pair + 1), out, ST(1)));
+  }
+  void emit_glist_slice(const Insn& in, const std::array<uint8_t, kMaxRegs>& st) {
+    const int d = in.d, a = in.a, b = in.b, h = in.imm;
+    // float bounds -> TypeError
+    for (int r : {b, h}) {
+      if (r == kNoReg) continue;
+      if (st[r] == TY_F) soft_raise(EXEC, EXC_TYPE);
+      else if (st[r] == TY_IF) { tag_mask(r, ST(0)); soft_raise(ST(0), EXC_TYPE); }
+    }
+    e(mk(V_AND_B32, X(3), ic(15), R(a)));                       // n
+    if (b != kNoReg) clamp_pos(R(b), X(3), (uint16_t)(X(3) + 1), T(2));
+    else e(mk(V_MOV_B32, (uint16_t)(X(3) + 1), ic(0)));           // lo
+    if (h != kNoReg) clamp_pos(R(h), X(3), T(1), T(2));
+    else e(mk(V_MOV_B32, T(1), X(3)));                           // hi
+    // m = max(hi - lo, 0)
+    e(mk(V_SUB_U32, Th(1), T(1), (uint16_t)(X(3) + 1)));
+    cmp(V_CMP_LT_I32, ST(0), Th(1), ic(0));
+    e(mk(V_CNDMASK_B32, Th(1), Th(1), ic(0), ST(0)));
+    // out = (((lst >> (4 + 4 lo)) & ((1 << 4m) - 1)) << 4) | m
+    e(mk(V_LSHLREV_B32, T(1), ic(2), (uint16_t)(X(3) + 1)));
+    e(mk(V_ADD_U32, T(1), ic(4), T(1)));
+    e(mk(V_LSHRREV_B64, T(0), T(1), R(a)));
+    e(mk(V_LSHLREV_B32, T(1), ic(2), Th(1)));
+    e(mk(V_LSHLREV_B64, T(2), T(1), ic(1)));
+    e(mk(V_LSHL_ADD_U64, T(2), T(2), ic(0), ic(-1)));
+    e(mk(V_AND_B32, T(0), T(0), T(2)));
+    e(mk(V_AND_B32, Th(0), Th(0), Th(2)));
+    e(mk(V_LSHLREV_B64, T(0), ic(4), T(0)));
+    e(mk(V_OR_B32, R(d), T(0), Th(1)));
+    e(mk(V_MOV_B32, Rh(d), Th(0)));
+    set_tag_static(d, false);
+  }
+  void emit_glist_append(const Insn& in) {
+    const int d = in.d, a = in.a, b = in.b;
+    e(mk(V_AND_B32, T(1), ic(15), R(a)));                       // n
+    cmp(V_CMP_GE_U32, ST(0), T(1), ic(15));
+    soft_raise(ST(0), EXC_UNSUPPORTED);
+    // item & 15 << (4 + 4n)
+    e(mk(V_AND_B32, T(2), ic(15), R(b)));
+    e(mk(V_MOV_B32, Th(2), ic(0)));
+    e(mk(V_LSHLREV_B32, Th(1), ic(2), T(1)));
+    e(mk(V_ADD_U32, Th(1), ic(4), Th(1)));
+    e(mk(V_LSHLREV_B64, T(2), Th(1), T(2)));
+    // (lst & ~15) | (n + 1)
+    e(mk(V_ADD_U32, T(1), ic(1), T(1)));
+    e(mk(V_AND_B32, T(0), ic(-16), R(a)));
+    e(mk(V_OR_B32, T(0), T(0), T(1)));
+    e(mk(V_OR_B32, R(d), T(0), T(2)));
+    e(mk(V_OR_B32, Rh(d), Rh(a), Th(2)));
+    set_tag_static(d, false);
+  }
+  void emit_glist_insert(const Insn& in, const std::array<uint8_t, kMaxRegs>& st) {
+    const int d = in.d, a = in.a, b = in.b, p = in.imm;
+    e(mk(V_AND_B32, X(3), ic(15), R(a)));                       // n
+    cmp(V_CMP_GE_U32, ST(0), X(3), ic(15));
+    soft_raise(ST(0), EXC_UNSUPPORTED);
+    if (st[p] == TY_F) soft_raise(EXEC, EXC_TYPE);
+    else if (st[p] == TY_IF) { tag_mask(p, ST(0)); soft_raise(ST(0), EXC_TYPE); }
+    clamp_pos(R(p), X(3), (uint16_t)(X(3) + 1), T(2));             // pos
+    // body = lst >> 4; low = (1 << 4pos) - 1
+    e(mk(V_LSHRREV_B64, T(0), ic(4), R(a)));
+    e(mk(V_LSHLREV_B32, T(1), ic(2), (uint16_t)(X(3) + 1)));     // 4 pos
+    e(mk(V_LSHLREV_B64, T(2), T(1), ic(1)));
+    e(mk(V_LSHL_ADD_U64, T(2), T(2), ic(0), ic(-1)));            // low mask
+    // nb = (body & low) | (item << 4pos) | ((body & ~low) << 4)
+    e(mk(V_NOT_B32, X(2), T(2)));
+    e(mk(V_NOT_B32, (uint16_t)(X(2) + 1), Th(2)));
+    e(mk(V_AND_B32, X(2), X(2), T(0)));
+    e(mk(V_AND_B32, (uint16_t)(X(2) + 1), (uint16_t)(X(2) + 1), Th(0)));
+    e(mk(V_LSHLREV_B64, X(2), ic(4), X(2)));                     // (body & ~low) << 4
+    e(mk(V_AND_B32, T(0), T(0), T(2)));
+    e(mk(V_AND_B32, Th(0), Th(0), Th(2)));                       // body & low
+    e(mk(V_OR_B32, T(0), T(0), X(2)));
+    e(mk(V_OR_B32, Th(0), Th(0), (uint16_t)(X(2) + 1)));
+    e(mk(V_AND_B32, T(2), ic(15), R(b)));
+    e(mk(V_MOV_B32, Th(2), ic(0)));
+    e(mk(V_LSHLREV_B64, T(2), T(1), T(2)));                      // item << 4pos
+    e(mk(V_OR_B32, T(0), T(0), T(2)));
+    e(mk(V_OR_B32, Th(0), Th(0), Th(2)));
+    // (nb << 4) | (n + 1)
+    e(mk(V_LSHLREV_B64, T(0), ic(4), T(0)));
+    e(mk(V_ADD_U32, X(3), ic(1), X(3)));
+    e(mk(V_OR_B32, R(d), T(0), X(3)));
+    e(mk(V_MOV_B32, Rh(d), Th(0)));
+    set_tag_static(d, false);
+  }
+
+  // ---- comparisons: result mask (lanes where true) in dst
+  void emit_compare(uint8_t op, int a, uint8_t ta, int b, uint8_t tb, uint16_t dst) {
+    static const Opc ci[6] = {V_CMP_LT_I64, V_CMP_LE_I64, V_CMP_GT_I64, V_CMP_GE_I64, V_CMP_EQ_I64, V_CMP_NE_I64};
+    static const Opc cf[6] = {V_CMP_LT_F64, V_CMP_LE_F64, V_CMP_GT_F64, V_CMP_GE_F64, V_CMP_EQ_F64, V_CMP_NEQ_F64};
+    const int k = op - OP_LT;
+    if (ta == TY_I && tb == TY_I) { cmp(ci[k], dst, R(a), R(b)); return; }
+    if (ta == TY_F && tb == TY_F) { cmp(cf[k], dst, R(a), R(b)); return; }
+    // mixed: int operands within +-2^53 convert exactly; others -> EXC_UNSUPPORTED
+    if (ta != TY_F) int_lanes_exact(a, ta);
+    if (tb != TY_F) int_lanes_exact(b, tb);
+    const uint16_t fa = as_f64(a, ta, 0), fb = as_f64(b, tb, 1);
+    if (ta == TY_IF || tb == TY_IF) {
+      // lanes where both are ints compare as int64 (exact for any value)
+      both_int_mask(a, ta, b, tb, ST(1));
+      cmp(cf[k], dst, fa, fb);
+      cmp(ci[k], ST(2), R(a), R(b));
+      e(mk(S_AND_B64, ST(2), ST(2), ST(1)));
+      e(mk(S_ANDN2_B64, dst, dst, ST(1)));
+      e(mk(S_OR_B64, dst, dst, ST(2)));
+    } else {
+      cmp(cf[k], dst, fa, fb);
+    }
+  }
+  // lanes where register r (type t) holds an int outside +-2^53 -> EXC_UNSUPPORTED
+  // (conservative for the int / int lanes of a dynamic pair: the next engine decides them)
+  void int_lanes_exact(int r, uint8_t t) {
+    if (t == TY_I) { check_exact_int(R(r), EXEC); return; }
+    tag_mask(r, ST(0));
+    e(mk(S_ANDN2_B64, ST(0), EXEC, ST(0)));
+    check_exact_int(R(r), ST(0));
+  }
+  void both_int_mask(int a, uint8_t ta, int b, uint8_t tb, uint16_t dst) {
+    // dst = lanes where a and b are both ints
+    e(mk(S_MOV_B64, dst, EXEC));
+    if (ta == TY_F || tb == TY_F) { e(mk(S_MOV_B64, dst, ic(0))); return; }
+    if (ta == TY_IF) { tag_mask(a, ST(2)); e(mk(S_ANDN2_B64, dst, dst, ST(2))); }
+    if (tb == TY_IF) { tag_mask(b, ST(2)); e(mk(S_ANDN2_B64, dst, dst, ST(2))); }
+  }
+  void emit_minmax(const Insn& in, uint8_t ta, uint8_t tb) {
+    const int d = in.d, a = in.a, b = in.b;
+    // max(a, b): b replaces a only if b > a (min: b < a); NaNs never replace
+    const uint8_t op = in.op == OP_MAX2 ? OP_GT : OP_LT;
+    emit_compare(op, b, tb, a, ta, ST(0));
+    // tags first (the value select may overwrite a / b when d aliases them)
+    if (tagbit_[d] >= 0) {
+      if (ta == tb && ta != TY_IF) set_tag_static(d, ta == TY_F);
+      else {
+        const uint16_t fa = flag_of(a, ta, X(2)), fb = flag_of(b, tb, (uint16_t)(X(2) + 1));
+        e(mk(V_CNDMASK_B32, X(3), fa, fb, ST(0)));
+        set_tag_flag(d, X(3));
+      }
+    }
+    e(mk(V_CNDMASK_B32, R(d), R(a), R(b), ST(0)));
+    e(mk(V_CNDMASK_B32, Rh(d), Rh(a), Rh(b), ST(0)));
+  }
+
+  // ---- return: out = int(max(0, value)) (soft exceptions for inf / >= 2^63)
+  void emit_finish(int a, uint8_t ta) {
+    auto finish_int = [&](uint16_t lanes) {
+      cmp(V_CMP_GT_I64, ST(0), R(a), ic(0));
+      if (lanes != EXEC) e(mk(S_AND_B64, ST(0), ST(0), lanes));
+      e(mk(V_CNDMASK_B32, T(0), ic(0), R(a), ST(0)));
+      e(mk(V_CNDMASK_B32, Th(0), ic(0), Rh(a), ST(0)));
+    };
+    auto finish_float = [&](uint16_t lanes) {
+      cmp(V_CMP_GT_F64, ST(0), R(a), ic(0));                       // !(x > 0) -> 0
+      if (lanes != EXEC) e(mk(S_AND_B64, ST(0), ST(0), lanes));
+      e(mklit(S_MOV_B32, s(S_LIT_), 0x200u));                      // +inf
+      cmp(V_CMP_CLASS_F64, ST(1), R(a), s(S_LIT_));
+      e(mk(S_AND_B64, ST(1), ST(1), ST(0)));
+      soft_raise(ST(1), EXC_OVERFLOW);
+      movk64(s(S_LIT_), 0x43E0000000000000ull);
+      cmp(V_CMP_GE_F64, ST(1), R(a), s(S_LIT_));
+      e(mk(S_AND_B64, ST(1), ST(1), ST(0)));
+      soft_raise(ST(1), EXC_UNSUPPORTED);
+      e(mk(M_CVT_I64_F64, T(1), R(a)));
+      e(mk(V_CNDMASK_B32, T(0), T(0), T(1), ST(0)));
+      e(mk(V_CNDMASK_B32, Th(0), Th(0), Th(1), ST(0)));
+    };
+    e(mk(V_MOV_B64, T(0), ic(0)));
+    if (ta == TY_I) finish_int(EXEC);
+    else if (ta == TY_F) finish_float(EXEC);
+    else {
+      // keep the float lanes in an SGPR pair of their own (finish_* use ST 0-2)
+      tag_mask(a, ST(1));
+      const int keep = take_spair();
+      e(mk(S_MOV_B64, s(keep), ST(1)));
+      e(mk(S_ANDN2_B64, s(S_LIT_), EXEC, s(keep)));
+      finish_int(s(S_LIT_));
+      finish_float(s(keep));
+      give_spair(keep);
+    }
+    e(mk(V_MOV_B64, v(v_out_), T(0)));
+  }
+};
+
+}  // namespace gcn
+}  // namespace fks

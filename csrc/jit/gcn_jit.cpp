@@ -1,0 +1,256 @@
+// Baseline program JIT: API of the code generator (gcn_codegen.hpp) and the
+// emulator-backed replays used to validate it on the CPU.  Compiled into the
+// _fks_cpu extension (ops/build.py) as its own translation unit, because the
+// runtime-library host build it emulates (pyops_dev.h under FKS_HOST_JIT)
+// defines HIP-style attribute macros.
+#include <chrono>
+#include <cstring>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../cpu/engine.hpp"
+#include "../cpu/parallel.hpp"
+#include "gcn_api.hpp"
+
+#define FKS_HOST_JIT 1
+#include "gcn_codegen.hpp"
+#include "gcn_emu.hpp"
+
+namespace fks {
+namespace gcnapi {
+
+namespace {
+
+gcn::ProgIn make_in(const ProgramDesc& p) {
+  if (p.code_bytes % 8 != 0) throw gcn::CodegenError("bytecode length is not a multiple of 8");
+  gcn::ProgIn in;
+  in.code = reinterpret_cast<const Insn*>(p.code);
+  in.n = (int)(p.code_bytes / 8);
+  in.ctag = p.ctag;
+  in.is_lit = p.is_lit;
+  in.iconst = p.iconst;
+  in.fconst = p.fconst;
+  in.n_const = (int)p.n_const;
+  return in;
+}
+
+const char* reg_name(uint16_t c, char* buf) {
+  using namespace gcn;
+  if (c == NONE) return "-";
+  if (c >= 256) { std::snprintf(buf, 16, "v%d", c - 256); return buf; }
+  if (c == VCC) return "vcc";
+  if (c == EXEC) return "exec";
+  if (c == LIT) return "lit";
+  if (c >= 128 && c <= 208) {
+    std::snprintf(buf, 16, "#%d", c <= 192 ? c - 128 : 192 - c);
+    return buf;
+  }
+  if (c >= 240 && c <= 247) {
+    static const char* f[] = {"0.5", "-0.5", "1.0", "-1.0", "2.0", "-2.0", "4.0", "-4.0"};
+    return f[c - 240];
+  }
+  std::snprintf(buf, 16, "s%d", c);
+  return buf;
+}
+
+}  // namespace
+
+Result compile(const ProgramDesc& p) {
+  Result r;
+  try {
+    gcn::ProgIn in = make_in(p);
+    gcn::Codegen cg(in);
+    gcn::GenStats st;
+    gcn::Func f = cg.run(&st);
+    gcn::Code code = gcn::assemble(f);
+    r.words = std::move(code.words);
+    for (const gcn::Reloc& rl : code.relocs) {
+      r.relocs.push_back(rl.lo_word);
+      r.relocs.push_back(rl.hi_word);
+      r.relocs.push_back(rl.pc_off);
+    }
+    r.n_insns = code.n_insns;
+    r.vgprs = st.vgprs_used;
+    r.sgprs = st.sgprs_used;
+    r.calls = st.calls;
+    r.vregs = st.vregs;
+    r.tagged = st.tagged;
+    r.mir = (int)f.mi.size();
+    r.ok = true;
+  } catch (const std::exception& e) {
+    r.ok = false;
+    r.reason = e.what();
+  }
+  return r;
+}
+
+std::string listing(const ProgramDesc& p) {
+  std::ostringstream os;
+  try {
+    gcn::ProgIn in = make_in(p);
+    gcn::Codegen cg(in);
+    gcn::Func f = cg.run();
+    char b0[16], b1[16], b2[16], b3[16], b4[16];
+    for (const gcn::MI& m : f.mi) {
+      if (m.op == gcn::LABEL) { os << "L" << m.imm << ":\n"; continue; }
+      os << "  " << gcn::info(m.op).name << " d=" << reg_name(m.d, b0) << " sd=" << reg_name(m.sd, b1)
+         << " s0=" << reg_name(m.s0, b2) << " s1=" << reg_name(m.s1, b3) << " s2=" << reg_name(m.s2, b4);
+      if (m.s0 == gcn::LIT || m.s1 == gcn::LIT || m.s2 == gcn::LIT) os << " lit=0x" << std::hex << m.lit << std::dec;
+      if (m.imm) os << " imm=" << m.imm;
+      if (m.neg) os << " neg=" << (int)m.neg;
+      if (m.abs) os << " abs=" << (int)m.abs;
+      os << "\n";
+    }
+  } catch (const std::exception& e) {
+    os << "error: " << e.what() << "\n";
+  }
+  return os.str();
+}
+
+namespace {
+
+constexpr uint64_t kRetMagic = 0xFEEDFACE00C0FFEEull;
+
+// Scorer: on the first node of every creation event, one emulated wave scores
+// all nodes (lanes = nodes), exactly as the replay kernel calls the program.
+struct EmuScorer {
+  const gcn::Func* f;
+  const std::vector<int64_t>* kc;
+  const std::vector<int64_t>* gmem8;
+  gcn::Emu* emu;
+  std::vector<int64_t> res;
+  int32_t exc = EXC_NONE;
+
+  ScoreOut operator()(const ScoreCtx& c, int n) {
+    if (n == 0) run_event(c);
+    ScoreOut o;
+    const int64_t r = res[(size_t)n];
+    if (r < 0) { o.exc = (int32_t)(-r); exc = o.exc; return o; }
+    o.v = Num::I(r);
+    return o;
+  }
+
+  void run_event(const ScoreCtx& c) {
+    const Workload& w = c.w;
+    const int N = w.n_nodes;
+    if (N > 64) throw std::runtime_error("emulated replays need <= 64 nodes");
+    gcn::Emu& E = *emu;
+    for (auto& row : E.vg)
+      for (auto& x : row) x = 0xBADC0DE5u;
+    for (auto& x : E.sg) x = 0x5CA1AB1Eu;
+    for (int l = 0; l < N; ++l) {
+      const int g0 = w.gpu_start[(size_t)l], ng = w.gpu_start[(size_t)l + 1] - g0;
+      E.vg[0][l] = (uint32_t)(int32_t)c.s.cpu_left[(size_t)l];
+      E.vg[1][l] = (uint32_t)(int32_t)w.cpu_total[(size_t)l];
+      E.vg[2][l] = (uint32_t)(int32_t)c.s.mem_left[(size_t)l];
+      E.vg[3][l] = (uint32_t)(int32_t)w.mem_total[(size_t)l];
+      E.vg[4][l] = ((uint32_t)c.s.gpu_left[(size_t)l] & 0xFFFFu) | ((uint32_t)w.ngpus[(size_t)l] << 16);
+      for (int j = 0; j < 8; ++j) {
+        E.vg[5 + j][l] = j < ng ? (uint32_t)c.s.gmilli_left[(size_t)(g0 + j)] : 0u;
+        E.vg[13 + j][l] = j < ng ? (uint32_t)w.gmilli_total[(size_t)(g0 + j)] : 0u;
+      }
+      const uint64_t gp = (uint64_t)(uintptr_t)(gmem8->data() + (size_t)l * 8);
+      E.vg[21][l] = (uint32_t)gp;
+      E.vg[22][l] = (uint32_t)(gp >> 32);
+      E.vg[23][l] = (uint32_t)(int32_t)w.pcpu[(size_t)c.pod];
+      E.vg[24][l] = (uint32_t)(int32_t)w.pmem[(size_t)c.pod];
+      E.vg[25][l] = (uint32_t)(w.pgmilli[(size_t)c.pod] | (w.pngpu[(size_t)c.pod] << 16));
+      E.vg[26][l] = (uint32_t)(uint64_t)c.pod_ctime;
+      E.vg[27][l] = (uint32_t)((uint64_t)c.pod_ctime >> 32);
+      E.vg[28][l] = (uint32_t)(int32_t)w.pdur[(size_t)c.pod];
+      E.vg[29][l] = 0;   // kc at LDS offset 0
+    }
+    E.sg[32] = 0;
+    E.wr64s(30, kRetMagic);
+    E.set_exec(N == 64 ? ~0ull : ((1ull << N) - 1));
+    E.scc = false;
+    E.run(*f, kRetMagic);
+    res.assign((size_t)N, 0);
+    for (int l = 0; l < N; ++l) res[(size_t)l] = (int64_t)((uint64_t)E.vg[0][l] | (uint64_t)E.vg[1][l] << 32);
+  }
+};
+
+}  // namespace
+
+std::vector<SimResult> emu_simulate_batch(const Workload& w, const std::vector<ProgramDesc>& progs,
+                                          const std::vector<std::vector<int64_t>>& kc, const SimOptions& o,
+                                          int threads) {
+  const int64_t P = (int64_t)progs.size();
+  std::vector<gcn::Func> funcs((size_t)P);
+  for (int64_t i = 0; i < P; ++i) {
+    gcn::ProgIn in = make_in(progs[(size_t)i]);
+    gcn::Codegen cg(in);
+    funcs[(size_t)i] = cg.run();
+  }
+  std::vector<int64_t> gmem8((size_t)w.n_nodes * 8, 0);
+  for (int n = 0; n < w.n_nodes; ++n)
+    for (int j = 0; j < std::min(8, w.gpu_start[(size_t)n + 1] - w.gpu_start[(size_t)n]); ++j)
+      gmem8[(size_t)n * 8 + (size_t)j] = w.gmem_total[(size_t)(w.gpu_start[(size_t)n] + j)];
+  std::vector<SimResult> out((size_t)P);
+  std::vector<std::string> errs((size_t)P);
+  parallel_for(P, threads, [&](int64_t i) {
+    try {
+      auto emu = std::make_unique<gcn::Emu>();
+      const std::vector<int64_t>& k = kc[(size_t)i];
+      emu->lds.resize(k.size() * 8 + 64, 0);
+      std::memcpy(emu->lds.data(), k.data(), k.size() * 8);
+      EmuScorer sc{&funcs[(size_t)i], &k, &gmem8, emu.get(), {}, EXC_NONE};
+      SimResult r = simulate(w, sc, o);
+      if (r.exc == EXC_NONE && sc.exc) r.exc = sc.exc;
+      out[(size_t)i] = std::move(r);
+    } catch (const std::exception& e) {
+      errs[(size_t)i] = e.what();
+    }
+  });
+  for (int64_t i = 0; i < P; ++i)
+    if (!errs[(size_t)i].empty())
+      throw std::runtime_error("emulated replay of program " + std::to_string(i) + ": " + errs[(size_t)i]);
+  return out;
+}
+
+std::vector<int64_t> emu_event(const ProgramDesc& p, const std::vector<int64_t>& kc,
+                               const std::vector<int64_t>& node, const std::vector<int32_t>& gl,
+                               const std::vector<int32_t>& gt, const std::vector<int64_t>& gmem,
+                               const std::vector<int64_t>& pod) {
+  const int N = (int)(node.size() / 6);
+  if (N < 1 || N > 64 || gl.size() != (size_t)N * 8 || gt.size() != (size_t)N * 8 || gmem.size() != (size_t)N * 8 ||
+      pod.size() != 6)
+    throw std::invalid_argument("emu_event: bad shapes");
+  gcn::ProgIn in = make_in(p);
+  gcn::Codegen cg(in);
+  gcn::Func f = cg.run();
+  auto E = std::make_unique<gcn::Emu>();
+  E->lds.resize(kc.size() * 8 + 64, 0);
+  std::memcpy(E->lds.data(), kc.data(), kc.size() * 8);
+  for (auto& row : E->vg)
+    for (auto& x : row) x = 0xBADC0DE5u;
+  for (auto& x : E->sg) x = 0x5CA1AB1Eu;
+  for (int l = 0; l < N; ++l) {
+    const int64_t* nd = node.data() + (size_t)l * 6;
+    E->vg[0][l] = (uint32_t)nd[0]; E->vg[1][l] = (uint32_t)nd[1];
+    E->vg[2][l] = (uint32_t)nd[2]; E->vg[3][l] = (uint32_t)nd[3];
+    E->vg[4][l] = ((uint32_t)nd[4] & 0xFFFFu) | ((uint32_t)nd[5] << 16);
+    for (int j = 0; j < 8; ++j) {
+      E->vg[5 + j][l] = (uint32_t)gl[(size_t)l * 8 + (size_t)j];
+      E->vg[13 + j][l] = (uint32_t)gt[(size_t)l * 8 + (size_t)j];
+    }
+    const uint64_t gp = (uint64_t)(uintptr_t)(gmem.data() + (size_t)l * 8);
+    E->vg[21][l] = (uint32_t)gp; E->vg[22][l] = (uint32_t)(gp >> 32);
+    E->vg[23][l] = (uint32_t)pod[0]; E->vg[24][l] = (uint32_t)pod[1];
+    E->vg[25][l] = (uint32_t)(pod[3] | (pod[2] << 16));
+    E->vg[26][l] = (uint32_t)(uint64_t)pod[4]; E->vg[27][l] = (uint32_t)((uint64_t)pod[4] >> 32);
+    E->vg[28][l] = (uint32_t)pod[5];
+    E->vg[29][l] = 0;
+  }
+  E->sg[32] = 0;
+  E->wr64s(30, kRetMagic);
+  E->set_exec(N == 64 ? ~0ull : ((1ull << N) - 1));
+  E->run(f, kRetMagic);
+  std::vector<int64_t> out((size_t)N);
+  for (int l = 0; l < N; ++l) out[(size_t)l] = (int64_t)((uint64_t)E->vg[0][l] | (uint64_t)E->vg[1][l] << 32);
+  return out;
+}
+
+}  // namespace gcnapi
+}  // namespace fks

@@ -54,13 +54,14 @@ def _deps(*globs: str) -> List[Path]:
 
 def build_cpu(force: bool = False) -> Path:
     target = NATIVE_DIR / f"_fks_cpu{_ext_suffix()}"
-    srcs = _deps("cpu/*.cpp", "cpu/*.hpp", "include/fks/*.hpp")
+    srcs = _deps("cpu/*.cpp", "cpu/*.hpp", "include/fks/*.hpp", "jit/*", "hip/jit_abi.h", "hip/pyops_dev.h",
+                 "hip/dd_math.h", "hip/jit_env.h", "hip/exc_codes.h")
     if force or _stale(target, srcs):
         cxx = os.environ.get("CXX", "g++")
         cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
                "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
                *_py_includes(), f"-I{CSRC_DIR / 'include'}", str(CSRC_DIR / "cpu" / "module.cpp"),
-               "-o", str(target), "-lpthread"]
+               str(CSRC_DIR / "jit" / "gcn_jit.cpp"), "-o", str(target), "-lpthread"]
         _run(cmd)
     return target
 

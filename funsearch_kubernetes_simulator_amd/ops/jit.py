@@ -1,7 +1,16 @@
 """Run-time compiler of policy programs for the MI355X (native program backend).
 
-Pipeline per batch of new program *shapes* (bytecode + constant tags; the
-constants themselves are data, `policy.native_codegen`):
+Two tiers (``FKS_JIT_TIER`` / ``NativeCompiler(tier=...)``):
+
+* ``baseline`` -- `ops.gcnjit`: bytecode -> gfx950 machine code generated in
+  C++ without LLVM (~0.1-0.3 ms per program), a whole batch patched into one
+  code-object skeleton and loaded with ``hipModuleLoadData``;
+* ``llvm`` -- the pipeline below (~140 ms of clang + llc per program);
+* ``auto`` (default) -- baseline for every new shape, LLVM only for the shapes
+  the baseline generator declines.
+
+LLVM-tier pipeline per batch of new program *shapes* (bytecode + constant tags;
+the constants themselves are data, `policy.native_codegen`):
 
   native_codegen.module_source  ->  clang -O3 -emit-llvm (gfx950, device
   only, no HIP headers, no device libraries)  ->  ``"amdgpu-agpr-alloc"="0"``
@@ -126,8 +135,16 @@ class CompiledModule:
     pointers: Optional[np.ndarray] = None
 
 
+#: wall-clock limit of one toolchain process (a pathological program must not
+#: stall an island forever; the shape is then marked non-native)
+TOOL_TIMEOUT_S = float(os.environ.get("FKS_JIT_TIMEOUT", "120"))
+
+
 def _run(cmd: List[str], what: str) -> None:
-    r = subprocess.run(cmd, capture_output=True, text=True)
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=TOOL_TIMEOUT_S)
+    except subprocess.TimeoutExpired as exc:
+        raise JitError(f"{what} timed out after {TOOL_TIMEOUT_S:.0f} s") from exc
     if r.returncode != 0:
         raise JitError(f"{what} failed ({r.returncode}): {r.stderr[-4000:]}")
 
@@ -189,7 +206,10 @@ class NativeBatch:
 class NativeCompiler:
     """Shape cache + parallel compiler + loader for one HIP device."""
 
-    def __init__(self, engine, device: int = 0, workers: int = 0, budget: int = 1 << 22, max_chunk: int = 16):
+    TIERS = ("auto", "baseline", "llvm")
+
+    def __init__(self, engine, device: int = 0, workers: int = 0, budget: int = 1 << 22, max_chunk: int = 16,
+                 tier: Optional[str] = None):
         from . import hip_engine
         self._hip = hip_engine.native()
         self._engine = engine            # _fks_hip.DeviceEngine (for the runtime table)
@@ -206,7 +226,17 @@ class NativeCompiler:
         self._lock = threading.Lock()
         self._inflight: Dict[str, threading.Event] = {}
         self._procs = threading.BoundedSemaphore(self.workers)
-        self.stats = {"modules": 0, "shapes": 0, "compile_s": 0.0, "rejected": 0, "hits": 0}
+        self.tier = (tier or os.environ.get("FKS_JIT_TIER", "auto")).lower()
+        if self.tier not in self.TIERS:
+            raise ValueError(f"unknown JIT tier {self.tier!r} (one of {self.TIERS})")
+        if self.budget >= 1 << 31:
+            raise ValueError("the per-call instruction budget must fit in int32 (baseline tier counter)")
+        self._baseline = None
+        if self.tier != "llvm":
+            from .gcnjit import BaselineJit
+            self._baseline = BaselineJit(self._hip, self._rt, device)
+        self.stats = {"modules": 0, "shapes": 0, "compile_s": 0.0, "rejected": 0, "hits": 0,
+                      "baseline_shapes": 0, "llvm_shapes": 0, "baseline_s": 0.0, "llvm_s": 0.0, "load_s": 0.0}
 
     def prepare(self, progs: Sequence[CompiledPolicy]) -> NativeBatch:
         """Compile every shape of `progs` not compiled yet (thread-safe: islands
@@ -258,12 +288,61 @@ class NativeCompiler:
         return NativeBatch(fn, np.concatenate(blocks) if blocks else np.zeros(1, np.int64), koff, ok, reasons, dt,
                            len(mine))
 
-    def _compile_one(self, chunk) -> CompiledModule:
+    def _compile_one(self, chunk):
+        """CompiledModule, or the toolchain error (never raises: one bad
+        program must not take down the batch or the search)."""
         with self._procs:   # bounds concurrent toolchain processes across all callers
-            return compile_device_module([p for _, p in chunk])
+            try:
+                return compile_device_module([p for _, p in chunk])
+            except (JitError, OSError) as exc:
+                return exc
+
+    def _compile_baseline(self, items):
+        """Baseline tier: generate every shape, load the batch as one module;
+        returns the (key, program, reason) the generator declined."""
+        from .gcnjit import compile_program
+        t0 = time.perf_counter()
+        codes, keys, declined = [], [], []
+        for k, p in items:
+            code, why = compile_program(p)
+            if code is None:
+                declined.append((k, p, why))
+            else:
+                codes.append(code)
+                keys.append(k)
+        t1 = time.perf_counter()
+        if codes:
+            mod = self._baseline.load(codes, t1 - t0)
+            t2 = time.perf_counter()
+            with self._lock:
+                mi = len(self._modules)
+                self._modules.append(mod)
+                self.stats["modules"] += 1
+                self.stats["compile_s"] += t2 - t0
+                self.stats["baseline_s"] += t1 - t0
+                self.stats["load_s"] += t2 - t1
+                for j, k in enumerate(keys):
+                    self._shapes[k] = (mi, j)
+                    self.stats["shapes"] += 1
+                    self.stats["baseline_shapes"] += 1
+        return declined
 
     def _compile_shapes(self, new: Dict[str, CompiledPolicy]) -> None:
         items = list(new.items())
+        if self._baseline is not None:
+            declined = self._compile_baseline(items)
+            if self.tier == "baseline":
+                with self._lock:
+                    for k, _, why in declined:
+                        self._bad[k] = why
+                        self.stats["rejected"] += 1
+                return
+            items = [(k, p) for k, p, _ in declined]
+            if not items:
+                return
+        self._compile_llvm(items)
+
+    def _compile_llvm(self, items) -> None:
         # code generation first (cheap, in-process): shapes it cannot lower are rejected
         good = []
         for k, p in items:
@@ -281,11 +360,35 @@ class NativeCompiler:
         chunks = [good[i:i + size] for i in range(0, len(good), size)]
         with ThreadPoolExecutor(max_workers=min(self.workers, len(chunks))) as ex:
             mods = list(ex.map(self._compile_one, chunks))
+        # a failed chunk: retry its programs one by one; the failing ones are
+        # marked non-native (with the toolchain's message) and go to the VMs
+        retry_ch, retry_mod = [], []
         for ch, mod in zip(chunks, mods):
+            if not isinstance(mod, Exception):
+                continue
+            if len(ch) == 1:
+                with self._lock:
+                    self._bad[ch[0][0]] = f"llvm: {mod}"[:500]
+                    self.stats["rejected"] += 1
+                continue
+            for item in ch:
+                m1 = self._compile_one([item])
+                if isinstance(m1, Exception):
+                    with self._lock:
+                        self._bad[item[0]] = f"llvm: {m1}"[:500]
+                        self.stats["rejected"] += 1
+                else:
+                    retry_ch.append([item])
+                    retry_mod.append(m1)
+        pairs = [(ch, mod) for ch, mod in zip(chunks, mods) if not isinstance(mod, Exception)]
+        pairs += list(zip(retry_ch, retry_mod))
+        for ch, mod in pairs:
             mod.handle = self._hip.JitModule(mod.image, self._rt, mod.n, self.device)
             mod.pointers = np.asarray(mod.handle.pointers(), dtype=np.uint64)
             with self._lock:
                 self.stats["compile_s"] += mod.compile_s
+                self.stats["llvm_s"] += mod.compile_s
+                self.stats["llvm_shapes"] += len(ch)
                 mi = len(self._modules)
                 self._modules.append(mod)
                 self.stats["modules"] += 1
