@@ -86,10 +86,16 @@ struct Emu {
 
   // Run `fn` (with labels resolved to indices) from index 0 until it executes
   // s_setpc_b64 to `ret` (the emulated caller's return address).
+  const Func* labels_of = nullptr;
+  std::vector<int> label_at;
+
   void run(const Func& f, uint64_t ret, int64_t max_steps = 200000000) {
-    std::vector<int> label_at((size_t)f.n_labels, -1);
-    for (size_t i = 0; i < f.mi.size(); ++i)
-      if (f.mi[i].op == LABEL) label_at[(size_t)f.mi[i].imm] = (int)i;
+    if (labels_of != &f) {
+      label_at.assign((size_t)f.n_labels, -1);
+      for (size_t i = 0; i < f.mi.size(); ++i)
+        if (f.mi[i].op == LABEL) label_at[(size_t)f.mi[i].imm] = (int)i;
+      labels_of = &f;
+    }
     size_t pc = 0;
     steps = 0;
     for (;;) {
@@ -99,8 +105,7 @@ struct Emu {
       const uint64_t ex = exec();
       size_t next = pc + 1;
       auto lanes = [&](auto fn) {
-        for (int l = 0; l < kW; ++l)
-          if (ex >> l & 1) fn(l);
+        for (uint64_t b = ex; b; b &= b - 1) fn(__builtin_ctzll(b));
       };
       auto jump = [&](int lab) { next = (size_t)label_at[(size_t)lab]; };
       switch (m.op) {

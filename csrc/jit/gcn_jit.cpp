@@ -136,8 +136,10 @@ struct EmuScorer {
     const int N = w.n_nodes;
     if (N > 64) throw std::runtime_error("emulated replays need <= 64 nodes");
     gcn::Emu& E = *emu;
-    for (auto& row : E.vg)
-      for (auto& x : row) x = 0xBADC0DE5u;
+    // registers the caller does not pass hold garbage (the first 120 VGPRs:
+    // everything the generator may allocate)
+    for (int g = 0; g < 120; ++g)
+      for (int l = 0; l < N; ++l) E.vg[g][l] = 0xBADC0DE5u;
     for (auto& x : E.sg) x = 0x5CA1AB1Eu;
     for (int l = 0; l < N; ++l) {
       const int g0 = w.gpu_start[(size_t)l], ng = w.gpu_start[(size_t)l + 1] - g0;

@@ -41,9 +41,12 @@ inline MI mkimm(Opc op, int32_t imm, uint16_t d = NONE) {
   m.op = op; m.imm = imm; m.d = d;
   return m;
 }
+// 32-bit constant operand: an inline constant when the value has one (the
+// canonical encoding), a literal otherwise
 inline MI mklit(Opc op, uint16_t d, uint32_t lit, uint16_t s1 = NONE) {
-  MI m = mk(op, d, LIT, s1);
-  m.lit = lit;
+  const uint16_t c = ic((int32_t)lit);
+  MI m = mk(op, d, c != NONE ? c : LIT, s1);
+  m.lit = c != NONE ? 0u : lit;
   return m;
 }
 
@@ -126,8 +129,11 @@ inline void expand(const Func& f, std::vector<MI>& out, int& next_label) {
           out.push_back(mk(V_MOV_B32, v(6), c.bfl));
         }
         const int frame = (off + 15) & ~15;
-        out.push_back(mklit(S_ADD_I32, s(32), (uint32_t)frame, s(32)));
-        out.back().s0 = s(32); out.back().s1 = LIT;
+        {
+          MI a = mklit(S_ADD_I32, s(32), (uint32_t)frame, s(32));
+          std::swap(a.s0, a.s1);   // s32 + frame
+          out.push_back(a);
+        }
         out.push_back(mk(S_GETPC_B64, s(r.sc)));
         {
           MI lo = mk(S_ADD_U32, s(r.sc), s(r.sc), LIT);
@@ -142,8 +148,11 @@ inline void expand(const Func& f, std::vector<MI>& out, int& next_label) {
         out.push_back(ld);
         out.push_back(mkimm(S_WAITCNT, 0xC07F));   // lgkmcnt(0)
         out.push_back(mk(S_SWAPPC_B64, s(30), s(r.sc)));
-        out.push_back(mklit(S_ADD_I32, s(32), (uint32_t)(-frame), s(32)));
-        out.back().s0 = s(32); out.back().s1 = LIT;
+        {
+          MI a = mklit(S_ADD_I32, s(32), (uint32_t)(-frame), s(32));
+          std::swap(a.s0, a.s1);
+          out.push_back(a);
+        }
         out.push_back(mk(V_MOV_B32, c.res, v(0)));
         out.push_back(mk(V_MOV_B32, (uint16_t)(c.res + 1), v(1)));
         out.push_back(mk(V_MOV_B32, c.resy, v(2)));

@@ -1,0 +1,211 @@
+"""Baseline program JIT (csrc/jit, ops/gcnjit.py) on the CPU: gfx950 encodings
+against the ROCm assembler, generated code against the CPU VM through the
+wave64 emulator (full replays and random single events), and the code-object
+skeleton's layout / relocation arithmetic."""
+import os
+import random
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from funsearch_kubernetes_simulator_amd.ops import cpu_engine as ce
+from funsearch_kubernetes_simulator_amd.ops import gcnjit
+from funsearch_kubernetes_simulator_amd.policy.compiler import compile_policy
+from funsearch_kubernetes_simulator_amd.policy.native_codegen import constant_block
+
+from program_corpus import programs
+
+MC = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib", "llvm", "bin", "llvm-mc")
+have_mc = pytest.mark.skipif(not os.path.exists(MC), reason="ROCm llvm-mc not installed")
+SKIP_EXC = (100, 101)   # UNSUPPORTED / BUDGET: the next engine decides
+
+
+@pytest.fixture(scope="module")
+def corpus():
+    from funsearch_kubernetes_simulator_amd.bench.programs import mutation_children
+    return programs() + mutation_children(24, seed=5)
+
+
+def test_every_corpus_program_compiles(corpus):
+    declined = []
+    for p in corpus:
+        code, why = gcnjit.compile_program(p)
+        if code is None:
+            declined.append(why)
+        else:
+            assert code.words.size > 10 and code.info["vgprs"] <= 128 and code.info["sgprs"] <= 96
+    assert not declined, declined
+
+
+@have_mc
+def test_opcode_table_is_what_llvm_mc_assembles(tmp_path):
+    """gcn_opcodes.inc regenerated from the assembler equals the checked-in table."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen", os.path.join(os.path.dirname(__file__), "..", "tools",
+                                                                      "gen_gcn_opcodes.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    gen.OUT = str(tmp_path / "ops.inc")
+    gen.main()
+    ours = open(os.path.join(os.path.dirname(__file__), "..", "csrc", "jit", "gcn_opcodes.inc")).read()
+    assert open(gen.OUT).read() == ours
+
+
+@have_mc
+def test_generated_code_round_trips_through_llvm_mc(corpus):
+    """Every generated word decodes to a valid gfx950 instruction and
+    re-assembles to the same bytes (canonical encodings, no stray bits)."""
+    for p in corpus[::3]:
+        code, why = gcnjit.compile_program(p)
+        assert code is not None, why
+        words = code.words.copy()
+        for lo, hi, _ in code.relocs.reshape(-1, 3):   # as the loader patches them (never inline-encodable)
+            words[int(lo)], words[int(hi)] = 0x12345678, 0xFFFFF000
+        raw = words.tobytes()
+        txt = " ".join(f"0x{b:02x}" for b in raw)
+        dis = subprocess.run([MC, "-disassemble", "-triple=amdgcn-amd-amdhsa", "-mcpu=gfx950"], input=txt,
+                             capture_output=True, text=True)
+        assert dis.returncode == 0 and not dis.stderr.strip(), dis.stderr[:2000]
+        # branch offsets are printed as immediates: re-assembling the listing gives the same words
+        asm = "\n".join(line.strip() for line in dis.stdout.splitlines() if line.strip() and not line.strip().startswith("."))
+        re = subprocess.run([MC, "-triple=amdgcn-amd-amdhsa", "-mcpu=gfx950", "-show-encoding"], input=asm,
+                            capture_output=True, text=True)
+        assert re.returncode == 0, re.stderr[:2000]
+        out = bytearray()
+        for line in re.stdout.splitlines():
+            if "encoding: [" in line:
+                out += bytes(int(x, 16) for x in line.split("encoding: [")[1].rstrip("]").split(","))
+        assert bytes(out) == raw
+
+
+def test_emulated_replays_equal_cpu_vm(default_workload, corpus):
+    """Full replays of the 8,152-pod trace with the generated machine code on
+    the wave64 emulator: rows bit-identical to the CPU VM."""
+    budget = 1 << 16   # runaway loops end quickly on both (BUDGET rows are skipped)
+    vm_all = ce.simulate_program_batch(default_workload, corpus, ce.SimOptions(budget=budget))
+    # the emulator runs ~10^7 instructions / s: replays with millions of events
+    # (a repush-heavy program, 2M events) are left to the GPU tests
+    keep = [i for i in range(0, len(corpus), 2) if vm_all[i, 8] < 60000]
+    progs = [corpus[i] for i in keep]
+    vm = vm_all[keep]
+    emu = gcnjit.emulate_programs(default_workload, progs, budget, ce.SimOptions(budget=budget))
+    compared = 0
+    for i, p in enumerate(progs):
+        if int(emu[i, 10]) in SKIP_EXC or int(vm[i, 10]) in SKIP_EXC:
+            continue
+        assert np.array_equal(emu[i], vm[i]), (i, p.source[-300:], emu[i], vm[i])
+        compared += 1
+    assert len(keep) >= len(corpus) // 2 - 4 and compared >= len(progs) - 4
+
+
+def _finish(kind, v):
+    if kind == "exc":
+        return -v
+    if kind == "none":
+        return -4
+    if kind == "int":
+        return max(0, v)
+    if v != v or not v > 0:
+        return 0
+    if v == float("inf"):
+        return -3
+    if v >= 2 ** 63:
+        return -100
+    return int(v)
+
+
+def _random_event(rng, n=16):
+    node, gl, gt, gm = [], [], [], []
+    for _ in range(n):
+        ct = rng.choice([32000, 64000, 96000, 128000])
+        mt = rng.choice([131072, 262144, 786432])
+        ng = rng.choice([0, 1, 2, 4, 8])
+        gls = [rng.choice([0, 1000, rng.randint(0, 1000)]) for _ in range(ng)] + [0] * (8 - ng)
+        node += [rng.randint(0, ct), ct, rng.randint(0, mt), mt, sum(1 for x in gls[:ng] if x == 1000), ng]
+        gl += gls
+        gt += [1000] * ng + [0] * (8 - ng)
+        gm += [16384] * ng + [0] * (8 - ng)
+    pod = [rng.choice([0, 1000, 4000, rng.randint(0, 96000)]), rng.choice([0, 1024, rng.randint(0, 400000)]),
+           rng.choice([0, 0, 1, 1, 2, 8]), rng.choice([0, 1000, rng.randint(0, 1000)]), rng.randint(0, 10 ** 7),
+           rng.randint(0, 10 ** 6)]
+    pod[3] = 1000 if pod[2] > 1 else (0 if pod[2] == 0 else pod[3])
+    return node, gl, gt, gm, pod
+
+
+def test_single_events_equal_cpu_vm_on_random_states(corpus):
+    """One emulated wave (lanes = 16 nodes, divergent control flow) per random
+    cluster state vs the VM per node: int(max(0, score)) or the exception."""
+    m = ce.native()
+    rng = random.Random(3)
+    for p in corpus[::2]:
+        kc = constant_block(p, 1 << 16).tolist()
+        lit = gcnjit.literal_mask(p).tolist()
+        for _ in range(6):
+            node, gl, gt, gm, pod = _random_event(rng)
+            emu = m.gcn_emu_event(p.code, list(map(int, p.ctag)), lit, list(map(int, p.iconst)),
+                                  list(map(float, p.fconst)), kc, node, gl, gt, gm, pod)
+            podd = dict(cpu_milli=pod[0], memory_mib=pod[1], num_gpu=pod[2], gpu_milli=pod[3], creation_time=pod[4],
+                        duration_time=pod[5])
+            for n in range(16):
+                nd = dict(cpu_milli_left=node[6 * n], cpu_milli_total=node[6 * n + 1], memory_mib_left=node[6 * n + 2],
+                          memory_mib_total=node[6 * n + 3], gpu_left=node[6 * n + 4])
+                ng = node[6 * n + 5]
+                k, v = m.score_program_once(p.code, list(p.fconst), list(p.iconst), list(p.ctag), podd, nd,
+                                            gl[8 * n:8 * n + ng], gt[8 * n:8 * n + ng], gm[8 * n:8 * n + ng])
+                ref = _finish(k, v)
+                if ref in (-100, -101) or emu[n] in (-100, -101):
+                    continue
+                assert emu[n] == ref, (p.source[-300:], n, pod, node[6 * n:6 * n + 6], (k, v), emu[n])
+
+
+def test_dynamic_types_runtime_calls_and_lists():
+    """Programs whose registers change type at run time (runtime-library calls,
+    tag bits), GPU-list slicing / insertion / sorting, and exceptions."""
+    bodies = [
+        "s = 0.0\n    if pod.cpu_milli > 30000:\n        s = int(pod.cpu_milli * 0.05)\n    s = max(1, s)\n"
+        "    if node.cpu_milli_left > pod.cpu_milli * 2:\n        s += 54.111\n    return max(1, int(s))",
+        "x = node.cpu_milli_left ** 0.5 + (node.memory_mib_left % 7) // 2\n    return x",
+        "g = sorted(node.gpus, key=lambda g: g.gpu_milli_left)[:2]\n    t = 0\n"
+        "    for q in g:\n        t += q.gpu_milli_left\n    return t + len(g) * 3",
+        "v = node.cpu_milli_left / (node.gpu_left - 1)\n    return v",
+        "a = [g for g in node.gpus if g.gpu_milli_left > 100]\n    return max(1, len(a) * 100 - node.gpus[0].gpu_milli_left)",
+        "r = round(node.memory_mib_left / 3.0) + abs(pod.cpu_milli - node.cpu_milli_left)\n    return -r if r % 2 else r",
+    ]
+    m = ce.native()
+    rng = random.Random(11)
+    for body in bodies:
+        p = compile_policy("def priority_function(pod, node):\n    " + body + "\n")
+        kc = constant_block(p, 1 << 16).tolist()
+        for _ in range(8):
+            node, gl, gt, gm, pod = _random_event(rng)
+            emu = m.gcn_emu_event(p.code, list(map(int, p.ctag)), gcnjit.literal_mask(p).tolist(),
+                                  list(map(int, p.iconst)), list(map(float, p.fconst)), kc, node, gl, gt, gm, pod)
+            podd = dict(cpu_milli=pod[0], memory_mib=pod[1], num_gpu=pod[2], gpu_milli=pod[3], creation_time=pod[4],
+                        duration_time=pod[5])
+            for n in range(16):
+                nd = dict(cpu_milli_left=node[6 * n], cpu_milli_total=node[6 * n + 1], memory_mib_left=node[6 * n + 2],
+                          memory_mib_total=node[6 * n + 3], gpu_left=node[6 * n + 4])
+                ng = node[6 * n + 5]
+                k, v = m.score_program_once(p.code, list(p.fconst), list(p.iconst), list(p.ctag), podd, nd,
+                                            gl[8 * n:8 * n + ng], gt[8 * n:8 * n + ng], gm[8 * n:8 * n + ng])
+                ref = _finish(k, v)
+                if ref in (-100, -101) or emu[n] in (-100, -101):
+                    continue
+                assert emu[n] == ref, (body, n, (k, v), emu[n])
+
+
+def test_skeleton_layout_and_relocations():
+    if not shutil.which(gcnjit.CLANG) and not os.path.exists(gcnjit.CLANG):
+        pytest.skip("ROCm clang not installed")
+    sk = gcnjit.Skeleton.load(gcnjit.SKELETON_SIZES[0])
+    assert sk.arena_vaddr % gcnjit.PROGRAM_ALIGN == 0 and sk.capacity > 200_000
+    assert sk.image[sk.arena_off:sk.arena_off + 4] == bytes.fromhex("000081bf")   # s_endpgm filler
+    p = compile_policy("def priority_function(pod, node):\n    return node.cpu_milli_left ** 0.5\n")
+    code, _ = gcnjit.compile_program(p)
+    assert code.relocs.size == 3 * code.info["calls"] and code.info["calls"] == 1
+    lo, hi, pc = (int(x) for x in code.relocs[:3])
+    # the two literal slots follow s_add_u32 / s_addc_u32 words of the runtime-table address
+    assert code.words[lo - 1] >> 23 == 0x100 and code.words[hi - 1] >> 23 == 0x104
+    assert pc % 4 == 0 and pc < code.words.size * 4
