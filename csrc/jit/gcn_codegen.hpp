@@ -441,6 +441,9 @@ class Codegen {
     s_dead_ = take_spair();
     for (int i = 0; i < 3; ++i) ST_[i] = take_spair();
     S_LIT_ = take_spair();
+    bm_pair_[0] = take_spair();
+    bm_pair_[1] = take_spair();
+    bm_of_.fill(-1);
     for (int f = 0; f < 6; ++f)
       if (pod_s_[f] > 0) pod_s_[f] = take_spair();
       else pod_s_[f] = -1;
@@ -457,7 +460,64 @@ class Codegen {
   }
 
   // ============================================================ emission helpers
-  void e(const MI& m) { F_.mi.push_back(m); }
+  // Emission.  LDS loads (constant reads) are waited for lazily: right before
+  // the first instruction that touches their destination, or at any label /
+  // branch / call (so every control-flow merge starts with nothing pending).
+  std::vector<uint16_t> lds_pending_;
+  void e(const MI& m) {
+    if (!lds_pending_.empty()) {
+      bool need = m.op == LABEL || is_branch(m.op) || m.op == S_SETPC_B64 || m.op == M_RTCALL || m.op == S_WAITCNT;
+      for (uint16_t b : lds_pending_)
+        for (uint16_t c : {m.s0, m.s1, m.s2, m.d, m.sd})
+          if (c != NONE && c + 1 >= b && c <= b + 1) need = true;
+      if (need) {
+        lds_pending_.clear();
+        if (m.op != S_WAITCNT) F_.mi.push_back(mkimm(S_WAITCNT, 0xC07F));
+      }
+    }
+    F_.mi.push_back(m);
+    if (m.op == DS_READ_B64) lds_pending_.push_back(m.d);
+  }
+  // Bool-mask cache: a register that holds a 0 / 1 produced in the current
+  // basic block also has its lane mask in one of two SGPR pairs, so IF /
+  // NOT / TRUTH / LOOP_TEST of it need no VALU compare.  Invalidated at every
+  // label, structural op, call and redefinition.
+  //
+  // Bools are materialised lazily: a compare only records its mask; the 0 / 1
+  // value is written to the register when something reads it as a number,
+  // when its mask slot is reused, or -- if it is still live -- before EXEC
+  // changes (structural ops, leaving lanes, calls), always under the EXEC it
+  // was computed with.
+  int bm_pair_[2] = {-1, -1};
+  std::array<int8_t, kMaxRegs> bm_of_{};
+  int bm_next_ = 0;
+  uint64_t pend_ = 0;   // registers whose value is only in their mask slot
+  void materialize(int r) {
+    if (!(pend_ >> r & 1)) return;
+    pend_ &= ~(1ull << r);
+    e(mk(V_CNDMASK_B32, R(r), ic(0), ic(1), s(bm_pair_[bm_of_[r]])));
+    e(mk(V_MOV_B32, Rh(r), ic(0)));
+  }
+  void materialize_live(uint64_t live) {
+    for (int r = 0; r < kMaxRegs; ++r)
+      if ((pend_ >> r & 1) && (live >> r & 1)) materialize(r);
+    pend_ = 0;
+  }
+  void bm_clear() {
+    if (pend_) throw CodegenError("internal: pending bools at an EXEC change");
+    bm_of_.fill(-1);
+  }
+  void bm_set(int r, uint16_t mask) {
+    const int slot = bm_next_++ & 1;
+    for (int q = 0; q < kMaxRegs; ++q)
+      if (bm_of_[q] == slot && q != r) {
+        if (mask == s(bm_pair_[slot])) continue;   // the source mask itself stays
+        materialize(q);
+        bm_of_[q] = -1;
+      }
+    if (mask != s(bm_pair_[slot])) e(mk(S_MOV_B64, s(bm_pair_[slot]), mask));
+    bm_of_[r] = (int8_t)slot;
+  }
   uint16_t R(int r) const {
     if (base_[r] < 0) throw CodegenError("register without a home");
     return v(base_[r]);
@@ -469,7 +529,10 @@ class Codegen {
   uint16_t ST(int i) const { return s(ST_[i]); }
   uint16_t TAGV(int r) const { return v(v_tag_[tagbit_[r] >> 5]); }
   int label() { return F_.new_label(); }
-  void place(int lab) { e(mkimm(LABEL, lab)); }
+  void place(int lab) {
+    e(mkimm(LABEL, lab));
+    bm_clear();
+  }
   int label_for_pc(int pc) {
     auto it = label_at_pc_.find(pc);
     if (it != label_at_pc_.end()) return it->second;
@@ -614,6 +677,7 @@ class Codegen {
   }
   // d = rt_binop / rt_unop(op, a[, b]) with Python semantics for any operand types
   void rtcall(int kind, int op, int pc, int d, int a, uint8_t ta, int b = -1, uint8_t tb = TY_I) {
+    materialize_live(slive_out_[pc] | live_out_[pc]);
     e(mk(V_MOV_B64, X(0), R(a)));
     CallInfo c;
     c.kind = kind;
@@ -636,6 +700,7 @@ class Codegen {
     m.ext = (int)F_.calls.size();
     F_.calls.push_back(c);
     e(m);
+    bm_clear();   // the callee clobbers the mask registers
     // exception code: fl | e << 8
     e(mk(V_LSHRREV_B32, Th(0), ic(8), X(3)));
     cmp(V_CMP_NE_U32, ST(0), ic(0), Th(0));
@@ -666,20 +731,22 @@ class Codegen {
     e(mk(S_MOV_B64, EXEC, ic(0)));
   }
   // truth(r) -> SGPR pair
-  void truth(int r, uint8_t t, uint16_t dst) {
-    if (t == TY_I) { cmp(V_CMP_NE_I64, dst, ic(0), R(r)); return; }
-    if (t == TY_F) { cmp(V_CMP_NEQ_F64, dst, ic(0), R(r)); return; }
+  uint16_t truth(int r, uint8_t t, uint16_t dst) {
+    if (bm_of_[r] >= 0) return s(bm_pair_[bm_of_[r]]);
+    if (t == TY_I) { cmp(V_CMP_NE_I64, dst, ic(0), R(r)); return dst; }
+    if (t == TY_F) { cmp(V_CMP_NEQ_F64, dst, ic(0), R(r)); return dst; }
     tag_mask(r, ST(1));
     cmp(V_CMP_NE_I64, dst, ic(0), R(r));
     cmp(V_CMP_NEQ_F64, ST(2), ic(0), R(r));
     e(mk(S_AND_B64, ST(2), ST(2), ST(1)));
     e(mk(S_ANDN2_B64, dst, dst, ST(1)));
     e(mk(S_OR_B64, dst, dst, ST(2)));
+    return dst;
   }
-  void set_bool(int d, uint16_t mask) {   // d = int(mask)
-    e(mk(V_CNDMASK_B32, R(d), ic(0), ic(1), mask));
-    e(mk(V_MOV_B32, Rh(d), ic(0)));
+  void set_bool(int d, uint16_t mask) {   // d = int(mask), materialised lazily
     set_tag_static(d, false);
+    bm_set(d, mask);
+    pend_ |= 1ull << d;
   }
 
   // ============================================================ per-op lowering
@@ -742,6 +809,28 @@ class Codegen {
     const uint8_t ta = in.a != kNoReg ? st[in.a] : TY_I;
     const uint8_t tb = in.b != kNoReg ? st[in.b] : TY_I;
     const int d = in.d, a = in.a, b = in.b;
+    const bool exec_change = structural(in.op) || in.op == OP_BREAK || in.op == OP_CONTINUE || in.op == OP_RET ||
+                             in.op == OP_RAISE || in.op == OP_END;
+    const bool via_mask = in.op == OP_IF || in.op == OP_LOOP_TEST || in.op == OP_NOT || in.op == OP_TRUTH;
+    // operands read as numbers must hold their value
+    if (!(in.op == OP_MOV || in.op == OP_POS || via_mask)) {
+      const uint64_t u = uses(pc) & pend_;
+      for (int r = 0; r < kMaxRegs; ++r)
+        if (u >> r & 1) materialize(r);
+    }
+    // bools still live must be written before EXEC changes (IF / LOOP_TEST
+    // take their operand's mask first, then materialise)
+    uint16_t mask_a = NONE;
+    if (exec_change) {
+      if (in.op == OP_IF || in.op == OP_LOOP_TEST) mask_a = truth(a, ta, ST(0));
+      if (mask_a != NONE && mask_a != ST(0)) { e(mk(S_MOV_B64, ST(0), mask_a)); mask_a = ST(0); }
+      materialize_live(slive_out_[pc] | live_out_[pc]);
+      bm_clear();
+    } else if (defines(in.op) && d != kNoReg && !via_mask) {
+      // (NOT / TRUTH read their operand's mask first and set d's state themselves)
+      if (!(in.op == OP_MOV || in.op == OP_POS)) bm_of_[d] = -1;
+      if (!((in.op == OP_MOV || in.op == OP_POS) && (pend_ >> a & 1))) pend_ &= ~(1ull << d);
+    }
     switch (in.op) {
       case OP_NOP: break;
       case OP_CONST: {
@@ -750,8 +839,7 @@ class Codegen {
         if (P_.is_lit[k]) {
           MI ld = mk(DS_READ_B64, R(d), v(29));
           ld.imm = 8 * (1 + k);
-          e(ld);
-          e(mkimm(S_WAITCNT, 0xC07F));
+          e(ld);   // waited for at the first use (e())
         } else {
           uint64_t bits;
           if (fl) std::memcpy(&bits, &P_.fconst[k], 8);
@@ -763,8 +851,15 @@ class Codegen {
         break;
       }
       case OP_MOV: case OP_POS:
+        if (pend_ >> a & 1) {          // a bool still in its mask: d shares it
+          bm_of_[d] = bm_of_[a];
+          pend_ |= 1ull << d;
+          set_tag_static(d, false);
+          break;
+        }
         if (base_[d] != base_[a]) e(mk(V_MOV_B64, R(d), R(a)));
         copy_tag(d, a, ta);
+        bm_of_[d] = bm_of_[a];
         break;
       case OP_POD: {
         const int f = (in.imm >= 0 && in.imm <= 5) ? in.imm : 5;
@@ -841,7 +936,11 @@ class Codegen {
           set_tag_static(d, true);
         }
         break;
-      case OP_FDIV: case OP_MOD: case OP_POW: case OP_LOGB: case OP_MPOW:
+      case OP_FDIV: case OP_MOD:
+        if (ta == TY_I && tb == TY_I) { emit_int_divmod(in); break; }
+        rtcall(0, in.op, pc, d, a, ta, b, tb);
+        break;
+      case OP_POW: case OP_LOGB: case OP_MPOW:
         rtcall(0, in.op, pc, d, a, ta, b, tb);
         break;
       case OP_SQRT: case OP_LOG: case OP_EXP: case OP_SIN: case OP_COS: case OP_TAN:
@@ -899,11 +998,27 @@ class Codegen {
         set_tag_static(d, true);
         break;
       }
-      case OP_NOT: case OP_TRUTH:
-        truth(a, ta, ST(0));
-        if (in.op == OP_NOT) e(mk(S_ANDN2_B64, ST(0), EXEC, ST(0)));
-        set_bool(d, ST(0));
+      case OP_NOT: case OP_TRUTH: {
+        if (in.op == OP_TRUTH && bm_of_[a] >= 0) {   // truth of a bool: the same bool
+          if (pend_ >> a & 1) {
+            pend_ |= 1ull << d;
+          } else {
+            pend_ &= ~(1ull << d);
+            if (base_[d] != base_[a]) e(mk(V_MOV_B64, R(d), R(a)));
+          }
+          bm_of_[d] = bm_of_[a];
+          set_tag_static(d, false);
+          break;
+        }
+        const uint16_t m = truth(a, ta, ST(0));
+        if (in.op == OP_NOT) {
+          e(mk(S_ANDN2_B64, ST(0), EXEC, m));
+          set_bool(d, ST(0));
+        } else {
+          set_bool(d, m);
+        }
         break;
+      }
       case OP_ISINT:
         if (ta == TY_IF) {
           tag_mask(a, ST(0));
@@ -924,7 +1039,6 @@ class Codegen {
         Frame fr{};
         fr.loop = false;
         fr.pc = pc;
-        truth(a, ta, ST(0));
         fr.s_save = take_spair();
         const int t = in.imm;
         if (t <= pc || t >= n_) throw CodegenError("bad IF target");
@@ -974,8 +1088,7 @@ class Codegen {
       case OP_LOOP_TEST: {
         Frame* l = innermost_loop();
         if (!l || frames_.back().pc != l->pc) throw CodegenError("LOOP_TEST not at loop level");
-        truth(a, ta, ST(0));
-        e(mk(S_AND_B64, EXEC, EXEC, ST(0)));
+        e(mk(S_AND_B64, EXEC, EXEC, mask_a));
         e(mkimm(S_CBRANCH_EXECZ, label_for_pc(in.imm)));
         break;
       }
@@ -1095,6 +1208,47 @@ class Codegen {
     cmp(V_CMP_LT_I32, ST(1), T(1), ic(0));
     soft_raise(ST(1), EXC_UNSUPPORTED);
     e(mk(V_MOV_B64, R(d), T(0)));
+    set_tag_static(d, false);
+  }
+
+  // ---- int // int and int % int (CPython floor semantics), exact for
+  // |a|, |b| <= 2^53: q0 = floor(fl(a / b)) is the true floor or one above it
+  // (a / b can round up onto the next integer, never below its floor), and
+  // r = a - q0 * b, corrected once when r and b differ in sign.  Wider
+  // operands -> EXC_UNSUPPORTED (the next engine decides).
+  void emit_int_divmod(const Insn& in) {
+    const int d = in.d, a = in.a, b = in.b;
+    cmp(V_CMP_EQ_I64, ST(0), ic(0), R(b));
+    soft_raise(ST(0), EXC_ZERO_DIVISION);
+    check_exact_int(R(a), EXEC);
+    check_exact_int(R(b), EXEC);
+    const uint16_t fa = as_f64(a, TY_I, 0), fb = as_f64(b, TY_I, 1);
+    e(mk(M_FDIV64, T(2), fa, fb));
+    e(mk(V_FLOOR_F64, T(2), T(2)));
+    e(mk(M_CVT_I64_F64, T(2), T(2)));                                   // q0
+    // q0 * b (low 64 bits; |q0 * b| < 2^54)
+    e(mk3b(V_MAD_U64_U32, X(0), VCC, T(2), R(b), ic(0)));
+    e(mk(V_MUL_LO_U32, X(1), Th(2), R(b)));
+    e(mk(V_MUL_LO_U32, (uint16_t)(X(1) + 1), T(2), Rh(b)));
+    e(mk(V_ADD_U32, (uint16_t)(X(0) + 1), (uint16_t)(X(0) + 1), X(1)));
+    e(mk(V_ADD_U32, (uint16_t)(X(0) + 1), (uint16_t)(X(0) + 1), (uint16_t)(X(1) + 1)));
+    // r = a - q0 b
+    MI lo = mk(V_SUB_CO_U32, X(1), R(a), X(0)); lo.sd = ST(0); e(lo);
+    MI hi = mk(V_SUBB_CO_U32, (uint16_t)(X(1) + 1), Rh(a), (uint16_t)(X(0) + 1), ST(0)); hi.sd = ST(0); e(hi);
+    // fix = r != 0 && sign(r) != sign(b)
+    cmp(V_CMP_NE_I64, ST(0), ic(0), X(1));
+    e(mk(V_XOR_B32, X(2), (uint16_t)(X(1) + 1), Rh(b)));
+    cmp(V_CMP_LT_I32, ST(1), X(2), ic(0));
+    e(mk(S_AND_B64, ST(0), ST(0), ST(1)));
+    if (in.op == OP_FDIV) {
+      e(mk(V_LSHL_ADD_U64, X(2), T(2), ic(0), ic(-1)));                 // q0 - 1
+      e(mk(V_CNDMASK_B32, R(d), T(2), X(2), ST(0)));
+      e(mk(V_CNDMASK_B32, Rh(d), Th(2), (uint16_t)(X(2) + 1), ST(0)));
+    } else {
+      e(mk(V_LSHL_ADD_U64, X(2), X(1), ic(0), R(b)));                   // r + b
+      e(mk(V_CNDMASK_B32, R(d), X(1), X(2), ST(0)));
+      e(mk(V_CNDMASK_B32, Rh(d), (uint16_t)(X(1) + 1), (uint16_t)(X(2) + 1), ST(0)));
+    }
     set_tag_static(d, false);
   }
 

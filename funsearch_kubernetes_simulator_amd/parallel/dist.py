@@ -63,12 +63,24 @@ def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = No
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     if not dist.is_initialized():
+        import datetime
         kw = {}
         if os.environ.get("FKS_DIST_TIMEOUT_S"):
             # failure detection: a collective whose peer is gone raises after this long
-            import datetime
             kw["timeout"] = datetime.timedelta(seconds=float(os.environ["FKS_DIST_TIMEOUT_S"]))
-        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+        attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT")
+        if attempt is not None:
+            # Under torchrun the agent's TCPStore outlives a restart round (same
+            # MASTER_PORT), so a restarted group would read the previous round's
+            # gloo / RCCL peer addresses from it and connect to dead sockets
+            # ("connectFullMesh ... Connection refused").  Every round gets its
+            # own key space instead.
+            store, _, _ = next(dist.rendezvous("env://", rank=rank, world_size=world,
+                                               timeout=kw.get("timeout", datetime.timedelta(minutes=10))))
+            store = dist.PrefixStore(f"/fks/attempt_{attempt}", store)
+            dist.init_process_group(backend=backend, store=store, rank=rank, world_size=world, **kw)
+        else:
+            dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
     _ctx = DistContext(rank=rank, world_size=world, local_rank=local, backend=backend, device=device)
     return _ctx
 

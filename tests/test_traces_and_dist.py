@@ -201,16 +201,16 @@ def test_torchrun_restart_resumes_after_rank_crash(tmp_path):
         "print(json.dumps({'gen': fs.generation, 'world': fs.ctx.world_size, 'score': score,\n"
         "                  'restart': os.environ.get('TORCHELASTIC_RESTART_COUNT')}))\n")
     env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1", FKS_DIST_TIMEOUT_S="60", GLOO_SOCKET_IFNAME="lo")
-    # dynamic (c10d) rendezvous: every restart round re-forms the group on a fresh store prefix.
-    # Spare restarts: on a loaded host gloo's full-mesh connect of a restarted group is sometimes
-    # refused (a peer address from the killed round); the agent then simply restarts once more.
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--max-restarts=3",
+    # dynamic (c10d) rendezvous; the agent's store outlives a round, so dist.init_distributed keys
+    # every round's group formation by TORCHELASTIC_RESTART_COUNT (a restarted group once read the
+    # killed round's peer addresses: "connectFullMesh ... Connection refused").  One restart is enough.
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--max-restarts=1",
            "--rdzv-backend=c10d", "--local-addr=127.0.0.1", f"--rdzv-endpoint=127.0.0.1:{33000 + os.getpid() % 1000}", str(script)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]
     import re
     outs = [json.loads(m) for m in re.findall(r"\{[^{}]*\}", r.stdout)]   # the two ranks' lines may interleave
-    assert outs and all(o["gen"] == 4 and o["world"] == 2 and o["restart"] in ("1", "2", "3") for o in outs)
+    assert outs and all(o["gen"] == 4 and o["world"] == 2 and o["restart"] == "1" for o in outs)
     assert max(o["score"] for o in outs) > 0.44
 
 

@@ -93,6 +93,7 @@ def main():
         n = int(sys.argv[2]) if len(sys.argv) > 2 else 64
         seed = int(sys.argv[3]) if len(sys.argv) > 3 else 21
         progs = mutation_children(n, seed)
+        tabs = {}
         for t in ("baseline", "llvm"):
             w, dev = evaluator(t)
             dev.submit_native(0, progs[:1])
@@ -105,13 +106,23 @@ def main():
             dev.submit_native(0, progs)
             dev.wait(0)
             t3 = time.perf_counter()
+            tabs[t] = tab
             say(stage="bench", tier=t, P=n, native=int(nb.ok.sum()), compile_s=round(t1 - t0, 4),
                 device_s=round(t2 - t1, 4), evals_per_s_incl_jit=round(n / (t2 - t0), 1),
                 evals_per_s_cached=round(n / (t3 - t2), 1), stats=dev.native_compiler.stats)
+            # one program per launch: replay latency (the latency-bound regime)
+            lat = []
+            for p in progs[:6]:
+                dev.evaluate_native([p])
+                s0 = time.perf_counter()
+                r = dev.evaluate_native([p])
+                lat.append((round((time.perf_counter() - s0) * 1e3, 2), int(r[0, 8])))
+            say(stage="latency", tier=t, ms_events=lat)
         t0 = time.perf_counter()
         vm = ce.simulate_program_batch(w, progs, threads=16)
         t1 = time.perf_counter()
-        say(stage="bench", tier="cpu_vm", P=n, evals_per_s=round(n / (t1 - t0), 1), bad=compare(tab, vm)[:10])
+        say(stage="bench", tier="cpu_vm", P=n, evals_per_s=round(n / (t1 - t0), 1),
+            bad_baseline=compare(tabs["baseline"], vm)[:10], bad_llvm=compare(tabs["llvm"], vm)[:10])
     else:
         raise SystemExit(f"unknown stage {stage}")
 
