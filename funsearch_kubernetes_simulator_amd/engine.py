@@ -137,6 +137,14 @@ def _object_worker(args):
 
 
 # ---------------------------------------------------------------------------- evaluator
+#: exception codes of a native-program row that hand the program to the next
+#: engine: UNSUPPORTED / BUDGET as for every engine, plus INVARIANT -- the
+#: two-wave kernel ends a replay with it when one wave stops hearing from the
+#: other (a bounded spin, replay_duo.hip.h), which depends on timing, not on
+#: the program, so it is never a final score
+NATIVE_DEFER = (int(Exc.UNSUPPORTED), int(Exc.BUDGET), int(Exc.INVARIANT))
+
+
 class Evaluator:
     """Batched exact evaluator bound to one workload.
 
@@ -263,7 +271,7 @@ class Evaluator:
                 self._absorb_native(dev_idx, compiled, out, slot)
             dev_idx = [i for i in dev_idx if out[i] is None]
             if len(dev_idx) >= self.device_min_batch:
-                tab = self.device.evaluate_programs([compiled[i] for i in dev_idx])
+                tab = self.device.evaluate_programs([compiled[i] for i in dev_idx], slot=slot)
                 for row, i in zip(tab, dev_idx):
                     if int(row[COLS["exc"]]) in (Exc.UNSUPPORTED, Exc.BUDGET) or row[COLS["inexact"]]:
                         continue
@@ -307,8 +315,7 @@ class Evaluator:
         if self.device is not None and self.native and progs:
             self.device.submit_native(slot, progs)
             tab = self.device.wait(slot)
-            ok = (tab[:, COLS["exc"]] != Exc.UNSUPPORTED) & (tab[:, COLS["exc"]] != Exc.BUDGET) \
-                & (tab[:, COLS["inexact"]] == 0)
+            ok = ~np.isin(tab[:, COLS["exc"]], NATIVE_DEFER) & (tab[:, COLS["inexact"]] == 0)
             out[ok] = tab[ok, COLS["score"]]
             rest = [i for i in range(len(progs)) if not ok[i]]
             self.stats["device_native"] += int(ok.sum())
@@ -358,14 +365,14 @@ class Evaluator:
             tab = self.device.wait(pend.slot)
             pend.t_done = time.perf_counter()
             for row, i in zip(tab, pend.native_idx):
-                if int(row[COLS["exc"]]) in (Exc.UNSUPPORTED, Exc.BUDGET) or row[COLS["inexact"]]:
+                if int(row[COLS["exc"]]) in NATIVE_DEFER or row[COLS["inexact"]]:
                     continue
                 out[i] = _row_to_result(row, "hip-native")
                 self.stats["device_native"] += 1
         rest = [i for i in range(n) if out[i] is None]
         if rest:
             sub = self._evaluate_compiled([pend.codes[i] for i in rest], [pend.compiled[i] for i in rest],
-                                          native=False)
+                                          native=False, slot=pend.slot)
             for i, r in zip(rest, sub):
                 out[i] = r
         if self.fault_rate > 0:
@@ -381,7 +388,7 @@ class Evaluator:
         self.stats["jit_shapes"] += batch.compiled
         tab = self.device.wait(slot)
         for row, i in zip(tab, idx):
-            if int(row[COLS["exc"]]) in (Exc.UNSUPPORTED, Exc.BUDGET) or row[COLS["inexact"]]:
+            if int(row[COLS["exc"]]) in NATIVE_DEFER or row[COLS["inexact"]]:
                 continue
             out[i] = _row_to_result(row, "hip-native")
             self.stats["device_native"] += 1

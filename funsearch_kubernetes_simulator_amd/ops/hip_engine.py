@@ -321,9 +321,15 @@ class DeviceEvaluator:
             return True
         return self._eng.ready(slot)
 
-    def evaluate_programs(self, progs: Sequence[CompiledPolicy]) -> np.ndarray:
+    def evaluate_programs(self, progs: Sequence[CompiledPolicy], slot: Optional[int] = None) -> np.ndarray:
+        """Device bytecode VM.  With `slot`, the batch runs on that slot's
+        stream and buffers (callers in island worker threads pass their own
+        slot, so two threads never stage into one slot)."""
         if not progs:
             return np.zeros((0, len(RESULT_COLUMNS)))
+        if slot is not None:
+            self.submit_programs(slot, progs)
+            return self.wait(slot)
         nregs = max(p.nregs for p in progs)
         return self._eng.evaluate_programs(*pack_programs(progs), nregs)
 
