@@ -336,8 +336,16 @@ class Evaluator:
         launches them; returns at once.  `ready` / `collect` finish the batch
         (programs the native backend declines run on the next engine at collect
         time).  Without a device everything happens at collect time."""
+        return self.submit_compiled(codes, self.compile_batch(list(codes)), slot, count_errors=False)
+
+    def submit_compiled(self, codes: Sequence[str], compiled: Sequence[Optional[CompiledPolicy]],
+                        slot: int, count_errors: bool = True) -> "PendingPrograms":
+        """`submit_programs` for programs whose bytecode was produced elsewhere
+        (the steady-state search compiles in its producer processes)."""
         pend = PendingPrograms(list(codes), slot)
-        pend.compiled = self.compile_batch(pend.codes)
+        pend.compiled = list(compiled)
+        if count_errors:
+            self.stats["compile_errors"] += sum(p is None for p in pend.compiled)
         if self.device is not None and self.native:
             idx = [i for i, p in enumerate(pend.compiled) if p is not None and p.device_ok]
             if idx:

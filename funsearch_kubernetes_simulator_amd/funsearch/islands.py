@@ -66,6 +66,10 @@ class IslandFunSearch:
         self._polished = set()
         # islands step independently (LLM / JIT / device stages overlap across islands)
         self.pipeline = bool(isl.get("pipeline", False))
+        # steady-state mode (funsearch/steady.py): hundreds of programs in flight,
+        # children sampled from the islands' current populations, no lockstep
+        self.mode = str(isl.get("mode", "steady" if isl.get("steady") else ("pipeline" if self.pipeline else "sync")))
+        self.steady_cfg = dict(isl.get("steady") or {})
         self.generation_base = 0
         self._last_migration = 0
         self.failures: List[dict] = []
@@ -189,36 +193,44 @@ class IslandFunSearch:
         try:
             return fn()
         except Exception as exc:        # DistBackendError / RuntimeError from a dead or timed-out peer
-            if not self.elastic:
-                raise
-            rec = dict(kind="rank_failure", rank=self.ctx.rank, generation=self.generation, collective=what,
-                       world_size=self.ctx.world_size, error=f"{type(exc).__name__}: {str(exc)[:300]}")
-            self.failures.append(rec)
-            self.log.write(**rec)
-            if self.verbose:
-                print(json.dumps(rec), flush=True)
-            self.ctx = dist.degrade_to_local(what)
-            if self.ck_dir:
-                self.save_checkpoint()
+            self.rank_lost(what, exc)
             return fn() if fallback is None else fallback
 
-    def migrate(self) -> None:
-        """Ring migration of each island's best programs across all ranks."""
-        k = self.n_migrants
+    def rank_lost(self, what: str, exc: BaseException) -> None:
+        """A collective failed (dead or timed-out peer): log it, leave the
+        group and continue as a single-rank job (raises unless elastic)."""
+        if not self.elastic:
+            raise exc
+        rec = dict(kind="rank_failure", rank=self.ctx.rank, generation=self.generation, collective=what,
+                   world_size=self.ctx.world_size, error=f"{type(exc).__name__}: {str(exc)[:300]}")
+        self.failures.append(rec)
+        self.log.write(**rec)
+        if self.verbose:
+            print(json.dumps(rec), flush=True)
+        self.ctx = dist.degrade_to_local(what)
+        if self.ck_dir:
+            self.save_checkpoint()
+
+    def migrant_blob(self):
+        """This rank's migrants (each island's top ``n_migrants``) as one
+        variable-length record blob (`dist.pack_migrants`; drops are logged)."""
         recs = []
-        for s in self.islands:
-            top = sorted(s.population, key=lambda x: x[1], reverse=True)[:k]
-            top += [("", float("-inf"))] * (k - len(top))
-            recs.append(dist.pack_programs([c for c, _ in top], [sc for _, sc in top]))
-        import numpy as np
-        local = np.stack(recs)                                  # [I, k, bytes]
-        glob = dist.all_gather_array(local)                     # [W, I, k, bytes]
-        W, I = glob.shape[0], glob.shape[1]
-        flat = glob.reshape(W * I, k, -1)
+        for li, s in enumerate(self.islands):
+            for code, score in sorted(s.population, key=lambda x: x[1], reverse=True)[:self.n_migrants]:
+                recs.append((li, code, score))
+        recs.sort(key=lambda r: r[2], reverse=True)
+        return dist.pack_migrants(recs, log=lambda rec: self.log.write(rank=self.ctx.rank, **rec))
+
+    def absorb_migrants(self, glob) -> None:
+        """Ring migration: global island g receives island g - 1's migrants."""
+        W, I = glob.shape[0], len(self.islands)
+        by_island = {}
+        for r in range(W):
+            for li, code, score in dist.unpack_migrants(glob[r]):
+                by_island.setdefault(r * I + li, []).append((code, score))
         for li, s in enumerate(self.islands):
             g = self.ctx.rank * I + li
-            src = flat[(g - 1) % (W * I)]
-            incoming = dist.unpack_programs(src)
+            incoming = by_island.get((g - 1) % (W * I), [])
             known = {c for c, _ in s.population}
             for code, score in incoming:
                 if code not in known:
@@ -226,6 +238,10 @@ class IslandFunSearch:
                     if score > s.best_score:
                         s.best_score, s.best_policy = score, code
             s.population = sorted(s.population, key=lambda x: x[1], reverse=True)[:s.population_size]
+
+    def migrate(self) -> None:
+        """Ring migration of each island's best programs across all ranks."""
+        self.absorb_migrants(dist.all_gather_array(self.migrant_blob()))
 
     # -- pipelined generations (SURVEY section 7.4(5)) ---------------------------------------
     def _plan(self, s: SimpleFunSearch):
@@ -512,6 +528,15 @@ class IslandFunSearch:
         generations = generations or self.islands[0].max_generations
         threshold = self.islands[0].early_stop_threshold
         start = self.generation
+        if self.mode == "steady":
+            from .steady import SteadyStateSearch
+            sc = self.steady_cfg
+            self.steady = SteadyStateSearch(self, batch=int(sc.get("batch", 256)), slots=sc.get("slots"),
+                                            producers=int(sc.get("producers", 0)),
+                                            task_size=int(sc.get("task_size", 8)),
+                                            status_every_s=float(sc.get("status_every_s", 5.0)))
+            self.steady.run(generations, threshold, wall_s=float(sc.get("wall_s", 0.0)))
+            return self.global_best()
         if self.pipeline:
             self.generation_base = start
             self._last_migration = start

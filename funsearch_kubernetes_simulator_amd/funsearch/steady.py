@@ -1,0 +1,368 @@
+"""Asynchronous steady-state island search: keep the MI355X full of programs.
+
+The reference evolves one population in lockstep generations of
+``min(8, population_size - elites)`` children (`funsearch/funsearch_integration.py:
+487-572`): every generation waits for its LLM calls, then for its slowest
+replay.  The generation-synchronous island modes here keep that contract
+(`islands.py`); this mode drops the lockstep to keep hundreds of programs in
+flight on one GPU:
+
+* **producers** -- a process pool (spawn: no HIP state) turns tasks (island,
+  current elites, n) into children: LLM (or offline mutation) call, template
+  fill, sandbox validation and bytecode compile, all off the main process;
+  parents are sampled from each island's population *at submission time*;
+* **dispatcher** -- the main thread packs ready children into batches of up to
+  ``batch`` programs and launches them on free HIP slots (up to ``slots``
+  batches in flight), JIT-compiling new shapes with the baseline tier
+  (`ops/gcnjit.py`, ~0.2 ms per program) right before the launch;
+* **merge** -- results land per batch and merge into their island one by one
+  with the reference's rules (dedup by difflib ratio against equal-or-better
+  members, keep the top ``population_size``): a steady-state GA instead of
+  generational replacement.  An island's *generation* is its merged-children
+  count divided by ``policies_per_generation``;
+* **migration without lockstep** -- when the slowest island passes a multiple
+  of ``migrate_every`` generations the rank *starts* an asynchronous
+  all-gather of its migrant blob (`dist.pack_migrants`: variable-length,
+  compressed, carrying each rank's best score -- so early stop needs no extra
+  all-reduce) and keeps evaluating; the incoming migrants merge when the
+  gather completes.  Ranks meet only inside collectives they have all posted,
+  never at a per-generation barrier;
+* **checkpoints** are written at migration points from the main thread, the
+  only thread that touches populations (a consistent cut).
+
+JSONL records: ``steady_batch`` (per batch: programs, new shapes, JIT and
+device seconds, programs in flight) and ``steady_status`` (every few seconds:
+evals/s, device busy fraction, new-shape fraction, best per island).
+"""
+
+from __future__ import annotations
+
+import concurrent.futures
+import multiprocessing
+import os
+import random
+import time
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+from ..parallel import dist
+from ..utils.trace import roctx_range
+from .search import FEEDBACK
+
+# ---------------------------------------------------------------------------- producer processes
+_W: dict = {}
+
+
+def _producer_init(llm_cfg: dict, timeout_s: int, seed: int) -> None:
+    from ..policy.sandbox import SafeExecutor
+    from .generator import LLMCodeGenerator
+    from .llm import make_client
+    cfg = dict(llm_cfg)
+    cfg["seed"] = int(cfg.get("seed", 0)) * 7919 + seed + os.getpid()
+    client = make_client(cfg)
+    _W["gen"] = LLMCodeGenerator(client, SafeExecutor(timeout_seconds=timeout_s), cfg.get("model"),
+                                 cfg.get("max_tokens", 400), cfg.get("temperature", 0.7))
+    _W["rng"] = random.Random(cfg["seed"])
+
+
+def _produce(task):
+    """(island, elites [(code, score)], n) -> [(island, code, CompiledPolicy | None)]."""
+    from ..policy.compiler import try_compile
+    island, elites, n = task
+    gen, rng = _W["gen"], _W["rng"]
+    out = []
+    for _ in range(n):
+        parents = rng.sample(elites, min(2, len(elites)))
+        code = gen.generate_policy(parent_policies=parents, performance_feedback=FEEDBACK)
+        if not code:             # LLM / validation failure: the child slot is spent
+            out.append((island, None, None))
+            continue
+        prog, _ = try_compile(code)
+        out.append((island, code, prog))
+    return out
+
+
+@dataclass
+class _Batch:
+    slot: int
+    items: list                    # [(island, code, prog)]
+    pend: object
+    t_launch: float
+    new_shapes: int = 0
+    jit_s: float = 0.0
+
+
+@dataclass
+class SteadyStats:
+    evaluations: int = 0
+    batches: int = 0
+    new_shapes: int = 0
+    native: int = 0
+    jit_s: float = 0.0
+    busy_s: float = 0.0
+    produced: int = 0
+    rejected: int = 0
+    migrations: int = 0
+    history: List[dict] = field(default_factory=list)
+
+
+class SteadyStateSearch:
+    """Steady-state driver over an `IslandFunSearch` (its islands, evaluator,
+    distributed context, log and checkpoint settings)."""
+
+    def __init__(self, fs, batch: int = 256, slots: Optional[int] = None, producers: int = 0,
+                 task_size: int = 8, status_every_s: float = 5.0):
+        self.fs = fs
+        self.batch = int(batch)
+        dev = getattr(fs.evaluator, "device", None)
+        n_slots = dev.n_slots if dev is not None else 1
+        self.slots = max(1, min(int(slots or n_slots), n_slots))
+        from ..ops.cpu_engine import default_threads
+        local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+        self.producers = int(producers or max(1, min(16, default_threads() // local - 1)))
+        self.task_size = int(task_size)
+        self.status_every_s = float(status_every_s)
+        self.stats = SteadyStats()
+
+    # -- helpers ------------------------------------------------------------------------
+    def _elites(self, s):
+        s.population.sort(key=lambda x: x[1], reverse=True)
+        return list(s.population[:s.elite_size])
+
+    def _merge_one(self, s, code: str, score: float) -> bool:
+        if s._is_too_similar(code, score):
+            return False
+        s.population.append((code, score))
+        if score > s.best_score:
+            s.best_score, s.best_policy = score, code
+        s.population.sort(key=lambda x: x[1], reverse=True)
+        del s.population[s.population_size:]
+        return True
+
+    def _blob(self, want_stop: bool) -> np.ndarray:
+        """Migration payload: [best score f64, stop vote f64] + migrant blob."""
+        hdr = np.array([self.fs.best[1], 1.0 if want_stop else 0.0], dtype=np.float64)
+        return np.concatenate([hdr.view(np.uint8), self.fs.migrant_blob()])
+
+    def _gen_of(self, merged: List[int]) -> List[int]:
+        return [m // max(1, s.policies_per_generation) for m, s in zip(merged, self.fs.islands)]
+
+    # -- main loop --------------------------------------------------------------------------
+    def run(self, generations: int, threshold: float, wall_s: float = 0.0) -> Tuple[Optional[str], float]:
+        fs = self.fs
+        islands = fs.islands
+        k = len(islands)
+        ev = fs.evaluator
+        log = fs.log
+        ctx = fs.ctx
+        start_gen = fs.generation
+        merged = [0] * k
+        target_children = [generations * max(1, s.policies_per_generation) for s in islands]
+        mig_every = fs.migrate_every
+        next_mig = start_gen + mig_every if mig_every else None
+        pending_gathers: List[Tuple[int, object]] = []   # (generation, PendingGather)
+        stop = False             # no more children: drain and finish
+        want_stop = False        # this rank's vote (threshold reached / wall time up)
+        stop_at: Optional[int] = None   # distributed stop: post migrations through this generation
+        global_best = fs.best[1]
+        s0 = islands[0]
+        llm_cfg = dict(fs.config.get("llm") or {})
+        if not llm_cfg:
+            llm_cfg = dict(fs.config.get("openrouter", {}))
+            llm_cfg.setdefault("backend", "openai")
+        timeout_s = int((fs.config.get("safe_execution") or {}).get("timeout_seconds", 3))
+        ctx_mp = multiprocessing.get_context("spawn")
+        pool = concurrent.futures.ProcessPoolExecutor(
+            max_workers=self.producers, mp_context=ctx_mp, initializer=_producer_init,
+            initargs=(llm_cfg, timeout_s, 1000 * ctx.rank + 1))
+        inflight_tasks: List[concurrent.futures.Future] = []
+        ready: List[tuple] = []          # produced children waiting for a batch
+        batches: List[Optional[_Batch]] = [None] * self.slots
+        # children requested per island: production stops at the island's target
+        requested = [0] * k
+        rr = 0
+        t_start = time.time()
+        t_status = t_start
+        busy_since = None
+        want_buffer = self.batch * (self.slots + 1)
+        try:
+            while True:
+                progressed = False
+                # 1) keep producers busy (children from the islands' CURRENT elites)
+                queued = len(ready) + sum(len(b.items) for b in batches if b is not None) + \
+                    self.task_size * len(inflight_tasks)
+                while (not stop and queued < want_buffer + self.task_size * self.producers
+                       and len(inflight_tasks) < 2 * self.producers):
+                    cands = [i for i in range(k) if requested[i] < target_children[i]]
+                    if not cands:
+                        break
+                    i = cands[rr % len(cands)]
+                    rr += 1
+                    elites = self._elites(islands[i])
+                    if not elites:
+                        requested[i] = target_children[i]
+                        continue
+                    n = min(self.task_size, target_children[i] - requested[i])
+                    requested[i] += n
+                    inflight_tasks.append(pool.submit(_produce, (i, elites, n)))
+                    queued += n
+                    progressed = True
+                # 2) collect produced children
+                still = []
+                for f in inflight_tasks:
+                    if f.done():
+                        for isl, code, prog in f.result():
+                            self.stats.produced += 1
+                            if prog is None:     # no program: counts toward the island's generation
+                                self.stats.rejected += 1
+                                if code is not None:
+                                    fs.evaluator.stats["compile_errors"] += 1
+                                merged[isl] += 1
+                                continue
+                            ready.append((isl, code, prog))
+                        progressed = True
+                    else:
+                        still.append(f)
+                inflight_tasks = still
+                # 3) launch full batches on free slots (a partial one when nothing else is coming)
+                for si in range(self.slots):
+                    if batches[si] is not None or not ready:
+                        continue
+                    tail = not inflight_tasks and all(requested[i] >= target_children[i] for i in range(k))
+                    if len(ready) < self.batch and not (tail or stop or all(b is None for b in batches)):
+                        continue
+                    take, ready = ready[:self.batch], ready[self.batch:]
+                    with roctx_range(f"steady.launch slot {si} ({len(take)} programs)"):
+                        pend = ev.submit_compiled([c for _, c, _ in take], [p for _, _, p in take], slot=si)
+                    b = _Batch(si, take, pend, time.time(), pend.new_shapes, pend.jit_s)
+                    batches[si] = b
+                    self.stats.jit_s += pend.jit_s
+                    self.stats.new_shapes += pend.new_shapes
+                    if busy_since is None:
+                        busy_since = time.time()
+                    progressed = True
+                # 4) finished batches -> merge
+                for si in range(self.slots):
+                    b = batches[si]
+                    if b is None or not ev.ready(b.pend):
+                        continue
+                    results = ev.collect(b.pend)
+                    t_done = time.time()
+                    batches[si] = None
+                    if busy_since is not None and all(x is None for x in batches):
+                        self.stats.busy_s += t_done - busy_since
+                        busy_since = None
+                    for (isl, code, _), res in zip(b.items, results):
+                        self._merge_one(islands[isl], code, res.score)
+                        merged[isl] += 1
+                        if res.engine == "hip-native":
+                            self.stats.native += 1
+                    self.stats.evaluations += len(b.items)
+                    self.stats.batches += 1
+                    fs.evaluations += len(b.items)
+                    inflight = sum(len(x.items) for x in batches if x is not None)
+                    log.write(kind="steady_batch", rank=ctx.rank, slot=si, programs=len(b.items),
+                              new_shapes=b.new_shapes, jit_s=round(b.jit_s, 4),
+                              device_s=round(t_done - b.t_launch, 4), inflight_after=inflight,
+                              queued=len(ready))
+                    progressed = True
+                gens = self._gen_of(merged)
+                g_min = start_gen + min(gens)
+                fs.generation = g_min
+                for s, g in zip(islands, gens):
+                    s.generation = start_gen + g
+                # 5) migration: post an async gather; absorb finished ones (in order)
+                if next_mig is not None:
+                    while (next_mig <= stop_at) if stop_at is not None else (g_min >= next_mig and not stop):
+                        with roctx_range(f"steady.migrate post gen {next_mig}"):
+                            try:
+                                pending_gathers.append((next_mig, dist.all_gather_array_async(self._blob(want_stop))))
+                            except Exception as exc:     # a dead peer: carry on alone (islands.elastic)
+                                fs.rank_lost("migrate", exc)
+                        next_mig += mig_every
+                        progressed = True
+                while pending_gathers:
+                    g, h = pending_gathers[0]
+                    # a rank never runs more than two migrations ahead of its slowest peer
+                    if not h.done() and len(pending_gathers) < 3 and stop_at is None:
+                        break
+                    try:
+                        glob = h.wait()
+                    except Exception as exc:
+                        pending_gathers.clear()
+                        fs.rank_lost("migrate", exc)
+                        break
+                    pending_gathers.pop(0)
+                    hdr = [np.frombuffer(glob[r, :16].tobytes(), np.float64) for r in range(glob.shape[0])]
+                    bests = [float(x[0]) for x in hdr]
+                    fs.absorb_migrants(glob[:, 16:])
+                    global_best = max([global_best] + bests)
+                    self.stats.migrations += 1
+                    log.write(kind="steady_migration", rank=ctx.rank, generation=g, best_global=global_best,
+                              bests=[round(x, 6) for x in bests], stop_votes=int(sum(x[1] > 0 for x in hdr)))
+                    if fs.ck_dir:
+                        fs.save_checkpoint()
+                    if stop_at is None and (global_best >= threshold or any(x[1] > 0 for x in hdr)):
+                        # every rank sees this same gather: all stop here and post the
+                        # gathers a peer may already have started (at most two ahead)
+                        stop = True
+                        stop_at = g + 2 * mig_every
+                    progressed = True
+                global_best = max(global_best, fs.best[1])
+                want_stop = want_stop or global_best >= threshold or bool(wall_s and time.time() - t_start > wall_s)
+                if want_stop and not (fs.ctx.distributed and next_mig is not None):
+                    stop = True        # alone (or no migrations): nobody to agree with
+                # 6) status
+                now = time.time()
+                if now - t_status >= self.status_every_s:
+                    t_status = now
+                    self._status(now, t_start, busy_since, batches, ready, inflight_tasks, merged, global_best)
+                # 7) done?
+                all_launched = all(requested[i] >= target_children[i] for i in range(k)) or stop
+                if (all_launched and not inflight_tasks and not ready and all(b is None for b in batches)
+                        and not pending_gathers):
+                    break
+                if stop and not inflight_tasks and all(b is None for b in batches):
+                    ready.clear()
+                    if not pending_gathers and (stop_at is None or next_mig > stop_at):
+                        break
+                if not progressed:
+                    time.sleep(0.0005)
+        finally:
+            pool.shutdown(wait=False, cancel_futures=True)
+        now = time.time()
+        rec = self._status(now, t_start, busy_since, batches, ready, inflight_tasks, merged, global_best, final=True)
+        if fs.ck_dir:
+            fs.save_checkpoint()
+        if fs.verbose and ctx.is_main:
+            import json
+            print(json.dumps(rec), flush=True)
+        return fs.best
+
+    def _status(self, now, t_start, busy_since, batches, ready, tasks, merged, best_global, final=False) -> dict:
+        st = self.stats
+        wall = max(1e-9, now - t_start)
+        busy = st.busy_s + (now - busy_since if busy_since is not None else 0.0)
+        fs = self.fs
+        rec = dict(kind="steady_final" if final else "steady_status", rank=fs.ctx.rank, wall_s=round(wall, 3),
+                   evaluations=st.evaluations, evals_per_s=round(st.evaluations / wall, 2),
+                   device_busy=round(busy / wall, 4),
+                   new_shape_fraction=round(st.new_shapes / max(1, st.evaluations), 4),
+                   native_fraction=round(st.native / max(1, st.evaluations), 4),
+                   inflight=sum(len(b.items) for b in batches if b is not None), queued=len(ready),
+                   producer_tasks=len(tasks), produced=st.produced, rejected=st.rejected, jit_s=round(st.jit_s, 3),
+                   generation=fs.generation, best=round(fs.best[1], 6), best_global=round(best_global, 6),
+                   islands=[round(s.best_score, 6) for s in fs.islands], migrations=st.migrations,
+                   engines={k: v for k, v in fs.evaluator.stats.items() if k in
+                            ("device_native", "device", "cpu_vm", "object", "compile_errors", "jit_shapes")})
+        fs.log.write(**rec)
+        st.history.append(rec)
+        if fs.verbose and fs.ctx.is_main and not final:
+            import json
+            print(json.dumps(rec), flush=True)
+        return rec
+
+
+__all__ = ["SteadyStateSearch", "SteadyStats"]

@@ -120,6 +120,9 @@ class PendingGather:
     def __init__(self, work=None, out=None, ready: Optional[np.ndarray] = None):
         self._work, self._out, self._ready = work, out, ready
 
+    def done(self) -> bool:
+        return self._ready is not None or self._work.is_completed()
+
     def wait(self) -> np.ndarray:
         if self._ready is None:
             self._work.wait()
@@ -194,7 +197,7 @@ def shutdown() -> None:
 
 
 # -------------------------------------------------------------------- program records
-RECORD_BYTES = 4096   # max packed program text per migrant (longer programs are not migrated)
+RECORD_BYTES = 4096   # fixed-width records (pack_programs): single programs, tests
 
 
 def pack_programs(codes, scores, width: int = RECORD_BYTES) -> np.ndarray:
@@ -219,3 +222,71 @@ def unpack_programs(rec: np.ndarray):
         score = float(np.frombuffer(row[:8].tobytes(), dtype=np.float64)[0])
         res.append((bytes(row[16:16 + n]).decode("utf-8"), score))
     return res
+
+
+# -------------------------------------------------------------------- migrant blobs
+#: bytes per rank in a migration all-gather.  A rank's migrants travel as one
+#: length-prefixed, zlib-compressed JSON blob; programs that follow the policy
+#: template ship only their LLM body (a 3 KB program is ~0.4 KB on the wire), so
+#: ~100+ migrants of any length fit.  One fixed size keeps the collective a
+#: single (async-capable) all-gather; the links are latency-bound at this size.
+MIGRANT_BLOB_BYTES = 1 << 18
+
+
+def _template_parts():
+    from ..policy.template import PolicyTemplate
+    marker = "\x00BODY\x00"
+    filled = PolicyTemplate.fill_template(marker)
+    pre, post = filled.split(marker)
+    return pre, post
+
+
+def program_body(code: str):
+    """(body, True) when `code` is the policy template around an LLM body,
+    else (code, False)."""
+    from ..policy.template import PolicyTemplate
+    pre, post = _template_parts()
+    if code.startswith(pre) and code.endswith(post) and len(code) >= len(pre) + len(post):
+        body = code[len(pre):len(code) - len(post)]
+        if PolicyTemplate.fill_template(body) == code:
+            return body, True
+    return code, False
+
+
+def pack_migrants(records, capacity: int = MIGRANT_BLOB_BYTES, log=None) -> np.ndarray:
+    """records: [(island, code, score)] best first -> uint8[capacity] blob.
+    If the compressed blob does not fit, the lowest-scoring records are left
+    out (each one logged through `log(dict)`) until it does."""
+    import json
+    import zlib
+    items = []
+    for isl, code, score in records:
+        body, templ = program_body(code)
+        items.append({"i": int(isl), "s": float(score), "t": int(templ), "c": body})
+    dropped = 0
+    while True:
+        raw = zlib.compress(json.dumps(items).encode("utf-8"), 6)
+        if len(raw) + 8 <= capacity or not items:
+            break
+        gone = items.pop()
+        dropped += 1
+        if log is not None:
+            log(dict(kind="migrant_dropped", island=gone["i"], score=gone["s"], bytes=len(gone["c"]),
+                     reason="migration blob full"))
+    out = np.zeros(capacity, dtype=np.uint8)
+    out[:8] = np.frombuffer(np.int64(len(raw)).tobytes(), dtype=np.uint8)
+    out[8:8 + len(raw)] = np.frombuffer(raw, dtype=np.uint8)
+    return out
+
+
+def unpack_migrants(blob: np.ndarray):
+    """[(island, code, score)] of one rank's blob."""
+    import json
+    import zlib
+    from ..policy.template import PolicyTemplate
+    b = np.ascontiguousarray(blob, dtype=np.uint8)
+    n = int(np.frombuffer(b[:8].tobytes(), dtype=np.int64)[0])
+    if n <= 0:
+        return []
+    items = json.loads(zlib.decompress(b[8:8 + n].tobytes()).decode("utf-8"))
+    return [(it["i"], PolicyTemplate.fill_template(it["c"]) if it["t"] else it["c"], it["s"]) for it in items]
