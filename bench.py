@@ -71,6 +71,9 @@ def main() -> None:
     ap.add_argument("--programs", type=int, default=64,
                     help="after the timed region: evaluate this many FunSearch candidate programs (offline-mutation "
                          "children) through the native program backend and report them as `program_path` (0: skip)")
+    ap.add_argument("--novel", type=int, default=256,
+                    help="after the timed region: this many programs, every one a NEW shape (JIT included), "
+                         "against the CPU VM on the same batch; reported as `program_path.novel` (0: skip)")
     ap.add_argument("--screen", type=int, default=1,
                     help="MFMA pre-filter: propose K x --candidates per island generation, screen them with "
                          "k_screen_linear (composite family), replay the best 1/K exactly (1: off)")
@@ -241,6 +244,13 @@ def main() -> None:
         program_path = measure_native(ev.device, mutation_children(args.programs, seed=args.seed + ctx.rank))
         program_path["vs_baseline"] = round(program_path["evals_per_s_incl_jit"] / BASELINE_EVALS_PER_S, 2)
         program_path["engine"] = "hip-native (JIT-compiled programs called from a precompiled replay kernel)"
+        program_path["note"] = ("top level: offline-mutation children, shapes may repeat within the batch; "
+                                "`novel`: every program a fresh shape (the real-LLM case)")
+        if args.novel > 0:
+            from funsearch_kubernetes_simulator_amd.bench.programs import measure_novel
+            nov = measure_novel(ev.device, workload, args.novel, seed=args.seed + 17 + 1000 * ctx.rank)
+            nov["vs_baseline"] = round(nov["evals_per_s_incl_jit"] / BASELINE_EVALS_PER_S, 2)
+            program_path["novel"] = nov
 
     per_step = args.islands * args.candidates
     total = per_step * args.steps * ctx.world_size

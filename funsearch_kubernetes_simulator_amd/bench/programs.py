@@ -67,3 +67,64 @@ def measure_native(dev, progs: List[CompiledPolicy]) -> dict:
             "jit_s": round(t1 - t0, 3), "device_s": round(t2 - t1, 3),
             "evals_per_s_incl_jit": round(n / (t2 - t0), 1), "evals_per_s_cached": round(n / (t3 - t2), 1),
             "events": int(tab[:, 8].sum()), "repeat_identical": bool((tab == tab2).all())}
+
+
+def novel_children(n: int, seed: int = 0) -> List[CompiledPolicy]:
+    """`n` mutation children with pairwise-distinct shapes (`shape_key`): every
+    one is a JIT compile, as with a real LLM, which almost never repeats a
+    program's structure."""
+    from ..policy.native_codegen import shape_key
+    out, keys = [], set()
+    s = seed
+    while len(out) < n:
+        for p in mutation_children(2 * (n - len(out)) + 8, seed=s):
+            k = shape_key(p)
+            if k not in keys:
+                keys.add(k)
+                out.append(p)
+                if len(out) == n:
+                    break
+        s += 7919
+    return out
+
+
+def measure_novel(dev, workload, n: int = 256, compile_batches: int = 4, seed: int = 0,
+                  cpu_threads: int = 0) -> dict:
+    """Novel-program throughput: `n` programs, every one a new shape, JIT
+    included, against the CPU VM on the same batch (bit-identical rows asserted
+    over programs neither engine defers).  Also the compile time of
+    `compile_batches` batches of 64 fresh shapes (median logged)."""
+    import numpy as np
+    from ..engine import COLS
+    from ..ops import cpu_engine as ce
+    progs = novel_children(n + 64 * compile_batches, seed)
+    main, extra = progs[:n], progs[n:]
+    t64 = []
+    for i in range(compile_batches):
+        b = dev.submit_native(0, extra[64 * i:64 * (i + 1)])
+        dev.wait(0)
+        t64.append(b.compile_s)
+    t0 = time.perf_counter()
+    batch = dev.submit_native(0, main)
+    t1 = time.perf_counter()
+    tab = dev.wait(0)
+    t2 = time.perf_counter()
+    threads = cpu_threads or ce.default_threads()
+    c0 = time.perf_counter()
+    vm = ce.simulate_program_batch(workload, main, threads=threads)
+    c1 = time.perf_counter()
+    skip = (100, 101)
+    exc, vexc = tab[:, COLS["exc"]].astype(int), vm[:, COLS["exc"]].astype(int)
+    cmp = ~np.isin(exc, skip) & ~np.isin(vexc, skip)
+    dev_rate, vm_rate = n / (t2 - t0), n / (c1 - c0)
+    st = dev.native_compiler.stats
+    return {"programs": n, "new_shapes": int(batch.compiled), "native": int(batch.ok.sum()),
+            "jit_tier": getattr(dev.native_compiler, "tier", "?"),
+            "jit_s": round(t1 - t0, 4), "device_s": round(t2 - t1, 4),
+            "evals_per_s_incl_jit": round(dev_rate, 1),
+            "cpu_vm_evals_per_s": round(vm_rate, 1), "cpu_vm_threads": threads,
+            "vs_cpu_vm": round(dev_rate / vm_rate, 2),
+            "compile_s_per_64_batch": [round(x, 4) for x in t64],
+            "compile_s_per_64_median": round(float(np.median(t64)), 4) if t64 else None,
+            "baseline_shapes": int(st.get("baseline_shapes", 0)), "llvm_shapes": int(st.get("llvm_shapes", 0)),
+            "compared": int(cmp.sum()), "bit_identical": bool((tab[cmp] == vm[cmp]).all())}

@@ -10,9 +10,13 @@ populations per process.  Each generation:
 3. each island merges its own children with the reference's rules
    (similarity filter, elites + children, truncate);
 4. every ``migrate_every`` generations the best ``migrants`` programs of every
-   island are all-gathered across ranks (fixed-size byte records over RCCL)
-   and injected into the next island of a global ring;
-5. global best / early stop via an all-reduce max.
+   island are all-gathered across ranks (`funsearch/migration.py`: one
+   compressed variable-length blob per rank over RCCL, posted asynchronously
+   in the pipelined and steady modes) and injected into the next island of a
+   global ring;
+5. global best / early stop: every migration payload carries the rank's best
+   score and stop vote, so ranks agree at migration points without a
+   per-generation all-reduce.
 
 With ``islands.per_rank = 1`` on one process this is exactly `SimpleFunSearch`.
 Checkpoints (``checkpoint.dir``) hold every island's population so a run can
@@ -70,8 +74,6 @@ class IslandFunSearch:
         # children sampled from the islands' current populations, no lockstep
         self.mode = str(isl.get("mode", "steady" if isl.get("steady") else ("pipeline" if self.pipeline else "sync")))
         self.steady_cfg = dict(isl.get("steady") or {})
-        self.generation_base = 0
-        self._last_migration = 0
         self.failures: List[dict] = []
         dev = (self.config.get("device") or {}).get("kind", "auto")
         if dev == "auto" and self.ctx.backend == "nccl":
@@ -123,6 +125,10 @@ class IslandFunSearch:
 
     # -- helpers --------------------------------------------------------------------------
     @property
+    def _threshold(self) -> float:
+        return self.islands[0].early_stop_threshold
+
+    @property
     def best(self) -> Tuple[Optional[str], float]:
         b = max(self.islands, key=lambda s: s.best_score)
         return b.best_policy, b.best_score
@@ -171,13 +177,23 @@ class IslandFunSearch:
         if self.coupler is not None and self.coupler.due(self.generation):
             for rec in self.run_coupling():
                 self.inject_coupled(rec)
-        if self.migrate_every and self.generation % self.migrate_every == 0:
-            with roctx_range(f"funsearch.migrate gen {self.generation}"):
-                self._collective("migrate", self.migrate, None)
         best_local = self.best[1]
-        best_global = self._collective("all_reduce_max", lambda: dist.all_reduce_max(best_local), best_local)
+        chan = self._sync_channel()
+        stop = best_local >= self._threshold and not chan.active
+        if self.migrate_every and self.generation % self.migrate_every == 0:
+            # lock-step mode: a blocking gather; its header carries every rank's
+            # best and stop vote (no per-generation all-reduce)
+            with roctx_range(f"funsearch.migrate gen {self.generation}"):
+                chan.post(self.generation, best_local >= self._threshold)
+                for res in chan.poll(self._threshold, block=True):
+                    for li, inc in res.incoming.items():
+                        self.apply_migrants(li, inc)
+                    stop = stop or chan.stopping
+            chan.stop_at = None    # lock-step: nobody posted ahead, the decision is `stop`
+        best_global = max(chan.best_global, best_local)
         rec = dict(kind="generation", rank=self.ctx.rank, generation=self.generation, best=best_local,
-                   best_global=best_global, children=len(children),
+                   best_global=best_global, stop=bool(stop), collective_wait_s=round(chan.wait_s, 4),
+                   children=len(children),
                    islands=[round(s.best_score, 6) for s in self.islands],
                    llm_s=round(t_gen - t0, 4), eval_s=round(t_eval - t_gen, 4),
                    evals_per_s=round(len(children) / max(1e-9, t_eval - t_gen), 2))
@@ -185,6 +201,12 @@ class IslandFunSearch:
         if self.ck_dir and self.ck_every and self.generation % self.ck_every == 0:
             self.save_checkpoint()
         return rec
+
+    def _sync_channel(self):
+        if getattr(self, "_chan", None) is None:
+            from .migration import MigrationChannel
+            self._chan = MigrationChannel(self, self.migrate_every, self.generation)
+        return self._chan
 
     def _collective(self, what: str, fn, fallback):
         """Run a collective; if a peer is gone, survive as a single-rank job."""
@@ -221,23 +243,29 @@ class IslandFunSearch:
         recs.sort(key=lambda r: r[2], reverse=True)
         return dist.pack_migrants(recs, log=lambda rec: self.log.write(rank=self.ctx.rank, **rec))
 
-    def absorb_migrants(self, glob) -> None:
-        """Ring migration: global island g receives island g - 1's migrants."""
+    def incoming_migrants(self, glob) -> dict:
+        """Ring migration: global island g receives island g - 1's migrants.
+        glob: [world, blob] -> {local island: [(code, score)]}."""
         W, I = glob.shape[0], len(self.islands)
         by_island = {}
         for r in range(W):
             for li, code, score in dist.unpack_migrants(glob[r]):
                 by_island.setdefault(r * I + li, []).append((code, score))
-        for li, s in enumerate(self.islands):
-            g = self.ctx.rank * I + li
-            incoming = by_island.get((g - 1) % (W * I), [])
-            known = {c for c, _ in s.population}
-            for code, score in incoming:
-                if code not in known:
-                    s.population.append((code, score))
-                    if score > s.best_score:
-                        s.best_score, s.best_policy = score, code
-            s.population = sorted(s.population, key=lambda x: x[1], reverse=True)[:s.population_size]
+        return {li: by_island.get((self.ctx.rank * I + li - 1) % (W * I), []) for li in range(I)}
+
+    def apply_migrants(self, li: int, incoming) -> None:
+        s = self.islands[li]
+        known = {c for c, _ in s.population}
+        for code, score in incoming:
+            if code not in known:
+                s.population.append((code, score))
+                if score > s.best_score:
+                    s.best_score, s.best_policy = score, code
+        s.population = sorted(s.population, key=lambda x: x[1], reverse=True)[:s.population_size]
+
+    def absorb_migrants(self, glob) -> None:
+        for li, inc in self.incoming_migrants(glob).items():
+            self.apply_migrants(li, inc)
 
     def migrate(self) -> None:
         """Ring migration of each island's best programs across all ranks."""
@@ -364,6 +392,11 @@ class IslandFunSearch:
         inflight = [False] * k
         global_rec = {}   # generation -> partial aggregate
         cpl = {"fut": None, "inbox": [], "last": self.generation}
+        from .migration import MigrationChannel
+        chan = MigrationChannel(self, self.migrate_every, self.generation)
+        self._chan = chan
+        inbox = [[] for _ in range(k)]     # migrants waiting for their island to be between generations
+        vote = [False]                     # this rank wants to stop (threshold reached)
 
         def set_busy():
             now = time.time()
@@ -389,13 +422,25 @@ class IslandFunSearch:
         with concurrent.futures.ThreadPoolExecutor(max_workers=workers) as pool:
             while True:
                 progressed = False
-                at_barrier = self.migrate_every and all(
-                    phase[i] == "idle" and gen[i] % self.migrate_every == 0 and gen[i] > self.generation_base
-                    for i in range(k)) and len(set(gen)) == 1 and gen[0] != self._last_migration
-                if at_barrier:
-                    with roctx_range(f"funsearch.migrate gen {gen[0]}"):
-                        self._collective("migrate", self.migrate, None)
-                    self._last_migration = gen[0]
+                if chan.every:
+                    # post a gather once the slowest island reaches a migration
+                    # generation; nobody waits for it (lookahead-bounded)
+                    with roctx_range("funsearch.migrate"):
+                        if chan.post_due(min(gen) if not stop[0] else -1, vote[0]):
+                            progressed = True
+                        for res in chan.poll(threshold):
+                            for li, inc in res.incoming.items():
+                                inbox[li].extend(inc)
+                            self.log.write(kind="migration", rank=self.ctx.rank, generation=res.generation,
+                                           bests=[round(x, 6) for x in res.bests], stop_votes=res.votes,
+                                           collective_wait_s=round(chan.wait_s, 4))
+                            progressed = True
+                    if chan.stopping:
+                        stop[0] = True
+                for i in range(k):
+                    if inbox[i] and phase[i] == "idle":     # between generations: elites not captured
+                        self.apply_migrants(i, inbox[i])
+                        inbox[i] = []
                 if self.coupler is not None:
                     # the family coupler runs on its own slot in a worker; its
                     # champions wait in an inbox until an island is idle
@@ -417,9 +462,6 @@ class IslandFunSearch:
                     if phase[i] == "idle":
                         if gen[i] >= target or stop[0]:
                             continue
-                        if (self.migrate_every and gen[i] % self.migrate_every == 0 and gen[i] > self.generation_base
-                                and gen[i] != self._last_migration):
-                            continue   # wait for the others at the migration point
                         s.generation += 1
                         plan[i] = self._plan(s)
                         stamp[i] = {"t0": time.time()}
@@ -468,7 +510,7 @@ class IslandFunSearch:
                         agg["t0"] = min(agg["t0"], st["t0"])
                         if agg["islands"] == k:
                             self._finish_generation(gen[i], global_rec.pop(gen[i]), busy_total, busy_since,
-                                                    t_start, threshold, stop)
+                                                    t_start, threshold, stop, chan, vote)
                         if self.polish_due(i):
                             # constant polish on the island's slot, in a worker: the
                             # other islands keep stepping; this island resumes after it
@@ -489,7 +531,19 @@ class IslandFunSearch:
                         progressed = True
                 if (all(phase[i] == "idle" and (gen[i] >= target or stop[0]) for i in range(k))
                         and cpl["fut"] is None and not cpl["inbox"]):
-                    break
+                    due = chan.every and chan.next is not None and (
+                        chan.next <= chan.stop_at if chan.stopping else (chan.next <= min(gen) and not stop[0]))
+                    if not due:
+                        if not chan.pending:
+                            for i in range(k):
+                                if inbox[i]:
+                                    self.apply_migrants(i, inbox[i])
+                                    inbox[i] = []
+                            break
+                        for res in chan.poll(threshold, block=True):
+                            for li, inc in res.incoming.items():
+                                inbox[li].extend(inc)
+                        continue
                 if not progressed:
                     time.sleep(0.0005)
 
@@ -498,17 +552,19 @@ class IslandFunSearch:
         return dev.n_slots if dev is not None else max(1, len(self.islands))
 
     def _finish_generation(self, g: int, agg: dict, busy_total, busy_since, t_start: float, threshold: float,
-                           stop) -> None:
+                           stop, chan, vote) -> None:
         self.generation = g
         best_local = self.best[1]
-        best_global = self._collective("all_reduce_max", lambda: dist.all_reduce_max(best_local), best_local)
+        # the global best is known from the last finished migration gather (no all-reduce here)
+        best_global = max(best_local, chan.best_global)
         now = time.time()
         busy = busy_total[0] + (now - busy_since[0] if busy_since[0] is not None else 0.0)
         wall = now - agg["t0"]
         rec = dict(kind="generation", rank=self.ctx.rank, generation=g, best=best_local, best_global=best_global,
                    children=agg["children"], islands=[round(s.best_score, 6) for s in self.islands],
                    llm_s=round(agg["llm_s"], 4), jit_s=round(agg["jit_s"], 4), eval_s=round(agg["eval_s"], 4),
-                   wall_s=round(wall, 4), pipelined=True,
+                   wall_s=round(wall, 4), pipelined=True, collective_wait_s=round(chan.wait_s, 4),
+                   collective_wait_frac=round(chan.wait_s / max(1e-9, now - t_start), 5),
                    device_busy=round(busy / max(1e-9, now - t_start), 4),
                    evals_per_s=round(self.evaluations / max(1e-9, now - t_start), 2),
                    engines={k: v for k, v in self.evaluator.stats.items() if k in
@@ -518,15 +574,17 @@ class IslandFunSearch:
             print(json.dumps(rec), flush=True)
         if self.ck_dir and self.ck_every and g % self.ck_every == 0:
             self.save_checkpoint()
-        if best_global >= threshold:
-            stop[0] = True
+        if best_local >= threshold:
+            vote[0] = True
+            if not chan.active:
+                stop[0] = True       # alone: nobody to agree with
 
     def run(self, generations: Optional[int] = None, resume: bool = False) -> Tuple[Optional[str], float]:
         if resume and self.ck_dir:
             self.load_elastic(self.ck_dir)
         self.initialize()
         generations = generations or self.islands[0].max_generations
-        threshold = self.islands[0].early_stop_threshold
+        threshold = self._threshold
         start = self.generation
         if self.mode == "steady":
             from .steady import SteadyStateSearch
@@ -538,15 +596,13 @@ class IslandFunSearch:
             self.steady.run(generations, threshold, wall_s=float(sc.get("wall_s", 0.0)))
             return self.global_best()
         if self.pipeline:
-            self.generation_base = start
-            self._last_migration = start
             self.run_pipelined(generations, threshold)
             return self.global_best()
         while self.generation - start < generations:
             rec = self.evolve()
             if self.verbose and self.ctx.is_main:
                 print(json.dumps(rec), flush=True)
-            if rec["best_global"] >= threshold:
+            if rec["stop"]:
                 break
         return self.global_best()
 

@@ -141,10 +141,19 @@ class SteadyStateSearch:
         del s.population[s.population_size:]
         return True
 
-    def _blob(self, want_stop: bool) -> np.ndarray:
-        """Migration payload: [best score f64, stop vote f64] + migrant blob."""
-        hdr = np.array([self.fs.best[1], 1.0 if want_stop else 0.0], dtype=np.float64)
-        return np.concatenate([hdr.view(np.uint8), self.fs.migrant_blob()])
+    def _absorb(self, results) -> bool:
+        """Merge finished migrations into the islands (main thread only)."""
+        fs = self.fs
+        for res in results:
+            for li, inc in res.incoming.items():
+                fs.apply_migrants(li, inc)
+            self.stats.migrations += 1
+            fs.log.write(kind="steady_migration", rank=fs.ctx.rank, generation=res.generation,
+                         best_global=self.channel.best_global, bests=[round(x, 6) for x in res.bests],
+                         stop_votes=res.votes, collective_wait_s=round(self.channel.wait_s, 4))
+            if fs.ck_dir:
+                fs.save_checkpoint()
+        return bool(results)
 
     def _gen_of(self, merged: List[int]) -> List[int]:
         return [m // max(1, s.policies_per_generation) for m, s in zip(merged, self.fs.islands)]
@@ -160,14 +169,12 @@ class SteadyStateSearch:
         start_gen = fs.generation
         merged = [0] * k
         target_children = [generations * max(1, s.policies_per_generation) for s in islands]
-        mig_every = fs.migrate_every
-        next_mig = start_gen + mig_every if mig_every else None
-        pending_gathers: List[Tuple[int, object]] = []   # (generation, PendingGather)
+        from .migration import MigrationChannel
+        chan = MigrationChannel(fs, fs.migrate_every, start_gen)
+        self.channel = chan
         stop = False             # no more children: drain and finish
         want_stop = False        # this rank's vote (threshold reached / wall time up)
-        stop_at: Optional[int] = None   # distributed stop: post migrations through this generation
         global_best = fs.best[1]
-        s0 = islands[0]
         llm_cfg = dict(fs.config.get("llm") or {})
         if not llm_cfg:
             llm_cfg = dict(fs.config.get("openrouter", {}))
@@ -273,61 +280,35 @@ class SteadyStateSearch:
                 fs.generation = g_min
                 for s, g in zip(islands, gens):
                     s.generation = start_gen + g
-                # 5) migration: post an async gather; absorb finished ones (in order)
-                if next_mig is not None:
-                    while (next_mig <= stop_at) if stop_at is not None else (g_min >= next_mig and not stop):
-                        with roctx_range(f"steady.migrate post gen {next_mig}"):
-                            try:
-                                pending_gathers.append((next_mig, dist.all_gather_array_async(self._blob(want_stop))))
-                            except Exception as exc:     # a dead peer: carry on alone (islands.elastic)
-                                fs.rank_lost("migrate", exc)
-                        next_mig += mig_every
+                # 5) migration: post async gathers; absorb finished ones (in order)
+                if chan.every:
+                    if chan.post_due(g_min if not stop else -1, want_stop):
                         progressed = True
-                while pending_gathers:
-                    g, h = pending_gathers[0]
-                    # a rank never runs more than two migrations ahead of its slowest peer
-                    if not h.done() and len(pending_gathers) < 3 and stop_at is None:
-                        break
-                    try:
-                        glob = h.wait()
-                    except Exception as exc:
-                        pending_gathers.clear()
-                        fs.rank_lost("migrate", exc)
-                        break
-                    pending_gathers.pop(0)
-                    hdr = [np.frombuffer(glob[r, :16].tobytes(), np.float64) for r in range(glob.shape[0])]
-                    bests = [float(x[0]) for x in hdr]
-                    fs.absorb_migrants(glob[:, 16:])
-                    global_best = max([global_best] + bests)
-                    self.stats.migrations += 1
-                    log.write(kind="steady_migration", rank=ctx.rank, generation=g, best_global=global_best,
-                              bests=[round(x, 6) for x in bests], stop_votes=int(sum(x[1] > 0 for x in hdr)))
-                    if fs.ck_dir:
-                        fs.save_checkpoint()
-                    if stop_at is None and (global_best >= threshold or any(x[1] > 0 for x in hdr)):
-                        # every rank sees this same gather: all stop here and post the
-                        # gathers a peer may already have started (at most two ahead)
+                    if self._absorb(chan.poll(threshold)):
+                        progressed = True
+                    if chan.stopping:
                         stop = True
-                        stop_at = g + 2 * mig_every
-                    progressed = True
-                global_best = max(global_best, fs.best[1])
+                global_best = max(chan.best_global, fs.best[1])
                 want_stop = want_stop or global_best >= threshold or bool(wall_s and time.time() - t_start > wall_s)
-                if want_stop and not (fs.ctx.distributed and next_mig is not None):
+                if want_stop and not chan.active:
                     stop = True        # alone (or no migrations): nobody to agree with
                 # 6) status
                 now = time.time()
                 if now - t_status >= self.status_every_s:
                     t_status = now
                     self._status(now, t_start, busy_since, batches, ready, inflight_tasks, merged, global_best)
-                # 7) done?
-                all_launched = all(requested[i] >= target_children[i] for i in range(k)) or stop
-                if (all_launched and not inflight_tasks and not ready and all(b is None for b in batches)
-                        and not pending_gathers):
-                    break
-                if stop and not inflight_tasks and all(b is None for b in batches):
+                # 7) done?  (every child merged, or stopping; then every agreed gather finished)
+                all_launched = all(requested[i] >= target_children[i] for i in range(k))
+                idle = not inflight_tasks and all(b is None for b in batches)
+                if idle and (stop or (all_launched and not ready)):
                     ready.clear()
-                    if not pending_gathers and (stop_at is None or next_mig > stop_at):
-                        break
+                    due = chan.every and chan.next is not None and (
+                        chan.next <= chan.stop_at if chan.stopping else (chan.next <= g_min and not stop))
+                    if not due:
+                        if not chan.pending:
+                            break
+                        self._absorb(chan.poll(threshold, block=True))
+                        continue
                 if not progressed:
                     time.sleep(0.0005)
         finally:
@@ -355,6 +336,8 @@ class SteadyStateSearch:
                    producer_tasks=len(tasks), produced=st.produced, rejected=st.rejected, jit_s=round(st.jit_s, 3),
                    generation=fs.generation, best=round(fs.best[1], 6), best_global=round(best_global, 6),
                    islands=[round(s.best_score, 6) for s in fs.islands], migrations=st.migrations,
+                   collective_wait_s=round(self.channel.wait_s, 4),
+                   collective_wait_frac=round(self.channel.wait_s / wall, 5),
                    engines={k: v for k, v in fs.evaluator.stats.items() if k in
                             ("device_native", "device", "cpu_vm", "object", "compile_errors", "jit_shapes")})
         fs.log.write(**rec)

@@ -29,9 +29,15 @@ stack frame would not fit the dynamic stack, is reported unsupported and
 evaluated by the VM / CPU engines instead.
 
 Compiles of independent module chunks run in parallel subprocesses (the
-clang processes release the GIL), and every compiled shape is cached for the
-life of the process, so re-evaluating a program -- or any program that differs
-from a compiled one only in its numeric constants -- costs no compile at all.
+clang processes release the GIL; at most 16 / ``LOCAL_WORLD_SIZE`` per rank),
+every compiled shape is cached for the life of the process, so re-evaluating a
+program -- or any program that differs from a compiled one only in its numeric
+constants -- costs no compile at all, and LLVM-tier code objects persist in an
+on-disk cache (``FKS_JIT_CACHE``, default ``~/.cache/fks_jit``; key: module
+source + flags + toolchain identity) shared by the ranks of a host and by
+``torchrun --max-restarts`` rounds.  In the ``auto`` tier a shape used in
+``FKS_JIT_TIERUP`` (default 4) batches is recompiled by LLVM in a background
+thread and swapped in when loaded (tier-up); no batch ever waits for it.
 """
 
 from __future__ import annotations
@@ -133,6 +139,7 @@ class CompiledModule:
     compile_s: float
     handle: object = None            # _fks_hip.JitModule once loaded
     pointers: Optional[np.ndarray] = None
+    cached: bool = False             # image came from the on-disk cache
 
 
 #: wall-clock limit of one toolchain process (a pathological program must not
@@ -149,10 +156,91 @@ def _run(cmd: List[str], what: str) -> None:
         raise JitError(f"{what} failed ({r.returncode}): {r.stderr[-4000:]}")
 
 
+def _cache_dir() -> Optional[str]:
+    """On-disk code-object cache shared by every rank and every restart on a
+    host (``FKS_JIT_CACHE``; ``off`` disables it)."""
+    d = os.environ.get("FKS_JIT_CACHE", "")
+    if d.lower() in ("off", "0", "none"):
+        return None
+    return d or os.path.join(os.environ.get("XDG_CACHE_HOME") or os.path.expanduser("~/.cache"), "fks_jit")
+
+
+_TOOL_ID: Optional[str] = None
+
+
+def _toolchain_id() -> str:
+    """Identity of the LLVM toolchain (its binaries' size + mtime): a ROCm
+    upgrade invalidates the cache."""
+    global _TOOL_ID
+    if _TOOL_ID is None:
+        parts = []
+        for t in (CLANG, LLC, LLVM_MC, LLD):
+            try:
+                st = os.stat(t)
+                parts.append(f"{os.path.basename(t)}:{st.st_size}:{int(st.st_mtime)}")
+            except OSError:
+                parts.append(f"{os.path.basename(t)}:missing")
+        _TOOL_ID = ";".join(parts)
+    return _TOOL_ID
+
+
+def _cache_key(src: str) -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for part in (src, " ".join(DEVICE_FLAGS), ARCH, _toolchain_id(), "v1"):
+        h.update(part.encode("utf-8"))
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def _cache_load(key: str, n: int) -> Optional[CompiledModule]:
+    d = _cache_dir()
+    if d is None:
+        return None
+    import json
+    try:
+        with open(os.path.join(d, key + ".json")) as f:
+            meta = json.load(f)
+        with open(os.path.join(d, key + ".co"), "rb") as f:
+            image = f.read()
+    except (OSError, ValueError):
+        return None
+    if meta.get("n") != n or len(image) != meta.get("bytes"):
+        return None
+    res = [Resources(**r) if r is not None else None for r in meta["resources"]]
+    return CompiledModule(image, n, res, 0.0, cached=True)
+
+
+def _cache_store(key: str, mod: CompiledModule) -> None:
+    """Atomic (tmp + rename): concurrent ranks writing the same key is harmless."""
+    d = _cache_dir()
+    if d is None:
+        return
+    import json
+    from dataclasses import asdict
+    try:
+        os.makedirs(d, exist_ok=True)
+        for ext, data, mode in ((".co", mod.image, "wb"),
+                                (".json", json.dumps({"n": mod.n, "bytes": len(mod.image), "resources": [
+                                    asdict(r) if r is not None else None for r in mod.resources]}), "w")):
+            tmp = os.path.join(d, f".{key}{ext}.{os.getpid()}.{threading.get_ident()}")
+            with open(tmp, mode) as f:
+                f.write(data)
+            os.replace(tmp, os.path.join(d, key + ext))   # the .json lands last: a reader sees both or neither
+    except OSError:
+        pass    # read-only home etc.: the cache is an optimisation
+
+
 def compile_device_module(progs: Sequence[CompiledPolicy], workdir: Optional[str] = None) -> CompiledModule:
-    """gfx950 code object holding ``fks_prog_<i>`` for every program."""
+    """gfx950 code object holding ``fks_prog_<i>`` for every program (from
+    the on-disk cache when this exact module was built before)."""
     t0 = time.perf_counter()
     src = module_source(progs, with_probes=False)
+    key = _cache_key(src)
+    hit = _cache_load(key, len(progs))
+    if hit is not None:
+        hit.compile_s = time.perf_counter() - t0
+        return hit
     with tempfile.TemporaryDirectory(prefix="fksjit_", dir=workdir) as d:
         cpp, ll, asm, obj, co = (os.path.join(d, n) for n in ("m.hip", "m.ll", "m.s", "m.o", "m.co"))
         with open(cpp, "w") as f:
@@ -173,8 +261,10 @@ def compile_device_module(progs: Sequence[CompiledPolicy], workdir: Optional[str
         with open(co, "rb") as f:
             image = f.read()
     res = function_resources(text)
-    return CompiledModule(image, len(progs), [res.get(f"fks_prog_{i}") for i in range(len(progs))],
-                          time.perf_counter() - t0)
+    mod = CompiledModule(image, len(progs), [res.get(f"fks_prog_{i}") for i in range(len(progs))],
+                         time.perf_counter() - t0)
+    _cache_store(key, mod)
+    return mod
 
 
 def compile_host_module(progs: Sequence[CompiledPolicy], path: str) -> str:
@@ -236,7 +326,17 @@ class NativeCompiler:
             from .gcnjit import BaselineJit
             self._baseline = BaselineJit(self._hip, self._rt, device)
         self.stats = {"modules": 0, "shapes": 0, "compile_s": 0.0, "rejected": 0, "hits": 0,
-                      "baseline_shapes": 0, "llvm_shapes": 0, "baseline_s": 0.0, "llvm_s": 0.0, "load_s": 0.0}
+                      "baseline_shapes": 0, "llvm_shapes": 0, "baseline_s": 0.0, "llvm_s": 0.0, "load_s": 0.0,
+                      "disk_hits": 0, "tierup_queued": 0, "tierup_done": 0, "tierup_s": 0.0}
+        # tier-up (auto tier): a baseline shape used in this many batches is
+        # recompiled by the LLVM tier in the background (its code runs ~1.3x
+        # faster on the device) and swapped in when ready; never on the
+        # critical path of a batch.  FKS_JIT_TIERUP=0 disables it.
+        self.tierup_after = int(os.environ.get("FKS_JIT_TIERUP", "4")) if self.tier == "auto" else 0
+        self._uses: Dict[str, int] = {}
+        self._tier_of: Dict[str, str] = {}
+        self._tierup_pool: Optional[ThreadPoolExecutor] = None
+        self._tierup_futs: List[object] = []
 
     def prepare(self, progs: Sequence[CompiledPolicy]) -> NativeBatch:
         """Compile every shape of `progs` not compiled yet (thread-safe: islands
@@ -285,8 +385,58 @@ class NativeCompiler:
                 else:
                     reasons[i] = self._bad.get(k, "not compiled")
             self.stats["hits"] += P - len(mine)
+            up = self._tierup_candidates(keys, progs) if self.tierup_after else []
+        for k, p in up:
+            self._tierup_futs.append(self._tierup_executor().submit(self._tierup, k, p))
         return NativeBatch(fn, np.concatenate(blocks) if blocks else np.zeros(1, np.int64), koff, ok, reasons, dt,
                            len(mine))
+
+    # -- background tier-up --------------------------------------------------------------
+    def _tierup_candidates(self, keys, progs):
+        """(key, program) of baseline shapes that just became hot (lock held)."""
+        out, seen = [], set()
+        for k, p in zip(keys, progs):
+            if k in seen or self._tier_of.get(k) != "baseline":
+                continue
+            seen.add(k)
+            n = self._uses.get(k, 0) + 1
+            self._uses[k] = n
+            if n == self.tierup_after:
+                self._tier_of[k] = "tierup"
+                self.stats["tierup_queued"] += 1
+                out.append((k, p))
+        return out
+
+    def _tierup_executor(self) -> ThreadPoolExecutor:
+        if self._tierup_pool is None:
+            self._tierup_pool = ThreadPoolExecutor(max_workers=max(1, self.workers // 4),
+                                                   thread_name_prefix="fks-tierup")
+        return self._tierup_pool
+
+    def _tierup(self, k: str, p: CompiledPolicy) -> bool:
+        mod = self._compile_one([(k, p)])
+        if isinstance(mod, Exception):
+            return False
+        res = mod.resources[0]
+        if res is None or res.fits(self.vgpr_cap, self.sgpr_cap):
+            return False    # the baseline code stays
+        mod.handle = self._hip.JitModule(mod.image, self._rt, mod.n, self.device)
+        mod.pointers = np.asarray(mod.handle.pointers(), dtype=np.uint64)
+        with self._lock:
+            mi = len(self._modules)
+            self._modules.append(mod)      # the baseline module stays loaded: batches in flight call it
+            self.stats["modules"] += 1
+            self._shapes[k] = (mi, 0)
+            self._tier_of[k] = "llvm"
+            self.stats["tierup_done"] += 1
+            self.stats["tierup_s"] += mod.compile_s
+            self.stats["disk_hits"] += int(mod.cached)
+        return True
+
+    def drain_tierup(self) -> None:
+        """Wait for every queued background recompile (tests, benchmarks)."""
+        while self._tierup_futs:
+            self._tierup_futs.pop(0).result()
 
     def _compile_one(self, chunk):
         """CompiledModule, or the toolchain error (never raises: one bad
@@ -323,6 +473,7 @@ class NativeCompiler:
                 self.stats["load_s"] += t2 - t1
                 for j, k in enumerate(keys):
                     self._shapes[k] = (mi, j)
+                    self._tier_of[k] = "baseline"
                     self.stats["shapes"] += 1
                     self.stats["baseline_shapes"] += 1
         return declined
@@ -389,6 +540,7 @@ class NativeCompiler:
                 self.stats["compile_s"] += mod.compile_s
                 self.stats["llvm_s"] += mod.compile_s
                 self.stats["llvm_shapes"] += len(ch)
+                self.stats["disk_hits"] += int(mod.cached)
                 mi = len(self._modules)
                 self._modules.append(mod)
                 self.stats["modules"] += 1
@@ -400,15 +552,19 @@ class NativeCompiler:
                         self.stats["rejected"] += 1
                     else:
                         self._shapes[k] = (mi, j)
+                        self._tier_of[k] = "llvm"
                         self.stats["shapes"] += 1
 
 
 def _default_workers() -> int:
+    """Toolchain processes per rank: the host's cores shared by the ranks on
+    it (``LOCAL_WORLD_SIZE``), at most 16."""
     env = os.environ.get("FKS_JIT_WORKERS", "")
     if env.isdigit() and int(env) > 0:
         return int(env)
     from .cpu_engine import default_threads
-    return max(1, min(16, default_threads()))
+    local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1))
+    return max(1, min(16, default_threads() // local))
 
 
 __all__ = ["CompiledModule", "JitError", "NativeBatch", "NativeCompiler", "Resources", "compile_device_module",

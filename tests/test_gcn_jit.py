@@ -209,3 +209,20 @@ def test_skeleton_layout_and_relocations():
     # the two literal slots follow s_add_u32 / s_addc_u32 words of the runtime-table address
     assert code.words[lo - 1] >> 23 == 0x100 and code.words[hi - 1] >> 23 == 0x104
     assert pc % 4 == 0 and pc < code.words.size * 4
+
+
+def test_llvm_tier_disk_cache(tmp_path, monkeypatch):
+    """LLVM-tier code objects persist on disk (shared by ranks / restarts):
+    the second build of the same module is a cache hit with the same image."""
+    from funsearch_kubernetes_simulator_amd.ops import jit
+    if not os.path.exists(jit.CLANG):
+        pytest.skip("ROCm clang not installed")
+    monkeypatch.setenv("FKS_JIT_CACHE", str(tmp_path / "cache"))
+    p = compile_policy("def priority_function(pod, node):\n    return node.cpu_milli_left - pod.cpu_milli // 3\n")
+    a = jit.compile_device_module([p])
+    b = jit.compile_device_module([p])
+    assert not a.cached and b.cached and a.image == b.image and a.resources == b.resources
+    assert b.compile_s < a.compile_s
+    assert len(list((tmp_path / "cache").glob("*.co"))) == 1
+    monkeypatch.setenv("FKS_JIT_CACHE", "off")
+    assert not jit.compile_device_module([p]).cached
