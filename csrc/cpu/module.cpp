@@ -168,7 +168,14 @@ static pybind11::object vm_score_once(const Program& prog, const pybind11::dict&
 
 }  // namespace fks
 
+#ifndef FKS_SOURCE_HASH
+#define FKS_SOURCE_HASH ""
+#endif
+// provenance marker, found by ops/build.py without importing the module
+extern "C" __attribute__((used, visibility("default"))) const char fks_source_mark[] = "FKS_SOURCE_HASH=" FKS_SOURCE_HASH;
+
 PYBIND11_MODULE(_fks_cpu, m) {
+  m.attr("SOURCE_HASH") = FKS_SOURCE_HASH;
   m.def("load_pod_csv", [](const std::string& path) {
     fks::PodColumns p;
     try {

@@ -61,6 +61,9 @@ struct DevBuf {
   size_t cap = 0;
   void reserve(size_t bytes) {
     if (bytes <= cap) return;
+    // geometric growth: hipFree waits for the whole device (every slot), so
+    // regrowing per batch would serialise the slots' streams
+    bytes = std::max(bytes, cap + cap / 2);
     if (p) HIP_OK(hipFree(p));
     HIP_OK(hipMalloc(&p, bytes));
     cap = bytes;

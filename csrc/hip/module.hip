@@ -12,7 +12,11 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -293,9 +297,44 @@ py::array_t<float> mfma_probe(int device) {
   return out;
 }
 
+// Loader state shared by every JIT module of a device: a private
+// non-blocking stream and persistent buffers.  Loading a module must never
+// synchronise with the replay slots' streams: no hipFree (which waits for the
+// whole device), no legacy-null-stream copies or launches -- the steady-state
+// search loads a module per batch while other batches replay.
+struct JitLoader {
+  std::mutex mu;
+  hipStream_t stream = nullptr;
+  uint64_t* dptrs = nullptr;     // program addresses written by fks_jit_table
+  uint64_t* hptrs = nullptr;     // pinned mirror
+  size_t cap = 0;
+  void reserve(size_t n) {
+    if (n <= cap) return;
+    const size_t want = std::max<size_t>(n, std::max<size_t>(4096, 2 * cap));
+    // the old buffers are kept (a hipFree would synchronise the device)
+    HIP_OK(hipMalloc(&dptrs, want * 8));
+    HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&hptrs), want * 8, hipHostMallocDefault));
+    cap = want;
+  }
+};
+
+JitLoader& jit_loader(int device) {
+  static std::mutex mu;
+  static std::map<int, std::unique_ptr<JitLoader>> loaders;
+  std::lock_guard<std::mutex> g(mu);
+  auto& p = loaders[device];
+  if (!p) {
+    p.reset(new JitLoader());
+    HIP_OK(hipSetDevice(device));
+    HIP_OK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+  }
+  return *p;
+}
+
 // A loaded JIT code object of natively compiled programs (ops/jit.py).
 // Load: hipModuleLoadData; the module's `fks_rt_table` global receives the
-// runtime-library addresses; `fks_jit_table` reports the program addresses.
+// runtime-library addresses; `fks_jit_table` reports the program addresses
+// (both on the loader's private stream).
 class JitModule {
  public:
   JitModule(py::bytes image, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> rt, int n_programs,
@@ -303,22 +342,26 @@ class JitModule {
       : device_(device), n_(n_programs) {
     if (n_programs < 1) throw std::invalid_argument("empty JIT module");
     const std::string img = image;
+    std::vector<uint64_t> rtv(rt.data(), rt.data() + rt.size());
+    py::gil_scoped_release rel;    // other islands / the tier-up thread keep running
+    JitLoader& L = jit_loader(device_);
+    std::lock_guard<std::mutex> g(L.mu);
     HIP_OK(hipSetDevice(device_));
     HIP_OK(hipModuleLoadData(&mod_, img.data()));
-    hipDeviceptr_t g = nullptr;
+    hipDeviceptr_t gp = nullptr;
     size_t gbytes = 0;
-    HIP_OK(hipModuleGetGlobal(&g, &gbytes, mod_, "fks_rt_table"));
-    if (gbytes < (size_t)rt.size() * 8) throw std::runtime_error("fks_rt_table too small");
-    HIP_OK(hipMemcpyHtoD(g, const_cast<uint64_t*>(rt.data()), (size_t)rt.size() * 8));
+    HIP_OK(hipModuleGetGlobal(&gp, &gbytes, mod_, "fks_rt_table"));
+    if (gbytes < rtv.size() * 8) throw std::runtime_error("fks_rt_table too small");
+    HIP_OK(hipMemcpyHtoDAsync(gp, rtv.data(), rtv.size() * 8, L.stream));
     hipFunction_t f;
     HIP_OK(hipModuleGetFunction(&f, mod_, "fks_jit_table"));
-    uint64_t* d = nullptr;
-    HIP_OK(hipMalloc(&d, (size_t)n_ * 8));
+    L.reserve((size_t)n_);
+    uint64_t* d = L.dptrs;
     void* args[] = {&d};
-    HIP_OK(hipModuleLaunchKernel(f, 1, 1, 1, 1, 1, 1, 0, nullptr, args, nullptr));
-    ptrs_.resize(n_);
-    HIP_OK(hipMemcpy(ptrs_.data(), d, (size_t)n_ * 8, hipMemcpyDeviceToHost));
-    (void)hipFree(d);
+    HIP_OK(hipModuleLaunchKernel(f, 1, 1, 1, 1, 1, 1, 0, L.stream, args, nullptr));
+    HIP_OK(hipMemcpyAsync(L.hptrs, L.dptrs, (size_t)n_ * 8, hipMemcpyDeviceToHost, L.stream));
+    HIP_OK(hipStreamSynchronize(L.stream));
+    ptrs_.assign(L.hptrs, L.hptrs + n_);
     for (uint64_t p : ptrs_)
       if (p == 0) throw std::runtime_error("JIT module reported a null program address");
   }
@@ -349,7 +392,14 @@ int device_count() {
 
 }  // namespace
 
+#ifndef FKS_SOURCE_HASH
+#define FKS_SOURCE_HASH ""
+#endif
+// provenance marker, found by ops/build.py without importing the module
+extern "C" __attribute__((used, visibility("default"))) const char fks_source_mark[] = "FKS_SOURCE_HASH=" FKS_SOURCE_HASH;
+
 PYBIND11_MODULE(_fks_hip, m) {
+  m.attr("SOURCE_HASH") = FKS_SOURCE_HASH;
   m.doc() = "MI355X replay kernels of funsearch_kubernetes_simulator_amd";
   m.def("device_count", &device_count);
   m.def("test_wave_ops", &test_wave_ops);

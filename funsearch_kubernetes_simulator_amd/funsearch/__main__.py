@@ -27,6 +27,8 @@ def main() -> None:
     ap.add_argument("--save", help="write the top-5 JSON (reference schema) here")
     ap.add_argument("--device-min-batch", type=int,
                     help="smallest program batch sent to the device VM (smaller ones run on the CPU VM)")
+    ap.add_argument("--wall-s", type=float, help="steady mode: stop after this many seconds (ranks agree)")
+    ap.add_argument("--mode", choices=["sync", "pipeline", "steady"], help="island loop (overrides islands.mode)")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args()
     cfg = load_config(a.config)
@@ -39,6 +41,11 @@ def main() -> None:
         cfg["funsearch"]["policies_per_generation"] = a.policies_per_generation
     if a.device:
         cfg.setdefault("device", {})["kind"] = a.device
+    if a.mode:
+        isl["mode"] = a.mode
+        isl["pipeline"] = a.mode == "pipeline"
+    if a.wall_s is not None:
+        isl.setdefault("steady", {})["wall_s"] = a.wall_s
     if a.device_min_batch is not None:
         cfg.setdefault("device", {})["min_batch"] = a.device_min_batch
     if a.checkpoint_dir:

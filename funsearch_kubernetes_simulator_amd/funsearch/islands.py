@@ -398,6 +398,15 @@ class IslandFunSearch:
         inbox = [[] for _ in range(k)]     # migrants waiting for their island to be between generations
         vote = [False]                     # this rank wants to stop (threshold reached)
 
+        def landed(results) -> bool:
+            for res in results:
+                for li, inc in res.incoming.items():
+                    inbox[li].extend(inc)
+                self.log.write(kind="migration", rank=self.ctx.rank, generation=res.generation,
+                               bests=[round(x, 6) for x in res.bests], stop_votes=res.votes,
+                               collective_wait_s=round(chan.wait_s, 4))
+            return bool(results)
+
         def set_busy():
             now = time.time()
             any_on = any(inflight)
@@ -428,12 +437,7 @@ class IslandFunSearch:
                     with roctx_range("funsearch.migrate"):
                         if chan.post_due(min(gen) if not stop[0] else -1, vote[0]):
                             progressed = True
-                        for res in chan.poll(threshold):
-                            for li, inc in res.incoming.items():
-                                inbox[li].extend(inc)
-                            self.log.write(kind="migration", rank=self.ctx.rank, generation=res.generation,
-                                           bests=[round(x, 6) for x in res.bests], stop_votes=res.votes,
-                                           collective_wait_s=round(chan.wait_s, 4))
+                        if landed(chan.poll(threshold)):
                             progressed = True
                     if chan.stopping:
                         stop[0] = True
@@ -540,9 +544,7 @@ class IslandFunSearch:
                                     self.apply_migrants(i, inbox[i])
                                     inbox[i] = []
                             break
-                        for res in chan.poll(threshold, block=True):
-                            for li, inc in res.incoming.items():
-                                inbox[li].extend(inc)
+                        landed(chan.poll(threshold, block=True))
                         continue
                 if not progressed:
                     time.sleep(0.0005)

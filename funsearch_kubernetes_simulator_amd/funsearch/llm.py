@@ -22,6 +22,7 @@ unchanged with any of them:
 from __future__ import annotations
 
 import ast
+import functools
 import json
 import os
 import random
@@ -162,6 +163,7 @@ TERM_LIBRARY = [
 ]
 
 
+@functools.lru_cache(maxsize=4096)   # parents repeat across thousands of children
 def _extract_body(program: str) -> Optional[str]:
     """The logic between ``score = 0.0`` and the final return of a
     template-shaped program, dedented to 4 spaces; else the whole function

@@ -72,6 +72,7 @@ def _produce(task):
     from ..policy.compiler import try_compile
     island, elites, n = task
     gen, rng = _W["gen"], _W["rng"]
+    t0 = time.process_time()
     out = []
     for _ in range(n):
         parents = rng.sample(elites, min(2, len(elites)))
@@ -81,7 +82,7 @@ def _produce(task):
             continue
         prog, _ = try_compile(code)
         out.append((island, code, prog))
-    return out
+    return out, time.process_time() - t0
 
 
 @dataclass
@@ -105,6 +106,7 @@ class SteadyStats:
     produced: int = 0
     rejected: int = 0
     migrations: int = 0
+    producer_cpu_s: float = 0.0
     history: List[dict] = field(default_factory=list)
 
 
@@ -191,6 +193,7 @@ class SteadyStateSearch:
         requested = [0] * k
         rr = 0
         t_start = time.time()
+        self._cpu0 = time.process_time()
         t_status = t_start
         busy_since = None
         want_buffer = self.batch * (self.slots + 1)
@@ -220,7 +223,9 @@ class SteadyStateSearch:
                 still = []
                 for f in inflight_tasks:
                     if f.done():
-                        for isl, code, prog in f.result():
+                        items, cpu_s = f.result()
+                        self.stats.producer_cpu_s += cpu_s
+                        for isl, code, prog in items:
                             self.stats.produced += 1
                             if prog is None:     # no program: counts toward the island's generation
                                 self.stats.rejected += 1
@@ -333,7 +338,9 @@ class SteadyStateSearch:
                    new_shape_fraction=round(st.new_shapes / max(1, st.evaluations), 4),
                    native_fraction=round(st.native / max(1, st.evaluations), 4),
                    inflight=sum(len(b.items) for b in batches if b is not None), queued=len(ready),
-                   producer_tasks=len(tasks), produced=st.produced, rejected=st.rejected, jit_s=round(st.jit_s, 3),
+                   producer_tasks=len(tasks), produced=st.produced,
+                   producer_ms_per_child=round(1e3 * st.producer_cpu_s / max(1, st.produced), 3),
+                   main_cpu_frac=round((time.process_time() - self._cpu0) / wall, 3), rejected=st.rejected, jit_s=round(st.jit_s, 3),
                    generation=fs.generation, best=round(fs.best[1], 6), best_global=round(best_global, 6),
                    islands=[round(s.best_score, 6) for s in fs.islands], migrations=st.migrations,
                    collective_wait_s=round(self.channel.wait_s, 4),

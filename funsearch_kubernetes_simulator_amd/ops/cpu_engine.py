@@ -47,6 +47,8 @@ def native():
             from .build import build_cpu
             build_cpu()
         from . import _fks_cpu  # noqa: F401  (in-tree extension)
+        from .build import verify
+        verify(_fks_cpu, "cpu")    # refuses a binary built from other sources
         _mod = _fks_cpu
     return _mod
 

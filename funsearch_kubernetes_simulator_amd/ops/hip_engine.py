@@ -46,6 +46,8 @@ def native():
             from .build import build_hip
             build_hip()
         from . import _fks_hip  # noqa: F401
+        from .build import verify
+        verify(_fks_hip, "hip")    # refuses a binary built from other sources
         _mod = _fks_hip
     return _mod
 

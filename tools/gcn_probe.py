@@ -123,6 +123,29 @@ def main():
         t1 = time.perf_counter()
         say(stage="bench", tier="cpu_vm", P=n, evals_per_s=round(n / (t1 - t0), 1),
             bad_baseline=compare(tabs["baseline"], vm)[:10], bad_llvm=compare(tabs["llvm"], vm)[:10])
+    elif stage == "overlap":
+        # a JIT compile + module load must not wait for batches replaying on other slots
+        from funsearch_kubernetes_simulator_amd.bench.programs import novel_children
+        w, dev = evaluator(os.environ.get("FKS_JIT_TIER", "auto"))
+        progs = novel_children(256 + 3 * 64, 41)
+        dev.submit_native(0, progs[:1])
+        dev.wait(0)
+        t0 = time.perf_counter()
+        dev.submit_native(0, progs[:256])
+        t1 = time.perf_counter()
+        loads = []
+        for i in range(3):
+            s0 = time.perf_counter()
+            nb = dev.native_compiler.prepare(progs[256 + 64 * i:256 + 64 * (i + 1)])
+            loads.append((round(time.perf_counter() - s0, 4), int(nb.compiled), bool(dev.ready(0))))
+        dev.submit_native(1, progs[256:320])
+        t2 = time.perf_counter()
+        busy = not dev.ready(0)
+        dev.wait(0)
+        t3 = time.perf_counter()
+        dev.wait(1)
+        say(stage="overlap", submit0_s=round(t1 - t0, 4), loads_s_shapes_ready0=loads, submit1_s=round(t2 - t1, 4),
+            slot0_still_busy_after=busy, slot0_total_s=round(t3 - t0, 4))
     else:
         raise SystemExit(f"unknown stage {stage}")
 
