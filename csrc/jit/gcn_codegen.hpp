@@ -106,7 +106,7 @@ class Codegen {
   std::array<int, kMaxRegs> tagbit_{};    // tag bit index (-1: untagged)
   uint64_t tagged_ = 0;
   bool use_node_ = false, use_gl_ = false, use_gmem_ = false, use_kc_ = false, has_loop_ = false;
-  std::array<int, 6> pod_s_{};            // SGPR pair per pod field (-1 unused)
+  std::array<int, 6> pod_s_{};            // argument VGPR of each pod field the program reads (-1 unused)
   int v_exc_ = -1, v_bud_ = -1, v_out_ = -1, v_spill_ = -1;
   int v_tag_[2] = {-1, -1};
   int T_[3] = {-1, -1, -1};               // temp VGPR pairs
@@ -361,17 +361,34 @@ class Codegen {
           if (live_out_[pc] >> q & 1 && q != r) adj[q] |= d;
       }
     }
-    // VGPR pools (caller-saved only; v0-v22 and v29 are the node arguments / kc)
-    std::vector<int> pairs = {24, 26, 30, 32, 34, 36, 38, 48, 50, 52, 54, 64, 66, 68, 70,
-                              80, 82, 84, 86, 96, 98, 100, 102, 112, 114, 116, 118};
-    std::vector<int> singles = {28};
+    // VGPR pools (caller-saved only; v0-v22 and v29 are the node arguments / kc).
+    // The pod arguments (v23-v28) a program reads stay in place for its whole
+    // run: they are per-lane, not wave-uniform -- in the four-programs-per-wave
+    // row kernel one call can cover several DPP rows (programs of one shape),
+    // each with its own pod.
+    const bool pv23 = pod_s_[0] > 0, pv24 = pod_s_[1] > 0, pv25 = pod_s_[2] > 0 || pod_s_[3] > 0;
+    const bool pv26 = pod_s_[4] > 0, pv28 = pod_s_[5] > 0;
+    std::vector<int> pairs;
+    if (!pv24 && !pv25) pairs.push_back(24);
+    if (!pv26) pairs.push_back(26);
+    for (int b : {30, 32, 34, 36, 38, 48, 50, 52, 54, 64, 66, 68, 70, 80, 82, 84, 86, 96, 98, 100, 102, 112, 114, 116,
+                  118})
+      pairs.push_back(b);
+    std::vector<int> singles;
+    if (!pv28) singles.push_back(28);
+    if (pv24 && !pv25) singles.push_back(25);
+    if (pv25 && !pv24) singles.push_back(24);
     if (!use_gl_) {
       for (int b = 6; b <= 18; b += 2) pairs.push_back(b);
       singles.push_back(5);
       singles.push_back(20);
     }
-    if (!use_gmem_) pairs.push_back(22);
-    else singles.push_back(23);
+    if (!use_gmem_) {
+      if (!pv23) pairs.push_back(22);
+      else singles.push_back(22);
+    } else if (!pv23) {
+      singles.push_back(23);
+    }
     if (!use_node_ && !use_gl_ && !use_gmem_) {
       // node fields unused: v0-v4 are free too (v0-v1 also carry the result)
       pairs.push_back(2);
@@ -444,9 +461,8 @@ class Codegen {
     bm_pair_[0] = take_spair();
     bm_pair_[1] = take_spair();
     bm_of_.fill(-1);
-    for (int f = 0; f < 6; ++f)
-      if (pod_s_[f] > 0) pod_s_[f] = take_spair();
-      else pod_s_[f] = -1;
+    static const int pod_arg[6] = {23, 24, 25, 25, 26, 28};
+    for (int f = 0; f < 6; ++f) pod_s_[f] = pod_s_[f] > 0 ? pod_arg[f] : -1;   // now: the argument VGPR
   }
   int take_spair() {
     if (free_spairs_.empty()) throw CodegenError("out of SGPR pairs");
@@ -644,8 +660,6 @@ class Codegen {
   // SGPR pairs live across a runtime call
   std::vector<int> live_sgprs() const {
     std::vector<int> out = {30, 31, s_entry_, s_entry_ + 1, s_dead_, s_dead_ + 1};
-    for (int f = 0; f < 6; ++f)
-      if (pod_s_[f] >= 0) { out.push_back(pod_s_[f]); out.push_back(pod_s_[f] + 1); }
     for (const Frame& fr : frames_)
       for (int b : {fr.s_save, fr.s_else, fr.s_entry, fr.s_brk, fr.s_cont})
         if (b >= 0) { out.push_back(b); out.push_back(b + 1); }
@@ -658,6 +672,11 @@ class Codegen {
     if (use_gl_)
       for (int g = 5; g <= 20; ++g) out.push_back(g);
     if (use_gmem_) { out.push_back(21); out.push_back(22); }
+    for (int f = 0; f < 6; ++f)   // pod arguments the program still reads
+      if (pod_s_[f] >= 0) {
+        out.push_back(pod_s_[f]);
+        if (f == 4) out.push_back(pod_s_[f] + 1);
+      }
     out.push_back(29);
     out.push_back(v_exc_);
     out.push_back(v_out_);
@@ -755,18 +774,6 @@ class Codegen {
     e(mkimm(S_WAITCNT, 0));
     e(mk(S_MOV_B64, s(s_entry_), EXEC));
     e(mk(S_MOV_B64, s(s_dead_), ic(0)));
-    static const int pod_arg[6] = {23, 24, 25, 25, 26, 28};
-    for (int f = 0; f < 6; ++f) {
-      const int sp = pod_s_[f];
-      if (sp < 0) continue;
-      e(mk(V_READFIRSTLANE_B32, s(sp), v(pod_arg[f])));
-      switch (f) {
-        case 0: case 1: case 5: e(mk(S_ASHR_I32, s(sp + 1), s(sp), ic(31))); break;
-        case 2: e(mk(S_LSHR_B32, s(sp), s(sp), ic(16))); e(mk(S_MOV_B32, s(sp + 1), ic(0))); break;
-        case 3: e(mklit(S_AND_B32, s(sp), 0xFFFFu, s(sp))); e(mk(S_MOV_B32, s(sp + 1), ic(0))); break;
-        case 4: e(mk(V_READFIRSTLANE_B32, s(sp + 1), v(27))); break;
-      }
-    }
     e(mk(V_MOV_B32, v(v_exc_), ic(0)));
     e(mk(V_MOV_B64, v(v_out_), ic(0)));
     for (int t : v_tag_)
@@ -861,9 +868,26 @@ class Codegen {
         copy_tag(d, a, ta);
         bm_of_[d] = bm_of_[a];
         break;
-      case OP_POD: {
+      case OP_POD: {   // from the (per-lane) argument VGPRs, kept intact
         const int f = (in.imm >= 0 && in.imm <= 5) ? in.imm : 5;
-        e(mk(V_MOV_B64, R(d), s(pod_s_[f])));
+        const int a = pod_s_[f];
+        switch (f) {
+          case 0: case 1: case 5:
+            e(mk(V_MOV_B32, R(d), v(a)));
+            e(mk(V_ASHRREV_I32, Rh(d), ic(31), v(a)));
+            break;
+          case 2:
+            e(mk(V_LSHRREV_B32, R(d), ic(16), v(a)));
+            e(mk(V_MOV_B32, Rh(d), ic(0)));
+            break;
+          case 3:
+            e(mklit(V_AND_B32, R(d), 0xFFFFu, v(a)));
+            e(mk(V_MOV_B32, Rh(d), ic(0)));
+            break;
+          default:
+            e(mk(V_MOV_B64, R(d), v(a)));
+            break;
+        }
         set_tag_static(d, false);
         break;
       }

@@ -217,8 +217,9 @@ std::vector<int64_t> emu_event(const ProgramDesc& p, const std::vector<int64_t>&
                                const std::vector<int64_t>& pod) {
   const int N = (int)(node.size() / 6);
   if (N < 1 || N > 64 || gl.size() != (size_t)N * 8 || gt.size() != (size_t)N * 8 || gmem.size() != (size_t)N * 8 ||
-      pod.size() != 6)
+      (pod.size() != 6 && pod.size() != (size_t)N * 6))
     throw std::invalid_argument("emu_event: bad shapes");
+  const bool per_lane_pod = pod.size() != 6;   // one pod per lane: several programs' rows in one call
   gcn::ProgIn in = make_in(p);
   gcn::Codegen cg(in);
   gcn::Func f = cg.run();
@@ -239,10 +240,11 @@ std::vector<int64_t> emu_event(const ProgramDesc& p, const std::vector<int64_t>&
     }
     const uint64_t gp = (uint64_t)(uintptr_t)(gmem.data() + (size_t)l * 8);
     E->vg[21][l] = (uint32_t)gp; E->vg[22][l] = (uint32_t)(gp >> 32);
-    E->vg[23][l] = (uint32_t)pod[0]; E->vg[24][l] = (uint32_t)pod[1];
-    E->vg[25][l] = (uint32_t)(pod[3] | (pod[2] << 16));
-    E->vg[26][l] = (uint32_t)(uint64_t)pod[4]; E->vg[27][l] = (uint32_t)((uint64_t)pod[4] >> 32);
-    E->vg[28][l] = (uint32_t)pod[5];
+    const int64_t* pd = pod.data() + (per_lane_pod ? (size_t)l * 6 : 0);
+    E->vg[23][l] = (uint32_t)pd[0]; E->vg[24][l] = (uint32_t)pd[1];
+    E->vg[25][l] = (uint32_t)(pd[3] | (pd[2] << 16));
+    E->vg[26][l] = (uint32_t)(uint64_t)pd[4]; E->vg[27][l] = (uint32_t)((uint64_t)pd[4] >> 32);
+    E->vg[28][l] = (uint32_t)pd[5];
     E->vg[29][l] = 0;
   }
   E->sg[32] = 0;

@@ -226,3 +226,31 @@ def test_llvm_tier_disk_cache(tmp_path, monkeypatch):
     assert len(list((tmp_path / "cache").glob("*.co"))) == 1
     monkeypatch.setenv("FKS_JIT_CACHE", "off")
     assert not jit.compile_device_module([p]).cached
+
+
+def test_per_lane_pods_several_rows_in_one_call(corpus):
+    """The four-programs-per-wave row kernel can call one shape for several
+    DPP rows at once, each row with its own pod: every pod field is per lane."""
+    m = ce.native()
+    rng = random.Random(17)
+    for p in corpus[::3]:
+        kc = constant_block(p, 1 << 16).tolist()
+        lit = gcnjit.literal_mask(p).tolist()
+        node, gl, gt, gm, _ = _random_event(rng, n=64)
+        pods = [_random_event(rng, n=1)[4] for _ in range(4)]          # one pod per 16-lane row
+        per_lane = [x for l in range(64) for x in pods[l // 16]]
+        emu = m.gcn_emu_event(p.code, list(map(int, p.ctag)), lit, list(map(int, p.iconst)),
+                              list(map(float, p.fconst)), kc, node, gl, gt, gm, per_lane)
+        for n in range(0, 64, 5):
+            pod = pods[n // 16]
+            podd = dict(cpu_milli=pod[0], memory_mib=pod[1], num_gpu=pod[2], gpu_milli=pod[3], creation_time=pod[4],
+                        duration_time=pod[5])
+            nd = dict(cpu_milli_left=node[6 * n], cpu_milli_total=node[6 * n + 1], memory_mib_left=node[6 * n + 2],
+                      memory_mib_total=node[6 * n + 3], gpu_left=node[6 * n + 4])
+            ng = node[6 * n + 5]
+            k, v = m.score_program_once(p.code, list(p.fconst), list(p.iconst), list(p.ctag), podd, nd,
+                                        gl[8 * n:8 * n + ng], gt[8 * n:8 * n + ng], gm[8 * n:8 * n + ng])
+            ref = _finish(k, v)
+            if ref in (-100, -101) or emu[n] in (-100, -101):
+                continue
+            assert emu[n] == ref, (p.source[-300:], n, pod, (k, v), emu[n])
