@@ -200,24 +200,50 @@ class Screener:
     def __init__(self, w: Workload, reference_weights=None, kind: str = "myopic", device="auto",
                  state_stride: int = 1):
         self.workload = w
-        st = record_states(w, "composite_linear", reference_weights)
-        if state_stride > 1:
-            keep = np.arange(0, st.n_states, int(state_stride))
-            st = RecordedStates(st.pod[keep], st.decision[keep], st.cpu_left[keep], st.mem_left[keep],
-                                st.gpu_left[keep], st.gml[keep])
-        self.states = st
+        self.kind = kind
+        self.state_stride = int(state_stride)
         self.Np = _pad_nodes(w.cluster.n_nodes)
-        self.X = composite_features(w, self.states)
-        self.R, self.Rfail = rewards(w, self.states, kind)
         self.device = None
         self._dev = None
+        self.refreshes = 0
         if device != "cpu":
             from . import hip_engine
             if hip_engine.device_available():
                 self.device = 0 if device == "auto" else int(device)
-                self._dev = hip_engine.native().ScreenDevice(self.X, self.R, self.Rfail, self.Np, self.device)
             elif device not in ("auto",):
                 raise RuntimeError("HIP device requested but none is visible")
+        self._load([reference_weights])
+
+    def _load(self, weight_list) -> None:
+        parts = []
+        stride = self.state_stride * max(1, len(weight_list))   # same state budget for any trajectory count
+        for i, wt in enumerate(weight_list):
+            st = record_states(self.workload, "composite_linear", wt)
+            keep = np.arange(i % stride, st.n_states, stride)
+            parts.append(RecordedStates(st.pod[keep], st.decision[keep], st.cpu_left[keep], st.mem_left[keep],
+                                        st.gpu_left[keep], st.gml[keep]))
+        self.states = RecordedStates(*(np.concatenate([getattr(q, f) for q in parts])
+                                       for f in ("pod", "decision", "cpu_left", "mem_left", "gpu_left", "gml")))
+        self.X = composite_features(self.workload, self.states)
+        self.R, self.Rfail = rewards(self.workload, self.states, self.kind)
+        if self.device is not None:
+            from . import hip_engine
+            self._dev = hip_engine.native().ScreenDevice(self.X, self.R, self.Rfail, self.Np, self.device)
+
+    def refresh(self, weight_list) -> None:
+        """Re-draw the surrogate states from the given candidates' own
+        trajectories (e.g. the islands' current elites, every migration epoch):
+        the surrogate then scores proposals on states the search actually
+        visits, not on one fixed policy's."""
+        self._load([np.asarray(wt, dtype=np.float64) for wt in weight_list])
+        self.refreshes += 1
+
+    @staticmethod
+    def spearman(surrogate: np.ndarray, exact: np.ndarray) -> float:
+        """Rank correlation of surrogate and exact scores (average ranks for ties)."""
+        from scipy.stats import spearmanr
+        r = spearmanr(np.asarray(surrogate, dtype=np.float64), np.asarray(exact, dtype=np.float64)).correlation
+        return float(r) if r == r else 0.0
 
     @property
     def n_states(self) -> int:
