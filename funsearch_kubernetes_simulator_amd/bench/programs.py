@@ -69,12 +69,13 @@ def measure_native(dev, progs: List[CompiledPolicy]) -> dict:
             "events": int(tab[:, 8].sum()), "repeat_identical": bool((tab == tab2).all())}
 
 
-def novel_children(n: int, seed: int = 0) -> List[CompiledPolicy]:
-    """`n` mutation children with pairwise-distinct shapes (`shape_key`): every
-    one is a JIT compile, as with a real LLM, which almost never repeats a
-    program's structure."""
+def novel_children(n: int, seed: int = 0, exclude=()) -> List[CompiledPolicy]:
+    """`n` mutation children with pairwise-distinct shapes (`shape_key`),
+    none in `exclude` (e.g. the shapes a compiler already holds): every one is
+    a JIT compile, as with a real LLM, which almost never repeats a program's
+    structure."""
     from ..policy.native_codegen import shape_key
-    out, keys = [], set()
+    out, keys = [], set(exclude)
     s = seed
     while len(out) < n:
         for p in mutation_children(2 * (n - len(out)) + 8, seed=s):
@@ -97,7 +98,7 @@ def measure_novel(dev, workload, n: int = 256, compile_batches: int = 4, seed: i
     import numpy as np
     from ..engine import COLS
     from ..ops import cpu_engine as ce
-    progs = novel_children(n + 64 * compile_batches, seed)
+    progs = novel_children(n + 64 * compile_batches, seed, exclude=set(dev.native_compiler._shapes))
     main, extra = progs[:n], progs[n:]
     t64 = []
     for i in range(compile_batches):
@@ -116,6 +117,9 @@ def measure_novel(dev, workload, n: int = 256, compile_batches: int = 4, seed: i
     skip = (100, 101)
     exc, vexc = tab[:, COLS["exc"]].astype(int), vm[:, COLS["exc"]].astype(int)
     cmp = ~np.isin(exc, skip) & ~np.isin(vexc, skip)
+    if not dev.options.get("trace_hash", True):
+        # the device skipped the per-event trace hash (bench.py turns it off): compare the rest
+        tab, vm = tab[:, :COLS["trace_hash_hi"]], vm[:, :COLS["trace_hash_hi"]]
     dev_rate, vm_rate = n / (t2 - t0), n / (c1 - c0)
     st = dev.native_compiler.stats
     return {"programs": n, "new_shapes": int(batch.compiled), "native": int(batch.ok.sum()),

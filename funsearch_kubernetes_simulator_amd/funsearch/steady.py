@@ -127,6 +127,9 @@ class SteadyStateSearch:
         self.task_size = int(task_size)
         self.status_every_s = float(status_every_s)
         self.stats = SteadyStats()
+        # main-thread wall time by phase (the dispatcher is one thread: its busy
+        # fraction bounds the steady-state rate)
+        self.phase = {"receive": 0.0, "submit": 0.0, "collect": 0.0, "merge": 0.0}
 
     # -- helpers ------------------------------------------------------------------------
     def _elites(self, s):
@@ -223,7 +226,9 @@ class SteadyStateSearch:
                 still = []
                 for f in inflight_tasks:
                     if f.done():
+                        t_ph = time.perf_counter()
                         items, cpu_s = f.result()
+                        self.phase["receive"] += time.perf_counter() - t_ph
                         self.stats.producer_cpu_s += cpu_s
                         for isl, code, prog in items:
                             self.stats.produced += 1
@@ -247,7 +252,9 @@ class SteadyStateSearch:
                         continue
                     take, ready = ready[:self.batch], ready[self.batch:]
                     with roctx_range(f"steady.launch slot {si} ({len(take)} programs)"):
+                        t_ph = time.perf_counter()
                         pend = ev.submit_compiled([c for _, c, _ in take], [p for _, _, p in take], slot=si)
+                        self.phase["submit"] += time.perf_counter() - t_ph
                     b = _Batch(si, take, pend, time.time(), pend.new_shapes, pend.jit_s)
                     batches[si] = b
                     self.stats.jit_s += pend.jit_s
@@ -260,7 +267,10 @@ class SteadyStateSearch:
                     b = batches[si]
                     if b is None or not ev.ready(b.pend):
                         continue
+                    t_ph = time.perf_counter()
                     results = ev.collect(b.pend)
+                    t_m = time.perf_counter()
+                    self.phase["collect"] += t_m - t_ph
                     t_done = time.time()
                     batches[si] = None
                     if busy_since is not None and all(x is None for x in batches):
@@ -271,6 +281,7 @@ class SteadyStateSearch:
                         merged[isl] += 1
                         if res.engine == "hip-native":
                             self.stats.native += 1
+                    self.phase["merge"] += time.perf_counter() - t_m
                     self.stats.evaluations += len(b.items)
                     self.stats.batches += 1
                     fs.evaluations += len(b.items)
@@ -344,6 +355,10 @@ class SteadyStateSearch:
                    generation=fs.generation, best=round(fs.best[1], 6), best_global=round(best_global, 6),
                    islands=[round(s.best_score, 6) for s in fs.islands], migrations=st.migrations,
                    collective_wait_s=round(self.channel.wait_s, 4),
+                   main_phase_s={k: round(v, 3) for k, v in self.phase.items()},
+                   jit={k: (round(v, 3) if isinstance(v, float) else v)
+                        for k, v in (getattr(getattr(fs.evaluator.device, "native_compiler", None), "stats", None)
+                                     or {}).items()},
                    collective_wait_frac=round(self.channel.wait_s / wall, 5),
                    engines={k: v for k, v in fs.evaluator.stats.items() if k in
                             ("device_native", "device", "cpu_vm", "object", "compile_errors", "jit_shapes")})
