@@ -38,6 +38,7 @@ import concurrent.futures
 import glob
 import json
 import os
+import threading
 import time
 from typing import List, Optional, Tuple
 
@@ -75,6 +76,8 @@ class IslandFunSearch:
         self.mode = str(isl.get("mode", "steady" if isl.get("steady") else ("pipeline" if self.pipeline else "sync")))
         self.steady_cfg = dict(isl.get("steady") or {})
         self.failures: List[dict] = []
+        self._count_lock = threading.Lock()
+        self._ck_due = False
         dev = (self.config.get("device") or {}).get("kind", "auto")
         if dev == "auto" and self.ctx.backend == "nccl":
             dev = self.ctx.local_rank
@@ -360,7 +363,8 @@ class IslandFunSearch:
                 if exact.score > s.best_score:
                     s.best_score, s.best_policy = exact.score, res.code
                 self._polished.add(res.code)
-        self.evaluations += res.evaluated
+        with self._count_lock:       # polish runs in a worker thread in pipelined mode
+            self.evaluations += res.evaluated
         if log:
             self.log.write(**rec)
         return rec
@@ -441,6 +445,11 @@ class IslandFunSearch:
                             progressed = True
                     if chan.stopping:
                         stop[0] = True
+                if self._ck_due and all(ph == "idle" for ph in phase) and cpl["fut"] is None:
+                    # every island between generations, no polish / coupler thread touching a
+                    # population: a consistent cut (the islands' own generation counters are saved)
+                    self._ck_due = False
+                    self.save_checkpoint()
                 for i in range(k):
                     if inbox[i] and phase[i] == "idle":     # between generations: elites not captured
                         self.apply_migrants(i, inbox[i])
@@ -494,7 +503,8 @@ class IslandFunSearch:
                         t_end = time.time()
                         children = done_children.pop(i)
                         self._merge(s, plan[i][0], children, results)
-                        self.evaluations += len(children)
+                        with self._count_lock:
+                            self.evaluations += len(children)
                         gen[i] += 1
                         st = stamp[i]
                         rec = dict(kind="island_generation", rank=self.ctx.rank, island=i, generation=gen[i],
@@ -575,7 +585,7 @@ class IslandFunSearch:
         if self.verbose and self.ctx.is_main:
             print(json.dumps(rec), flush=True)
         if self.ck_dir and self.ck_every and g % self.ck_every == 0:
-            self.save_checkpoint()
+            self._ck_due = True      # written when every island is idle (a consistent cut)
         if best_local >= threshold:
             vote[0] = True
             if not chan.active:
@@ -599,6 +609,9 @@ class IslandFunSearch:
             return self.global_best()
         if self.pipeline:
             self.run_pipelined(generations, threshold)
+            if self._ck_due:
+                self._ck_due = False
+                self.save_checkpoint()
             return self.global_best()
         while self.generation - start < generations:
             rec = self.evolve()
