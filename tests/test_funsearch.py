@@ -389,3 +389,73 @@ def test_compile_workers_give_identical_results(default_workload):
     assert all(x.code == y.code and x.source == y.source for x, y in zip(ca, cb) if x is not None)
     assert [r.score for r in a.evaluate_programs(codes)] == [r.score for r in b.evaluate_programs(codes)]
     assert b.stats["compile_errors"] == 2
+
+
+class _DecliningDevice:
+    """Stand-in for `DeviceEvaluator` whose native backend declines every
+    program: its device VM answers with the CPU VM's rows, and every slot
+    refuses a second batch while one is in flight (the real engine's rule)."""
+
+    def __init__(self, workload, n_slots=5):
+        import threading
+        self.workload = workload
+        self.n_slots = n_slots
+        self.busy = {}
+        self.lock = threading.Lock()
+        self.vm_slots = []
+
+    def _take(self, slot, payload):
+        with self.lock:
+            if slot in self.busy:
+                raise RuntimeError(f"slot busy: wait() for its batch first (slot {slot})")
+            self.busy[slot] = payload
+
+    def submit_native(self, slot, progs):
+        import numpy as np
+        from funsearch_kubernetes_simulator_amd.ops.jit import NativeBatch
+        n = len(progs)
+        tab = np.zeros((n, 13))
+        tab[:, 10] = 100.0                                   # EXC_UNSUPPORTED: not native
+        self._take(slot, tab)
+        return NativeBatch(np.zeros(n, np.uint64), np.zeros(1, np.int64), np.zeros(n, np.int32),
+                           np.zeros(n, bool), {i: "declined" for i in range(n)}, 0.0, 0)
+
+    def ready(self, slot):
+        return True
+
+    def wait(self, slot):
+        with self.lock:
+            return self.busy.pop(slot)
+
+    def evaluate_programs(self, progs, slot=None):
+        from funsearch_kubernetes_simulator_amd.ops import cpu_engine as ce
+        assert slot is not None, "device VM fallback must run on the caller's slot"
+        self.vm_slots.append(slot)
+        self._take(slot, None)
+        try:
+            return ce.simulate_program_batch(self.workload, list(progs), threads=2)
+        finally:
+            self.wait(slot)
+
+
+def test_pipelined_islands_native_declines_everything(tmp_path):
+    """when the native backend declines a whole batch, the device
+    VM fallback runs on the island's own slot (no 'slot busy' between
+    pipelined islands), and every child still gets its exact score."""
+    import numpy as np
+    from funsearch_kubernetes_simulator_amd.core.arrays import Workload
+    from funsearch_kubernetes_simulator_amd.core import load_default_workload
+    from funsearch_kubernetes_simulator_amd.engine import Evaluator
+    from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
+    w = load_default_workload()
+    sub = Workload(w.cluster, w.pods.subset(np.arange(0, 600)))
+    ev = Evaluator(sub, device="cpu", options={"device_min_batch": 1})
+    ev.device = _DecliningDevice(sub)
+    cfg = _cfg(tmp_path)
+    cfg["islands"] = {"per_rank": 2, "migrate_every": 0, "migrants": 1, "pipeline": True}
+    cfg["checkpoint"] = {}
+    fs = IslandFunSearch(cfg, evaluator=ev)
+    fs.run(2)
+    assert fs.generation == 2
+    assert ev.stats["device"] > 0 and ev.stats["device_native"] == 0
+    assert set(ev.device.vm_slots) <= {0, 1} and len(set(ev.device.vm_slots)) == 2
