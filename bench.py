@@ -74,22 +74,10 @@ def main() -> None:
     ap.add_argument("--novel", type=int, default=256,
                     help="after the timed region: this many programs, every one a NEW shape (JIT included), "
                          "against the CPU VM on the same batch; reported as `program_path.novel` (0: skip)")
-    ap.add_argument("--screen", type=int, default=1,
-                    help="MFMA pre-filter: propose K x --candidates per island generation, screen them with "
-                         "k_screen_linear (composite family), replay the best 1/K exactly (1: off)")
-    ap.add_argument("--screen-stride", type=int, default=4, help="screen on every k-th recorded state")
-    ap.add_argument("--screen-refresh", type=int, default=1,
-                    help="with --screen: re-draw the surrogate states from the islands' best elites' own "
-                         "trajectories at every migration epoch, and measure the surrogate's Spearman rank "
-                         "correlation with exact scores on an unscreened sample (0: one fixed trajectory)")
-    ap.add_argument("--screen-probe", type=int, default=512,
-                    help="unscreened proposals replayed exactly per refresh for the Spearman measurement")
     ap.add_argument("--time-budget", type=float, default=0.0,
                     help="run generations until this many seconds have passed (instead of --steps); "
                          "steps = generations completed")
     args = ap.parse_args()
-    if args.screen > 1 and args.family != "composite_linear":
-        raise SystemExit("--screen needs --family composite_linear (the screened feature basis)")
 
     from funsearch_kubernetes_simulator_amd.parallel import dist
     ctx = dist.init_distributed(use_gpu=args.device == "gpu")
@@ -127,23 +115,8 @@ def main() -> None:
             (ctx.device, device, ev.device.device, torch.cuda.current_device())
     islands = make_islands(args.islands, args.family, args.candidates, args.elite,
                            seed=args.seed + 104729 * ctx.rank)
-    screener = None
-    screen_stats = {"screened": 0, "screen_s": 0.0}
-    if args.screen > 1:
-        from funsearch_kubernetes_simulator_amd.ops.screening import Screener
-        screener = Screener(workload, device=device if args.device == "gpu" else "cpu",
-                            state_stride=args.screen_stride)
-
     def propose(isl) -> np.ndarray:
-        if screener is None:
-            return isl.propose()
-        cand = isl.propose(args.screen * args.candidates)
-        t = time.perf_counter()
-        with roctx_range("bench.screen"):
-            keep = screener.select(cand, args.candidates)
-        screen_stats["screen_s"] += time.perf_counter() - t
-        screen_stats["screened"] += len(cand)
-        return cand[keep]
+        return isl.propose()
 
     def sync():
         if args.device == "gpu":
@@ -202,26 +175,6 @@ def main() -> None:
             if not progressed:
                 time.sleep(0.0002)
 
-    screen_log = []
-
-    def refresh_screener(gen: int) -> None:
-        """Surrogate states from the current elites' trajectories, then the
-        surrogate's rank correlation with exact replay on an unscreened sample
-        (outside the island update; its replays are not counted in `value`)."""
-        t = time.perf_counter()
-        elites = sorted(((float(sc), tuple(w)) for isl in islands for w, sc in zip(isl.elites, isl.elite_scores)),
-                        reverse=True)[:4]
-        if elites:
-            screener.refresh([np.asarray(w) for _, w in elites])
-        probe = np.concatenate([isl.propose(max(1, args.screen_probe // len(islands))) for isl in islands])
-        sur = screener.score(probe)
-        ex = ev.evaluate_family(args.family, probe)[:, COLS["score"]]
-        rho = screener.spearman(sur, ex)
-        dt = time.perf_counter() - t
-        screen_stats["refresh_s"] = screen_stats.get("refresh_s", 0.0) + dt
-        screen_log.append({"generation": gen, "spearman": round(rho, 4), "states": screener.n_states,
-                           "probe": int(len(probe)), "seconds": round(dt, 3)})
-
     def run(g0: int, count: int) -> None:
         """`count` generations of every island; migration at every multiple of
         --migrate-every.  Across ranks the elite all-gather (RCCL) is started
@@ -235,8 +188,6 @@ def main() -> None:
             with roctx_range(f"bench.generations {g}-{g + n - 1}"):
                 (epoch_sync if args.sync_islands else epoch_async)(g, n)
             g += n
-            if screener is not None and args.screen_refresh and args.migrate_every and g % M == 0:
-                refresh_screener(g)
             if args.migrate_every and g % M == 0:
                 with roctx_range("bench.migrate"):
                     if pending is not None:
@@ -248,7 +199,6 @@ def main() -> None:
     run(0, args.warmup)
     sync()
     events[0] = 0.0
-    screen_stats.update(screened=0, screen_s=0.0, refresh_s=0.0)
     t0 = time.perf_counter()
     if args.time_budget > 0:
         # whole migration epochs until the budget is spent (ranks agree on when to stop)
@@ -335,18 +285,6 @@ def main() -> None:
                                 "is the program-for-program comparison",
             "program_path": program_path,
         }
-        if screener is not None:
-            out["screen"] = {"k": args.screen, "state_stride": args.screen_stride, "states": screener.n_states,
-                             "kernel": "k_screen_linear (v_mfma_f32_32x32x2f32)",
-                             "screened_per_s": round(screen_stats["screened"] * ctx.world_size / elapsed, 1),
-                             "screen_s_rank0": round(screen_stats["screen_s"], 3),
-                             "refresh": bool(args.screen_refresh),
-                             "refresh_s_rank0": round(screen_stats.get("refresh_s", 0.0), 3),
-                             "spearman": [r["spearman"] for r in screen_log],
-                             "spearman_median": (float(np.median([r["spearman"] for r in screen_log]))
-                                                 if screen_log else None),
-                             "note": "value counts exact replays only; each replayed candidate is the best 1/k "
-                                     "of k proposals by the MFMA surrogate"}
         if args.time_budget > 0:
             out["time_budget_s"] = args.time_budget
         if args.save_best:

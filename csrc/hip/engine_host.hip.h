@@ -134,6 +134,11 @@ class DeviceEngine {
       s = std::make_unique<Slot>();
       HIP_OK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
       HIP_OK(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
+      // the persistent-queue counter, zeroed now, before any replay occupies the
+      // CUs (launches then offset their claims; nothing is re-zeroed later)
+      s->queue.reserve(64);
+      zero_queue(*s);
+      s->qbase = 0;
     }
     hipStream_t st = slots_[0]->stream;
     auto geti = [&](const char* k) { return d[k].cast<int64_t>(); };
@@ -713,11 +718,6 @@ class DeviceEngine {
     const int cap = std::max(1, (int)(row_share_ * lay.second * num_cus_));
     const int waves = std::max(1, std::min((P + kRowsPerWave - 1) / kRowsPerWave, cap));
     s.gheap.reserve((size_t)row_heap_entries(W_.n_pods) * 8 * (size_t)waves * kRowsPerWave);
-    if (s.queue.p == nullptr) {   // zeroed once; launches then offset their claims
-      s.queue.reserve(64);
-      zero_queue(s);
-      s.qbase = 0;
-    }
     if (profiled) s.prof.reserve((size_t)waves * 64);
     const size_t wb = (size_t)P * kWeights * 8;
     const fksk::BuiltinArgs a{Wl, upload_workload(s, Wl), reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + wb),
@@ -770,11 +770,6 @@ class DeviceEngine {
     const int cap = std::max(1, (int)(row_share_ * per_cu * num_cus_));
     const int waves = std::max(1, std::min((P + ra - 1) / ra, cap));
     s.gheap.reserve((size_t)entries * 8 * (size_t)waves * kRowsPerWave);
-    if (s.queue.p == nullptr) {
-      s.queue.reserve(64);
-      zero_queue(s);
-      s.qbase = 0;
-    }
     if (profiled) s.prof.reserve((size_t)waves * 64);
     const fksk::BuiltinArgs a{Wl, upload_workload(s, Wl), nullptr, nullptr, nullptr, s.res.as<DevResult>(),
                               s.gheap.as<uint64_t>(), profiled ? s.prof.as<uint64_t>() : nullptr, s.h_tab.dev<double>()};
@@ -812,18 +807,13 @@ class DeviceEngine {
     HIP_OK(hipStreamSynchronize(s.stream));
   }
 
-  // the launch's workload struct, also resident in HBM (the kernels' cold-field copy)
-  const DevWorkload* upload_workload(Slot& s, const DevWorkload& Wl) {
-    // the device copy is re-sent only when the launch configuration changes
-    const bool fresh = s.wc.p == nullptr;
-    s.wc.reserve(sizeof(DevWorkload));
-    s.h_wc.reserve(sizeof(DevWorkload));
-    if (fresh || std::memcmp(s.h_wc.p, &Wl, sizeof(DevWorkload)) != 0) {
-      std::memcpy(s.h_wc.p, &Wl, sizeof(DevWorkload));
-      HIP_OK(hipMemcpyAsync(s.wc.p, s.h_wc.p, sizeof(DevWorkload), hipMemcpyHostToDevice, s.stream));
-    }
-    return s.wc.as<const DevWorkload>();
-  }
+  // The kernels read their cold workload fields from their own kernarg
+  // segment (replay_kernels.hip kernarg_workload), so a launch copies nothing
+  // to the device.  A per-slot HBM copy used to be sent with hipMemcpyAsync,
+  // which the runtime runs as a copy kernel: on a slot's first launch it had
+  // to wait for a CU slot behind the other slots' persistent replay waves
+  // (0.9-1.1 s per slot at config-5 shape, profiles/r3_config5_copy_trace.txt).
+  static const DevWorkload* upload_workload(Slot&, const DevWorkload&) { return nullptr; }
 
   // k_eval_reduce, result table -> pinned host, completion event
   void finish(Slot& s) {

@@ -108,9 +108,4 @@ hipError_t launch_builtin_prof(bool gheap, int P, size_t lds, hipStream_t s, con
 hipError_t launch_vm_prof(bool gheap, int P, size_t lds, hipStream_t s, const VmArgs& a);
 hipError_t set_prof_attrs(int max_lds);
 
-// MFMA surrogate screening (screen.hip)
-hipError_t launch_screen_linear(const float* X, const float* Wt, const float* R, const float* Rfail, int S, int Np,
-                                int KP, int Ppad, float* fit, hipStream_t stream);
-hipError_t launch_mfma_probe(float* out, hipStream_t stream);
-
 }  // namespace fksk

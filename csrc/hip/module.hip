@@ -185,118 +185,6 @@ py::tuple test_heap(py::array_t<uint64_t, py::array::c_style | py::array::forcec
   return py::make_tuple(out, popped);
 }
 
-// Surrogate screening on one device (ops/screening.py): X [S*Np, KP], Wt [KP, Ppad],
-// R [S*Np], Rfail [S] (float32) -> fit [Ppad].
-py::array_t<float> screen_linear(py::array_t<float, py::array::c_style | py::array::forcecast> X,
-                                 py::array_t<float, py::array::c_style | py::array::forcecast> Wt,
-                                 py::array_t<float, py::array::c_style | py::array::forcecast> R,
-                                 py::array_t<float, py::array::c_style | py::array::forcecast> Rfail, int Np,
-                                 int device) {
-  if (X.ndim() != 2 || Wt.ndim() != 2 || X.shape(1) != Wt.shape(0)) throw std::invalid_argument("X [M,K] / Wt [K,P]");
-  const int KP = (int)X.shape(1), Ppad = (int)Wt.shape(1);
-  const int64_t M = X.shape(0);
-  if (Np <= 0 || M % Np != 0 || R.size() != M) throw std::invalid_argument("R must have S*Np entries");
-  const int S = (int)(M / Np);
-  if (Rfail.size() != S) throw std::invalid_argument("Rfail must have S entries");
-  HIP_OK(hipSetDevice(device));
-  float *dX, *dW, *dR, *dF, *dfit;
-  HIP_OK(hipMalloc(&dX, X.size() * 4));
-  HIP_OK(hipMalloc(&dW, Wt.size() * 4));
-  HIP_OK(hipMalloc(&dR, R.size() * 4));
-  HIP_OK(hipMalloc(&dF, Rfail.size() * 4 + 4));
-  HIP_OK(hipMalloc(&dfit, (size_t)Ppad * 4));
-  HIP_OK(hipMemcpy(dX, X.data(), X.size() * 4, hipMemcpyHostToDevice));
-  HIP_OK(hipMemcpy(dW, Wt.data(), Wt.size() * 4, hipMemcpyHostToDevice));
-  HIP_OK(hipMemcpy(dR, R.data(), R.size() * 4, hipMemcpyHostToDevice));
-  HIP_OK(hipMemcpy(dF, Rfail.data(), Rfail.size() * 4, hipMemcpyHostToDevice));
-  HIP_OK(hipMemset(dfit, 0, (size_t)Ppad * 4));
-  {
-    py::gil_scoped_release rel;
-    HIP_OK(fksk::launch_screen_linear(dX, dW, dR, dF, S, Np, KP, Ppad, dfit, nullptr));
-    HIP_OK(hipDeviceSynchronize());
-  }
-  py::array_t<float> out(Ppad);
-  HIP_OK(hipMemcpy(out.mutable_data(), dfit, (size_t)Ppad * 4, hipMemcpyDeviceToHost));
-  for (void* p : {(void*)dX, (void*)dW, (void*)dR, (void*)dF, (void*)dfit}) (void)hipFree(p);
-  return out;
-}
-
-// Device-resident screener (ops/screening.py Screener): the recorded state
-// features X, rewards R / Rfail stay in HBM for the whole search; each call
-// uploads only the candidates' weight columns and reads back their fitness.
-class ScreenDevice {
- public:
-  ScreenDevice(py::array_t<float, py::array::c_style | py::array::forcecast> X,
-               py::array_t<float, py::array::c_style | py::array::forcecast> R,
-               py::array_t<float, py::array::c_style | py::array::forcecast> Rfail, int Np, int device)
-      : device_(device), Np_(Np) {
-    if (X.ndim() != 2) throw std::invalid_argument("X [M,K]");
-    KP_ = (int)X.shape(1);
-    const int64_t M = X.shape(0);
-    if (Np <= 0 || M % Np != 0 || R.size() != M) throw std::invalid_argument("R must have S*Np entries");
-    S_ = (int)(M / Np);
-    if (Rfail.size() != S_) throw std::invalid_argument("Rfail must have S entries");
-    HIP_OK(hipSetDevice(device_));
-    HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    HIP_OK(hipMalloc(&dX_, X.size() * 4));
-    HIP_OK(hipMalloc(&dR_, R.size() * 4));
-    HIP_OK(hipMalloc(&dF_, Rfail.size() * 4 + 4));
-    HIP_OK(hipMemcpy(dX_, X.data(), X.size() * 4, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(dR_, R.data(), R.size() * 4, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(dF_, Rfail.data(), Rfail.size() * 4, hipMemcpyHostToDevice));
-  }
-  ~ScreenDevice() {
-    (void)hipSetDevice(device_);
-    for (void* p : {(void*)dX_, (void*)dR_, (void*)dF_, (void*)dW_, (void*)dfit_}) if (p) (void)hipFree(p);
-    if (stream_) (void)hipStreamDestroy(stream_);
-  }
-  ScreenDevice(const ScreenDevice&) = delete;
-  ScreenDevice& operator=(const ScreenDevice&) = delete;
-
-  py::array_t<float> score(py::array_t<float, py::array::c_style | py::array::forcecast> Wt) {
-    if (Wt.ndim() != 2 || Wt.shape(0) != KP_) throw std::invalid_argument("Wt must be [KP, Ppad]");
-    const int Ppad = (int)Wt.shape(1);
-    if (Ppad % 32 != 0) throw std::invalid_argument("Ppad must be a multiple of 32");
-    HIP_OK(hipSetDevice(device_));
-    if (Ppad > cap_) {
-      if (dW_) HIP_OK(hipFree(dW_));
-      if (dfit_) HIP_OK(hipFree(dfit_));
-      HIP_OK(hipMalloc(&dW_, (size_t)KP_ * Ppad * 4));
-      HIP_OK(hipMalloc(&dfit_, (size_t)Ppad * 4));
-      zeros_.assign((size_t)Ppad, 0.0f);
-      cap_ = Ppad;
-    }
-    py::array_t<float> out(Ppad);
-    {
-      py::gil_scoped_release rel;
-      HIP_OK(hipMemcpyAsync(dW_, Wt.data(), (size_t)KP_ * Ppad * 4, hipMemcpyHostToDevice, stream_));
-      HIP_OK(hipMemcpyAsync(dfit_, zeros_.data(), (size_t)Ppad * 4, hipMemcpyHostToDevice, stream_));
-      HIP_OK(fksk::launch_screen_linear(dX_, dW_, dR_, dF_, S_, Np_, KP_, Ppad, dfit_, stream_));
-      HIP_OK(hipMemcpyAsync(out.mutable_data(), dfit_, (size_t)Ppad * 4, hipMemcpyDeviceToHost, stream_));
-      HIP_OK(hipStreamSynchronize(stream_));
-    }
-    return out;
-  }
-  int n_states() const { return S_; }
-
- private:
-  int device_, Np_, KP_ = 0, S_ = 0, cap_ = 0;
-  hipStream_t stream_ = nullptr;
-  float *dX_ = nullptr, *dR_ = nullptr, *dF_ = nullptr, *dW_ = nullptr, *dfit_ = nullptr;
-  std::vector<float> zeros_;
-};
-
-py::array_t<float> mfma_probe(int device) {
-  HIP_OK(hipSetDevice(device));
-  float* d;
-  HIP_OK(hipMalloc(&d, 64 * 16 * 4));
-  HIP_OK(fksk::launch_mfma_probe(d, nullptr));
-  py::array_t<float> out({64, 16});
-  HIP_OK(hipMemcpy(out.mutable_data(), d, 64 * 16 * 4, hipMemcpyDeviceToHost));
-  (void)hipFree(d);
-  return out;
-}
-
 // Loader state shared by every JIT module of a device: a private
 // non-blocking stream and persistent buffers.  Loading a module must never
 // synchronise with the replay slots' streams: no hipFree (which waits for the
@@ -345,9 +233,9 @@ class JitModule {
     std::vector<uint64_t> rtv(rt.data(), rt.data() + rt.size());
     py::gil_scoped_release rel;    // other islands / the tier-up thread keep running
     JitLoader& L = jit_loader(device_);
-    std::lock_guard<std::mutex> g(L.mu);
     HIP_OK(hipSetDevice(device_));
     HIP_OK(hipModuleLoadData(&mod_, img.data()));
+    std::lock_guard<std::mutex> g(L.mu);   // the loader's stream and pointer buffers
     hipDeviceptr_t gp = nullptr;
     size_t gbytes = 0;
     HIP_OK(hipModuleGetGlobal(&gp, &gbytes, mod_, "fks_rt_table"));
@@ -404,16 +292,6 @@ PYBIND11_MODULE(_fks_hip, m) {
   m.def("device_count", &device_count);
   m.def("test_wave_ops", &test_wave_ops);
   m.def("test_heap", &test_heap);
-  m.def("screen_linear", &screen_linear, py::arg("X"), py::arg("Wt"), py::arg("R"), py::arg("Rfail"), py::arg("Np"),
-        py::arg("device") = 0);
-  m.def("mfma_probe", &mfma_probe, py::arg("device") = 0);
-  py::class_<ScreenDevice>(m, "ScreenDevice")
-      .def(py::init<py::array_t<float, py::array::c_style | py::array::forcecast>,
-                    py::array_t<float, py::array::c_style | py::array::forcecast>,
-                    py::array_t<float, py::array::c_style | py::array::forcecast>, int, int>(),
-           py::arg("X"), py::arg("R"), py::arg("Rfail"), py::arg("Np"), py::arg("device") = 0)
-      .def("score", &ScreenDevice::score)
-      .def_property_readonly("n_states", &ScreenDevice::n_states);
   py::class_<DeviceEngine>(m, "DeviceEngine")
       .def(py::init<py::dict, int, int>(), py::arg("workload"), py::arg("device") = 0, py::arg("n_slots") = 4)
       .def("set_options", &DeviceEngine::set_options)

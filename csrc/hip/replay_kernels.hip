@@ -16,6 +16,24 @@
 #include "vm_dev.hip.h"
 #include "replay_rows.hip.h"
 #include "replay_duo.hip.h"
+
+namespace {
+// The launch's workload struct as the kernel received it: every kernel's
+// first parameter is an argument struct whose first member is the
+// DevWorkload, so it sits at offset 0 of the kernarg segment.  The kernels
+// re-read their cold fields from there with scalar loads -- no per-slot HBM
+// copy, hence no copy kernel that would have to wait for a CU slot behind
+// the other slots' persistent replay waves (~1 s at config-5 shape).
+// (`&a.W` would not do: taking a by-value parameter's address makes clang
+// copy the struct to scratch.)
+__device__ __forceinline__ const fksd::DevWorkload* kernarg_workload() {
+  // constant (4) -> flat: the same 64-bit address (the kernarg segment is ordinary global memory)
+  return reinterpret_cast<const fksd::DevWorkload*>((uintptr_t)__builtin_amdgcn_kernarg_segment_ptr());
+}
+static_assert(offsetof(fksk::BuiltinArgs, W) == 0, "DevWorkload must open the kernel arguments");
+static_assert(offsetof(fksk::VmArgs, W) == 0, "DevWorkload must open the kernel arguments");
+static_assert(offsetof(fksk::NativeArgs, W) == 0, "DevWorkload must open the kernel arguments");
+}  // namespace
 #include "jit_abi.h"
 
 #ifndef FKS_KIND
@@ -114,7 +132,7 @@ __global__ FKS_FAM_BOUNDS(GHEAP, FAM, NPASS) void k_replay_builtin(fksk::Builtin
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   BuiltinScorerDev<FAM> sc;
   load_policy<FAM>(sc, s, a, p);
-  replay_one<NPASS>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p);
+  replay_one<NPASS>(a.W, kernarg_workload(), sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p);
 }
 
 template <int NPASS, bool GHEAP>
@@ -154,7 +172,7 @@ __global__ FKS_VM_BOUNDS(GHEAP) void k_replay_vm(fksk::VmArgs a) {
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   VmScorerDev sc;
   sc.init(a.T, p, a.W, a.budget, s.vregs);
-  replay_one<NPASS>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p);
+  replay_one<NPASS>(a.W, kernarg_workload(), sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p);
 }
 #endif
 
@@ -165,7 +183,7 @@ __global__ FKS_BOUNDS(GHEAP) void k_replay_builtin_prof(fksk::BuiltinArgs a) {
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   BuiltinScorerDev<-1> sc;
   load_policy<-1>(sc, s, a, p);
-  replay_one<1, BuiltinScorerDev<-1>, PhaseProf>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p,
+  replay_one<1, BuiltinScorerDev<-1>, PhaseProf>(a.W, kernarg_workload(), sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p,
                                                  a.prof + (size_t)p * 8);
 }
 
@@ -175,7 +193,7 @@ __global__ FKS_VM_BOUNDS(GHEAP) void k_replay_vm_prof(fksk::VmArgs a) {
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   VmScorerDev sc;
   sc.init(a.T, p, a.W, a.budget, s.vregs);
-  replay_one<1, VmScorerDev, PhaseProf>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p, a.prof + (size_t)p * 8);
+  replay_one<1, VmScorerDev, PhaseProf>(a.W, kernarg_workload(), sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p, a.prof + (size_t)p * 8);
 }
 #endif
 
@@ -192,7 +210,7 @@ __global__ FKS_VM_BOUNDS(GHEAP) void k_replay_vm_prof(fksk::VmArgs a) {
 #endif
 template <int FAM>
 __global__ __launch_bounds__(64, FAM < 0 ? 2 : (FAM == 3 || FAM == 4) ? FKS_ROW_HEAVY_WAVES : FKS_ROW_WAVES) void k_replay_rows(fksk::BuiltinArgs a, int P, uint32_t* queue, uint32_t qbase) {
-  replay_rows<FAM>(a.W, a.Wc, a.fam, a.weights, a.gheap, a.out, P, queue, qbase, nullptr,
+  replay_rows<FAM>(a.W, kernarg_workload(), a.fam, a.weights, a.gheap, a.out, P, queue, qbase, nullptr,
                    RowNativeArgs{nullptr, nullptr, nullptr}, kRowsPerWave, a.table);
 }
 #endif
@@ -201,7 +219,7 @@ __global__ __launch_bounds__(64, FAM < 0 ? 2 : (FAM == 3 || FAM == 4) ? FKS_ROW_
 template <int FAM>
 __global__ __launch_bounds__(64, FAM < 0 ? 2 : (FAM == 3 || FAM == 4) ? FKS_ROW_HEAVY_WAVES : FKS_ROW_WAVES)
 void k_replay_rows_prof(fksk::BuiltinArgs a, int P, uint32_t* queue, uint32_t qbase) {
-  replay_rows<FAM, RowProf>(a.W, a.Wc, a.fam, a.weights, a.gheap, a.out, P, queue, qbase, a.prof,
+  replay_rows<FAM, RowProf>(a.W, kernarg_workload(), a.fam, a.weights, a.gheap, a.out, P, queue, qbase, a.prof,
                             RowNativeArgs{nullptr, nullptr, nullptr}, kRowsPerWave, a.table);
 }
 #endif
@@ -261,22 +279,22 @@ __global__ void k_native_rt_table(uint64_t* out) {
 // latency-bound LLM-sized batches, 4 for large ones).
 __global__ __launch_bounds__(64, 1) void k_replay_rows_native(fksk::BuiltinArgs a, RowNativeArgs nat, int P,
                                                              uint32_t* queue, uint32_t qbase, int rows_active) {
-  replay_rows<kFamNative>(a.W, a.Wc, nullptr, nullptr, a.gheap, a.out, P, queue, qbase, nullptr, nat, rows_active,
+  replay_rows<kFamNative>(a.W, kernarg_workload(), nullptr, nullptr, a.gheap, a.out, P, queue, qbase, nullptr, nat, rows_active,
                           a.table);
 }
 // s_memtime phase-profiled build (diagnostics): a.prof = [waves, 8] cycles
 __global__ __launch_bounds__(64, 1) void k_replay_rows_native_prof(fksk::BuiltinArgs a, RowNativeArgs nat, int P,
                                                                   uint32_t* queue, uint32_t qbase, int rows_active) {
-  replay_rows<kFamNative, RowProf>(a.W, a.Wc, nullptr, nullptr, a.gheap, a.out, P, queue, qbase, a.prof, nat,
+  replay_rows<kFamNative, RowProf>(a.W, kernarg_workload(), nullptr, nullptr, a.gheap, a.out, P, queue, qbase, a.prof, nat,
                                    rows_active, a.table);
 }
 // Two waves per program (wave 0: heap, wave 1: scoring; replay_duo.hip.h).
 __global__ __launch_bounds__(128, 1) void k_replay_native_duo(fksk::BuiltinArgs a, RowNativeArgs nat) {
-  replay_duo<false>(a.W, a.Wc, a.gheap, a.out, nat, a.table);
+  replay_duo<false>(a.W, kernarg_workload(), a.gheap, a.out, nat, a.table);
 }
 // s_memtime-profiled build (diagnostics): a.prof = [blocks, 2 waves, 8] cycles
 __global__ __launch_bounds__(128, 1) void k_replay_native_duo_prof(fksk::BuiltinArgs a, RowNativeArgs nat) {
-  replay_duo<true>(a.W, a.Wc, a.gheap, a.out, nat, a.table, a.prof);
+  replay_duo<true>(a.W, kernarg_workload(), a.gheap, a.out, nat, a.table, a.prof);
 }
 #endif
 
@@ -294,7 +312,7 @@ __global__ __launch_bounds__(64, GHEAP ? 2 : 1) void k_replay_native(fksk::Nativ
   FKS_LDS int64_t* kl = reinterpret_cast<FKS_LDS int64_t*>(lds_ptr(s.vregs));
   for (int i = lane_id(); i < kKcLds; i += kWave) kl[i] = ksrc[i];
   sc.kc = kl;
-  replay_one<NPASS>(a.W, a.Wc, sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p);
+  replay_one<NPASS>(a.W, kernarg_workload(), sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p);
 }
 #endif
 

@@ -604,7 +604,8 @@ class IslandFunSearch:
             self.steady = SteadyStateSearch(self, batch=int(sc.get("batch", 256)), slots=sc.get("slots"),
                                             producers=int(sc.get("producers", 0)),
                                             task_size=int(sc.get("task_size", 8)),
-                                            status_every_s=float(sc.get("status_every_s", 5.0)))
+                                            status_every_s=float(sc.get("status_every_s", 5.0)),
+                                            tierup=bool(sc.get("tierup", False)))
             self.steady.run(generations, threshold, wall_s=float(sc.get("wall_s", 0.0)))
             return self.global_best()
         if self.pipeline:

@@ -115,10 +115,15 @@ class SteadyStateSearch:
     distributed context, log and checkpoint settings)."""
 
     def __init__(self, fs, batch: int = 256, slots: Optional[int] = None, producers: int = 0,
-                 task_size: int = 8, status_every_s: float = 5.0):
+                 task_size: int = 8, status_every_s: float = 5.0, tierup: bool = False):
         self.fs = fs
         self.batch = int(batch)
         dev = getattr(fs.evaluator, "device", None)
+        if dev is not None and not tierup:
+            # background LLVM recompiles of hot shapes compete with the producer
+            # processes for the host's cores and with the batches' module loads;
+            # at steady state almost every shape is evaluated once or twice
+            dev.native_compiler.tierup_after = 0
         n_slots = dev.n_slots if dev is not None else 1
         self.slots = max(1, min(int(slots or n_slots), n_slots))
         from ..ops.cpu_engine import default_threads
@@ -137,6 +142,10 @@ class SteadyStateSearch:
         return list(s.population[:s.elite_size])
 
     def _merge_one(self, s, code: str, score: float) -> bool:
+        if len(s.population) >= s.population_size and score <= min(sc for _, sc in s.population):
+            # truncation would drop it anyway (a tie sorts after the members it
+            # ties with): skip the similarity scan, same resulting population
+            return False
         if s._is_too_similar(code, score):
             return False
         s.population.append((code, score))

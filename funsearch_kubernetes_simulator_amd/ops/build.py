@@ -116,7 +116,7 @@ def build_cpu(force: bool = False) -> Path:
 #: Device translation units of _fks_hip: (object name, extra defines).  The
 #: replay kernels are split per NPASS and kind so their many template
 #: instances compile in parallel.
-HIP_UNITS = [("module", "module.hip", []), ("screen", "screen.hip", [])] + [
+HIP_UNITS = [("module", "module.hip", [])] + [
     (f"replay_k{kind}_np{npass}", "replay_kernels.hip", [f"-DFKS_KIND={kind}", f"-DFKS_NPASS={npass}"])
     for kind, npasses in ((0, (1, 2, 4)), (1, (1, 2, 4)), (2, (1,)), (3, (1,)), (4, (1, 2, 4))) for npass in npasses]
 

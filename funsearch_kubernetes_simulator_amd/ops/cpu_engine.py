@@ -92,7 +92,7 @@ class SimOptions:
     record_values: bool = False
     record_placements: bool = False
     check_invariants: int = 0       # verify resource accounting every K events + at the end (debug)
-    record_states: bool = False     # per creation event: pod, decision, node/GPU state (screening data)
+    record_states: bool = False     # per creation event: pod, decision, node/GPU state (analysis tools)
 
     def as_dict(self) -> dict:
         return dict(self.__dict__)

@@ -27,9 +27,14 @@ S = ("wait", "pod", "score", "verdict", "delete", "eval")
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--programs", type=int, default=48)
+    ap.add_argument("--tier", default="auto", choices=["auto", "baseline", "llvm"],
+                    help="JIT tier of the programs (ops/jit.py)")
     a = ap.parse_args()
     from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
+    from funsearch_kubernetes_simulator_amd.ops.jit import NativeCompiler
     dev = he.DeviceEvaluator(load_default_workload(), options={"native_rows": 1, "native_duo": True})
+    dev._jit = NativeCompiler(dev._eng, dev.device, budget=int(dev.options["budget"]), tier=a.tier)
+    dev._jit.tierup_after = 0
     sets = {"first_fit": [compile_policy(reference_policies()["first_fit"])],
             "funsearch_4901": [compile_policy(reference_policies()["funsearch_4901"])],
             "children": mutation_children(a.programs, 0)}
@@ -38,7 +43,7 @@ def main():
         tab, prof = dev.profile_native(progs)
         prof = prof.reshape(len(progs), 2, 8)
         ev = float(tab[:, 8].sum())
-        rec = {"set": name, "P": len(progs), "events": int(ev),
+        rec = {"set": name, "tier": a.tier, "P": len(progs), "events": int(ev),
                "heap_wave": {H[i]: round(float(prof[:, 0, i].sum()) / ev, 1) for i in range(len(H))},
                "score_wave": {S[i]: round(float(prof[:, 1, i].sum()) / ev, 1) for i in range(len(S))}}
         rec["heap_total"] = round(sum(rec["heap_wave"].values()), 1)

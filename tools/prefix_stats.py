@@ -17,7 +17,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from funsearch_kubernetes_simulator_amd.core import load_default_workload  # noqa: E402
 from funsearch_kubernetes_simulator_amd.models import families as fam  # noqa: E402
-from funsearch_kubernetes_simulator_amd.ops import cpu_engine as ce, screening  # noqa: E402
+from funsearch_kubernetes_simulator_amd.ops import cpu_engine as ce  # noqa: E402
 
 w = load_default_workload()
 p = w.pods
@@ -43,9 +43,11 @@ W = fam.SAMPLERS[family](n, np.random.default_rng(0))
 tab = ce.simulate_builtin_batch(w, family, fam.pad_weights(W))
 fr, share = [], []
 for wv, row in zip(W, tab):
-    st = screening.record_states(w, family, list(wv))
-    fails = np.nonzero(st.decision < 0)[0]
-    c = int(fails[0]) if fails.size else len(st.decision)
+    r = ce.simulate_builtin(w, family, list(wv), ce.SimOptions(record_states=True))
+    N, G = w.cluster.n_nodes, int(w.cluster.gpu_start[-1])
+    decision = np.asarray(r["states"], dtype=np.int64).reshape(-1, 2 + 3 * N + G)[:, 1]
+    fails = np.nonzero(decision < 0)[0]
+    c = int(fails[0]) if fails.size else len(decision)
     e = create_ev[c] if c < len(create_ev) else ev
     fr.append(e)
     share.append(e / max(1.0, row[8]))
