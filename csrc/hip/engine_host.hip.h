@@ -25,6 +25,7 @@
 #include <pybind11/pybind11.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -54,6 +55,36 @@ T* dev_upload(const py::array& a, hipStream_t s, std::vector<void*>& owned) {
   if (bytes) HIP_OK(hipMemcpyAsync(d, bi.ptr, bytes, hipMemcpyHostToDevice, s));
   owned.push_back(d);
   return reinterpret_cast<T*>(d);
+}
+
+template <class T>
+T* dev_upload_vec(const std::vector<T>& v, std::vector<void*>& owned) {
+  void* d = nullptr;
+  HIP_OK(hipMalloc(&d, v.empty() ? 16 : v.size() * sizeof(T)));
+  if (!v.empty()) HIP_OK(hipMemcpy(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  owned.push_back(d);
+  return reinterpret_cast<T*>(d);
+}
+
+// z = RN(1/d) if div_by_recip(n, d, z) equals the IEEE quotient n / d, bit for
+// bit, for every integer n in [0, hi]; 0.0 otherwise.  Verified per distinct
+// divisor (cache), so the device's reciprocal division is exact on exactly
+// the numerators the replay can form.
+inline double fks_recip_verified(int64_t d, int64_t hi, std::vector<std::pair<std::pair<int64_t, int64_t>, double>>& cache) {
+  for (const auto& c : cache)
+    if (c.first.first == d && c.first.second >= hi) return c.second;
+  double z = 0.0;
+  if (d >= 1 && hi >= 0 && hi < (int64_t(1) << 31)) {
+    const double dd = (double)d, zz = 1.0 / dd;
+    bool ok = true;
+    for (int64_t n = 0; n <= hi && ok; ++n) {
+      const double x = (double)n, q = x / dd, f = div_by_recip(x, dd, zz);
+      ok = std::memcmp(&q, &f, sizeof(double)) == 0;
+    }
+    if (ok) z = zz;
+  }
+  cache.push_back({{d, hi}, z});
+  return z;
 }
 
 struct DevBuf {
@@ -184,6 +215,7 @@ class DeviceEngine {
     W_.low_bits = (int32_t)geti("low_bits"); W_.time_bits = (int32_t)geti("time_bits");
     W_.snapshot_interval = 0.05;
     W_.trace_hash = 1;
+    prepare_recips(d);
     HIP_OK(hipStreamSynchronize(st));
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, device_));
@@ -231,6 +263,11 @@ class DeviceEngine {
       native_rows_opt_ = r;
     }
     if (o.contains("row_heap_top")) row_top_opt_ = o["row_heap_top"].cast<int>();   // -1: auto
+    if (o.contains("row_composite_waves")) {
+      const int w = o["row_composite_waves"].cast<int>();
+      if (w != 4 && w != 5) throw std::invalid_argument("row_composite_waves must be 4 or 5");
+      comp_waves_ = w;
+    }
     if (o.contains("row_wave_share")) {
       const double f = o["row_wave_share"].cast<double>();
       if (!(f > 0.0 && f <= 4.0)) throw std::invalid_argument("row_wave_share must be in (0, 4]");
@@ -494,6 +531,8 @@ class DeviceEngine {
     d["row_heap_top"] = row_top();
     d["row_waves_per_cu"] = row_layout(FAM_COMPOSITE_LINEAR).second;
     d["row_wave_share"] = row_share_;
+    d["fast_div"] = (int)W_.fast_div;
+    d["row_composite_waves"] = comp_waves_;
     d["native_rows_last"] = last_native_rows_;
     d["native_waves_last"] = last_native_waves_;
     return d;
@@ -508,6 +547,44 @@ class DeviceEngine {
   static constexpr int kWeightWords = kWeights;   // LDS copy of a builtin policy's weights
   static constexpr size_t kPoliciesPerCu = 16;   // HBM-heap builtin kernels: 4 waves per SIMD
   static constexpr size_t kVmPoliciesPerCu = 8;  // HBM-heap VM kernels: 2 waves per SIMD
+
+  // Reciprocals for the row kernel's composite scorer.  A node's cpu_left
+  // stays in [0, cpu_total] (likewise mem) when it starts there and no pod
+  // asks for a negative amount (placements need pod <= left, deletions give
+  // back what their placement took), so max(total, 1) is verified on
+  // numerators [0, total]; max(ngpus, 1) on idle-GPU counts [0, 8]; 1000 on
+  // best-fit GPU remainders [0, 2^21) (gpu milli < 2^20 by construction).
+  // Any failure clears fast_div and every division runs as a division.
+  void prepare_recips(py::dict d) {
+    auto i32 = [&](const char* k) {
+      return py::array_t<int32_t, py::array::c_style | py::array::forcecast>(d[k].cast<py::array>());
+    };
+    const auto ct = i32("cpu_total"), cl = i32("cpu_left"), mt = i32("mem_total"), ml = i32("mem_left"), ng = i32("ngpus");
+    const auto pod = i32("pod");
+    const int nn = (int)ct.size(), np = W_.n_pods;
+    std::vector<std::pair<std::pair<int64_t, int64_t>, double>> cache;
+    bool ok = true;
+    std::vector<double> rec((size_t)nn * 3, 0.0), cm((size_t)std::max(np, 1), 0.0);
+    for (int r = 0; r < np; ++r) {
+      const int32_t c = pod.data()[4 * r], m = pod.data()[4 * r + 1];
+      ok = ok && c >= 0 && m >= 0;
+      cm[r] = (double)c / (double)(m > 1 ? m : 1);
+    }
+    for (int n = 0; n < nn; ++n) {
+      const int32_t a = ct.data()[n], b = mt.data()[n];
+      ok = ok && 0 <= cl.data()[n] && cl.data()[n] <= a && 0 <= ml.data()[n] && ml.data()[n] <= b;
+      if (!ok) break;
+      rec[3 * n + 0] = fks_recip_verified(a > 1 ? a : 1, a, cache);
+      rec[3 * n + 1] = fks_recip_verified(b > 1 ? b : 1, b, cache);
+      rec[3 * n + 2] = fks_recip_verified(ng.data()[n] > 1 ? ng.data()[n] : 1, kGmax, cache);
+      ok = rec[3 * n] != 0.0 && rec[3 * n + 1] != 0.0 && rec[3 * n + 2] != 0.0;
+    }
+    const double z1000 = fks_recip_verified(1000, (int64_t(1) << 21) - 1, cache);
+    W_.fast_div = ok && z1000 != 0.0 ? 1 : 0;
+    W_.z1000 = z1000;
+    W_.node_recip = dev_upload_vec(rec, owned_);
+    W_.pod_cm = dev_upload_vec(cm, owned_);
+  }
 
   Slot& slot_at(int i) {
     if (i < 0 || i >= (int)slots_.size()) throw std::out_of_range("slot index");
@@ -643,6 +720,13 @@ class DeviceEngine {
     s.fam_spec = P > 0 ? fam[0] : -1;
     for (int i = 1; i < P && s.fam_spec >= 0; ++i)
       if (fam[i] != s.fam_spec) s.fam_spec = -1;
+    // the composite instance of the row kernel (composite_row) needs finite
+    // weights and verified reciprocals; any other batch of that family runs
+    // the mixed-family instance
+    if (s.fam_spec == FAM_COMPOSITE_LINEAR && !W_.fast_div) s.fam_spec = -1;
+    if (s.fam_spec == FAM_COMPOSITE_LINEAR)
+      for (size_t i = 0; i < (size_t)P * kWeights; ++i)
+        if (!std::isfinite(weights[i])) { s.fam_spec = -1; break; }
     const size_t fb = (size_t)P * 4, wb = (size_t)P * kWeights * 8;
     s.h_in.reserve(fb + wb + 16);
     char* h = s.h_in.as<char>();
@@ -706,7 +790,8 @@ class DeviceEngine {
   int launch_rows(Slot& s, bool profiled) {
     const int P = s.P;
     DevWorkload Wl = W_;
-    const std::pair<int, int> lay = row_layout(s.fam_spec);
+    const int kf = s.fam_spec == FAM_COMPOSITE_LINEAR && comp_waves_ == 5 ? kRowCompositeW5 : s.fam_spec;
+    const std::pair<int, int> lay = row_layout(kf);
     Wl.heap_top = lay.first;
     const size_t lds = rows_lds_bytes(W_.n_pods, Wl.heap_top) + (profiled ? kRowProfBytes : 0);
     if (lds > kMaxLds) throw std::invalid_argument("row kernel layout exceeds the 160 KiB LDS");
@@ -724,8 +809,8 @@ class DeviceEngine {
                               s.h_in.dev<double>(), s.w.as<double>(), s.res.as<DevResult>(), s.gheap.as<uint64_t>(),
                               profiled ? s.prof.as<uint64_t>() : nullptr, s.h_tab.dev<double>()};
     s.fused_table = true;
-    if (profiled) HIP_OK(fksk::launch_builtin_rows_prof(s.fam_spec, P, waves, s.queue.as<uint32_t>(), s.qbase, lds, s.stream, a));
-    else HIP_OK(fksk::launch_builtin_rows(s.fam_spec, P, waves, s.queue.as<uint32_t>(), s.qbase, lds, s.stream, a));
+    if (profiled) HIP_OK(fksk::launch_builtin_rows_prof(kf, P, waves, s.queue.as<uint32_t>(), s.qbase, lds, s.stream, a));
+    else HIP_OK(fksk::launch_builtin_rows(kf, P, waves, s.queue.as<uint32_t>(), s.qbase, lds, s.stream, a));
     s.qbase += (uint32_t)P + (uint32_t)waves * kRowsPerWave;   // every row makes one final, empty claim
     return waves;
   }
@@ -842,6 +927,7 @@ class DeviceEngine {
   bool native_duo_ = true;     // two-wave kernel for one-program-per-wave batches
   int native_rows_opt_ = 0;    // rows per wave for native programs (0: auto)
   int last_native_rows_ = 0, last_native_waves_ = 0;
+  int comp_waves_ = 4;   // composite row kernel: 4 or 5 waves per SIMD (row_composite_waves)
   mutable std::vector<std::pair<int, int>> row_layout_cache_ = std::vector<std::pair<int, int>>(8, {0, 0});
   int num_cus_ = 0;
   std::string arch_;

@@ -62,7 +62,24 @@ struct DevWorkload {
   int32_t inv_words;          // LDS u64 words reserved for the invariant check (0: off)
   int32_t trace_hash;         // 1: fold every event into DevResult.hash (cross-engine trace check)
   const uint64_t* heap0p;     // initial heap shifted by one slot (row kernel layout: address = slot + 1)
+  // Row-kernel composite scorer (scorers.hip.h composite_row): host-verified
+  // reciprocals RN(1/d) of the node-constant divisors max(cpu_total, 1),
+  // max(mem_total, 1), max(ngpus, 1) ([node][3]) and of 1000 (z1000), valid
+  // for every numerator a replay can form (fast_div = 1 iff all verified),
+  // and pod.cpu / max(pod.mem, 1) by rank.
+  const double* node_recip;
+  const double* pod_cm;
+  double z1000;
+  int32_t fast_div;
 };
+
+// RN(n / d) from z = RN(1/d) with one remainder step (Markstein): exact for
+// the numerators the host checked (fks_recip_verified), not in general.
+__host__ __device__ __forceinline__ double div_by_recip(double n, double d, double z) {
+  const double q = n * z;
+  const double r = __builtin_fma(-q, d, n);
+  return __builtin_fma(r, z, q);
+}
 
 struct DevResult {
   int64_t n_events, n_snap, n_frag, n_unplaced, n_repush, max_nodes;

@@ -160,13 +160,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
 
   if (wave == 0) {
     if (lane < W.n_classes) cls_lds[lane] = *global_ptr(&W.class_value[lane]);
-    if (lane < kRow) {
-      ntab[lane * kNodeConsts + 0] = W.cpu_total[lane];
-      ntab[lane * kNodeConsts + 1] = W.mem_total[lane];
-      ntab[lane * kNodeConsts + 2] = W.ngpus[lane];
-#pragma unroll
-      for (int g = 0; g < kGmax; ++g) ntab[lane * kNodeConsts + 3 + g] = W.gml_total[lane * kGmax + g];
-    }
+    fill_node_tables(W, ntab, lane);
     if (lane == 0) {
       box->item = 0; box->head = 0; box->tail = 0; box->rseq = 0; box->code = DUO_NONE; box->term = 0;
       box->h_exc = EXC_NONE; box->n_repush = 0; box->n_dropped = 0;

@@ -33,6 +33,8 @@ namespace fksd {
 // FAM value of the native-program instance: every row calls its own
 // JIT-compiled scorer (jit_abi.h ProgFn) instead of a built-in family.
 constexpr int kFamNative = 100;
+// host family code of the composite row kernel built for 5 waves per SIMD
+constexpr int kRowCompositeW5 = 5;
 struct RowNativeArgs {
   const uint64_t* fn;     // [P] device addresses of the programs' scorers
   const int64_t* kc;      // concatenated constant blocks
@@ -248,10 +250,26 @@ struct RowAcc {
   }
 };
 
-// LDS per wave: [4 x 16 weights | 64 class values | 16 x 11 node constants] then
-// per row [deletion bitmap | heap top].
-constexpr int kNodeConsts = 3 + kGmax;
-constexpr int kRowClassBytes = (kRow * kRowClassSlots * 4 + kRow * kNodeConsts * 4 + 15) & ~15;
+// LDS per wave: [4 x 16 weights | 64 class values | 16 x 4 node constants |
+// 16 x 3 node reciprocals] then per row [deletion bitmap | heap top].
+constexpr int kNodeConsts = 4;   // cpu_total, mem_total, ngpus, per-GPU milli total
+constexpr int kNodeRecips = 3;   // DevWorkload::node_recip
+constexpr int kRowClassBytes = (kRow * kRowClassSlots * 4 + kRow * kNodeConsts * 4 + kRow * kNodeRecips * 8 + 15) & ~15;
+__device__ __forceinline__ FKS_LDS double* row_node_recips(FKS_LDS int32_t* ntab) {
+  return reinterpret_cast<FKS_LDS double*>(ntab + kRow * kNodeConsts);
+}
+// the node tables (lanes < 16 of one wave)
+__device__ __forceinline__ void fill_node_tables(const DevWorkload& W, FKS_LDS int32_t* ntab, int lane) {
+  if (lane < kRow) {
+    ntab[lane * kNodeConsts + 0] = W.cpu_total[lane];
+    ntab[lane * kNodeConsts + 1] = W.mem_total[lane];
+    ntab[lane * kNodeConsts + 2] = W.ngpus[lane];
+    ntab[lane * kNodeConsts + 3] = W.gml_total[lane * kGmax];
+    FKS_LDS double* z = row_node_recips(ntab);
+#pragma unroll
+    for (int k = 0; k < kNodeRecips; ++k) z[lane * kNodeRecips + k] = W.node_recip[lane * kNodeRecips + k];
+  }
+}
 __host__ __device__ inline size_t rows_row_bytes(int n_pods, int T) {
   return (size_t)lds_delmap_words(n_pods) * 4 + (size_t)(T + 1) * 8;
 }
@@ -342,13 +360,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
   // per-GPU milli totals -- read back only by creation events, so they hold no
   // registers through the pop
   FKS_LDS int32_t* ntab = cls_lds + kRow * kRowClassSlots;
-  if (lane < kRow) {
-    ntab[lane * kNodeConsts + 0] = W.cpu_total[lane];
-    ntab[lane * kNodeConsts + 1] = W.mem_total[lane];
-    ntab[lane * kNodeConsts + 2] = W.ngpus[lane];
-#pragma unroll
-    for (int g = 0; g < kGmax; ++g) ntab[lane * kNodeConsts + 3 + g] = W.gml_total[lane * kGmax + g];
-  }
+  fill_node_tables(W, ntab, lane);
   RowHeap heap;
   heap.delmap = reinterpret_cast<FKS_LDS uint32_t*>(rowbase);
   heap.top = reinterpret_cast<FKS_LDS uint64_t*>(rowbase + (size_t)lds_delmap_words(N) * 4);
@@ -488,6 +500,11 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
         prof.mark(PH_DELETE);
       } else {
         // ---------------- creation: score the row's nodes, first maximum wins
+        // composite: composite_row (the host runs this instance only on
+        // finite weights and verified reciprocals, engine_host stage_builtin)
+        constexpr bool kComp = FAM == FAM_COMPOSITE_LINEAR;
+        double pcm = 0.0;
+        if (kComp) pcm = *global_ptr(&cold()->pod_cm[rank]);
         load_consts();
         int lexc = EXC_NONE;
         int64_t s = 0;
@@ -507,7 +524,13 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
         } else if (node_valid && feasible<1>(0, nr, pod)) {
           // weights read from LDS where each term uses them (no 32-VGPR weight vector)
           const FKS_LDS double* wq = wl;
-          s = BuiltinScorerDev<FAM>::template score_weights<1>(family, wq, 0, nr, pod, lexc);
+          if constexpr (kComp) {
+            const FKS_LDS double* z = row_node_recips(ntab) + jv * kNodeRecips;
+            const typename BuiltinScorerDev<FAM>::RowRecip rz{z[0], z[1], z[2], W.z1000, pcm};
+            s = trunc_score(BuiltinScorerDev<FAM>::composite_row(nr, pod, wq, rz), lexc);
+          } else {
+            s = BuiltinScorerDev<FAM>::template score_weights<1>(family, wq, 0, nr, pod, lexc);
+          }
           if (lexc != EXC_NONE) s = 0;
         }
         const uint32_t bad = row_ballot(lexc != EXC_NONE, rbase);

@@ -172,6 +172,64 @@ struct BuiltinScorerDev {
     return s;
   }
 
+  // composite() on the row kernel, bit for bit, with less f64 work:
+  //  * the divisions by max(cpu_total, 1), max(mem_total, 1), max(ngpus, 1)
+  //    and 1000 run as div_by_recip on host-verified reciprocals (rz, see
+  //    DeviceEngine::prepare_recips); pod.cpu / max(pod.mem, 1) is the host's
+  //    per-pod quotient (rz.pcm);
+  //  * no `w != 0` tests: every feature is finite and the sum starts at +0.0
+  //    and can never become -0.0, so a zero weight adds +-0 and changes
+  //    nothing;
+  //  * each complementary threshold pair (f1/f2, f3/f4, f5/f6) adds only its
+  //    nonzero member, and 0/1 indicators add the weight itself: the other
+  //    member's w * 0.0 is +-0 -- which needs every weight finite (inf * 0 is
+  //    NaN), so the caller passes here only policies whose weights all are.
+  struct RowRecip {
+    double zc, zm, zg, z1000, pcm;
+  };
+  template <class WP>
+  __device__ static double composite_row(const NodeRegs<1>& nr, const PodView& pod, WP w, const RowRecip& rz) {
+    const int ng = nr.ngpus[0];
+    const bool gpod = pod.ngpu > 0;
+    const int32_t ct = nr.cpu_total[0], mt = nr.mem_total[0];
+    const int32_t cl = nr.cpu_left[0], ml = nr.mem_left[0];
+    // numerators in [0, total]: the host's invariant check behind rz
+    const double cpu_u = div_by_recip((double)(ct - cl), (double)(ct > 1 ? ct : 1), rz.zc);
+    const double mem_u = div_by_recip((double)(mt - ml), (double)(mt > 1 ? mt : 1), rz.zm);
+    int32_t free_m = 0, idle = 0, gmax = 0, gmin = 0, best = -1;
+#pragma unroll
+    for (int j = 0; j < kGmax; ++j) {
+      if (j < ng) {
+        const int32_t l = nr.gml[0][j];
+        free_m += l;
+        idle += (l == nr.gmt1[0]);
+        gmax = (j == 0 || l > gmax) ? l : gmax;
+        gmin = (j == 0 || l < gmin) ? l : gmin;
+        if (gpod && l >= pod.gmilli && (best < 0 || l - pod.gmilli < best)) best = l - pod.gmilli;
+      }
+    }
+    double s = 0.0 + w[0];
+    s = s + (cpu_u < 0.7 ? w[1] : w[2]) * (1.0 - cpu_u);
+    s = s + (mem_u < 0.7 ? w[3] : w[4]) * (1.0 - mem_u);
+    if (gpod) {
+      const int64_t cap = (int64_t)nr.gpu_left[0] * nr.gt(0, 0);
+      const double gpu_u = (double)(cap - free_m) / (double)(cap > 1 ? cap : 1);
+      s = s + (gpu_u < 0.7 ? w[5] : w[6]) * (1.0 - gpu_u);
+      const uint32_t d = pod.gmilli > 1 ? (uint32_t)pod.gmilli : 1u;
+      s = s + w[7] * (double)((uint32_t)free_m % d);
+    }
+    const double a = (double)cl / (double)(ml > 1 ? ml : 1);
+    s = s + w[8] * fabs(a - rz.pcm);
+    if (cl > (int64_t)pod.cpu * 2 && ml > (int64_t)pod.mem * 2) s = s + w[9];
+    if (gpod) s = s + w[10] * (double)(gmax - gmin);
+    if (ct > 10000 && mt > 64) s = s + w[11];
+    if (cpu_u > 0.9 || mem_u > 0.9) s = s + w[12];
+    if (best >= 0) s = s + w[13] * div_by_recip((double)best, 1000.0, rz.z1000);
+    s = s + w[14] * div_by_recip((double)idle, (double)(ng > 1 ? ng : 1), rz.zg);
+    if (!gpod && ng > 0) s = s + w[15];
+    return s;
+  }
+
   template <int NPASS>
   __device__ static void features(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, double* f) {
     const int ng = nr.ngpus[ps];

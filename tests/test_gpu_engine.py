@@ -153,6 +153,36 @@ def test_row_kernel_matches_cpu(default_workload, top):
                           ce.simulate_builtin_batch(default_workload, "composite_linear", w))
 
 
+@pytest.mark.parametrize("waves", [4, 5])
+def test_row_composite_reciprocal_path_matches_cpu(default_workload, waves):
+    """The composite row instance (host-verified reciprocal divisions, no zero-weight tests,
+    one member per threshold pair) at 4 and 5 waves per SIMD == CPU oracle, including
+    zero weights and a huge-weight row that overflows."""
+    from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
+    dev = he.DeviceEvaluator(default_workload, options={"row_kernel": "on", "row_composite_waves": waves})
+    assert dev.info()["fast_div"] == 1 and dev.info()["row_composite_waves"] == waves
+    w = fam.sample_composite_linear(70, np.random.default_rng(31 + waves))
+    w[1, ::2] = 0.0
+    w[2, :] = -0.0
+    w[3, 13] = 1e308
+    gpu = dev.evaluate_builtin("composite_linear", w)
+    assert np.array_equal(gpu, ce.simulate_builtin_batch(default_workload, "composite_linear", w))
+
+
+def test_row_composite_nonfinite_weights_take_mixed_instance(default_workload):
+    """inf * 0.0 is NaN: a composite batch with a non-finite weight runs the generic instance
+    (engine_host stage_builtin) and still equals the CPU oracle."""
+    from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
+    dev = he.DeviceEvaluator(default_workload, options={"row_kernel": "on"})
+    w = fam.sample_composite_linear(8, np.random.default_rng(5))
+    w[0, 2] = np.inf
+    w[1, 9] = np.nan
+    w[2, 15] = -np.inf
+    gpu = dev.evaluate_builtin("composite_linear", w)
+    assert np.array_equal(gpu, ce.simulate_builtin_batch(default_workload, "composite_linear", w))
+    assert (gpu[:3, 10] != 0).all()
+
+
 def test_row_kernel_mixed_families_and_exceptions(default_workload):
     """Mixed-family batch (one kernel, divergent scorers per row) incl. rows that raise."""
     from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
