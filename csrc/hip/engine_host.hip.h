@@ -225,7 +225,8 @@ class DeviceEngine {
     delmap_bytes_ = (size_t)lds_delmap_words(W_.n_pods) * 4;
     lds_heap_ok_ = heap_bytes_ + delmap_bytes_ <= kMaxLds;
     rows_ok_ = npass_ == 1 && W_.n_nodes <= kRow && W_.n_classes <= kRow * kRowClassSlots &&
-               W_.n_pods <= kRowMaxHeap;
+               W_.n_pods <= kRowMaxHeap && W_.tot_cpu < (int64_t(1) << 31) && W_.tot_mem < (int64_t(1) << 31) &&
+               W_.tot_gcnt < (int64_t(1) << 31) && W_.tot_gmilli < (int64_t(1) << 31);   // int32 row totals
     set_attrs();
   }
 
@@ -268,6 +269,7 @@ class DeviceEngine {
       if (w != 4 && w != 5) throw std::invalid_argument("row_composite_waves must be 4 or 5");
       comp_waves_ = w;
     }
+    if (o.contains("row_flat")) row_flat_ = o["row_flat"].cast<bool>();
     if (o.contains("row_wave_share")) {
       const double f = o["row_wave_share"].cast<double>();
       if (!(f > 0.0 && f <= 4.0)) throw std::invalid_argument("row_wave_share must be in (0, 4]");
@@ -532,7 +534,10 @@ class DeviceEngine {
     d["row_waves_per_cu"] = row_layout(FAM_COMPOSITE_LINEAR).second;
     d["row_wave_share"] = row_share_;
     d["fast_div"] = (int)W_.fast_div;
+    d["cap_recips"] = W_.cap_recip[1] != 0.0;
+    d["frag_recip"] = W_.z_tg != 0.0;
     d["row_composite_waves"] = comp_waves_;
+    d["row_flat"] = row_flat_;
     d["native_rows_last"] = last_native_rows_;
     d["native_waves_last"] = last_native_waves_;
     return d;
@@ -581,6 +586,31 @@ class DeviceEngine {
     }
     const double z1000 = fks_recip_verified(1000, (int64_t(1) << 21) - 1, cache);
     W_.fast_div = ok && z1000 != 0.0 ? 1 : 0;
+    // GPU capacity divisors max(k * G, 1), k = 0..8, when every GPU node's
+    // per-GPU milli total is one G: numerators cap - free_m lie in
+    // [-8G, 8G] and RN is odd, so [0, 8G] is checked
+    {
+      const auto gt = i32("gml_total");
+      int32_t G = -1;
+      bool uni = true;
+      for (int n = 0; n < std::min<int>(nn, W_.n_nodes); ++n)
+        if (ng.data()[n] > 0) {
+          const int32_t g0 = gt.data()[(size_t)n * kGmax];
+          if (G < 0) G = g0;
+          uni = uni && g0 == G;
+        }
+      W_.cap_milli = uni && G > 0 && G < (1 << 20) ? G : 0;
+      for (int k = 0; k <= kGmax; ++k) {
+        const int64_t dv = std::max<int64_t>(1, (int64_t)k * W_.cap_milli);
+        W_.cap_recip[k] = W_.cap_milli > 0 ? fks_recip_verified(dv, 8 * (int64_t)W_.cap_milli, cache) : 0.0;
+      }
+      for (int k = 0; k <= kGmax; ++k)
+        if (W_.cap_recip[k] == 0.0)
+          for (int j = 0; j <= kGmax; ++j) W_.cap_recip[j] = 0.0;   // all or none
+    }
+    // fragmentation divisor: stranded milli in [0, tot_gmilli]
+    W_.z_tg = W_.tot_gmilli > 0 && W_.tot_gmilli <= (int64_t(1) << 24)
+                  ? fks_recip_verified(W_.tot_gmilli, W_.tot_gmilli, cache) : 0.0;
     W_.z1000 = z1000;
     W_.node_recip = dev_upload_vec(rec, owned_);
     W_.pod_cm = dev_upload_vec(cm, owned_);
@@ -790,7 +820,10 @@ class DeviceEngine {
   int launch_rows(Slot& s, bool profiled) {
     const int P = s.P;
     DevWorkload Wl = W_;
-    const int kf = s.fam_spec == FAM_COMPOSITE_LINEAR && comp_waves_ == 5 ? kRowCompositeW5 : s.fam_spec;
+    const int kf = s.fam_spec != FAM_COMPOSITE_LINEAR ? s.fam_spec
+                   : comp_waves_ == 5                  ? kRowCompositeW5
+                   : !row_flat_                        ? kRowCompositeSplit
+                                                       : s.fam_spec;
     const std::pair<int, int> lay = row_layout(kf);
     Wl.heap_top = lay.first;
     const size_t lds = rows_lds_bytes(W_.n_pods, Wl.heap_top) + (profiled ? kRowProfBytes : 0);
@@ -927,6 +960,7 @@ class DeviceEngine {
   bool native_duo_ = true;     // two-wave kernel for one-program-per-wave batches
   int native_rows_opt_ = 0;    // rows per wave for native programs (0: auto)
   int last_native_rows_ = 0, last_native_waves_ = 0;
+  bool row_flat_ = true;  // composite row kernel: flat heap accesses (false: exec-masked ds / global)
   int comp_waves_ = 4;   // composite row kernel: 4 or 5 waves per SIMD (row_composite_waves)
   mutable std::vector<std::pair<int, int>> row_layout_cache_ = std::vector<std::pair<int, int>>(8, {0, 0});
   int num_cus_ = 0;

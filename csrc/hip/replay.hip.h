@@ -71,6 +71,13 @@ struct DevWorkload {
   const double* pod_cm;
   double z1000;
   int32_t fast_div;
+  // composite GPU utilisation: every GPU node has per-GPU milli total
+  // cap_milli; cap_recip[k] = RN(1 / max(k * cap_milli, 1)), k = 0..8,
+  // verified on |numerators| <= 8 * cap_milli (all 0 when not uniform)
+  int32_t cap_milli;
+  double cap_recip[kGmax + 1];
+  // fragmentation: RN(1 / tot_gmilli) verified on [0, tot_gmilli] (0: divide)
+  double z_tg;
 };
 
 // RN(n / d) from z = RN(1/d) with one remainder step (Markstein): exact for

@@ -181,6 +181,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
     heap.delmap = reinterpret_cast<FKS_LDS uint32_t*>(rowbase);
     heap.top = reinterpret_cast<FKS_LDS uint64_t*>(rowbase + (size_t)lds_delmap_words(N) * 4);
     heap.h = global_ptr(gheap + (size_t)p * row_heap_entries(N));
+    heap.bind();
     heap.T = T;
     heap.lb = lb;
     heap.j = jv;

@@ -222,6 +222,12 @@ __global__ __launch_bounds__(64, 5) void k_replay_rows_c5(fksk::BuiltinArgs a, i
   replay_rows<FAM_COMPOSITE_LINEAR>(a.W, kernarg_workload(), a.fam, a.weights, a.gheap, a.out, P, queue, qbase, nullptr,
                                     RowNativeArgs{nullptr, nullptr, nullptr}, kRowsPerWave, a.table);
 }
+__global__ __launch_bounds__(64, FKS_ROW_HEAVY_WAVES) void k_replay_rows_split(fksk::BuiltinArgs a, int P, uint32_t* queue,
+                                                                               uint32_t qbase) {
+  replay_rows<FAM_COMPOSITE_LINEAR, RowNoProf, false>(a.W, kernarg_workload(), a.fam, a.weights, a.gheap, a.out, P, queue,
+                                                      qbase, nullptr, RowNativeArgs{nullptr, nullptr, nullptr}, kRowsPerWave,
+                                                      a.table);
+}
 template <int FAM>
 __global__ __launch_bounds__(64, FAM < 0 ? 2 : (FAM == 3 || FAM == 4) ? FKS_ROW_HEAVY_WAVES : FKS_ROW_WAVES)
 void k_replay_rows_prof(fksk::BuiltinArgs a, int P, uint32_t* queue, uint32_t qbase) {
@@ -385,6 +391,7 @@ hipError_t launch_builtin_rows(int fam, int P, int waves, uint32_t* queue, uint3
     FKS_CASE(FAM_FEATURE_LINEAR)
     FKS_CASE(FAM_COMPOSITE_LINEAR)
     case kRowCompositeW5: hipLaunchKernelGGL(k_replay_rows_c5, grid, dim3(64), lds, st, a, P, queue, qbase); break;
+    case kRowCompositeSplit: hipLaunchKernelGGL(k_replay_rows_split, grid, dim3(64), lds, st, a, P, queue, qbase); break;
     default: hipLaunchKernelGGL((k_replay_rows<-1>), grid, dim3(64), lds, st, a, P, queue, qbase);
   }
 #undef FKS_CASE
@@ -403,6 +410,7 @@ int rows_waves_per_cu(int fam, size_t lds) {
     case FAM_COMPOSITE_LINEAR:
       e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_replay_rows<FAM_COMPOSITE_LINEAR>, 64, lds); break;
     case kRowCompositeW5: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_replay_rows_c5, 64, lds); break;
+    case kRowCompositeSplit: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_replay_rows_split, 64, lds); break;
     default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_replay_rows<-1>, 64, lds);
   }
   return e == hipSuccess ? n : -1;
@@ -411,7 +419,7 @@ hipError_t launch_builtin_rows_prof(int fam, int P, int waves, uint32_t* queue, 
                                    const BuiltinArgs& a) {
   const dim3 grid(waves);
   if (fam == FAM_RANDOM_LINEAR) hipLaunchKernelGGL((k_replay_rows_prof<FAM_RANDOM_LINEAR>), grid, dim3(64), lds, st, a, P, queue, qbase);
-  else if (fam == FAM_COMPOSITE_LINEAR || fam == kRowCompositeW5)
+  else if (fam == FAM_COMPOSITE_LINEAR || fam == kRowCompositeW5 || fam == kRowCompositeSplit)
     hipLaunchKernelGGL((k_replay_rows_prof<FAM_COMPOSITE_LINEAR>), grid, dim3(64), lds, st, a, P, queue, qbase);
   else hipLaunchKernelGGL((k_replay_rows_prof<-1>), grid, dim3(64), lds, st, a, P, queue, qbase);
   return hipGetLastError();
@@ -424,7 +432,8 @@ hipError_t set_rows_attrs(int mx) {
   for (hipError_t r : {raise_lds(&k_replay_rows<-1>, mx), raise_lds(&k_replay_rows<FAM_FIRST_FIT>, mx),
                        raise_lds(&k_replay_rows<FAM_BEST_FIT>, mx), raise_lds(&k_replay_rows<FAM_RANDOM_LINEAR>, mx),
                        raise_lds(&k_replay_rows<FAM_FEATURE_LINEAR>, mx),
-                       raise_lds(&k_replay_rows<FAM_COMPOSITE_LINEAR>, mx), raise_lds(&k_replay_rows_c5, mx)})
+                       raise_lds(&k_replay_rows<FAM_COMPOSITE_LINEAR>, mx), raise_lds(&k_replay_rows_c5, mx),
+                       raise_lds(&k_replay_rows_split, mx)})
     if (r != hipSuccess) e = r;
   return e;
 }

@@ -30,11 +30,17 @@
 
 namespace fksd {
 
+// heap slot accesses through flat (generic) addresses: RowHeapT<FLAT>
+#ifndef FKS_ROW_FLAT
+#define FKS_ROW_FLAT 1
+#endif
 // FAM value of the native-program instance: every row calls its own
 // JIT-compiled scorer (jit_abi.h ProgFn) instead of a built-in family.
 constexpr int kFamNative = 100;
-// host family code of the composite row kernel built for 5 waves per SIMD
+// host family codes of composite row-kernel variants: built for 5 waves per
+// SIMD; with exec-masked LDS / HBM heap accesses instead of flat ones
 constexpr int kRowCompositeW5 = 5;
+constexpr int kRowCompositeSplit = 6;
 struct RowNativeArgs {
   const uint64_t* fn;     // [P] device addresses of the programs' scorers
   const int64_t* kc;      // concatenated constant blocks
@@ -84,7 +90,8 @@ __device__ __forceinline__ int row_read(int v, int rbase, int k) {
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
 // ---- one policy's heap, driven by the 16 lanes of its row ---------------------
-struct RowHeap {
+template <bool FLAT = FKS_ROW_FLAT != 0>
+struct RowHeapT {
   FKS_GLOBAL uint64_t* h;     // HBM slice (address = slot + 1)
   FKS_LDS uint64_t* top;      // LDS copy of addresses [0, T + 1)
   int T;                      // slots [0, T) in LDS, T = 2^k - 1
@@ -93,14 +100,34 @@ struct RowHeap {
   int j, rbase;               // lane within the row, first lane of the row
   uint32_t anc, dir;          // subtree node j: BFS indices of its ancestors / of those stepping right
 
-  __device__ __forceinline__ uint64_t ld(int i) const { return i < T ? top[i + 1] : h[i + 1]; }
+  // FLAT: slot i through one generic (flat) address -- the LDS aperture
+  // below T, the HBM slice above: one flat_load / flat_store per access
+  // instead of an exec-masked ds_* / global_* pair (a subtree or ancestor
+  // gather often straddles T within a row, which ran both sides, the LDS
+  // side behind a vmcnt(0) for the shared destination registers).
+  uint64_t* gtop;   // generic address of `top`
+  uint64_t* gh;     // generic address of `h`
+  __device__ __forceinline__ void bind() {   // after setting top and h
+    gtop = (uint64_t*)top;
+    gh = (uint64_t*)h;
+  }
+  __device__ __forceinline__ uint64_t* slot(int i) const { return (i < T ? gtop : gh) + (i + 1); }
+  __device__ __forceinline__ uint64_t ld(int i) const {
+    if constexpr (FLAT) return *slot(i);
+    else return i < T ? top[i + 1] : h[i + 1];
+  }
   __device__ __forceinline__ void st(int i, uint64_t v) const {
-    if (i < T) top[i + 1] = v;
-    else h[i + 1] = v;
+    if constexpr (FLAT) {
+      *slot(i) = v;
+    } else {
+      if (i < T) top[i + 1] = v;
+      else h[i + 1] = v;
+    }
   }
   // children (c, c + 1) of a node, c odd: one aligned 16-byte pair, never
   // split between LDS and HBM (T is odd)
   __device__ __forceinline__ u64x2 ld_pair(int c) const {
+    if constexpr (FLAT) return *reinterpret_cast<const u64x2*>(slot(c));
     if (c < T) return *reinterpret_cast<const FKS_LDS u64x2*>(top + c + 1);
     return *reinterpret_cast<const FKS_GLOBAL u64x2*>(h + c + 1);
   }
@@ -147,17 +174,12 @@ struct RowHeap {
       }
       const bool go_r = valid && (c + 1 < n) && !(vl < vr);
       const uint32_t m = row_ballot(go_r, rbase);
-      const uint32_t ex = row_ballot(valid, rbase);
-      // node j is on the path iff every ancestor in the subtree has children
-      // and chooses the child towards j (lane constants anc / dir), and it
-      // is a path *parent* iff it has children itself: no serial walk
-      const bool on = valid && (ex & anc) == anc && ((m ^ dir) & anc) == 0;
+      // node j is on the path iff every ancestor in the subtree chooses the
+      // child towards j (lane constants anc / dir), and it is a path *parent*
+      // iff it has children itself: no serial walk.  (A valid node's
+      // ancestors are valid: their child pairs sit at smaller heap indices.)
+      const bool on = valid && ((m ^ dir) & anc) == 0;
       const uint32_t onm = row_ballot(on, rbase);
-      const int jd = 31 - __clz(onm);                 // deepest path parent
-      const int kd = jd == 0 ? 0 : jd < 3 ? 1 : jd < 7 ? 2 : 3;
-      const int taken = kd + 1;                       // levels descended this round
-      const int qd = ((pos + 1) << kd) - 1 + (jd - ((1 << kd) - 1));
-      const int next = 2 * qd + 1 + (int)((m >> jd) & 1);   // its chosen child: the new path end
       const uint64_t v = go_r ? vr : vl;
       const uint32_t g = row_ballot(on && last < v, rbase);
       const int jl = g ? __ffs(g) - 1 : kRow;
@@ -165,13 +187,16 @@ struct RowHeap {
         st(q, v);
         mark(q, v);
       }
-      if (g) {
-        const int kk = jl == 0 ? 0 : jl < 3 ? 1 : jl < 7 ? 2 : 3;
-        target = ((pos + 1) << kk) - 1 + (jl - ((1 << kk) - 1));
+      if (g) {   // `last` lands on the slot of the first path entry greater than it
+        target = row_read(q, rbase, jl);
         break;
       }
-      pos = next;
-      if (taken < 4) break;   // reached a leaf
+      // the deepest path parent jd hands over its chosen child (the new path
+      // end) and its depth in the subtree (levels descended this round - 1)
+      const int jd = 31 - __clz(onm);
+      const int nk = row_read(((c + (int)go_r) << 2) | k, rbase, jd);
+      pos = nk >> 2;
+      if ((nk & 3) < 3) break;   // reached a leaf
     }
     if (target < 0) target = pos;
     if (j == 0) { st(target, last); mark(target, last); }
@@ -208,6 +233,7 @@ struct RowHeap {
     return -1;
   }
 };
+using RowHeap = RowHeapT<>;
 
 // Exact fixed-point accumulators 0-4 on lanes 0-4 of the row: sum of v * 2^96
 // over the added doubles (LaneAcc's grid and contract).  Everything the row
@@ -248,15 +274,55 @@ struct RowAcc {
       if (hi >> 62) inexact = 1;   // keep LaneAcc's 2^126 headroom
     }
   }
+  // add() for a quotient n / d of integers 0 <= n <= d < 2^31 (utilisation
+  // ratios, fragmentation): +0.0 or 2^-31 <= v <= 1, so v * 2^96 = M << s
+  // with s in [13, 44] -- always on the grid, no range or sign cases (a value
+  // outside that band still marks the replay inexact)
+  __device__ void add_unit(int k, double v, int j) {
+    const bool mine = j == k;
+    const uint64_t bits = (uint64_t)__double_as_longlong(v);
+    if (mine) ++count;
+    if (bits == 0) return;
+    const int s = (int)(bits >> 52) - 979;
+    const uint64_t M = (bits & ((1ull << 52) - 1)) | (1ull << 52);
+    const uint64_t tl = M << (s & 63), th = M >> ((64 - s) & 63);
+    if (mine) {
+      if (s < 13 || s > 44) inexact = 1;
+      lo += tl;
+      hi += th + (lo < tl);
+    }
+  }
 };
 
 // LDS per wave: [4 x 16 weights | 64 class values | 16 x 4 node constants |
-// 16 x 3 node reciprocals] then per row [deletion bitmap | heap top].
+// 16 x 3 node reciprocals | 10 GPU-capacity reciprocals] then per row
+// [deletion bitmap | heap top].
 constexpr int kNodeConsts = 4;   // cpu_total, mem_total, ngpus, per-GPU milli total
 constexpr int kNodeRecips = 3;   // DevWorkload::node_recip
-constexpr int kRowClassBytes = (kRow * kRowClassSlots * 4 + kRow * kNodeConsts * 4 + kRow * kNodeRecips * 8 + 15) & ~15;
+constexpr int kCapRecips = 10;   // DevWorkload::cap_recip (9) + pad
+constexpr int kRowClassBytes =
+    (kRow * kRowClassSlots * 4 + kRow * kNodeConsts * 4 + kRow * kNodeRecips * 8 + kCapRecips * 8 + 15) & ~15;
 __device__ __forceinline__ FKS_LDS double* row_node_recips(FKS_LDS int32_t* ntab) {
   return reinterpret_cast<FKS_LDS double*>(ntab + kRow * kNodeConsts);
+}
+__device__ __forceinline__ FKS_LDS double* row_cap_recips(FKS_LDS int32_t* ntab) {
+  return row_node_recips(ntab) + kRow * kNodeRecips;
+}
+// sum over the row of a per-lane int32 (|total| < 2^31)
+__device__ __forceinline__ int32_t row_sum_i32(int32_t v) {
+  v += (int32_t)row_ror32<8>((uint32_t)v);
+  v += (int32_t)row_ror32<4>((uint32_t)v);
+  v += (int32_t)row_ror32<2>((uint32_t)v);
+  v += (int32_t)row_ror32<1>((uint32_t)v);
+  return v;
+}
+__device__ __forceinline__ double row_max_f64(double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  v = fmax(v, __longlong_as_double((long long)row_ror64<8>(b)));
+  v = fmax(v, __longlong_as_double((long long)row_ror64<4>((uint64_t)__double_as_longlong(v))));
+  v = fmax(v, __longlong_as_double((long long)row_ror64<2>((uint64_t)__double_as_longlong(v))));
+  v = fmax(v, __longlong_as_double((long long)row_ror64<1>((uint64_t)__double_as_longlong(v))));
+  return v;
 }
 // the node tables (lanes < 16 of one wave)
 __device__ __forceinline__ void fill_node_tables(const DevWorkload& W, FKS_LDS int32_t* ntab, int lane) {
@@ -269,6 +335,7 @@ __device__ __forceinline__ void fill_node_tables(const DevWorkload& W, FKS_LDS i
 #pragma unroll
     for (int k = 0; k < kNodeRecips; ++k) z[lane * kNodeRecips + k] = W.node_recip[lane * kNodeRecips + k];
   }
+  if (lane <= kGmax) row_cap_recips(ntab)[lane] = W.cap_recip[lane];
 }
 __host__ __device__ inline size_t rows_row_bytes(int n_pods, int T) {
   return (size_t)lds_delmap_words(n_pods) * 4 + (size_t)(T + 1) * 8;
@@ -321,7 +388,7 @@ constexpr int kRowProfBytes = 128;
 // FAM == kFamNative: natively compiled programs (`nat`), one per row; only
 // rows < rows_active claim policies, so small batches can run one program per
 // wave (the whole heap in LDS, no other row's divergence in the event loop).
-template <int FAM, class Prof = RowNoProf>
+template <int FAM, class Prof = RowNoProf, bool FLAT = FKS_ROW_FLAT != 0>
 __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const int32_t* fam, const double* weights,
                             uint64_t* gheap, DevResult* out, int P, uint32_t* queue, uint32_t qbase,
                             uint64_t* prof_out = nullptr, RowNativeArgs nat = RowNativeArgs{nullptr, nullptr, nullptr},
@@ -361,10 +428,11 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
   // registers through the pop
   FKS_LDS int32_t* ntab = cls_lds + kRow * kRowClassSlots;
   fill_node_tables(W, ntab, lane);
-  RowHeap heap;
+  RowHeapT<FLAT> heap;
   heap.delmap = reinterpret_cast<FKS_LDS uint32_t*>(rowbase);
   heap.top = reinterpret_cast<FKS_LDS uint64_t*>(rowbase + (size_t)lds_delmap_words(N) * 4);
   heap.h = global_ptr(gheap + (size_t)slot * row_heap_entries(N));
+  heap.bind();
   heap.T = T;
   heap.lb = lb;
   heap.j = jv;
@@ -508,6 +576,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
         load_consts();
         int lexc = EXC_NONE;
         int64_t s = 0;
+        double sd = 0.0;   // composite: the truncated score as a double (trunc_score_f)
         if constexpr (kNative) {
           // the program holds the template's feasibility prologue itself
           if (node_valid) {
@@ -526,20 +595,27 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
           const FKS_LDS double* wq = wl;
           if constexpr (kComp) {
             const FKS_LDS double* z = row_node_recips(ntab) + jv * kNodeRecips;
-            const typename BuiltinScorerDev<FAM>::RowRecip rz{z[0], z[1], z[2], W.z1000, pcm};
-            s = trunc_score(BuiltinScorerDev<FAM>::composite_row(nr, pod, wq, rz), lexc);
+            const double zcap = pod.ngpu > 0 ? row_cap_recips(ntab)[nr.gpu_left[0]] : 0.0;
+            const typename BuiltinScorerDev<FAM>::RowRecip rz{z[0], z[1], z[2], W.z1000, pcm, zcap};
+            sd = trunc_score_f(BuiltinScorerDev<FAM>::composite_row(nr, pod, wq, rz), lexc);
           } else {
             s = BuiltinScorerDev<FAM>::template score_weights<1>(family, wq, 0, nr, pod, lexc);
           }
-          if (lexc != EXC_NONE) s = 0;
+          if (lexc != EXC_NONE) { s = 0; sd = 0.0; }
         }
         const uint32_t bad = row_ballot(lexc != EXC_NONE, rbase);
         if (bad) {
           exc = row_read(lexc, rbase, __ffs(bad) - 1);
           break;
         }
-        const int64_t m = (int64_t)row_max_u64((uint64_t)s);   // scores are >= 0
-        const int best_node = m > 0 ? __ffs(row_ballot(s == m, rbase)) - 1 : -1;
+        int best_node;
+        if constexpr (kComp) {
+          const double md = row_max_f64(sd);   // scores are >= 0
+          best_node = md > 0.0 ? __ffs(row_ballot(sd == md, rbase)) - 1 : -1;
+        } else {
+          const int64_t m = (int64_t)row_max_u64((uint64_t)s);   // scores are >= 0
+          best_node = m > 0 ? __ffs(row_ballot(s == m, rbase)) - 1 : -1;
+        }
         uint64_t push_item = 0;   // never 0 for a real entry: keys hold the pod rank's time > 0 or kind
         prof.mark(PH_SCORE);
 
@@ -559,17 +635,19 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
           }
           if (mcls >= 0) {
             const int mv = cls_lds[mcls];
-            int64_t stranded = 0;
+            int32_t stranded = 0;   // the cluster's GPU milli total < 2^31 (host-checked)
 #pragma unroll
             for (int g = 0; g < kGmax; ++g) {
               const int l = nr.gml[0][g];
               if (g < nr.ngpus[0] && 0 < l && l < mv) stranded += l;
             }
-            stranded = row_sum_i64(node_valid ? stranded : 0);
+            stranded = row_sum_i32(node_valid ? stranded : 0);
             const int64_t tg = cold()->tot_gmilli;
-            frag = tg > 0 ? (double)stranded / (double)tg : 0.0;
+            // stranded in [0, tg]: W.z_tg is verified there
+            frag = tg <= 0 ? 0.0 : W.z_tg != 0.0 ? div_by_recip((double)stranded, (double)tg, W.z_tg)
+                                                 : (double)stranded / (double)tg;
           }
-          acc.add(4, frag, jv);
+          acc.add_unit(4, frag, jv);
           const int f = heap.first_deletion(n);
           if (f >= 0) {
             const uint64_t nt = (heap.ld(f) >> tshift) + 1;
@@ -631,7 +709,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
         const double r1 = Ws->tot_mem > 0 ? (double)used_mem / (double)Ws->tot_mem : 0.0;
         const double r2 = Ws->tot_gcnt > 0 ? (double)used_gcnt / (double)Ws->tot_gcnt : 0.0;
         const double r3 = Ws->tot_gmilli > 0 ? (double)used_gml / (double)Ws->tot_gmilli : 0.0;
-        acc.add(0, r0, jv); acc.add(1, r1, jv); acc.add(2, r2, jv); acc.add(3, r3, jv);
+        acc.add_unit(0, r0, jv); acc.add_unit(1, r1, jv); acc.add_unit(2, r2, jv); acc.add_unit(3, r3, jv);
         ++ksnap;
         if (ksnap < Ws->n_fire) {
           next_fire = (int32_t)*global_ptr(&Ws->snap_fire[ksnap]);

@@ -23,6 +23,17 @@ __device__ __forceinline__ int64_t trunc_score(double s, int& exc) {
   return v > 1 ? v : 1;
 }
 
+// trunc_score as a double: |s| < 2^63, so trunc(s) is exactly the int64 the
+// integer path produces and doubles order like those integers (row kernel:
+// no f64 -> i64 conversion, 64-bit max as v_max_f64)
+__device__ __forceinline__ double trunc_score_f(double s, int& exc) {
+  if (isnan(s)) { exc = EXC_VALUE; return 0.0; }
+  if (isinf(s)) { exc = EXC_OVERFLOW; return 0.0; }
+  if (fabs(s) >= 9.2233720368547758e18) { exc = EXC_UNSUPPORTED; return 0.0; }
+  const double v = trunc(s);
+  return v > 1.0 ? v : 1.0;
+}
+
 template <int NPASS>
 __device__ __forceinline__ bool feasible(int ps, const NodeRegs<NPASS>& nr, const PodView& pod) {
   if (pod.cpu > nr.cpu_left[ps] || pod.mem > nr.mem_left[ps] || pod.ngpu > nr.gpu_left[ps]) return false;
@@ -186,6 +197,7 @@ struct BuiltinScorerDev {
   //    NaN), so the caller passes here only policies whose weights all are.
   struct RowRecip {
     double zc, zm, zg, z1000, pcm;
+    double zcap;   // RN(1 / max(gpu_left * gmilli_total, 1)) when fast_cap, else 0
   };
   template <class WP>
   __device__ static double composite_row(const NodeRegs<1>& nr, const PodView& pod, WP w, const RowRecip& rz) {
@@ -213,7 +225,9 @@ struct BuiltinScorerDev {
     s = s + (mem_u < 0.7 ? w[3] : w[4]) * (1.0 - mem_u);
     if (gpod) {
       const int64_t cap = (int64_t)nr.gpu_left[0] * nr.gt(0, 0);
-      const double gpu_u = (double)(cap - free_m) / (double)(cap > 1 ? cap : 1);
+      const double nu = (double)(cap - free_m), du = (double)(cap > 1 ? cap : 1);
+      // zcap: verified for |numerator| <= 8 x the cluster's one per-GPU milli total
+      const double gpu_u = rz.zcap != 0.0 ? div_by_recip(nu, du, rz.zcap) : nu / du;
       s = s + (gpu_u < 0.7 ? w[5] : w[6]) * (1.0 - gpu_u);
       const uint32_t d = pod.gmilli > 1 ? (uint32_t)pod.gmilli : 1u;
       s = s + w[7] * (double)((uint32_t)free_m % d);

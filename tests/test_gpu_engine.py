@@ -153,14 +153,18 @@ def test_row_kernel_matches_cpu(default_workload, top):
                           ce.simulate_builtin_batch(default_workload, "composite_linear", w))
 
 
-@pytest.mark.parametrize("waves", [4, 5])
-def test_row_composite_reciprocal_path_matches_cpu(default_workload, waves):
-    """The composite row instance (host-verified reciprocal divisions, no zero-weight tests,
-    one member per threshold pair) at 4 and 5 waves per SIMD == CPU oracle, including
-    zero weights and a huge-weight row that overflows."""
+@pytest.mark.parametrize("waves,flat", [(4, True), (5, True), (4, False)])
+def test_row_composite_reciprocal_path_matches_cpu(default_workload, waves, flat):
+    """The composite row instances (host-verified reciprocal divisions, no zero-weight tests,
+    one member per threshold pair, double-valued argmax; 4 / 5 waves per SIMD; flat or
+    exec-masked LDS/HBM heap accesses) == CPU oracle, including zero weights and a
+    huge-weight row that overflows."""
     from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
-    dev = he.DeviceEvaluator(default_workload, options={"row_kernel": "on", "row_composite_waves": waves})
-    assert dev.info()["fast_div"] == 1 and dev.info()["row_composite_waves"] == waves
+    dev = he.DeviceEvaluator(default_workload, options={"row_kernel": "on", "row_composite_waves": waves,
+                                                        "row_flat": flat})
+    info = dev.info()
+    assert info["fast_div"] == 1 and info["cap_recips"] and info["frag_recip"]
+    assert info["row_composite_waves"] == waves and info["row_flat"] == flat
     w = fam.sample_composite_linear(70, np.random.default_rng(31 + waves))
     w[1, ::2] = 0.0
     w[2, :] = -0.0
