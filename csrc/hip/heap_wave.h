@@ -31,21 +31,37 @@ constexpr int kDelKind = 2;
 
 __device__ __forceinline__ bool key_lt(uint64_t a, uint64_t b, int lb) { return (a >> lb) < (b >> lb); }
 
-struct WaveHeap {
+// FLAT (HBM heaps with an LDS top): slot i through one generic address --
+// one flat_load / flat_store instead of an exec-masked ds_* / global_* pair,
+// which ran both sides whenever a gather straddled T (and the LDS side waited
+// for the HBM side: same destination registers).
+template <bool FLAT = false>
+struct WaveHeapT {
   FKS_GLOBAL uint64_t* h;   // keys (slots >= T), the policy's HBM slice
   FKS_LDS uint64_t* top;    // LDS copy of slots [0, T)
   int T;
   FKS_LDS uint32_t* delmap; // bit p set <=> slot p holds a deletion
   int lb;             // low (payload) bits below the (time, rank) compare key
   int lane;           // this lane's id, refreshed (opaquely) per event by the caller
+  uint64_t* gtop;     // FLAT: generic addresses of top / h (bind())
+  uint64_t* gh;
 
+  __device__ __forceinline__ void bind() {   // after setting top and h
+    gtop = (uint64_t*)top;
+    gh = (uint64_t*)h;
+  }
   __device__ __forceinline__ uint64_t ld(int i) const {
+    if constexpr (FLAT) return *((i < T ? gtop : gh) + i);
     if (i < T) return top[i];
     return h[i];
   }
   __device__ __forceinline__ void st(int i, uint64_t v) const {
-    if (i < T) top[i] = v;
-    else h[i] = v;
+    if constexpr (FLAT) {
+      *((i < T ? gtop : gh) + i) = v;
+    } else {
+      if (i < T) top[i] = v;
+      else h[i] = v;
+    }
   }
 
   __device__ __forceinline__ void mark(int pos, uint64_t v) const {
@@ -166,5 +182,6 @@ struct WaveHeap {
     return -1;
   }
 };
+using WaveHeap = WaveHeapT<false>;
 
 }  // namespace fksd

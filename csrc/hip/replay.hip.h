@@ -199,8 +199,8 @@ __device__ __forceinline__ int pick_gpus(const NodeRegs<NPASS>& nr, int ps, int 
 constexpr int kInvCols = 3 + kGmax;   // cpu, mem, gpu count, per-GPU milli
 __host__ __device__ inline int inv_words_for(int npass) { return (kWave * npass * kInvCols * 4 + 7) / 8; }
 
-template <int NPASS>
-__device__ bool invariants_hold(const DevWorkload& W, const WaveHeap& heap, int n, const NodeRegs<NPASS>& nr,
+template <int NPASS, class Heap>
+__device__ bool invariants_hold(const DevWorkload& W, const Heap& heap, int n, const NodeRegs<NPASS>& nr,
                                 FKS_LDS int32_t* inv, int lane) {
   for (int i = lane; i < kWave * NPASS * kInvCols; i += kWave) inv[i] = 0;
   __syncthreads();
@@ -243,7 +243,7 @@ __device__ bool invariants_hold(const DevWorkload& W, const WaveHeap& heap, int 
 }
 
 // ----------------------------------------------------------------------------
-template <int NPASS, class Scorer, class Prof = NoProf>
+template <int NPASS, class Scorer, class Prof = NoProf, bool FLAT = false>
 __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Scorer& scorer, FKS_GLOBAL uint64_t* hbuf,
                            FKS_LDS uint64_t* htop, int T, FKS_LDS uint32_t* delmap, FKS_LDS int32_t* inv,
                            DevResult* out,
@@ -264,9 +264,10 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
   const uint64_t time_max = (W.time_bits >= 63) ? ~0ull : ((1ull << W.time_bits) - 1);
   const int N = W.n_pods;
 
-  WaveHeap heap;
+  WaveHeapT<FLAT> heap;
   heap.h = hbuf;
   heap.top = htop;
+  heap.bind();
   heap.T = T;
   heap.delmap = delmap;
   heap.lb = lb;

@@ -42,6 +42,9 @@ static_assert(offsetof(fksk::NativeArgs, W) == 0, "DevWorkload must open the ker
 #ifndef FKS_NPASS
 #define FKS_NPASS 1
 #endif
+#ifndef FKS_WAVE_FLAT
+#define FKS_WAVE_FLAT 1   // HBM-heap wave kernels: flat heap accesses (heap_wave.h WaveHeapT)
+#endif
 
 using namespace fksd;
 
@@ -132,7 +135,8 @@ __global__ FKS_FAM_BOUNDS(GHEAP, FAM, NPASS) void k_replay_builtin(fksk::Builtin
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   BuiltinScorerDev<FAM> sc;
   load_policy<FAM>(sc, s, a, p);
-  replay_one<NPASS>(a.W, kernarg_workload(), sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p);
+  replay_one<NPASS, BuiltinScorerDev<FAM>, NoProf, GHEAP && FKS_WAVE_FLAT>(a.W, kernarg_workload(), sc, s.h, s.top, s.T,
+                                                                           s.delmap, s.inv, a.out + p);
 }
 
 template <int NPASS, bool GHEAP>

@@ -316,12 +316,26 @@ __device__ __forceinline__ int32_t row_sum_i32(int32_t v) {
   v += (int32_t)row_ror32<1>((uint32_t)v);
   return v;
 }
+__device__ __forceinline__ uint32_t row_min_u32(uint32_t v) {
+  v = min(v, row_ror32<8>(v));
+  v = min(v, row_ror32<4>(v));
+  v = min(v, row_ror32<2>(v));
+  v = min(v, row_ror32<1>(v));
+  return v;
+}
+// max of two non-NaN doubles: one v_max_f64 (fmax() adds two canonicalising
+// v_max_f64 for IEEE NaN quieting, which scores never need)
+__device__ __forceinline__ double max_nn(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// row maximum of finite scores
 __device__ __forceinline__ double row_max_f64(double v) {
-  const uint64_t b = (uint64_t)__double_as_longlong(v);
-  v = fmax(v, __longlong_as_double((long long)row_ror64<8>(b)));
-  v = fmax(v, __longlong_as_double((long long)row_ror64<4>((uint64_t)__double_as_longlong(v))));
-  v = fmax(v, __longlong_as_double((long long)row_ror64<2>((uint64_t)__double_as_longlong(v))));
-  v = fmax(v, __longlong_as_double((long long)row_ror64<1>((uint64_t)__double_as_longlong(v))));
+  v = max_nn(v, __longlong_as_double((long long)row_ror64<8>((uint64_t)__double_as_longlong(v))));
+  v = max_nn(v, __longlong_as_double((long long)row_ror64<4>((uint64_t)__double_as_longlong(v))));
+  v = max_nn(v, __longlong_as_double((long long)row_ror64<2>((uint64_t)__double_as_longlong(v))));
+  v = max_nn(v, __longlong_as_double((long long)row_ror64<1>((uint64_t)__double_as_longlong(v))));
   return v;
 }
 // the node tables (lanes < 16 of one wave)
@@ -540,6 +554,9 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
       const int rank = (int)((top >> lb) & ((1ull << rb) - 1));
       typedef int v4i __attribute__((ext_vector_type(4)));
       const v4i precv = *reinterpret_cast<const FKS_GLOBAL v4i*>(global_ptr(&W.pod[rank]));
+      // composite: the pod's cpu / mem quotient, in flight during the pop
+      double pcm = 0.0;
+      if (FAM == FAM_COMPOSITE_LINEAR) pcm = *global_ptr(&W.pod_cm[rank]);
       const uint64_t last = heap.ld(n - 1);
       --n;
       if (n > 0) heap.pop_reinsert(n, last);
@@ -571,8 +588,6 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
         // composite: composite_row (the host runs this instance only on
         // finite weights and verified reciprocals, engine_host stage_builtin)
         constexpr bool kComp = FAM == FAM_COMPOSITE_LINEAR;
-        double pcm = 0.0;
-        if (kComp) pcm = *global_ptr(&cold()->pod_cm[rank]);
         load_consts();
         int lexc = EXC_NONE;
         int64_t s = 0;
@@ -627,13 +642,16 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
               if (sl == (pod.cls >> 4) && jv == (pod.cls & 15)) wcnt[sl] += 1;
           }
           double frag = 0.0;
-          int mcls = -1;
+          // smallest waiting class: each lane offers its lowest nonempty slot's
+          // class (sl * 16 + j), the row takes the minimum (64: none waits)
+          uint32_t nzs = 0;
 #pragma unroll
-          for (int sl = 0; sl < kRowClassSlots; ++sl) {
-            const uint32_t b = row_ballot(wcnt[sl] > 0, rbase);
-            if (mcls < 0 && b) mcls = sl * kRow + __ffs(b) - 1;
-          }
-          if (mcls >= 0) {
+          for (int sl = kRowClassSlots - 1; sl >= 0; --sl) nzs = wcnt[sl] > 0 ? (uint32_t)sl : nzs;
+          bool any = false;
+#pragma unroll
+          for (int sl = 0; sl < kRowClassSlots; ++sl) any = any || wcnt[sl] > 0;
+          const int mcls = (int)row_min_u32(any ? nzs * kRow + (uint32_t)jv : 64u);
+          if (mcls < 64) {
             const int mv = cls_lds[mcls];
             int32_t stranded = 0;   // the cluster's GPU milli total < 2^31 (host-checked)
 #pragma unroll

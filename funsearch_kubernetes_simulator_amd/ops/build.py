@@ -123,7 +123,7 @@ HIP_UNITS = [("module", "module.hip", [])] + [
 
 def _hip_flags() -> List[str]:
     # occupancy knobs of the replay kernels (waves per SIMD), for A/B builds
-    knobs = [f"-D{k}={os.environ[k]}" for k in ("FKS_LIGHT_WAVES", "FKS_HEAVY_WAVES", "FKS_ROW_WAVES", "FKS_ROW_HEAVY_WAVES", "FKS_NP4_WAVES", "FKS_DUO_SLEEP") if os.environ.get(k)]
+    knobs = [f"-D{k}={os.environ[k]}" for k in ("FKS_LIGHT_WAVES", "FKS_HEAVY_WAVES", "FKS_ROW_WAVES", "FKS_ROW_HEAVY_WAVES", "FKS_NP4_WAVES", "FKS_DUO_SLEEP", "FKS_WAVE_FLAT") if os.environ.get(k)]
     return [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-ffp-contract=off",
             "-fno-fast-math", "-munsafe-fp-atomics", "-Wno-unused-result", *knobs,
             *_py_includes(), f"-I{CSRC_DIR / 'include'}", f"-I{CSRC_DIR / 'hip'}"]
