@@ -133,12 +133,16 @@ def migration_records(islands: List[ParamIsland], k: int) -> np.ndarray:
 def inject(islands: List[ParamIsland], glob: np.ndarray, rank: int = 0) -> None:
     """Ring migration over the global island index (rank-major): island g
     receives island g-1's migrants.  glob: [W, I, k, R] all-gathered records."""
+    for li in range(len(islands)):
+        inject_one(islands, li, glob, rank)
+
+
+def inject_one(islands: List[ParamIsland], li: int, glob: np.ndarray, rank: int = 0) -> None:
+    """inject() for local island `li` alone (asynchronous migration: each
+    island takes its ring predecessor's migrants when it reaches a boundary)."""
     W, I, k = glob.shape[0], glob.shape[1], glob.shape[2]
     flat = glob.reshape(W * I, k, -1)
-    for li, isl in enumerate(islands):
-        g = rank * I + li
-        src = (g - 1) % (W * I)
-        isl.accept(flat[src])
+    islands[li].accept(flat[(rank * I + li - 1) % (W * I)])
 
 
 def migrate(islands: List[ParamIsland], k: int, all_gather=None) -> None:

@@ -95,6 +95,29 @@ def test_gloo_collectives_and_migration(tmp_path):
     assert out["ok"] and out["best_island0"] >= 100
 
 
+def test_inject_one_per_island_equals_ring_inject():
+    """bench.py's asynchronous migration injects island by island (inject_one);
+    applied to every island it is the ring migration of inject()."""
+    import numpy as np
+    from funsearch_kubernetes_simulator_amd.funsearch.param_islands import (
+        inject, inject_one, make_islands, migration_records)
+
+    def fresh():
+        isl = make_islands(3, "random_linear", 8, 4, seed=5)
+        for k, i in enumerate(isl):
+            w = i.propose()
+            i.update(w, np.arange(len(w)) + 100.0 * k)
+        return isl
+    a, b = fresh(), fresh()
+    glob = np.stack([migration_records(a, 2), migration_records(a, 2) + 0.5])   # two ranks
+    inject(a, glob, rank=1)
+    for li in range(len(b)):
+        inject_one(b, li, glob, rank=1)
+    for x, y in zip(a, b):
+        assert np.array_equal(x.elite_scores, y.elite_scores)
+        assert np.array_equal(x.elites, y.elites)
+
+
 def test_bench_two_ranks_cpu():
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                         "--master-addr", "127.0.0.1", "--master-port", str(30000 + os.getpid() % 1000),
