@@ -60,6 +60,8 @@ def main() -> None:
                     help="wave kernel (> 16 nodes): heap slots kept in LDS per policy (2^k - 1; -1: auto)")
     ap.add_argument("--row-composite-waves", type=int, default=4, choices=[4, 5],
                     help="waves per SIMD of the composite row kernel (register budget 128 / 96 VGPRs)")
+    ap.add_argument("--row-min-lds", type=int, default=0,
+                    help="occupancy experiments: at least this many LDS bytes per row-kernel wave")
     ap.add_argument("--row-split-heap", action="store_true",
                     help="composite row kernel with exec-masked LDS/HBM heap accesses instead of flat ones")
     ap.add_argument("--row-wave-share", type=float, default=1.0,
@@ -106,7 +108,8 @@ def main() -> None:
         device = "cpu"
     # the per-event trace hash only serves cross-engine equality tests: off here
     opts = {"heap_mode": args.heap_mode, "trace_hash": False, "row_wave_share": args.row_wave_share,
-            "row_composite_waves": args.row_composite_waves, "row_flat": not args.row_split_heap}
+            "row_composite_waves": args.row_composite_waves, "row_flat": not args.row_split_heap,
+            "row_min_lds": args.row_min_lds}
     if args.heap_top >= 0:
         opts["heap_top"] = args.heap_top
     ev = Evaluator(workload, device=device, options=opts,

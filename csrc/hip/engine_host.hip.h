@@ -270,6 +270,8 @@ class DeviceEngine {
       comp_waves_ = w;
     }
     if (o.contains("row_flat")) row_flat_ = o["row_flat"].cast<bool>();
+    // occupancy experiments: at least this much LDS per row-kernel wave (fewer resident waves)
+    if (o.contains("row_min_lds")) row_min_lds_ = (size_t)std::max<int64_t>(0, o["row_min_lds"].cast<int64_t>());
     if (o.contains("row_wave_share")) {
       const double f = o["row_wave_share"].cast<double>();
       if (!(f > 0.0 && f <= 4.0)) throw std::invalid_argument("row_wave_share must be in (0, 4]");
@@ -609,6 +611,7 @@ class DeviceEngine {
           for (int j = 0; j <= kGmax; ++j) W_.cap_recip[j] = 0.0;   // all or none
     }
     // fragmentation divisor: stranded milli in [0, tot_gmilli]
+    W_.tot_gmilli_d = (double)W_.tot_gmilli;
     W_.z_tg = W_.tot_gmilli > 0 && W_.tot_gmilli <= (int64_t(1) << 24)
                   ? fks_recip_verified(W_.tot_gmilli, W_.tot_gmilli, cache) : 0.0;
     W_.z1000 = z1000;
@@ -826,7 +829,7 @@ class DeviceEngine {
                                                        : s.fam_spec;
     const std::pair<int, int> lay = row_layout(kf);
     Wl.heap_top = lay.first;
-    const size_t lds = rows_lds_bytes(W_.n_pods, Wl.heap_top) + (profiled ? kRowProfBytes : 0);
+    const size_t lds = std::max(rows_lds_bytes(W_.n_pods, Wl.heap_top) + (profiled ? kRowProfBytes : 0), row_min_lds_);
     if (lds > kMaxLds) throw std::invalid_argument("row kernel layout exceeds the 160 KiB LDS");
     // persistent waves: at most `row_wave_share` of what stays resident on the
     // chip, each row draining the policy queue.  A wave holds its slot until
@@ -960,6 +963,7 @@ class DeviceEngine {
   bool native_duo_ = true;     // two-wave kernel for one-program-per-wave batches
   int native_rows_opt_ = 0;    // rows per wave for native programs (0: auto)
   int last_native_rows_ = 0, last_native_waves_ = 0;
+  size_t row_min_lds_ = 0;
   bool row_flat_ = true;  // composite row kernel: flat heap accesses (false: exec-masked ds / global)
   int comp_waves_ = 4;   // composite row kernel: 4 or 5 waves per SIMD (row_composite_waves)
   mutable std::vector<std::pair<int, int>> row_layout_cache_ = std::vector<std::pair<int, int>>(8, {0, 0});

@@ -78,6 +78,7 @@ struct DevWorkload {
   double cap_recip[kGmax + 1];
   // fragmentation: RN(1 / tot_gmilli) verified on [0, tot_gmilli] (0: divide)
   double z_tg;
+  double tot_gmilli_d;        // (double)tot_gmilli
 };
 
 // RN(n / d) from z = RN(1/d) with one remainder step (Markstein): exact for
@@ -121,6 +122,7 @@ struct PodView {
   int32_t cpu, mem, dur, gmilli, ngpu, cls;
   int64_t ctime;  // current creation time (event time)
   int32_t rank;
+  double cm;      // cpu / max(mem, 1) (DevWorkload::pod_cm; set where a scorer reads it)
 };
 
 // Scorer contract:  score<NPASS>(pass, node_regs, pod, exc) -> int64 priority
@@ -339,6 +341,7 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
     pod.cpu = uni(precv.x); pod.mem = uni(precv.y); pod.dur = uni(precv.z);
     pod.gmilli = pw & 0xFFFF; pod.ngpu = (pw >> 16) & 0xFF; pod.cls = (pw >> 24) & 0xFF;
     pod.ctime = t; pod.rank = rank;
+    pod.cm = W.pod_cm[rank];   // scalar load (dropped by the compiler where no scorer reads it)
     prof.mark(PH_POP);
 
     if (kind == kDelete) {

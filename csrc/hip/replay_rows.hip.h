@@ -298,7 +298,7 @@ struct RowAcc {
 // 16 x 3 node reciprocals | 10 GPU-capacity reciprocals] then per row
 // [deletion bitmap | heap top].
 constexpr int kNodeConsts = 4;   // cpu_total, mem_total, ngpus, per-GPU milli total
-constexpr int kNodeRecips = 3;   // DevWorkload::node_recip
+constexpr int kNodeRecips = 6;   // DevWorkload::node_recip (3), then the same divisors as doubles
 constexpr int kCapRecips = 10;   // DevWorkload::cap_recip (9) + pad
 constexpr int kRowClassBytes =
     (kRow * kRowClassSlots * 4 + kRow * kNodeConsts * 4 + kRow * kNodeRecips * 8 + kCapRecips * 8 + 15) & ~15;
@@ -347,7 +347,13 @@ __device__ __forceinline__ void fill_node_tables(const DevWorkload& W, FKS_LDS i
     ntab[lane * kNodeConsts + 3] = W.gml_total[lane * kGmax];
     FKS_LDS double* z = row_node_recips(ntab);
 #pragma unroll
-    for (int k = 0; k < kNodeRecips; ++k) z[lane * kNodeRecips + k] = W.node_recip[lane * kNodeRecips + k];
+    for (int k = 0; k < 3; ++k) z[lane * kNodeRecips + k] = W.node_recip[lane * 3 + k];
+    // max(cpu_total, 1), max(mem_total, 1), max(ngpus, 1) as doubles: an LDS read
+    // per creation event instead of an int -> f64 conversion on the VALU
+    const int32_t ct = W.cpu_total[lane], mt = W.mem_total[lane], ng = W.ngpus[lane];
+    z[lane * kNodeRecips + 3] = (double)(ct > 1 ? ct : 1);
+    z[lane * kNodeRecips + 4] = (double)(mt > 1 ? mt : 1);
+    z[lane * kNodeRecips + 5] = (double)(ng > 1 ? ng : 1);
   }
   if (lane <= kGmax) row_cap_recips(ntab)[lane] = W.cap_recip[lane];
 }
@@ -611,7 +617,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
           if constexpr (kComp) {
             const FKS_LDS double* z = row_node_recips(ntab) + jv * kNodeRecips;
             const double zcap = pod.ngpu > 0 ? row_cap_recips(ntab)[nr.gpu_left[0]] : 0.0;
-            const typename BuiltinScorerDev<FAM>::RowRecip rz{z[0], z[1], z[2], W.z1000, pcm, zcap};
+            const typename BuiltinScorerDev<FAM>::RowRecip rz{z[0], z[1], z[2], W.z1000, pcm, zcap, z[3], z[4], z[5]};
             sd = trunc_score_f(BuiltinScorerDev<FAM>::composite_row(nr, pod, wq, rz), lexc);
           } else {
             s = BuiltinScorerDev<FAM>::template score_weights<1>(family, wq, 0, nr, pod, lexc);
@@ -657,13 +663,13 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
 #pragma unroll
             for (int g = 0; g < kGmax; ++g) {
               const int l = nr.gml[0][g];
-              if (g < nr.ngpus[0] && 0 < l && l < mv) stranded += l;
+              if (0 < l && l < mv) stranded += l;   // GPUs past ngpus hold 0 milli (host padding)
             }
             stranded = row_sum_i32(node_valid ? stranded : 0);
             const int64_t tg = cold()->tot_gmilli;
             // stranded in [0, tg]: W.z_tg is verified there
-            frag = tg <= 0 ? 0.0 : W.z_tg != 0.0 ? div_by_recip((double)stranded, (double)tg, W.z_tg)
-                                                 : (double)stranded / (double)tg;
+            frag = tg <= 0 ? 0.0 : W.z_tg != 0.0 ? div_by_recip((double)stranded, W.tot_gmilli_d, W.z_tg)
+                                                 : (double)stranded / W.tot_gmilli_d;
           }
           acc.add_unit(4, frag, jv);
           const int f = heap.first_deletion(n);

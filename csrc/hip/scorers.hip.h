@@ -27,9 +27,10 @@ __device__ __forceinline__ int64_t trunc_score(double s, int& exc) {
 // integer path produces and doubles order like those integers (row kernel:
 // no f64 -> i64 conversion, 64-bit max as v_max_f64)
 __device__ __forceinline__ double trunc_score_f(double s, int& exc) {
-  if (isnan(s)) { exc = EXC_VALUE; return 0.0; }
-  if (isinf(s)) { exc = EXC_OVERFLOW; return 0.0; }
-  if (fabs(s) >= 9.2233720368547758e18) { exc = EXC_UNSUPPORTED; return 0.0; }
+  if (!(fabs(s) < 9.2233720368547758e18)) {   // NaN, infinity or beyond int64: one compare on the common path
+    exc = isnan(s) ? EXC_VALUE : isinf(s) ? EXC_OVERFLOW : EXC_UNSUPPORTED;
+    return 0.0;
+  }
   const double v = trunc(s);
   return v > 1.0 ? v : 1.0;
 }
@@ -119,6 +120,9 @@ struct BuiltinScorerDev {
         return trunc_score(s, exc);
       }
       case FAM_COMPOSITE_LINEAR:
+        // the composite instance (FAM fixed): the host runs it only on finite
+        // weights with verified reciprocals (engine_host stage_builtin)
+        if constexpr (FAM == FAM_COMPOSITE_LINEAR) return trunc_score(composite_fast<NPASS>(ps, nr, pod, w), exc);
         return trunc_score(composite<NPASS>(ps, nr, pod, w), exc);
     }
     exc = EXC_UNSUPPORTED;
@@ -183,6 +187,54 @@ struct BuiltinScorerDev {
     return s;
   }
 
+  // composite() on the wave kernel for finite weights, bit for bit: no `w != 0`
+  // tests, one member per threshold pair, 0/1 indicators add the weight (see
+  // composite_row), the host's pod quotient and the verified 1/1000 (the
+  // literal 0.001 is RN(1/1000); the host's fast_div check covers [0, 2^21)).
+  // The per-node divisions stay divisions: reciprocals for 4 node slots per
+  // lane would cost more registers than the config-5 kernel has.
+  template <int NPASS, class WP>
+  __device__ static double composite_fast(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, WP w) {
+    const int ng = nr.ngpus[ps];
+    const bool gpod = pod.ngpu > 0;
+    const int32_t ct = nr.cpu_total[ps], mt = nr.mem_total[ps];
+    const int32_t cl = nr.cpu_left[ps], ml = nr.mem_left[ps];
+    const double cpu_u = (double)((int64_t)ct - cl) / (double)(ct > 1 ? ct : 1);
+    const double mem_u = (double)((int64_t)mt - ml) / (double)(mt > 1 ? mt : 1);
+    int32_t free_m = 0, idle = 0, gmax = 0, gmin = 0, best = -1;
+#pragma unroll
+    for (int j = 0; j < kGmax; ++j) {
+      if (j < ng) {
+        const int32_t l = nr.gml[ps][j];
+        free_m += l;
+        idle += (l == nr.gt(ps, j));
+        gmax = (j == 0 || l > gmax) ? l : gmax;
+        gmin = (j == 0 || l < gmin) ? l : gmin;
+        if (gpod && l >= pod.gmilli && (best < 0 || l - pod.gmilli < best)) best = l - pod.gmilli;
+      }
+    }
+    double s = 0.0 + w[0];
+    s = s + (cpu_u < 0.7 ? w[1] : w[2]) * (1.0 - cpu_u);
+    s = s + (mem_u < 0.7 ? w[3] : w[4]) * (1.0 - mem_u);
+    if (gpod) {
+      const int64_t cap = (int64_t)nr.gpu_left[ps] * nr.gt(ps, 0);
+      const double gpu_u = (double)(cap - free_m) / (double)(cap > 1 ? cap : 1);
+      s = s + (gpu_u < 0.7 ? w[5] : w[6]) * (1.0 - gpu_u);
+      const uint32_t d = pod.gmilli > 1 ? (uint32_t)pod.gmilli : 1u;
+      s = s + w[7] * (double)((uint32_t)free_m % d);
+    }
+    const double a = (double)cl / (double)(ml > 1 ? ml : 1);
+    s = s + w[8] * fabs(a - pod.cm);
+    if (cl > (int64_t)pod.cpu * 2 && ml > (int64_t)pod.mem * 2) s = s + w[9];
+    if (gpod) s = s + w[10] * (double)(gmax - gmin);
+    if (ct > 10000 && mt > 64) s = s + w[11];
+    if (cpu_u > 0.9 || mem_u > 0.9) s = s + w[12];
+    if (best >= 0) s = s + w[13] * div_by_recip((double)best, 1000.0, 0.001);
+    s = s + w[14] * ((double)idle / (double)(ng > 1 ? ng : 1));
+    if (!gpod && ng > 0) s = s + w[15];
+    return s;
+  }
+
   // composite() on the row kernel, bit for bit, with less f64 work:
   //  * the divisions by max(cpu_total, 1), max(mem_total, 1), max(ngpus, 1)
   //    and 1000 run as div_by_recip on host-verified reciprocals (rz, see
@@ -197,7 +249,8 @@ struct BuiltinScorerDev {
   //    NaN), so the caller passes here only policies whose weights all are.
   struct RowRecip {
     double zc, zm, zg, z1000, pcm;
-    double zcap;   // RN(1 / max(gpu_left * gmilli_total, 1)) when fast_cap, else 0
+    double zcap;         // RN(1 / max(gpu_left * gmilli_total, 1)) when fast_cap, else 0
+    double dc, dm, dg;   // max(cpu_total, 1), max(mem_total, 1), max(ngpus, 1) as doubles
   };
   template <class WP>
   __device__ static double composite_row(const NodeRegs<1>& nr, const PodView& pod, WP w, const RowRecip& rz) {
@@ -206,8 +259,8 @@ struct BuiltinScorerDev {
     const int32_t ct = nr.cpu_total[0], mt = nr.mem_total[0];
     const int32_t cl = nr.cpu_left[0], ml = nr.mem_left[0];
     // numerators in [0, total]: the host's invariant check behind rz
-    const double cpu_u = div_by_recip((double)(ct - cl), (double)(ct > 1 ? ct : 1), rz.zc);
-    const double mem_u = div_by_recip((double)(mt - ml), (double)(mt > 1 ? mt : 1), rz.zm);
+    const double cpu_u = div_by_recip((double)(ct - cl), rz.dc, rz.zc);
+    const double mem_u = div_by_recip((double)(mt - ml), rz.dm, rz.zm);
     int32_t free_m = 0, idle = 0, gmax = 0, gmin = 0, best = -1;
 #pragma unroll
     for (int j = 0; j < kGmax; ++j) {
@@ -239,7 +292,7 @@ struct BuiltinScorerDev {
     if (ct > 10000 && mt > 64) s = s + w[11];
     if (cpu_u > 0.9 || mem_u > 0.9) s = s + w[12];
     if (best >= 0) s = s + w[13] * div_by_recip((double)best, 1000.0, rz.z1000);
-    s = s + w[14] * div_by_recip((double)idle, (double)(ng > 1 ? ng : 1), rz.zg);
+    s = s + w[14] * div_by_recip((double)idle, rz.dg, rz.zg);
     if (!gpod && ng > 0) s = s + w[15];
     return s;
   }
