@@ -226,7 +226,8 @@ class DeviceEngine {
     lds_heap_ok_ = heap_bytes_ + delmap_bytes_ <= kMaxLds;
     rows_ok_ = npass_ == 1 && W_.n_nodes <= kRow && W_.n_classes <= kRow * kRowClassSlots &&
                W_.n_pods <= kRowMaxHeap && W_.tot_cpu < (int64_t(1) << 31) && W_.tot_mem < (int64_t(1) << 31) &&
-               W_.tot_gcnt < (int64_t(1) << 31) && W_.tot_gmilli < (int64_t(1) << 31);   // int32 row totals
+               W_.tot_gcnt < (int64_t(1) << 31) && W_.tot_gmilli < (int64_t(1) << 31) &&   // int32 row totals
+               max_class_pods_ < (1 << 16);   // 16-bit waiting-class counters
     set_attrs();
   }
 
@@ -572,11 +573,15 @@ class DeviceEngine {
     std::vector<std::pair<std::pair<int64_t, int64_t>, double>> cache;
     bool ok = true;
     std::vector<double> rec((size_t)nn * 3, 0.0), cm((size_t)std::max(np, 1), 0.0);
+    std::vector<int32_t> per_class(256, 0);
     for (int r = 0; r < np; ++r) {
       const int32_t c = pod.data()[4 * r], m = pod.data()[4 * r + 1];
       ok = ok && c >= 0 && m >= 0;
       cm[r] = (double)c / (double)(m > 1 ? m : 1);
+      const uint32_t pw = (uint32_t)pod.data()[4 * r + 3];
+      if ((pw >> 16) & 0xFF) ++per_class[pw >> 24];
     }
+    max_class_pods_ = *std::max_element(per_class.begin(), per_class.end());
     for (int n = 0; n < nn; ++n) {
       const int32_t a = ct.data()[n], b = mt.data()[n];
       ok = ok && 0 <= cl.data()[n] && cl.data()[n] <= a && 0 <= ml.data()[n] && ml.data()[n] <= b;
@@ -964,6 +969,7 @@ class DeviceEngine {
   int native_rows_opt_ = 0;    // rows per wave for native programs (0: auto)
   int last_native_rows_ = 0, last_native_waves_ = 0;
   size_t row_min_lds_ = 0;
+  int32_t max_class_pods_ = 0;   // most GPU pods of one gpu_milli class (row kernel: < 2^16)
   bool row_flat_ = true;  // composite row kernel: flat heap accesses (false: exec-masked ds / global)
   int comp_waves_ = 4;   // composite row kernel: 4 or 5 waves per SIMD (row_composite_waves)
   mutable std::vector<std::pair<int, int>> row_layout_cache_ = std::vector<std::pair<int, int>>(8, {0, 0});

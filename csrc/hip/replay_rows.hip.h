@@ -357,8 +357,12 @@ __device__ __forceinline__ void fill_node_tables(const DevWorkload& W, FKS_LDS i
   }
   if (lane <= kGmax) row_cap_recips(ntab)[lane] = W.cap_recip[lane];
 }
+// per row: deletion bitmap | heap top (T + 1 slots) | cold state (trace hash,
+// snapshot threshold beyond the host's schedule: read rarely, so kept out of
+// the registers the 4- and 5-waves-per-SIMD register budgets are tight on)
+constexpr int kRowColdBytes = 16;
 __host__ __device__ inline size_t rows_row_bytes(int n_pods, int T) {
-  return (size_t)lds_delmap_words(n_pods) * 4 + (size_t)(T + 1) * 8;
+  return (size_t)lds_delmap_words(n_pods) * 4 + (size_t)(T + 1) * 8 + kRowColdBytes;
 }
 // native programs (kc = true) also stage each active row's constant block
 // (kKcLds int64) after the rows' heap areas
@@ -484,13 +488,16 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
     nr.ngpus[0] = e[2];
     nr.gmt1[0] = e[3];
   };
-  int32_t wcnt[kRowClassSlots];
+  // waiting-class histogram, two 16-bit counters per register (slot sl in
+  // word sl / 2, half sl % 2; the host allows the row kernel only when every
+  // class has fewer than 2^16 GPU pods)
+  uint32_t wcp[kRowClassSlots / 2];
+  auto wcount = [&](int sl) -> uint32_t { return (wcp[sl >> 1] >> (16 * (sl & 1))) & 0xFFFFu; };
   int32_t used_cpu = 0, used_mem = 0, used_gcnt = 0, used_gml = 0;   // host: totals < 2^31
   RowAcc acc;
   int32_t processed = 0, next_fire = INT32_MAX;
   int n_repush = 0, n_dropped = 0, ksnap = 0, n = 0;
-  double thr = 0.0;
-  uint64_t hsh = 0;
+  FKS_LDS uint64_t* rcs = heap.top + (T + 1);   // [0] trace hash, [1] threshold bits
   int32_t exc = EXC_NONE;
   ProgFn prog = nullptr;          // native: the row's scorer
   // native: its constant block, staged in LDS after the active rows' heap areas
@@ -512,8 +519,14 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
     const int words = row_heap_entries(N) / 2;   // 16-byte pairs of the shifted heap
     for (int i = jv; i < words; i += kRow) {
       const u64x2 v = heap_src[i];
-      if (2 * i < T + 1) *reinterpret_cast<FKS_LDS u64x2*>(heap.top + 2 * i) = v;
-      else *reinterpret_cast<FKS_GLOBAL u64x2*>(heap.h + 2 * i) = v;
+      if constexpr (FLAT) {
+        // through the generic addresses the event loop uses (no separate
+        // LDS / HBM pointers held live across the loop)
+        *reinterpret_cast<u64x2*>((2 * i < T + 1 ? heap.gtop : heap.gh) + 2 * i) = v;
+      } else {
+        if (2 * i < T + 1) *reinterpret_cast<FKS_LDS u64x2*>(heap.top + 2 * i) = v;
+        else *reinterpret_cast<FKS_GLOBAL u64x2*>(heap.h + 2 * i) = v;
+      }
     }
     for (int i = jv; i < lds_delmap_words(N); i += kRow) heap.delmap[i] = 0u;
     const FKS_CONST DevWorkload* Wb = cold();
@@ -525,12 +538,13 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
       nr.gml[0][g] = Wb->gml_left0[jv * kGmax + g];
     }
 #pragma unroll
-    for (int sl = 0; sl < kRowClassSlots; ++sl) wcnt[sl] = 0;
+    for (int k = 0; k < kRowClassSlots / 2; ++k) wcp[k] = 0u;
     used_cpu = (int32_t)Wb->used_cpu0; used_mem = (int32_t)Wb->used_mem0;
     used_gcnt = (int32_t)Wb->used_gcnt0; used_gml = (int32_t)Wb->used_gmilli0;
     acc.init();
     processed = 0; n_repush = 0; n_dropped = 0; ksnap = 0;
-    thr = Wb->thr_after_fire;
+    const double thr = Wb->thr_after_fire;
+    rcs[1] = (uint64_t)__double_as_longlong(thr);
     if (Wb->n_fire > 0) {
       next_fire = (int32_t)*global_ptr(&Wb->snap_fire[0]);
     } else {
@@ -538,7 +552,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
       while ((double)c / (double)N < thr) ++c;
       next_fire = c;
     }
-    hsh = 0xcbf29ce484222325ull;
+    rcs[0] = 0xcbf29ce484222325ull;
     exc = EXC_NONE;
     n = N;
     __builtin_amdgcn_s_waitcnt(0);   // heap image stored before the first pop reads it
@@ -560,9 +574,6 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
       const int rank = (int)((top >> lb) & ((1ull << rb) - 1));
       typedef int v4i __attribute__((ext_vector_type(4)));
       const v4i precv = *reinterpret_cast<const FKS_GLOBAL v4i*>(global_ptr(&W.pod[rank]));
-      // composite: the pod's cpu / mem quotient, in flight during the pop
-      double pcm = 0.0;
-      if (FAM == FAM_COMPOSITE_LINEAR) pcm = *global_ptr(&W.pod_cm[rank]);
       const uint64_t last = heap.ld(n - 1);
       --n;
       if (n > 0) heap.pop_reinsert(n, last);
@@ -587,13 +598,15 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
         }
         used_cpu -= pod.cpu; used_mem -= pod.mem; used_gcnt -= pod.ngpu;
         used_gml -= pod.gmilli * __popc(mask);
-        if (cold()->trace_hash) hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 1, (uint64_t)t);
+        if (cold()->trace_hash) rcs[0] = mix_event(rcs[0], ((uint64_t)(uint32_t)rank << 2) | 1, (uint64_t)t);
         prof.mark(PH_DELETE);
       } else {
         // ---------------- creation: score the row's nodes, first maximum wins
         // composite: composite_row (the host runs this instance only on
         // finite weights and verified reciprocals, engine_host stage_builtin)
         constexpr bool kComp = FAM == FAM_COMPOSITE_LINEAR;
+        double pcm = 0.0;   // the pod's cpu / mem quotient
+        if (kComp) pcm = *global_ptr(&W.pod_cm[rank]);
         load_consts();
         int lexc = EXC_NONE;
         int64_t s = 0;
@@ -645,17 +658,17 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
           if (kind == kFresh && pod.ngpu > 0) {
 #pragma unroll
             for (int sl = 0; sl < kRowClassSlots; ++sl)
-              if (sl == (pod.cls >> 4) && jv == (pod.cls & 15)) wcnt[sl] += 1;
+              if (sl == (pod.cls >> 4) && jv == (pod.cls & 15)) wcp[sl >> 1] += 1u << (16 * (sl & 1));
           }
           double frag = 0.0;
           // smallest waiting class: each lane offers its lowest nonempty slot's
           // class (sl * 16 + j), the row takes the minimum (64: none waits)
           uint32_t nzs = 0;
 #pragma unroll
-          for (int sl = kRowClassSlots - 1; sl >= 0; --sl) nzs = wcnt[sl] > 0 ? (uint32_t)sl : nzs;
+          for (int sl = kRowClassSlots - 1; sl >= 0; --sl) nzs = wcount(sl) > 0 ? (uint32_t)sl : nzs;
           bool any = false;
 #pragma unroll
-          for (int sl = 0; sl < kRowClassSlots; ++sl) any = any || wcnt[sl] > 0;
+          for (int k = 0; k < kRowClassSlots / 2; ++k) any = any || wcp[k] != 0u;
           const int mcls = (int)row_min_u32(any ? nzs * kRow + (uint32_t)jv : 64u);
           if (mcls < 64) {
             const int mv = cls_lds[mcls];
@@ -681,7 +694,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
           } else {
             ++n_dropped;
           }
-          if (cold()->trace_hash) hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 2, (uint64_t)t);
+          if (cold()->trace_hash) rcs[0] = mix_event(rcs[0], ((uint64_t)(uint32_t)rank << 2) | 2, (uint64_t)t);
           prof.mark(PH_FAIL);
         } else {
           // ---------------- commit on best_node
@@ -707,14 +720,14 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
           if (kind == kRetry && pod.ngpu > 0) {
 #pragma unroll
             for (int sl = 0; sl < kRowClassSlots; ++sl)
-              if (sl == (pod.cls >> 4) && jv == (pod.cls & 15)) wcnt[sl] -= 1;
+              if (sl == (pod.cls >> 4) && jv == (pod.cls & 15)) wcp[sl >> 1] -= 1u << (16 * (sl & 1));
           }
           const uint64_t dt = (uint64_t)(t + pod.dur);
           if (t + pod.dur < 0 || dt > time_max) { exc = EXC_UNSUPPORTED; break; }
           push_item = (dt << tshift) | ((uint64_t)rank << lb) | ((uint64_t)gmask << (2 + nb)) |
                       ((uint64_t)best_node << 2) | kDelete;
           if (cold()->trace_hash)
-            hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2), ((uint64_t)t << 8) ^ (uint64_t)best_node);
+            rcs[0] = mix_event(rcs[0], ((uint64_t)(uint32_t)rank << 2), ((uint64_t)t << 8) ^ (uint64_t)best_node);
           prof.mark(PH_COMMIT);
         }
         // one heappush for both outcomes (re-queued creation or deletion): rows
@@ -741,7 +754,11 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
           // past the host's precomputed schedule: the next count c > processed
           // with c / N >= thr (the evaluator's IEEE test), thr += interval after
           // every snapshot beyond it (simulator/evaluator.py:55-67)
-          if (ksnap > Ws->n_fire) thr += Ws->snapshot_interval;
+          double thr = __longlong_as_double((long long)rcs[1]);
+          if (ksnap > Ws->n_fire) {
+            thr += Ws->snapshot_interval;
+            rcs[1] = (uint64_t)__double_as_longlong(thr);
+          }
           int32_t c = processed + 1;
           while ((double)c / (double)N < thr) ++c;
           next_fire = c;
@@ -767,7 +784,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
       o->n_unplaced = n_dropped;
       o->n_repush = n_repush;
       o->max_nodes = 0;
-      o->hash = hsh;
+      o->hash = rcs[0];
       o->exc = exc;
       o->inexact = inexact;
     }
@@ -803,7 +820,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
         case 9: v = (double)n_dropped; break;
         case 10: v = (double)exc; break;
         case 11: v = (double)inexact; break;
-        case 12: v = (double)(hsh >> 11); break;
+        case 12: v = (double)(rcs[0] >> 11); break;
         default: break;
       }
       if (!ok && jv != 10) v = 0.0;
