@@ -58,8 +58,9 @@ def main() -> None:
     ap.add_argument("--heap-mode", default="auto", choices=["auto", "lds", "hbm"])
     ap.add_argument("--heap-top", type=int, default=-1,
                     help="wave kernel (> 16 nodes): heap slots kept in LDS per policy (2^k - 1; -1: auto)")
-    ap.add_argument("--row-composite-waves", type=int, default=4, choices=[4, 5],
-                    help="waves per SIMD of the composite row kernel (register budget 128 / 96 VGPRs)")
+    ap.add_argument("--row-composite-waves", type=int, default=5, choices=[4, 5],
+                    help="waves per SIMD of the composite row kernel (register budget 128 / 96 VGPRs; "
+                         "5: heap top 63 slots in LDS instead of 127)")
     ap.add_argument("--row-min-lds", type=int, default=0,
                     help="occupancy experiments: at least this many LDS bytes per row-kernel wave")
     ap.add_argument("--row-split-heap", action="store_true",

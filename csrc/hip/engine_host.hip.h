@@ -681,7 +681,7 @@ class DeviceEngine {
     if (key >= 0 && key < (int)row_layout_cache_.size()) row_layout_cache_[key] = best;
     return best;
   }
-  int row_top() const { return row_layout(FAM_COMPOSITE_LINEAR).first; }
+  int row_top() const { return row_layout(comp_waves_ == 5 ? kRowCompositeW5 : FAM_COMPOSITE_LINEAR).first; }
 
   // resident row-kernel waves per CU at heap top T: the occupancy query
   // (registers, LDS) is optimistic about LDS allocation granules, so LDS is
@@ -971,7 +971,7 @@ class DeviceEngine {
   size_t row_min_lds_ = 0;
   int32_t max_class_pods_ = 0;   // most GPU pods of one gpu_milli class (row kernel: < 2^16)
   bool row_flat_ = true;  // composite row kernel: flat heap accesses (false: exec-masked ds / global)
-  int comp_waves_ = 4;   // composite row kernel: 4 or 5 waves per SIMD (row_composite_waves)
+  int comp_waves_ = 5;   // composite row kernel: 4 or 5 waves per SIMD (row_composite_waves)
   mutable std::vector<std::pair<int, int>> row_layout_cache_ = std::vector<std::pair<int, int>>(8, {0, 0});
   int num_cus_ = 0;
   std::string arch_;

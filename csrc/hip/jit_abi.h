@@ -45,6 +45,15 @@ typedef int64_t (*ProgFn)(int32_t n_cpu_left, int32_t n_cpu_total, int32_t n_mem
                           int32_t p_cpu, int32_t p_mem, int32_t p_gpu, int64_t p_ctime, int32_t p_dur,
                           KcPtr kc);
 
+// A launch's per-policy function table entry: the scorer's device address with
+// bit 0 set when the program opens with the template's feasibility prologue
+// (CompiledPolicy.feasibility_prologue): it then scores 0, with no other
+// effect, exactly where the kernels' feasible() is false, so the kernels call
+// it only for feasible nodes (function addresses are at least 4-byte aligned).
+constexpr uint64_t kFnFeasBit = 1;
+__host__ __device__ __forceinline__ ProgFn prog_of(uint64_t e) { return reinterpret_cast<ProgFn>(e & ~kFnFeasBit); }
+__host__ __device__ __forceinline__ bool prog_feas(uint64_t e) { return (e & kFnFeasBit) != 0; }
+
 // ---- runtime library -------------------------------------------------------------
 // The float // and %, **, math.log / exp / sqrt / pow machinery (double-double
 // exp/log, CPython float_pow) is compiled once, into the extension, and the

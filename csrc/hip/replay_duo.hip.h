@@ -289,7 +289,9 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
   }
 
   // ================= S: nodes, program, evaluator
-  const ProgFn prog = reinterpret_cast<ProgFn>(*global_ptr(&nat.fn[p]));
+  const uint64_t fne = *global_ptr(&nat.fn[p]);
+  const ProgFn prog = prog_of(fne);
+  const bool feas_pro = prog_feas(fne);   // call only for feasible nodes
   NodeRegs<1> nr;
   {
     const FKS_CONST DevWorkload* Wb = cold();
@@ -384,7 +386,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
       }
       int lexc = EXC_NONE;
       int64_t s = 0;
-      if (node_valid) {
+      if (node_valid && (!feas_pro || feasible<1>(0, nr, pod))) {
         const int32_t* gl = nr.gml[0];
         int32_t gt[kGmax];
 #pragma unroll

@@ -319,7 +319,7 @@ __global__ __launch_bounds__(64, GHEAP ? 2 : 1) void k_replay_native(fksk::Nativ
   const int p = blockIdx.x;
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   NativeScorerDev sc;
-  sc.fn = reinterpret_cast<ProgFn>(uniu64(a.fn[p]));
+  sc.fn = prog_of(uniu64(a.fn[p]));
   sc.gmem = a.W.gmem_total;
   // the constant block moves into the slot's register area (the host reserves
   // kKcLds / 64 VM registers for it; the allocation is padded by kKcLds entries,

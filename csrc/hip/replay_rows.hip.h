@@ -360,7 +360,7 @@ __device__ __forceinline__ void fill_node_tables(const DevWorkload& W, FKS_LDS i
 // per row: deletion bitmap | heap top (T + 1 slots) | cold state (trace hash,
 // snapshot threshold beyond the host's schedule: read rarely, so kept out of
 // the registers the 4- and 5-waves-per-SIMD register budgets are tight on)
-constexpr int kRowColdBytes = 16;
+constexpr int kRowColdBytes = 32;   // hash, threshold, repush / dropped / snapshot counters
 __host__ __device__ inline size_t rows_row_bytes(int n_pods, int T) {
   return (size_t)lds_delmap_words(n_pods) * 4 + (size_t)(T + 1) * 8 + kRowColdBytes;
 }
@@ -493,13 +493,18 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
   // class has fewer than 2^16 GPU pods)
   uint32_t wcp[kRowClassSlots / 2];
   auto wcount = [&](int sl) -> uint32_t { return (wcp[sl >> 1] >> (16 * (sl & 1))) & 0xFFFFu; };
-  int32_t used_cpu = 0, used_mem = 0, used_gcnt = 0, used_gml = 0;   // host: totals < 2^31
   RowAcc acc;
   int32_t processed = 0, next_fire = INT32_MAX;
-  int n_repush = 0, n_dropped = 0, ksnap = 0, n = 0;
+  int n = 0;
   FKS_LDS uint64_t* rcs = heap.top + (T + 1);   // [0] trace hash, [1] threshold bits
+  // [0] repushes, [1] dropped pods, [2] snapshots taken (per-row counters)
+  FKS_LDS uint32_t* rcn = reinterpret_cast<FKS_LDS uint32_t*>(rcs + 2);
+  auto bump = [&](int k) {   // one lane of the row adds 1
+    if (jv == 0) __hip_atomic_fetch_add(&rcn[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
   int32_t exc = EXC_NONE;
   ProgFn prog = nullptr;          // native: the row's scorer
+  bool feas_pro = false;          // native: it opens with the feasibility prologue (call feasible nodes only)
   // native: its constant block, staged in LDS after the active rows' heap areas
   FKS_LDS int64_t* kcp = reinterpret_cast<FKS_LDS int64_t*>(
       reinterpret_cast<FKS_LDS char*>(lds + kRowsPerWave * kWeights) + kRowClassBytes +
@@ -508,7 +513,9 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
   // start policy p on this row: weights, heap image, bitmap, node state, counters
   auto begin = [&]() {
     if constexpr (kNative) {
-      prog = reinterpret_cast<ProgFn>(*global_ptr(&nat.fn[p]));
+      const uint64_t fne = *global_ptr(&nat.fn[p]);
+      prog = prog_of(fne);
+      feas_pro = prog_feas(fne);
       // fixed-size copy: the host pads the kc allocation by kKcLds entries
       const FKS_GLOBAL int64_t* ksrc = global_ptr(nat.kc + *global_ptr(&nat.koff[p]));
       for (int i = jv; i < kKcLds; i += kRow) kcp[i] = ksrc[i];
@@ -539,10 +546,9 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
     }
 #pragma unroll
     for (int k = 0; k < kRowClassSlots / 2; ++k) wcp[k] = 0u;
-    used_cpu = (int32_t)Wb->used_cpu0; used_mem = (int32_t)Wb->used_mem0;
-    used_gcnt = (int32_t)Wb->used_gcnt0; used_gml = (int32_t)Wb->used_gmilli0;
     acc.init();
-    processed = 0; n_repush = 0; n_dropped = 0; ksnap = 0;
+    processed = 0;
+    rcn[0] = 0u; rcn[1] = 0u; rcn[2] = 0u;
     const double thr = Wb->thr_after_fire;
     rcs[1] = (uint64_t)__double_as_longlong(thr);
     if (Wb->n_fire > 0) {
@@ -596,8 +602,6 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
           for (int g = 0; g < kGmax; ++g)
             if ((mask >> g) & 1) nr.gml[0][g] += pod.gmilli;
         }
-        used_cpu -= pod.cpu; used_mem -= pod.mem; used_gcnt -= pod.ngpu;
-        used_gml -= pod.gmilli * __popc(mask);
         if (cold()->trace_hash) rcs[0] = mix_event(rcs[0], ((uint64_t)(uint32_t)rank << 2) | 1, (uint64_t)t);
         prof.mark(PH_DELETE);
       } else {
@@ -612,8 +616,9 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
         int64_t s = 0;
         double sd = 0.0;   // composite: the truncated score as a double (trunc_score_f)
         if constexpr (kNative) {
-          // the program holds the template's feasibility prologue itself
-          if (node_valid) {
+          // the program holds the template's feasibility prologue itself; one
+          // that opens with it is not called for nodes feasible() rejects
+          if (node_valid && (!feas_pro || feasible<1>(0, nr, pod))) {
             const int32_t* gl = nr.gml[0];
             int32_t gt[kGmax];
 #pragma unroll
@@ -690,9 +695,9 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
             const uint64_t nt = (heap.ld(f) >> tshift) + 1;
             if (nt > time_max) { exc = EXC_UNSUPPORTED; break; }
             push_item = (nt << tshift) | ((uint64_t)rank << lb) | kRetry;
-            ++n_repush;
+            bump(0);
           } else {
-            ++n_dropped;
+            bump(1);
           }
           if (cold()->trace_hash) rcs[0] = mix_event(rcs[0], ((uint64_t)(uint32_t)rank << 2) | 2, (uint64_t)t);
           prof.mark(PH_FAIL);
@@ -715,8 +720,6 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
             for (int g = 0; g < kGmax; ++g)
               if ((gmask >> g) & 1) nr.gml[0][g] -= pod.gmilli;
           }
-          used_cpu += pod.cpu; used_mem += pod.mem; used_gcnt += pod.ngpu;
-          used_gml += pod.gmilli * __popc(gmask);
           if (kind == kRetry && pod.ngpu > 0) {
 #pragma unroll
             for (int sl = 0; sl < kRowClassSlots; ++sl)
@@ -742,12 +745,22 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
       ++processed;
       if (processed >= next_fire) {
         const FKS_CONST DevWorkload* Ws = cold();
+        // cluster usage = totals minus the row's sums of what is left (nodes past
+        // n_nodes and GPUs past ngpus hold 0): no per-event used counters
+        int32_t gl_sum = 0;
+#pragma unroll
+        for (int g = 0; g < kGmax; ++g) gl_sum += nr.gml[0][g];
+        const int32_t used_cpu = (int32_t)Ws->tot_cpu - row_sum_i32(nr.cpu_left[0]);
+        const int32_t used_mem = (int32_t)Ws->tot_mem - row_sum_i32(nr.mem_left[0]);
+        const int32_t used_gcnt = (int32_t)Ws->tot_gcnt - row_sum_i32(nr.gpu_left[0]);
+        const int32_t used_gml = (int32_t)Ws->tot_gmilli - row_sum_i32(gl_sum);   // host: totals < 2^31
         const double r0 = Ws->tot_cpu > 0 ? (double)used_cpu / (double)Ws->tot_cpu : 0.0;
         const double r1 = Ws->tot_mem > 0 ? (double)used_mem / (double)Ws->tot_mem : 0.0;
         const double r2 = Ws->tot_gcnt > 0 ? (double)used_gcnt / (double)Ws->tot_gcnt : 0.0;
         const double r3 = Ws->tot_gmilli > 0 ? (double)used_gml / (double)Ws->tot_gmilli : 0.0;
         acc.add_unit(0, r0, jv); acc.add_unit(1, r1, jv); acc.add_unit(2, r2, jv); acc.add_unit(3, r3, jv);
-        ++ksnap;
+        bump(2);
+        const int ksnap = (int)rcn[2];
         if (ksnap < Ws->n_fire) {
           next_fire = (int32_t)*global_ptr(&Ws->snap_fire[ksnap]);
         } else {
@@ -769,6 +782,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
 
     if (n > 0 && exc == EXC_NONE) continue;
     // ---------------- replay done (or aborted): result, then the next policy
+    const int n_dropped = (int)rcn[1];
     const int64_t n_snap = row_read(acc.count, rbase, 0);
     const int64_t n_frag = row_read(acc.count, rbase, 4);
     const int inexact = row_ballot(jv < 5 && acc.inexact != 0, rbase) != 0;
@@ -782,7 +796,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
       o->n_snap = n_snap;
       o->n_frag = n_frag;
       o->n_unplaced = n_dropped;
-      o->n_repush = n_repush;
+      o->n_repush = (int64_t)rcn[0];
       o->max_nodes = 0;
       o->hash = rcs[0];
       o->exc = exc;

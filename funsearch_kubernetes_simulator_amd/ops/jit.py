@@ -79,6 +79,10 @@ RT_FRAME_BYTES = 256
 STACK_LIMIT_BYTES = 1024   # HIP's default per-lane stack for dynamic-stack kernels
 
 
+#: FKS_FEAS_SKIP=0 calls every program for every node (A/B of the feasibility-prologue skip)
+_FEAS_SKIP = os.environ.get("FKS_FEAS_SKIP", "1") != "0"
+
+
 class JitError(RuntimeError):
     """The toolchain failed on a module (a bug, not an unsupported program)."""
 
@@ -284,7 +288,7 @@ def compile_host_module(progs: Sequence[CompiledPolicy], path: str) -> str:
 @dataclass
 class NativeBatch:
     """Per-policy launch data of one batch (programs in input order)."""
-    fn: np.ndarray                   # uint64 [P] device addresses (0: not native)
+    fn: np.ndarray                   # uint64 [P] device addresses | feasibility-prologue bit (0: not native)
     kc: np.ndarray                   # int64 concatenated constant blocks
     koff: np.ndarray                 # int32 [P]
     ok: np.ndarray                   # bool [P]
@@ -380,7 +384,9 @@ class NativeCompiler:
                 pos += len(kb)
                 if k in self._shapes:
                     mi, pi_ = self._shapes[k]
-                    fn[i] = self._modules[mi].pointers[pi_]
+                    # bit 0: the program opens with the template's feasibility
+                    # prologue, so the kernels call it for feasible nodes only
+                    fn[i] = self._modules[mi].pointers[pi_] | (1 if _FEAS_SKIP and p.feasibility_prologue else 0)
                     ok[i] = True
                 else:
                     reasons[i] = self._bad.get(k, "not compiled")

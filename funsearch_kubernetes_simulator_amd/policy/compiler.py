@@ -89,6 +89,18 @@ class CompiledPolicy:
         back to the host (trigonometry: no correctly rounded device version)."""
         return "trig" not in self.features
 
+    @property
+    def feasibility_prologue(self) -> bool:
+        """The scoring function opens with the template's feasibility prologue
+        (`policy.template.FEASIBILITY_PROLOGUE`, AST-equal, literals included):
+        it then scores 0 -- with no other effect -- exactly on the (pod, node)
+        pairs the replay kernels' own `feasible()` rejects, so a kernel may skip
+        the call for those nodes."""
+        v = self.__dict__.get("_feas_prologue")
+        if v is None:
+            v = self.__dict__["_feas_prologue"] = starts_with_feasibility_prologue(self.source)
+        return v
+
     def digest(self) -> str:
         h = hashlib.sha1(self.code)
         h.update(struct.pack(f"<{len(self.fconst)}d", *self.fconst))
@@ -1413,6 +1425,35 @@ class Compiler:
 
     def call_enumerate(self, e):
         raise CompileError("enumerate() outside a for loop")
+
+
+_PROLOGUE_DUMPS: Optional[List[str]] = None
+
+
+def starts_with_feasibility_prologue(source: str) -> bool:
+    """True when the program's `priority_function(pod, node)` body (after an
+    optional docstring) starts with the template's feasibility prologue."""
+    global _PROLOGUE_DUMPS
+    from .template import FEASIBILITY_PROLOGUE
+    if _PROLOGUE_DUMPS is None:
+        ref = ast.parse("def priority_function(pod, node):\n" + FEASIBILITY_PROLOGUE + "\n")
+        _PROLOGUE_DUMPS = [ast.dump(st) for st in ref.body[0].body]
+    try:
+        tree = ast.parse(source)
+    except (SyntaxError, ValueError, RecursionError):
+        return False
+    fn = None
+    for st in tree.body:
+        if isinstance(st, ast.FunctionDef) and st.name == "priority_function":
+            fn = st
+    if fn is None or [a.arg for a in fn.args.args] != ["pod", "node"]:
+        return False
+    body = list(fn.body)
+    if body and isinstance(body[0], ast.Expr) and isinstance(body[0].value, ast.Constant) \
+            and isinstance(body[0].value.value, str):
+        body = body[1:]
+    k = len(_PROLOGUE_DUMPS)
+    return len(body) > k and [ast.dump(st) for st in body[:k]] == _PROLOGUE_DUMPS
 
 
 def compile_policy(source: str) -> CompiledPolicy:

@@ -167,3 +167,26 @@ def test_unsupported_constructs_raise_compile_error():
                  "return {1: 2}[1]", "return pod.gpu_spec"):
         with pytest.raises(CompileError):
             compile_policy(f"def priority_function(pod, node):\n    {body}\n")
+
+
+def test_feasibility_prologue_detection():
+    """Programs that open with the template's feasibility prologue (AST-equal, literals
+    included) let the native kernels skip the call for infeasible nodes; anything else
+    is called for every node."""
+    from funsearch_kubernetes_simulator_amd.policy.compiler import starts_with_feasibility_prologue
+    from funsearch_kubernetes_simulator_amd.policy.template import PolicyTemplate
+    prog = PolicyTemplate.fill_template("score = node.cpu_milli_left * 2")
+    assert starts_with_feasibility_prologue(prog)
+    assert compile_policy(prog).feasibility_prologue
+    # the same without the docstring
+    nodoc = prog.split('"""')[0] + prog.split('"""')[2]
+    assert starts_with_feasibility_prologue(nodoc)
+    # a changed literal, a changed comparison, renamed parameters, a statement before it
+    assert not starts_with_feasibility_prologue(prog.replace("        return 0\n    \n    if pod.num_gpu",
+                                                             "        return 5\n    \n    if pod.num_gpu"))
+    assert not starts_with_feasibility_prologue(prog.replace("gpu.gpu_milli_left >= pod.gpu_milli",
+                                                             "gpu.gpu_milli_left > pod.gpu_milli"))
+    assert not starts_with_feasibility_prologue(prog.replace("(pod, node)", "(p, node)"))
+    assert not starts_with_feasibility_prologue(prog.replace("    # Basic feasibility check\n",
+                                                             "    x = 1\n    # Basic feasibility check\n"))
+    assert not starts_with_feasibility_prologue("def priority_function(pod, node):\n    return 1\n")
