@@ -108,6 +108,8 @@ __device__ __forceinline__ void load_policy(BuiltinScorerDev<FAM>& sc, const Slo
   const int fam = uni(lane == 0 ? a.fam[p] : 0);
   __threadfence();   // stores visible to the scalar loads that follow
   sc.load(fam, wd);
+  sc.zp = a.W.node_recip;
+  sc.capz = kernarg_workload()->cap_recip;
 }
 
 template <class T>

@@ -60,6 +60,10 @@ template <int FAM = -1>
 struct BuiltinScorerDev {
   int32_t family;
   const double* wp;   // this policy's kWeights weights (device copy, HBM)
+  // composite instance (FAM fixed): DevWorkload::node_recip ([node][3]) and
+  // cap_recip, for the reciprocal divisions of composite_fast
+  const double* zp = nullptr;
+  const double* capz = nullptr;
 
   __device__ void load(int32_t fam_id, const double* p) {
     family = FAM >= 0 ? FAM : fam_id;
@@ -78,6 +82,17 @@ struct BuiltinScorerDev {
     double w[kWeights];
 #pragma unroll
     for (int k = 0; k < kWeights; ++k) w[k] = k < family_weights(FAM) ? q[k] : 0.0;
+    if constexpr (FAM == FAM_COMPOSITE_LINEAR) {
+      // the composite instance: the host runs it only on finite weights with
+      // verified reciprocals (engine_host stage_builtin).  The truncated score
+      // (>= 0) is returned as its double's bit pattern: non-negative doubles
+      // order like their bits, so the wave argmax (u64) is unchanged and no
+      // f64 -> i64 conversion is needed.
+      const double* z = zp + (size_t)(ps * kWave + lane_id()) * 3;
+      const double zcap = pod.ngpu > 0 ? capz[nr.gpu_left[ps]] : 0.0;
+      return (int64_t)__double_as_longlong(
+          trunc_score_f(composite_fast<NPASS>(ps, nr, pod, (const double*)w, z, zcap), exc));
+    }
     return score_weights<NPASS>(family, (const double*)w, ps, nr, pod, exc);
   }
 
@@ -120,10 +135,7 @@ struct BuiltinScorerDev {
         return trunc_score(s, exc);
       }
       case FAM_COMPOSITE_LINEAR:
-        // the composite instance (FAM fixed): the host runs it only on finite
-        // weights with verified reciprocals (engine_host stage_builtin)
-        if constexpr (FAM == FAM_COMPOSITE_LINEAR) return trunc_score(composite_fast<NPASS>(ps, nr, pod, w), exc);
-        return trunc_score(composite<NPASS>(ps, nr, pod, w), exc);
+            return trunc_score(composite<NPASS>(ps, nr, pod, w), exc);
     }
     exc = EXC_UNSUPPORTED;
     return 0;
@@ -189,18 +201,20 @@ struct BuiltinScorerDev {
 
   // composite() on the wave kernel for finite weights, bit for bit: no `w != 0`
   // tests, one member per threshold pair, 0/1 indicators add the weight (see
-  // composite_row), the host's pod quotient and the verified 1/1000 (the
-  // literal 0.001 is RN(1/1000); the host's fast_div check covers [0, 2^21)).
-  // The per-node divisions stay divisions: reciprocals for 4 node slots per
-  // lane would cost more registers than the config-5 kernel has.
+  // composite_row), the host's pod quotient, the verified 1/1000 (the literal
+  // 0.001 is RN(1/1000); the host's fast_div check covers [0, 2^21)) and the
+  // host-verified node / GPU-capacity reciprocals, read per node pass from the
+  // workload's tables (no registers held across passes).
   template <int NPASS, class WP>
-  __device__ static double composite_fast(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, WP w) {
+  __device__ static double composite_fast(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, WP w,
+                                          const double* z, double zcap) {
     const int ng = nr.ngpus[ps];
     const bool gpod = pod.ngpu > 0;
     const int32_t ct = nr.cpu_total[ps], mt = nr.mem_total[ps];
     const int32_t cl = nr.cpu_left[ps], ml = nr.mem_left[ps];
-    const double cpu_u = (double)((int64_t)ct - cl) / (double)(ct > 1 ? ct : 1);
-    const double mem_u = (double)((int64_t)mt - ml) / (double)(mt > 1 ? mt : 1);
+    // the host's verified reciprocals (DeviceEngine::prepare_recips): numerators in [0, total]
+    const double cpu_u = div_by_recip((double)(ct - cl), (double)(ct > 1 ? ct : 1), z[0]);
+    const double mem_u = div_by_recip((double)(mt - ml), (double)(mt > 1 ? mt : 1), z[1]);
     int32_t free_m = 0, idle = 0, gmax = 0, gmin = 0, best = -1;
 #pragma unroll
     for (int j = 0; j < kGmax; ++j) {
@@ -218,7 +232,8 @@ struct BuiltinScorerDev {
     s = s + (mem_u < 0.7 ? w[3] : w[4]) * (1.0 - mem_u);
     if (gpod) {
       const int64_t cap = (int64_t)nr.gpu_left[ps] * nr.gt(ps, 0);
-      const double gpu_u = (double)(cap - free_m) / (double)(cap > 1 ? cap : 1);
+      const double nu = (double)(cap - free_m), du = (double)(cap > 1 ? cap : 1);
+      const double gpu_u = zcap != 0.0 ? div_by_recip(nu, du, zcap) : nu / du;
       s = s + (gpu_u < 0.7 ? w[5] : w[6]) * (1.0 - gpu_u);
       const uint32_t d = pod.gmilli > 1 ? (uint32_t)pod.gmilli : 1u;
       s = s + w[7] * (double)((uint32_t)free_m % d);
@@ -230,7 +245,7 @@ struct BuiltinScorerDev {
     if (ct > 10000 && mt > 64) s = s + w[11];
     if (cpu_u > 0.9 || mem_u > 0.9) s = s + w[12];
     if (best >= 0) s = s + w[13] * div_by_recip((double)best, 1000.0, 0.001);
-    s = s + w[14] * ((double)idle / (double)(ng > 1 ? ng : 1));
+    s = s + w[14] * div_by_recip((double)idle, (double)(ng > 1 ? ng : 1), z[2]);
     if (!gpod && ng > 0) s = s + w[15];
     return s;
   }

@@ -19,3 +19,5 @@ for sk in 1 0; do
 done
 timeout -k 10 300 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
 cut -c1-300 $O/bench.json
+timeout -k 10 300 python -u bench.py --programs 0 --novel 0 --row-composite-waves 4 > $O/bench_w4.json 2> $O/bench_w4.err || { echo "bench w4 failed"; tail -20 $O/bench_w4.err; exit 1; }
+echo "w4: $(cut -c70-170 $O/bench_w4.json)"
