@@ -1434,7 +1434,19 @@ def starts_with_feasibility_prologue(source: str) -> bool:
     """True when the program's `priority_function(pod, node)` body (after an
     optional docstring) starts with the template's feasibility prologue."""
     global _PROLOGUE_DUMPS
-    from .template import FEASIBILITY_PROLOGUE
+    from .template import FEASIBILITY_PROLOGUE, PolicyTemplate
+    # fast path (template-filled programs): the template's own head verbatim, the
+    # only priority_function, and the line after the prologue back at the
+    # function body's indentation -- then the body's first statements are the
+    # prologue's, token for token (no AST parse on the batch-preparation path)
+    head = PolicyTemplate.TEMPLATE.split("\n    \n    # LLM fills in this part")[0]
+    i = source.find(head)
+    if i >= 0 and source.count("def priority_function") == 1:
+        rest = source[i + len(head):]
+        if rest == "" or rest.startswith("\n"):
+            nxt = next((ln for ln in rest.split("\n")[1:] if ln.strip()), "")
+            if len(nxt) - len(nxt.lstrip(" ")) <= 4 and not nxt.startswith("\t"):
+                return True
     if _PROLOGUE_DUMPS is None:
         ref = ast.parse("def priority_function(pod, node):\n" + FEASIBILITY_PROLOGUE + "\n")
         _PROLOGUE_DUMPS = [ast.dump(st) for st in ref.body[0].body]

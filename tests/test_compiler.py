@@ -190,3 +190,9 @@ def test_feasibility_prologue_detection():
     assert not starts_with_feasibility_prologue(prog.replace("    # Basic feasibility check\n",
                                                              "    x = 1\n    # Basic feasibility check\n"))
     assert not starts_with_feasibility_prologue("def priority_function(pod, node):\n    return 1\n")
+    # the textual fast path must not accept a statement continuing the prologue's last block
+    deeper = prog.replace("            return 0\n    \n    # LLM", "            return 0\n                x = 1\n    \n    # LLM")
+    assert deeper != prog and not starts_with_feasibility_prologue(deeper)
+    # two definitions: the compiler takes the last one, the fast path declines and the AST path decides
+    twice = prog + "\ndef priority_function(pod, node):\n    return 7\n"
+    assert not starts_with_feasibility_prologue(twice)
