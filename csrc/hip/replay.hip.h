@@ -364,23 +364,43 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
       prof.mark(PH_DELETE);
     } else {
       // ---------------- creation: score all nodes, argmax (first node wins ties)
-      int64_t best = 0;
-      int best_node = -1;
+      // Each lane keeps the best of its node slots (strict >: the lowest slot
+      // wins ties) and its first exception; ONE wave max per event then finds
+      // the winning score, and the lowest node index holding it is the lowest
+      // slot whose ballot hits -- the same node as a pass-by-pass argmax, with
+      // NPASS - 1 fewer DPP reductions.  A score of 0 never places.
+      uint64_t lbest = 0;
+      // packed per-lane state (one VGPR): bits 0-1 slot of lbest, bits 2-3
+      // slot of the first exception, bits 8+ its code (EXC_NONE = 0)
+      int lst = 0;
 #pragma unroll
       for (int ps = 0; ps < NPASS; ++ps) {
         const bool valid = (ps * kWave + lane) < W.n_nodes;
         int lexc = EXC_NONE;
-        int64_t s = valid ? scorer.template score<NPASS>(ps, nr, pod, lexc) : 0;
-        if (!valid) lexc = EXC_NONE;
-        const uint64_t bad = ballot(lexc != EXC_NONE);
-        if (bad) { exc = readlane(lexc, first_lane(bad)); break; }
-        const int64_t m = (int64_t)wave_max_u64((uint64_t)s);   // scores are >= 0
-        if (m > best) {
-          best = m;
-          best_node = ps * kWave + first_lane(ballot(s == m));
+        const uint64_t s = valid ? (uint64_t)scorer.template score<NPASS>(ps, nr, pod, lexc) : 0;   // >= 0
+        if (valid && lexc != EXC_NONE && (lst >> 8) == 0) lst |= (lexc << 8) | (ps << 2);
+        if (s > lbest) { lbest = s; lst = (lst & ~3) | ps; }
+        __builtin_amdgcn_sched_barrier(0);   // one slot at a time: no interleaved live ranges
+      }
+      if (ballot((lst >> 8) != 0)) {
+        // the first raising node in node order (slot-major, then lane); the
+        // slots after an exception were scored too, which has no side effects
+#pragma unroll
+        for (int ps = 0; ps < NPASS; ++ps) {
+          const uint64_t b = ballot((lst >> 8) != 0 && ((lst >> 2) & 3) == ps);
+          if (b) { exc = readlane(lst >> 8, first_lane(b)); break; }
+        }
+        break;
+      }
+      int best_node = -1;
+      const uint64_t m = wave_max_u64(lbest);
+      if (m > 0) {
+#pragma unroll
+        for (int ps = NPASS - 1; ps >= 0; --ps) {
+          const uint64_t b = ballot(lbest == m && (lst & 3) == ps);
+          if (b) best_node = ps * kWave + first_lane(b);
         }
       }
-      if (exc != EXC_NONE) break;
       prof.mark(PH_SCORE);
 
       if (best_node < 0) {
