@@ -465,7 +465,8 @@ class DeviceEngine {
   }
 
   py::tuple profile(py::object fam_or_none, py::object weights_or_none, py::object programs_or_none) {
-    if (npass_ != 1) throw std::invalid_argument("profiling supports <= 64 nodes");
+    const bool c5 = npass_ == 4 && programs_or_none.is_none();
+    if (npass_ != 1 && !c5) throw std::invalid_argument("profiling supports <= 64 nodes, or the composite family on 256");
     HIP_OK(hipSetDevice(device_));
     Slot& s = idle_slot(0);
     bool is_vm = !programs_or_none.is_none();
@@ -496,7 +497,14 @@ class DeviceEngine {
       const fksk::BuiltinArgs a{Wl, wc, reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + wb),
                                 s.h_in.dev<double>(), s.w.as<double>(), s.res.as<DevResult>(), gh,
                                 s.prof.as<uint64_t>()};
-      HIP_OK(fksk::launch_builtin_prof(g, P, lds, s.stream, a));
+      if (c5) {
+        // the production composite instance only (fast reciprocal path, HBM heap)
+        if (s.fam_spec != FAM_COMPOSITE_LINEAR || !g)
+          throw std::invalid_argument("256-node profiling: composite batch with verified reciprocals and an HBM heap");
+        HIP_OK(fksk::launch_c5_prof(P, lds, s.stream, a));
+      } else {
+        HIP_OK(fksk::launch_builtin_prof(g, P, lds, s.stream, a));
+      }
     }
     finish(s);
     py::array_t<uint64_t> prof({(py::ssize_t)P, (py::ssize_t)8});

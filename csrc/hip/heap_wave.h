@@ -55,6 +55,13 @@ struct WaveHeapT {
     if (i < T) return top[i];
     return h[i];
   }
+  // Slot i with i uniform: a ds_read or a global_load behind a scalar branch.
+  // A flat load counts in both vmcnt and lgkmcnt, so an LDS read issued after
+  // a flat HBM load waits for it; these wait on their own counter only.
+  __device__ __forceinline__ uint64_t ld_u(int i) const {
+    if (i < T) return top[i];
+    return h[i];
+  }
   __device__ __forceinline__ void st(int i, uint64_t v) const {
     if constexpr (FLAT) {
       *((i < T ? gtop : gh) + i) = v;
@@ -96,7 +103,8 @@ struct WaveHeapT {
       rounds = rd + 1;
       const int idx = ((pos + 1) << r) - 1 + i;
       const bool valid = lane < 62 && idx < n;
-      const uint64_t v = valid ? ld(idx) : ~0ull;
+      // the first round (slots < 63) is LDS-resident whenever T >= 63: ds_read
+      const uint64_t v = !valid ? ~0ull : (FLAT && rd == 0 && T >= 63) ? top[idx] : ld(idx);
       const uint64_t sib = swap_pairs64(v);
       const bool go_right = ((lane & 1) == 0) && valid && (idx + 1 < n) && !key_lt(v, sib, lb);
       const uint64_t right_mask = ballot(go_right);

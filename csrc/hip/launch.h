@@ -106,6 +106,8 @@ hipError_t native_rt_table(uint64_t* dev_out, hipStream_t s);
 // phase-profiled variants (NPASS = 1)
 hipError_t launch_builtin_prof(bool gheap, int P, size_t lds, hipStream_t s, const BuiltinArgs& a);
 hipError_t launch_vm_prof(bool gheap, int P, size_t lds, hipStream_t s, const VmArgs& a);
+// composite family, 4 node slots per lane, HBM heap (config-5 shape)
+hipError_t launch_c5_prof(int P, size_t lds, hipStream_t s, const BuiltinArgs& a);
 hipError_t set_prof_attrs(int max_lds);
 
 }  // namespace fksk

@@ -327,10 +327,10 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
       for (int ps = 0; ps < NPASS; ++ps) asm volatile("" : "+v"(nr.ngpus[ps]));
     }
     // ---------------- pop (pod record load issued first, consumed after the sift)
-    const uint64_t top = uniu64(heap.ld(0));
+    const uint64_t top = uniu64(heap.ld_u(0));
     const int rank = (int)((top >> lb) & ((1ull << rb) - 1));
     const int4 precv = load_vgpr(&W.pod[rank]);
-    const uint64_t last = uniu64(heap.ld(n - 1));
+    const uint64_t last = uniu64(heap.ld_u(n - 1));
     --n;
     if (n > 0) heap.pop_reinsert(n, last);
 

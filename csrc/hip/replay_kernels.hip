@@ -193,6 +193,17 @@ __global__ FKS_BOUNDS(GHEAP) void k_replay_builtin_prof(fksk::BuiltinArgs a) {
                                                  a.prof + (size_t)p * 8);
 }
 
+// 256-node clusters: the production composite instance (4 node slots per
+// lane, HBM heap, same launch bounds) with the s_memtime phase profiler
+__global__ __launch_bounds__(64, FKS_NP4_WAVES) void k_replay_c5_prof(fksk::BuiltinArgs a) {
+  const int p = blockIdx.x;
+  const Slot s = policy_slot<true>(a.W, a.gheap, p);
+  BuiltinScorerDev<FAM_COMPOSITE_LINEAR> sc;
+  load_policy<FAM_COMPOSITE_LINEAR>(sc, s, a, p);
+  replay_one<4, BuiltinScorerDev<FAM_COMPOSITE_LINEAR>, PhaseProf, FKS_WAVE_FLAT>(
+      a.W, kernarg_workload(), sc, s.h, s.top, s.T, s.delmap, s.inv, a.out + p, a.prof + (size_t)p * 8);
+}
+
 template <bool GHEAP>
 __global__ FKS_VM_BOUNDS(GHEAP) void k_replay_vm_prof(fksk::VmArgs a) {
   const int p = blockIdx.x;
@@ -369,6 +380,10 @@ hipError_t launch_builtin_prof(bool gheap, int P, size_t lds, hipStream_t s, con
   else hipLaunchKernelGGL(k_replay_builtin_prof<false>, dim3(P), dim3(64), lds, s, a);
   return hipGetLastError();
 }
+hipError_t launch_c5_prof(int P, size_t lds, hipStream_t s, const BuiltinArgs& a) {
+  hipLaunchKernelGGL(k_replay_c5_prof, dim3(P), dim3(64), lds, s, a);
+  return hipGetLastError();
+}
 hipError_t launch_vm_prof(bool gheap, int P, size_t lds, hipStream_t s, const VmArgs& a) {
   if (gheap) hipLaunchKernelGGL(k_replay_vm_prof<true>, dim3(P), dim3(64), lds, s, a);
   else hipLaunchKernelGGL(k_replay_vm_prof<false>, dim3(P), dim3(64), lds, s, a);
@@ -377,7 +392,8 @@ hipError_t launch_vm_prof(bool gheap, int P, size_t lds, hipStream_t s, const Vm
 hipError_t set_prof_attrs(int mx) {
   hipError_t e = hipSuccess;
   for (hipError_t r : {raise_lds(&k_replay_builtin_prof<true>, mx), raise_lds(&k_replay_builtin_prof<false>, mx),
-                       raise_lds(&k_replay_vm_prof<true>, mx), raise_lds(&k_replay_vm_prof<false>, mx)})
+                       raise_lds(&k_replay_vm_prof<true>, mx), raise_lds(&k_replay_vm_prof<false>, mx),
+                       raise_lds(&k_replay_c5_prof, mx)})
     if (r != hipSuccess) e = r;
   return e;
 }

@@ -77,7 +77,7 @@ def test_async_slots_match_sync(dev, default_workload):
     assert dev.ready(1) and dev.ready(2)
 
 
-@pytest.mark.parametrize("top", [0, 63, 1023, 2047])
+@pytest.mark.parametrize("top", [0, 3, 7, 63, 127, 511, 1023, 2047])
 def test_hbm_heap_with_lds_top_matches_cpu(default_workload, top):
     """Heap slots split between LDS (top levels) and HBM give the CPU oracle's tables."""
     from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
