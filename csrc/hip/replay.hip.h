@@ -380,7 +380,6 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
         const uint64_t s = valid ? (uint64_t)scorer.template score<NPASS>(ps, nr, pod, lexc) : 0;   // >= 0
         if (valid && lexc != EXC_NONE && (lst >> 8) == 0) lst |= (lexc << 8) | (ps << 2);
         if (s > lbest) { lbest = s; lst = (lst & ~3) | ps; }
-        __builtin_amdgcn_sched_barrier(0);   // one slot at a time: no interleaved live ranges
       }
       if (ballot((lst >> 8) != 0)) {
         // the first raising node in node order (slot-major, then lane); the
