@@ -1,6 +1,10 @@
 """`evaluate()`: score policy programs on the fastest exact engine available.
 
-Routing per program (every path yields the reference's score bit-for-bit):
+Routing per program (every path yields the reference's score bit-for-bit, with
+one documented exception: a device pow/exp/log result is correctly rounded, and
+where glibc -- what CPython calls -- rounds the other way (~0.08% of such calls,
+outside the narrow near-midpoint defer band) a program using them can score
+differently; docs/ARCHITECTURE.md "Exactness", parity unpinned there):
 
 1. compile to bytecode (`policy.compiler`); programs outside the native
    subset go straight to the object engine (CPython ``exec``, step 4);
