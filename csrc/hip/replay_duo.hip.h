@@ -18,7 +18,7 @@
 //     pointer, argmax, GPU pick, snapshot schedule) and answers creations.
 // The two waves of a workgroup are co-resident, and each waits on the other
 // through LDS counters with release/acquire ordering and a bounded spin (a
-// lost partner ends the replay with EXC_INVARIANT instead of hanging).
+// lost partner ends the replay with EXC_TIMEOUT instead of hanging).
 // Event order, heap operations and arithmetic are exactly those of
 // replay_rows (bit-identical results; tests/test_gpu_native.py).
 #pragma once
@@ -213,7 +213,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
         tail_seen = duo_ld(&box->tail);
         if (k - tail_seen < (uint32_t)kDuoRing) break;
         __builtin_amdgcn_s_sleep(FKS_DUO_SLEEP);
-        if (++spins > kDuoSpinCap) { hexc = EXC_INVARIANT; return false; }
+        if (++spins > kDuoSpinCap) { hexc = EXC_TIMEOUT; return false; }
       }
       if (lane == 0) box->ev[k % kDuoRing] = key;
       if (lane == 0) duo_st(&box->head, k + 1);
@@ -240,7 +240,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
         uint32_t spins = 0;
         while (duo_ld(&box->rseq) != k + 1) {
           __builtin_amdgcn_s_sleep(FKS_DUO_SLEEP);
-          if (++spins > kDuoSpinCap) { hexc = EXC_INVARIANT; break; }
+          if (++spins > kDuoSpinCap) { hexc = EXC_TIMEOUT; break; }
         }
         if (hexc != EXC_NONE) break;
         mark(3);
@@ -343,7 +343,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
       if (duo_ld(&box->head) > k) { have = true; break; }
       if (duo_ld(&box->term)) { have = duo_ld(&box->head) > k; break; }
       __builtin_amdgcn_s_sleep(FKS_DUO_SLEEP);
-      if (++spins > kDuoSpinCap) { exc = EXC_INVARIANT; break; }
+      if (++spins > kDuoSpinCap) { exc = EXC_TIMEOUT; break; }
     }
     if (!have) break;
     mark(0);
@@ -498,7 +498,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
     uint32_t spins = 0;
     while (!duo_ld(&box->term)) {
       __builtin_amdgcn_s_sleep(FKS_DUO_SLEEP);
-      if (++spins > kDuoSpinCap) { exc = exc != EXC_NONE ? exc : EXC_INVARIANT; break; }
+      if (++spins > kDuoSpinCap) { exc = exc != EXC_NONE ? exc : EXC_TIMEOUT; break; }
     }
   }
   if (exc == EXC_NONE && box->h_exc != EXC_NONE) {

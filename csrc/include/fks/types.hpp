@@ -27,6 +27,7 @@ enum ExcCode : int32_t {
   EXC_UNSUPPORTED = 100,   // semantics outside the native subset (bigint, ...): re-run exactly on host
   EXC_BUDGET = 101,        // instruction budget exhausted (runaway program)
   EXC_INVARIANT = 102,     // resource accounting invariant violated (debug check)
+  EXC_TIMEOUT = 103,       // engine-internal timeout (two-wave kernel spin cap): re-run on the next engine
 };
 
 enum RepushMode : int32_t { REPUSH_FIRST = 0, REPUSH_EARLIEST = 1 };

@@ -142,11 +142,26 @@ def _object_worker(args):
 
 # ---------------------------------------------------------------------------- evaluator
 #: exception codes of a native-program row that hand the program to the next
-#: engine: UNSUPPORTED / BUDGET as for every engine, plus INVARIANT -- the
-#: two-wave kernel ends a replay with it when one wave stops hearing from the
-#: other (a bounded spin, replay_duo.hip.h), which depends on timing, not on
-#: the program, so it is never a final score
-NATIVE_DEFER = (int(Exc.UNSUPPORTED), int(Exc.BUDGET), int(Exc.INVARIANT))
+#: engine: UNSUPPORTED / BUDGET as for every engine, TIMEOUT -- the two-wave
+#: kernel ends a replay with it when one wave stops hearing from the other (a
+#: bounded spin, replay_duo.hip.h), which depends on timing, not on the
+#: program -- and INVARIANT, a failed accounting check, i.e. a kernel bug: the
+#: program is re-scored by the next engine (so the score stays exact) but the
+#: row is counted in ``stats["native_invariant"]`` and logged, never hidden
+NATIVE_DEFER = (int(Exc.UNSUPPORTED), int(Exc.BUDGET), int(Exc.TIMEOUT), int(Exc.INVARIANT))
+
+
+def _native_deferred(row, stats) -> bool:
+    """True: this native-program row goes to the next engine (counted)."""
+    exc = int(row[COLS["exc"]])
+    if exc == Exc.TIMEOUT:
+        stats["native_timeout"] += 1
+    elif exc == Exc.INVARIANT:
+        stats["native_invariant"] += 1
+        import warnings
+        warnings.warn("native replay failed its invariant check (kernel bug?); program re-scored on the CPU VM",
+                      RuntimeWarning, stacklevel=3)
+    return exc in NATIVE_DEFER or bool(row[COLS["inexact"]])
 
 
 class Evaluator:
@@ -195,7 +210,7 @@ class Evaluator:
                     if device != "auto":
                         raise
         self.stats = {"device": 0, "device_native": 0, "cpu_vm": 0, "object": 0, "compile_errors": 0,
-                      "jit_s": 0.0, "jit_shapes": 0}
+                      "jit_s": 0.0, "jit_shapes": 0, "native_timeout": 0, "native_invariant": 0}
         self._done: Dict[int, np.ndarray] = {}   # CPU stand-in for in-flight slots
 
     @property
@@ -319,7 +334,7 @@ class Evaluator:
         if self.device is not None and self.native and progs:
             self.device.submit_native(slot, progs)
             tab = self.device.wait(slot)
-            ok = ~np.isin(tab[:, COLS["exc"]], NATIVE_DEFER) & (tab[:, COLS["inexact"]] == 0)
+            ok = np.array([not _native_deferred(row, self.stats) for row in tab], dtype=bool)
             out[ok] = tab[ok, COLS["score"]]
             rest = [i for i in range(len(progs)) if not ok[i]]
             self.stats["device_native"] += int(ok.sum())
@@ -377,7 +392,7 @@ class Evaluator:
             tab = self.device.wait(pend.slot)
             pend.t_done = time.perf_counter()
             for row, i in zip(tab, pend.native_idx):
-                if int(row[COLS["exc"]]) in NATIVE_DEFER or row[COLS["inexact"]]:
+                if _native_deferred(row, self.stats):
                     continue
                 out[i] = _row_to_result(row, "hip-native")
                 self.stats["device_native"] += 1
@@ -400,7 +415,7 @@ class Evaluator:
         self.stats["jit_shapes"] += batch.compiled
         tab = self.device.wait(slot)
         for row, i in zip(tab, idx):
-            if int(row[COLS["exc"]]) in NATIVE_DEFER or row[COLS["inexact"]]:
+            if _native_deferred(row, self.stats):
                 continue
             out[i] = _row_to_result(row, "hip-native")
             self.stats["device_native"] += 1

@@ -183,7 +183,7 @@ class IslandFunSearch:
         best_local = self.best[1]
         chan = self._sync_channel()
         stop = best_local >= self._threshold and not chan.active
-        if self.migrate_every and self.generation % self.migrate_every == 0:
+        if chan.every and self.generation % chan.every == 0:
             # lock-step mode: a blocking gather; its header carries every rank's
             # best and stop vote (no per-generation all-reduce)
             with roctx_range(f"funsearch.migrate gen {self.generation}"):
@@ -463,7 +463,7 @@ class IslandFunSearch:
                         progressed = True
                     g_min = min(gen)
                     if (cpl["fut"] is None and g_min > cpl["last"] and self.coupler.due(g_min)
-                            and g_min < target and not stop[0]):
+                            and g_min < target and not stop[0] and not self._ck_due):
                         cpl["last"] = g_min
                         cpl["fut"] = pool.submit(self.run_coupling)
                     idle = [j for j in range(k) if phase[j] == "idle"]
@@ -473,7 +473,9 @@ class IslandFunSearch:
                 for i in range(k):
                     s = self.islands[i]
                     if phase[i] == "idle":
-                        if gen[i] >= target or stop[0]:
+                        if gen[i] >= target or stop[0] or self._ck_due:
+                            # a due checkpoint holds idle islands back until every
+                            # island is between generations (the consistent cut above)
                             continue
                         s.generation += 1
                         plan[i] = self._plan(s)
@@ -623,13 +625,18 @@ class IslandFunSearch:
         return self.global_best()
 
     def global_best(self) -> Tuple[Optional[str], float]:
+        """(code, score) of the best program on any rank.  Programs of any
+        length travel (`dist.all_gather_bytes`, as the reference saves any
+        program, funsearch_integration.py:599-679); ties go to the lowest rank,
+        so every rank returns the same program."""
         code, score = self.best
         if not self.ctx.distributed:
             return code, score
-        rec = dist.pack_programs([code or ""], [score])
-        allr = self._collective("global_best", lambda: dist.all_gather_array(rec), rec[None])
-        best = max(dist.unpack_programs(allr), key=lambda cs: cs[1], default=(code, score))
-        return best
+        mine = json.dumps({"code": code, "score": float(score)}).encode("utf-8")
+        allb = self._collective("global_best", lambda: dist.all_gather_bytes(mine), [mine])
+        recs = [json.loads(b.decode("utf-8")) for b in allb]
+        best = max(recs, key=lambda r: r["score"])      # first (lowest rank) of equal scores
+        return best["code"], float(best["score"])
 
     # -- checkpoint ----------------------------------------------------------------------
     def save_checkpoint(self) -> str:

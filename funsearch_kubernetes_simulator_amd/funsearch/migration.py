@@ -21,6 +21,16 @@ with the slowest one (its slowest replay plus its JIT), so a migration is
   its peers may already have started (through ``m + lookahead * every``) and
   the ranks leave with equal collective sequences.
 
+* **stop delay**: a stop takes effect ``lookahead * every`` generations after
+  the migration whose gather first carries a vote (or a best over the
+  threshold), so a run may continue up to ``(lookahead + 1) * every``
+  generations past the generation that reached the threshold.
+* **no migrations, several ranks** (``migrate_every = 0``): the channel still
+  runs, as a *stop-only* channel -- every generation an async all-gather of
+  the 16-byte header plus an empty blob -- so ranks never stop on their own
+  local best (a rank leaving early would sit in the final champion gather
+  while its peers run on, and time out as a "lost" peer).
+
 `wait_s` accumulates the wall time a rank spent blocked in collectives (the
 "collective wait" of the multi-rank logs).
 """
@@ -51,6 +61,10 @@ class MigrationChannel:
     def __init__(self, fs, every: int, start: int, lookahead: int = 2):
         self.fs = fs
         self.every = int(every)
+        #: False: a stop-only channel (several ranks, no migrations configured)
+        self.migrate = self.every > 0
+        if not self.every and fs.ctx.distributed:
+            self.every = 1
         self.next = start + self.every if self.every else None
         self.lookahead = max(1, int(lookahead))
         self.pending: deque = deque()
@@ -71,7 +85,8 @@ class MigrationChannel:
 
     def payload(self, vote: bool) -> np.ndarray:
         hdr = np.array([self.fs.best[1], 1.0 if vote else 0.0], dtype=np.float64)
-        return np.concatenate([hdr.view(np.uint8), self.fs.migrant_blob()])
+        blob = self.fs.migrant_blob() if self.migrate else np.zeros(8, dtype=np.uint8)   # length 0: no migrants
+        return np.concatenate([hdr.view(np.uint8), blob])
 
     def post(self, generation: int, vote: bool) -> None:
         t = time.perf_counter()

@@ -211,6 +211,9 @@ def _cache_load(key: str, n: int) -> Optional[CompiledModule]:
         return None
     if meta.get("n") != n or len(image) != meta.get("bytes"):
         return None
+    import hashlib
+    if meta.get("sha256") != hashlib.sha256(image).hexdigest():
+        return None    # corrupted / replaced image (the directory is shared): a miss, recompile
     res = [Resources(**r) if r is not None else None for r in meta["resources"]]
     return CompiledModule(image, n, res, 0.0, cached=True)
 
@@ -220,12 +223,14 @@ def _cache_store(key: str, mod: CompiledModule) -> None:
     d = _cache_dir()
     if d is None:
         return
+    import hashlib
     import json
     from dataclasses import asdict
     try:
         os.makedirs(d, exist_ok=True)
         for ext, data, mode in ((".co", mod.image, "wb"),
-                                (".json", json.dumps({"n": mod.n, "bytes": len(mod.image), "resources": [
+                                (".json", json.dumps({"n": mod.n, "bytes": len(mod.image),
+                                                      "sha256": hashlib.sha256(mod.image).hexdigest(), "resources": [
                                     asdict(r) if r is not None else None for r in mod.resources]}), "w")):
             tmp = os.path.join(d, f".{key}{ext}.{os.getpid()}.{threading.get_ident()}")
             with open(tmp, mode) as f:
@@ -392,6 +397,7 @@ class NativeCompiler:
                     reasons[i] = self._bad.get(k, "not compiled")
             self.stats["hits"] += P - len(mine)
             up = self._tierup_candidates(keys, progs) if self.tierup_after else []
+        self._reap_tierup()
         for k, p in up:
             self._tierup_futs.append(self._tierup_executor().submit(self._tierup, k, p))
         return NativeBatch(fn, np.concatenate(blocks) if blocks else np.zeros(1, np.int64), koff, ok, reasons, dt,
@@ -438,6 +444,21 @@ class NativeCompiler:
             self.stats["tierup_s"] += mod.compile_s
             self.stats["disk_hits"] += int(mod.cached)
         return True
+
+    def _reap_tierup(self) -> None:
+        """Drop finished tier-up futures; an exception in one (e.g. a failed
+        module load in the worker) is counted and logged, not lost."""
+        keep = []
+        for f in self._tierup_futs:
+            if not f.done():
+                keep.append(f)
+                continue
+            exc = f.exception()
+            if exc is not None:
+                self.stats["tierup_errors"] = self.stats.get("tierup_errors", 0) + 1
+                import warnings
+                warnings.warn(f"background tier-up failed: {type(exc).__name__}: {exc}", RuntimeWarning)
+        self._tierup_futs = keep
 
     def drain_tierup(self) -> None:
         """Wait for every queued background recompile (tests, benchmarks)."""

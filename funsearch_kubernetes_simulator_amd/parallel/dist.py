@@ -196,17 +196,38 @@ def shutdown() -> None:
     _ctx = None
 
 
+def all_gather_bytes(payload: bytes):
+    """Every rank's byte string, whatever its length: one all-gather of the
+    lengths, then one of the payloads padded to the longest (two small
+    collectives; used where a record must never be truncated, e.g. the
+    final cross-rank champion)."""
+    ctx = context()
+    if not ctx.distributed:
+        return [bytes(payload)]
+    n = all_gather_array(np.array([len(payload)], dtype=np.int64)).reshape(-1)
+    buf = np.zeros(max(1, int(n.max())), dtype=np.uint8)
+    buf[:len(payload)] = np.frombuffer(payload, dtype=np.uint8)
+    allb = all_gather_array(buf)
+    return [allb[r, :int(n[r])].tobytes() for r in range(ctx.world_size)]
+
+
 # -------------------------------------------------------------------- program records
 RECORD_BYTES = 4096   # fixed-width records (pack_programs): single programs, tests
 
 
+class RecordTooLong(ValueError):
+    """A program does not fit a fixed-width record (never sent truncated or empty)."""
+
+
 def pack_programs(codes, scores, width: int = RECORD_BYTES) -> np.ndarray:
-    """Fixed-size byte records [E, 16 + width]: score (f64), length (i64), utf-8 text."""
+    """Fixed-size byte records [E, 16 + width]: score (f64), length (i64), utf-8 text.
+    Raises `RecordTooLong` rather than emitting an empty slot; variable-length
+    payloads go through `all_gather_bytes` / `pack_migrants`."""
     out = np.zeros((len(codes), 16 + width), dtype=np.uint8)
     for i, (c, s) in enumerate(zip(codes, scores)):
         b = c.encode("utf-8")
         if len(b) > width:
-            b = b""   # too long: sent as an empty slot
+            raise RecordTooLong(f"program {i} is {len(b)} bytes, record width {width}")
         out[i, :8] = np.frombuffer(np.float64(s).tobytes(), dtype=np.uint8)
         out[i, 8:16] = np.frombuffer(np.int64(len(b)).tobytes(), dtype=np.uint8)
         out[i, 16:16 + len(b)] = np.frombuffer(b, dtype=np.uint8)

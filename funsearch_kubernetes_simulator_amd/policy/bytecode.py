@@ -97,6 +97,7 @@ class Exc(enum.IntEnum):
     UNSUPPORTED = 100
     BUDGET = 101
     INVARIANT = 102
+    TIMEOUT = 103
 
 
 _INSN = struct.Struct("<BBBBi")

@@ -300,6 +300,33 @@ def test_pipelined_islands_migrate_at_barrier(tmp_path):
     assert (tmp_path / "ck" / "islands_rank0.json").exists()
 
 
+def test_pipelined_islands_checkpoint_mid_run(tmp_path):
+    """A due checkpoint holds idle islands back until all are between
+    generations, so the file is written mid-run (not only by run()'s final
+    save) and holds a consistent generation."""
+    from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
+    cfg = _cfg(tmp_path)
+    cfg["islands"] = {"per_rank": 3, "migrate_every": 0, "migrants": 1, "pipeline": True}
+    cfg["checkpoint"] = {"dir": str(tmp_path / "ck"), "every": 2}
+    fs = IslandFunSearch(cfg)
+    saved = []
+    orig = fs.save_checkpoint
+
+    def spy():
+        saved.append((fs.generation, [s.generation for s in fs.islands]))
+        return orig()
+    fs.save_checkpoint = spy
+    fs.run(6)
+    assert fs.generation == 6
+    mid = [s for s in saved if s[0] < 6]
+    assert mid, saved                                   # written before the last generation
+    for g, per_island in mid:
+        # every island between generations, none behind the completed global generation
+        assert g % 2 == 0 and all(x >= g for x in per_island), saved
+    st = json.load(open(tmp_path / "ck" / "islands_rank0.json"))
+    assert st["generation"] == 6
+
+
 def test_islands_with_constant_polish(tmp_path):
     """polish.every: island champions get a batched constant search; the
     rewritten program enters the population only with its exact re-score."""

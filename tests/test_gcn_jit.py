@@ -224,8 +224,33 @@ def test_llvm_tier_disk_cache(tmp_path, monkeypatch):
     assert not a.cached and b.cached and a.image == b.image and a.resources == b.resources
     assert b.compile_s < a.compile_s
     assert len(list((tmp_path / "cache").glob("*.co"))) == 1
+    # a cached image whose bytes no longer match its recorded sha256 is a miss
+    co = next((tmp_path / "cache").glob("*.co"))
+    raw = bytearray(co.read_bytes())
+    raw[-1] ^= 0xFF
+    co.write_bytes(bytes(raw))
+    assert not jit.compile_device_module([p]).cached
     monkeypatch.setenv("FKS_JIT_CACHE", "off")
     assert not jit.compile_device_module([p]).cached
+
+
+def test_skeleton_provenance_rebuilds_stale_files(tmp_path, monkeypatch):
+    """A skeleton is reused only if built from the current source and its bytes
+    are unchanged; an edited source or a modified file triggers a rebuild."""
+    if not os.path.exists(gcnjit.CLANG):
+        pytest.skip("ROCm clang not installed")
+    monkeypatch.setattr(gcnjit, "skeleton_path", lambda size: tmp_path / f"skel_{size >> 10}k.co")
+    size = gcnjit.SKELETON_SIZES[0]
+    path = gcnjit.build_skeleton(size)
+    assert gcnjit.skeleton_is_current(size)
+    raw = bytearray(path.read_bytes())
+    raw[100] ^= 0xFF
+    path.write_bytes(bytes(raw))
+    assert not gcnjit.skeleton_is_current(size)
+    gcnjit.build_skeleton(size)
+    assert gcnjit.skeleton_is_current(size)
+    monkeypatch.setattr(gcnjit, "SKELETON_SOURCE", gcnjit.SKELETON_SOURCE + "// edited\n")
+    assert not gcnjit.skeleton_is_current(size)
 
 
 def test_per_lane_pods_several_rows_in_one_call(corpus):

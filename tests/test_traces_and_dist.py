@@ -95,6 +95,85 @@ def test_gloo_collectives_and_migration(tmp_path):
     assert out["ok"] and out["best_island0"] >= 100
 
 
+def test_global_best_carries_long_program_across_ranks(tmp_path):
+    """The cross-rank champion travels whatever its length: rank 1 holds a
+    >8 KB best program, both ranks return it (no fixed-width record)."""
+    _rank_loss_config(tmp_path)
+    script = tmp_path / "w.py"
+    script.write_text(
+        "import json\n"
+        "from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch\n"
+        "from funsearch_kubernetes_simulator_amd.parallel import dist\n"
+        f"fs = IslandFunSearch({str(tmp_path / 'cfg.json')!r})\n"
+        "s = fs.islands[0]\n"
+        "if fs.ctx.rank == 1:\n"
+        "    s.best_policy = 'def priority_function(pod, node):\\n' + '    x = 1\\n' * 1200 + '    return 7\\n'\n"
+        "    s.best_score = 0.9\n"
+        "else:\n"
+        "    s.best_policy, s.best_score = 'def priority_function(pod, node):\\n    return 1\\n', 0.5\n"
+        "code, score = fs.global_best()\n"
+        "try:\n"
+        "    dist.pack_programs([code], [score])\n"
+        "    raised = False\n"
+        "except dist.RecordTooLong:\n"
+        "    raised = True\n"
+        "print(json.dumps({'rank': fs.ctx.rank, 'len': len(code), 'score': score, 'raised': raised,\n"
+        "                  'same': code == s.best_policy}))\n"
+        "dist.shutdown()\n")
+    r = _run_torchrun(str(script))
+    assert r.returncode == 0, r.stderr[-2000:]
+    import re
+    outs = [json.loads(m) for m in re.findall(r"\{[^{}]*\}", r.stdout)]
+    assert sorted(o["rank"] for o in outs) == [0, 1]
+    for o in outs:
+        assert o["len"] > 8192 and o["score"] == 0.9 and o["raised"]
+        assert o["same"] == (o["rank"] == 1)
+
+
+def test_no_migration_ranks_agree_on_stop(tmp_path):
+    """migrate_every = 0 with two ranks: a stop-only channel makes both ranks
+    stop at the same generation (threshold 0 is reached at once), so neither
+    waits in the champion gather for a peer that runs on."""
+    cfg = {"llm": {"backend": "mutation", "seed": 3}, "safe_execution": {"timeout_seconds": 3},
+           "funsearch": {"population_size": 6, "generations": 6, "early_stop_threshold": 0.0, "elite_size": 3,
+                         "max_workers": 2, "policies_per_generation": 2},
+           "islands": {"per_rank": 2, "migrate_every": 0, "migrants": 1},
+           "device": {"kind": "cpu"}}
+    outs = []
+    for mode in ("sync", "pipeline"):
+        c = json.loads(json.dumps(cfg))
+        c["islands"]["pipeline"] = mode == "pipeline"
+        (tmp_path / f"{mode}.json").write_text(json.dumps(c))
+    script = tmp_path / "w.py"
+    script.write_text(
+        "import json, sys\n"
+        "from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch\n"
+        "from funsearch_kubernetes_simulator_amd.parallel import dist\n"
+        "res = {}\n"
+        "for mode in ('sync', 'pipeline'):\n"
+        f"    fs = IslandFunSearch({str(tmp_path)!r} + '/' + mode + '.json')\n"
+        "    code, score = fs.run()\n"
+        "    res[mode] = [fs.generation, [s.generation for s in fs.islands], score]\n"
+        "print(json.dumps({'rank': fs.ctx.rank, 'res': res}))\n"
+        "dist.shutdown()\n")
+    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1", FKS_DIST_TIMEOUT_S="120")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(35000 + os.getpid() % 1000), str(script)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    import re
+    outs = [json.loads(m) for m in re.findall(r"\{\"rank.*\}", r.stdout)]
+    assert len(outs) == 2
+    a, b = outs
+    assert a["res"]["sync"][0] == b["res"]["sync"][0] == 1          # lock-step: stop agreed in generation 1
+    assert a["res"]["sync"][2] == b["res"]["sync"][2]                 # same champion score on both ranks
+    # pipelined: both ranks stop well before the configured 6 generations, each within the
+    # channel's documented delay (lookahead * every generations after the first vote)
+    for o in (a, b):
+        assert o["res"]["pipeline"][0] <= 4, outs
+    assert a["res"]["pipeline"][2] == b["res"]["pipeline"][2]
+
+
 def test_inject_one_per_island_equals_ring_inject():
     """bench.py's asynchronous migration injects island by island (inject_one);
     applied to every island it is the ring migration of inject()."""
