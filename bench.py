@@ -81,6 +81,9 @@ def main() -> None:
     ap.add_argument("--novel", type=int, default=256,
                     help="after the timed region: this many programs, every one a NEW shape (JIT included), "
                          "against the CPU VM on the same batch; reported as `program_path.novel` (0: skip)")
+    ap.add_argument("--novel-large", type=int, default=2048,
+                    help="after the timed region: an LLM-scale batch of this many new-shape programs (JIT included, "
+                         "chunks over the slots, all in flight at once); reported as `program_path.novel_large` (0: skip)")
     ap.add_argument("--time-budget", type=float, default=0.0,
                     help="run generations until this many seconds have passed (instead of --steps); "
                          "steps = generations completed")
@@ -263,6 +266,11 @@ def main() -> None:
             nov = measure_novel(ev.device, workload, args.novel, seed=args.seed + 17 + 1000 * ctx.rank)
             nov["vs_baseline"] = round(nov["evals_per_s_incl_jit"] / BASELINE_EVALS_PER_S, 2)
             program_path["novel"] = nov
+        if args.novel_large > 0:
+            from funsearch_kubernetes_simulator_amd.bench.programs import measure_novel_large
+            big = measure_novel_large(ev.device, workload, args.novel_large, seed=args.seed + 31 + 1000 * ctx.rank)
+            big["vs_baseline"] = round(big["evals_per_s_incl_jit"] / BASELINE_EVALS_PER_S, 2)
+            program_path["novel_large"] = big
 
     per_step = args.islands * args.candidates
     total = per_step * args.steps * ctx.world_size

@@ -361,6 +361,108 @@ PYBIND11_MODULE(_fks_cpu, m) {
     out["vregs"] = r.vregs; out["tagged"] = r.tagged; out["mir"] = r.mir;
     return out;
   }, py::arg("code"), py::arg("ctag"), py::arg("is_lit"), py::arg("iconst"), py::arg("fconst"));
+  // A batch of programs on `threads` host threads (the generator is
+  // re-entrant): one dict per program, as gcn_compile.  The steady-state
+  // search and the novel-program bench compile hundreds of new shapes at once.
+  m.def("gcn_compile_many", [](py::list progs, int threads) {
+    struct Owned {
+      std::string code;
+      std::vector<uint8_t> ctag, is_lit;
+      std::vector<int64_t> iconst;
+      std::vector<double> fconst;
+    };
+    const size_t n = progs.size();
+    std::vector<Owned> own(n);
+    for (size_t i = 0; i < n; ++i) {
+      py::tuple t = progs[i].cast<py::tuple>();
+      if (t.size() != 5) throw std::invalid_argument("program tuple: (code, ctag, is_lit, iconst, fconst)");
+      own[i].code = t[0].cast<std::string>();
+      auto ct = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>(t[1]);
+      auto il = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>(t[2]);
+      auto ic = py::array_t<int64_t, py::array::c_style | py::array::forcecast>(t[3]);
+      auto fc = py::array_t<double, py::array::c_style | py::array::forcecast>(t[4]);
+      if (il.size() != ct.size() || ic.size() != ct.size() || fc.size() != ct.size())
+        throw std::invalid_argument("constant arrays differ in length");
+      own[i].ctag.assign(ct.data(), ct.data() + ct.size());
+      own[i].is_lit.assign(il.data(), il.data() + il.size());
+      own[i].iconst.assign(ic.data(), ic.data() + ic.size());
+      own[i].fconst.assign(fc.data(), fc.data() + fc.size());
+    }
+    std::vector<gcnapi::Result> res(n);
+    {
+      py::gil_scoped_release rel;
+      std::atomic<size_t> next{0};
+      auto work = [&]() {
+        for (size_t i = next++; i < n; i = next++) {
+          gcnapi::ProgramDesc p;
+          p.code = reinterpret_cast<const uint8_t*>(own[i].code.data());
+          p.code_bytes = own[i].code.size();
+          p.ctag = own[i].ctag.data(); p.is_lit = own[i].is_lit.data();
+          p.iconst = own[i].iconst.data(); p.fconst = own[i].fconst.data();
+          p.n_const = own[i].ctag.size();
+          res[i] = gcnapi::compile(p);
+        }
+      };
+      const int nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(1, threads), n));
+      std::vector<std::thread> pool;
+      for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+      work();
+      for (auto& th : pool) th.join();
+    }
+    py::list out;
+    for (const auto& r : res) {
+      py::dict d;
+      d["ok"] = r.ok;
+      d["reason"] = r.reason;
+      d["words"] = np_of(r.words);
+      d["relocs"] = np_of(r.relocs);
+      d["n_insns"] = r.n_insns; d["vgprs"] = r.vgprs; d["sgprs"] = r.sgprs; d["calls"] = r.calls;
+      d["vregs"] = r.vregs; d["tagged"] = r.tagged; d["mir"] = r.mir;
+      out.append(d);
+    }
+    return out;
+  }, py::arg("programs"), py::arg("threads") = 1);
+  // Link a batch into a code-object skeleton: program i at arena offset
+  // offsets[i] (align-byte aligned), its runtime-table references relocated
+  // (PC-relative: lo / hi literal words at byte pc of the s_getpc), and the
+  // runtime table's initial value written into the image, so loading needs no
+  // device-side fix-up.  Returns (image, offsets) or raises if the arena is
+  // too small.
+  m.def("gcn_link", [](py::bytes skel, int64_t arena_off, int64_t arena_vaddr, int64_t capacity, int64_t rt_vaddr,
+                       int64_t rt_off, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> rt_vals,
+                       py::list words, py::list relocs, int64_t align) {
+    std::string img = skel;
+    const size_t n = words.size();
+    if (relocs.size() != n) throw std::invalid_argument("one relocation array per program");
+    if (align <= 0 || (align & (align - 1))) throw std::invalid_argument("align must be a power of two");
+    py::array_t<int64_t> offs((py::ssize_t)n);
+    int64_t pos = 0;
+    for (size_t i = 0; i < n; ++i) {
+      auto w = py::array_t<uint32_t, py::array::c_style | py::array::forcecast>(words[i]);
+      auto r = py::array_t<uint32_t, py::array::c_style | py::array::forcecast>(relocs[i]);
+      const int64_t bytes = (int64_t)w.size() * 4;
+      if (pos + bytes > capacity) throw std::length_error("batch exceeds the skeleton arena");
+      if (arena_off + pos + bytes > (int64_t)img.size()) throw std::length_error("arena outside the image");
+      std::vector<uint32_t> code(w.data(), w.data() + w.size());
+      if (r.size() % 3) throw std::invalid_argument("relocations come in triples");
+      for (py::ssize_t k = 0; k + 2 < r.size(); k += 3) {
+        const uint32_t lo = r.data()[k], hi = r.data()[k + 1], pc = r.data()[k + 2];
+        if (lo >= code.size() || hi >= code.size()) throw std::out_of_range("relocation outside the program");
+        const int64_t d = rt_vaddr - (arena_vaddr + pos + (int64_t)pc);
+        code[lo] = (uint32_t)((uint64_t)d & 0xFFFFFFFFull);
+        code[hi] = (uint32_t)(((uint64_t)d >> 32) & 0xFFFFFFFFull);
+      }
+      std::memcpy(&img[(size_t)(arena_off + pos)], code.data(), (size_t)bytes);
+      offs.mutable_data()[i] = pos;
+      pos += (bytes + align - 1) / align * align;
+    }
+    if (rt_off >= 0) {
+      if (rt_off + rt_vals.size() * 8 > (py::ssize_t)img.size()) throw std::length_error("runtime table outside the image");
+      std::memcpy(&img[(size_t)rt_off], rt_vals.data(), (size_t)rt_vals.size() * 8);
+    }
+    return py::make_tuple(py::bytes(img), offs);
+  }, py::arg("skeleton"), py::arg("arena_off"), py::arg("arena_vaddr"), py::arg("capacity"), py::arg("rt_vaddr"),
+     py::arg("rt_off"), py::arg("rt_vals"), py::arg("words"), py::arg("relocs"), py::arg("align") = 256);
   m.def("gcn_listing", [](py::bytes code, std::vector<uint8_t> ctag, std::vector<uint8_t> is_lit,
                           std::vector<int64_t> iconst, std::vector<double> fconst) {
     const std::string c = code;

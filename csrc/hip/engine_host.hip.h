@@ -118,6 +118,8 @@ struct HostBuf {
   size_t cap = 0;
   void reserve(size_t bytes) {
     if (bytes <= cap) return;
+    // geometric growth, as DevBuf: batch sizes vary (native constant blocks)
+    bytes = std::max(bytes, cap + cap / 2);
     if (p) HIP_OK(hipHostFree(p));
     HIP_OK(hipHostMalloc(&p, bytes, hipHostMallocMapped));
     HIP_OK(hipHostGetDevicePointer(&d, p, 0));
@@ -259,6 +261,10 @@ class DeviceEngine {
       row_mode_ = m;
     }
     if (o.contains("native_duo")) native_duo_ = o["native_duo"].cast<bool>();
+    // programs the caller keeps in flight on the device at once (all slots): the
+    // two-wave kernel sizes its LDS heap top so that many stay resident
+    if (o.contains("native_inflight")) native_inflight_ = std::max(0, o["native_inflight"].cast<int>());
+    if (o.contains("native_duo_top")) native_duo_top_ = o["native_duo_top"].cast<int>();   // -1: auto
     if (o.contains("native_rows")) {
       const int r = o["native_rows"].cast<int>();
       if (r < 0 || r > kRowsPerWave) throw std::invalid_argument("native_rows must be in [0, 4]");
@@ -374,17 +380,22 @@ class DeviceEngine {
     ensure_batch(s, P);
     s.fam_spec = -1;
     const size_t fb = (size_t)P * 8, ob = (size_t)P * 4, kb = (size_t)kc.size() * 8;
-    s.h_in.reserve(fb + ob + 64);
-    std::memcpy(s.h_in.as<char>(), fn.data(), fb);       // read by the kernel through the mapping
+    // fn | koff | kc, all read by the kernel straight from pinned host memory
+    // (once per policy: kc is staged into LDS when the policy starts).  No copy
+    // is queued: GPU_MAX_HW_QUEUES is 4, so a copy on this slot's stream could
+    // share a hardware queue with another slot and wait for its whole batch.
+    const size_t kco = (fb + ob + 63) & ~size_t(63);
+    s.h_in.reserve(kco + kb + (size_t)kKcLds * 8 + 64);   // the kernels read kKcLds entries from every block start
+    std::memcpy(s.h_in.as<char>(), fn.data(), fb);
     std::memcpy(s.h_in.as<char>() + fb, koff.data(), ob);
-    s.kc.reserve(kb + (size_t)kKcLds * 8 + 16);   // the kernels copy kKcLds entries from every block start
+    std::memcpy(s.h_in.as<char>() + kco, kc.data(), kb);
+    std::memset(s.h_in.as<char>() + kco + kb, 0, (size_t)kKcLds * 8);
+    const int64_t* kc_dev = reinterpret_cast<const int64_t*>(s.h_in.dev<char>() + kco);
     s.h_wc.reserve(sizeof(DevWorkload));
-    HIP_OK(hipMemcpyAsync(s.kc.p, kc.data(), kb, hipMemcpyHostToDevice, s.stream));
-    HIP_OK(hipStreamSynchronize(s.stream));   // kc is pageable: finish the copy while it is alive
     {
       py::gil_scoped_release rel;
       if (use_rows(P)) {
-        launch_rows_native(s, P, fb, profiled);
+        launch_rows_native(s, P, fb, kc_dev, profiled);
         finish(s);
         return;
       }
@@ -394,7 +405,7 @@ class DeviceEngine {
       const size_t lds = lds_bytes(g, Wl.heap_top, kKcLds / kWave);
       if (lds > kMaxLds) throw std::invalid_argument("replay layout exceeds the 160 KiB LDS");
       uint64_t* gh = g ? gheap_for(s, P) : nullptr;
-      const fksk::NativeArgs a{Wl, upload_workload(s, Wl), s.h_in.dev<const uint64_t>(), s.kc.as<const int64_t>(),
+      const fksk::NativeArgs a{Wl, upload_workload(s, Wl), s.h_in.dev<const uint64_t>(), kc_dev,
                                reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + fb), s.res.as<DevResult>(), gh};
       if (npass_ == 1) HIP_OK(fksk::launch_native_np1(g, P, lds, s.stream, a));
       else if (npass_ == 2) HIP_OK(fksk::launch_native_np2(g, P, lds, s.stream, a));
@@ -551,6 +562,10 @@ class DeviceEngine {
     d["row_flat"] = row_flat_;
     d["native_rows_last"] = last_native_rows_;
     d["native_waves_last"] = last_native_waves_;
+    d["native_duo_top_last"] = last_duo_top_;
+    d["native_duo_per_cu_last"] = last_duo_per_cu_;   // resident programs per CU at that heap top
+    d["native_duo_reg_cap"] = fksk::native_duo_blocks_per_cu(0);   // register-limited programs per CU
+    d["native_inflight"] = native_inflight_;
     return d;
   }
 
@@ -868,15 +883,42 @@ class DeviceEngine {
   // CU) run one program per wave with the whole heap in LDS -- the replay is
   // latency-bound there, and a lone row has no other row's divergence in its
   // event loop; larger batches pack four programs per wave.
-  void launch_rows_native(Slot& s, int P, size_t fn_bytes, bool profiled = false) {
-    const int ra = native_rows_opt_ > 0 ? native_rows_opt_ : (P <= 2 * num_cus_ ? 1 : kRowsPerWave);
+  // Heap top of the two-wave kernel: the largest 2^k - 1 (at most the whole
+  // heap) with which `want` programs stay resident at once -- the whole heap in
+  // LDS (two programs per CU on the OpenB trace) for LLM-sized batches, a
+  // shallower LDS top over the HBM slice when the caller keeps thousands of
+  // programs in flight (up to the register limit: 128 VGPRs, 8 per CU).
+  int duo_top(int want) const {
+    const int entries = row_heap_entries(W_.n_pods);
+    if (native_duo_top_ >= 0) {
+      int T = 1;
+      while (T < entries - 1 && 2 * T + 1 <= native_duo_top_) T = 2 * T + 1;
+      return T;
+    }
+    const int reg_cap = std::max(1, fksk::native_duo_blocks_per_cu(0));
+    const int need = std::min(reg_cap, std::max(1, (want + num_cus_ - 1) / std::max(1, num_cus_)));
+    auto per_cu = [&](int T) {
+      const size_t lds = duo_lds_bytes(W_.n_pods, T);
+      if (lds > kMaxLds) return 0;
+      return std::max(0, fksk::native_duo_blocks_per_cu(lds));
+    };
+    int T = 63;
+    while (T < entries - 1 && per_cu(2 * T + 1) >= std::max(2, need)) T = 2 * T + 1;
+    return T;
+  }
+
+  void launch_rows_native(Slot& s, int P, size_t fn_bytes, const int64_t* kc_dev, bool profiled = false) {
+    // the two-wave kernel for every batch (its heap top follows the programs in
+    // flight); four programs per wave only on request (native_rows = 4)
+    const int ra = native_rows_opt_ > 0 ? native_rows_opt_ : (native_duo_ || P <= 2 * num_cus_ ? 1 : kRowsPerWave);
     DevWorkload Wl = W_;
     const int entries = row_heap_entries(W_.n_pods);
     if (ra == 1 && native_duo_) {
-      // latency regime: two waves per program (heap wave + scoring wave, replay_duo.hip.h)
-      int T = 1;
-      while (T < entries - 1 && duo_lds_bytes(W_.n_pods, 2 * T + 1) <= kMaxLds / 2) T = 2 * T + 1;
+      // two waves per program (heap wave + scoring wave, replay_duo.hip.h)
+      const int T = duo_top(std::max(P, native_inflight_));
       Wl.heap_top = T;
+      last_duo_top_ = T;
+      last_duo_per_cu_ = fksk::native_duo_blocks_per_cu(duo_lds_bytes(W_.n_pods, T));
       const size_t lds = duo_lds_bytes(W_.n_pods, T);
       if (lds > kMaxLds) throw std::invalid_argument("native duo layout exceeds the 160 KiB LDS");
       s.gheap.reserve((size_t)entries * 8 * (size_t)P);
@@ -885,10 +927,11 @@ class DeviceEngine {
                                 s.gheap.as<uint64_t>(), profiled ? s.prof.as<uint64_t>() : nullptr,
                                 s.h_tab.dev<double>()};
       s.fused_table = true;
-      const RowNativeArgs nat{s.h_in.dev<const uint64_t>(), s.kc.as<const int64_t>(),
+      const RowNativeArgs nat{s.h_in.dev<const uint64_t>(), kc_dev,
                               reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + fn_bytes)};
       if (std::getenv("FKS_DEBUG_LAUNCH"))
-        std::fprintf(stderr, "[fks] native duo: P=%d T=%d lds=%zu stream=%p\n", P, T, lds, (void*)s.stream);
+        std::fprintf(stderr, "[fks] native duo: P=%d T=%d lds=%zu per_cu=%d stream=%p\n", P, T, lds,
+                     last_duo_per_cu_, (void*)s.stream);
       HIP_OK(fksk::launch_native_duo(P, lds, s.stream, a, nat));
       last_native_rows_ = 0;   // 0: the two-wave kernel
       last_native_waves_ = 2 * P;
@@ -908,7 +951,7 @@ class DeviceEngine {
     const fksk::BuiltinArgs a{Wl, upload_workload(s, Wl), nullptr, nullptr, nullptr, s.res.as<DevResult>(),
                               s.gheap.as<uint64_t>(), profiled ? s.prof.as<uint64_t>() : nullptr, s.h_tab.dev<double>()};
     s.fused_table = true;
-    const RowNativeArgs nat{s.h_in.dev<const uint64_t>(), s.kc.as<const int64_t>(),
+    const RowNativeArgs nat{s.h_in.dev<const uint64_t>(), kc_dev,
                             reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + fn_bytes)};
     if (std::getenv("FKS_DEBUG_LAUNCH"))
       std::fprintf(stderr, "[fks] native rows: P=%d rows=%d waves=%d T=%d lds=%zu qbase=%u stream=%p\n", P, ra, waves, T,
@@ -975,6 +1018,9 @@ class DeviceEngine {
   double row_share_ = 1.0;
   bool native_duo_ = true;     // two-wave kernel for one-program-per-wave batches
   int native_rows_opt_ = 0;    // rows per wave for native programs (0: auto)
+  int native_inflight_ = 0;    // programs kept in flight across slots (two-wave heap-top sizing)
+  int native_duo_top_ = -1;    // forced two-wave heap top (-1: auto)
+  int last_duo_top_ = 0, last_duo_per_cu_ = 0;
   int last_native_rows_ = 0, last_native_waves_ = 0;
   size_t row_min_lds_ = 0;
   int32_t max_class_pods_ = 0;   // most GPU pods of one gpu_milli class (row kernel: < 2^16)

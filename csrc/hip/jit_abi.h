@@ -55,8 +55,8 @@ __host__ __device__ __forceinline__ ProgFn prog_of(uint64_t e) { return reinterp
 __host__ __device__ __forceinline__ bool prog_feas(uint64_t e) { return (e & kFnFeasBit) != 0; }
 
 // ---- runtime library -------------------------------------------------------------
-// The float // and %, **, math.log / exp / sqrt / pow machinery (double-double
-// exp/log, CPython float_pow) is compiled once, into the extension, and the
+// The float // and %, **, math.log / exp / sqrt / pow machinery (glibc's
+// exp / log / pow, glibc_math.h; CPython float_pow) is compiled once, into the extension, and the
 // generated code reaches it through `fks_rt_table` (filled by the loader with
 // the addresses k_native_rt_table reports).  Keeps every JIT compile small.
 typedef Ret2 (*RtBinFn)(int op, int64_t ab, int32_t afl, int64_t bb, int32_t bfl);

@@ -6,7 +6,7 @@
 //                 libraries, so a batch compiles in tens of milliseconds.
 //                 Math comes from LLVM intrinsics (floor, trunc, sqrt, fma,
 //                 ... are exact or correctly rounded) plus the exact integer
-//                 fmod and the double log seed below.
+//                 fmod below (exp / log / pow: glibc_math.h).
 //   FKS_HOST_JIT  the same generated C++ built for the host with g++
 //                 (CPU-native program path and codegen tests).
 #pragma once
@@ -128,18 +128,6 @@ __host__ __device__ inline double exact_fmod(double x, double y) {
 
 #if defined(FKS_JIT)
 __device__ inline double fmod(double x, double y) { return exact_fmod(x, y); }
-// log seed for dd_log (which refines it with one double-double Newton step, so
-// ~1e-16 relative accuracy here is plenty): x = 2^e m, m in [sqrt(1/2), sqrt(2)),
-// log m = 2 atanh((m - 1) / (m + 1)) by its series.
-__device__ inline double log(double x) {
-  int e;
-  double m = __builtin_frexp(x, &e);   // m in [0.5, 1)
-  if (m < 0.7071067811865476) { m *= 2.0; e -= 1; }
-  const double f = (m - 1.0) / (m + 1.0), f2 = f * f;
-  double s = 0.0;
-  for (int k = 23; k >= 1; k -= 2) s = s * f2 + 1.0 / (double)k;
-  return (double)e * 0.6931471805599453 + 2.0 * f * s;
-}
 #endif
 
 }  // namespace fksd

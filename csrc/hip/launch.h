@@ -99,9 +99,12 @@ hipError_t launch_native_duo(int P, size_t lds, hipStream_t stream, const Builti
                              const fksd::RowNativeArgs& nat);
 hipError_t set_native_duo_attrs(int max_lds);
 int native_rows_waves_per_cu(size_t lds);
+int native_duo_blocks_per_cu(size_t lds);   // resident two-wave workgroups per CU
 
 // addresses of the native programs' runtime library (fks_rt_binop, fks_rt_unop, register floor)
 hipError_t native_rt_table(uint64_t* dev_out, hipStream_t s);
+// glibc_math.h on the device (tests): fn 0 exp, 1 log, 2 pow; n arguments, one per lane
+hipError_t launch_gm_batch(int fn, const double* x, const double* y, double* out, int32_t* st, int64_t n);
 
 // phase-profiled variants (NPASS = 1)
 hipError_t launch_builtin_prof(bool gheap, int P, size_t lds, hipStream_t s, const BuiltinArgs& a);

@@ -17,6 +17,8 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <random>
+#include <cmath>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -220,21 +222,38 @@ JitLoader& jit_loader(int device) {
 }
 
 // A loaded JIT code object of natively compiled programs (ops/jit.py).
-// Load: hipModuleLoadData; the module's `fks_rt_table` global receives the
-// runtime-library addresses; `fks_jit_table` reports the program addresses
-// (both on the loader's private stream).
+// Load: hipModuleLoadData.  With `probe` (LLVM-tier modules, and the first
+// baseline module of each skeleton size) the module's `fks_rt_table` global
+// receives the runtime-library addresses and the `fks_jit_table` kernel
+// reports the program addresses, both on the loader's private stream.
+// Without it (baseline modules: the runtime table is already written into
+// the image, ops/gcnjit.py) nothing touches the device after the load: the
+// only result is the device address of `fks_rt_table` (a host-side symbol
+// lookup), from which the caller derives the program addresses with the
+// image's fixed layout.  That matters at steady state: GPU_MAX_HW_QUEUES is 4,
+// so the loader stream shares a hardware queue with a replay slot, and a
+// probe kernel or copy queued there waits for that slot's whole batch.
 class JitModule {
  public:
   JitModule(py::bytes image, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> rt, int n_programs,
-            int device)
+            int device, bool probe)
       : device_(device), n_(n_programs) {
     if (n_programs < 1) throw std::invalid_argument("empty JIT module");
     const std::string img = image;
     std::vector<uint64_t> rtv(rt.data(), rt.data() + rt.size());
     py::gil_scoped_release rel;    // other islands / the tier-up thread keep running
-    JitLoader& L = jit_loader(device_);
     HIP_OK(hipSetDevice(device_));
     HIP_OK(hipModuleLoadData(&mod_, img.data()));
+    if (!probe) {
+      hipDeviceptr_t gp = nullptr;
+      size_t gbytes = 0;
+      HIP_OK(hipModuleGetGlobal(&gp, &gbytes, mod_, "fks_rt_table"));
+      if (gbytes < rtv.size() * 8) throw std::runtime_error("fks_rt_table too small");
+      n_ = 1;
+      ptrs_.assign(1, reinterpret_cast<uint64_t>(gp));
+      return;
+    }
+    JitLoader& L = jit_loader(device_);
     std::lock_guard<std::mutex> g(L.mu);   // the loader's stream and pointer buffers
     hipDeviceptr_t gp = nullptr;
     size_t gbytes = 0;
@@ -260,6 +279,41 @@ class JitModule {
       (void)hipModuleUnload(mod_);
     }
   }
+  // Retirement (ops/jit.py): the caller guarantees that every batch that
+  // called into this module has completed (per-batch module references), so
+  // no device-wide synchronisation is needed.
+  void unload() {
+    if (!mod_) return;
+    hipModule_t m = mod_;
+    mod_ = nullptr;
+    py::gil_scoped_release rel;
+    HIP_OK(hipSetDevice(device_));
+    HIP_OK(hipModuleUnload(m));
+  }
+  bool loaded() const { return mod_ != nullptr; }
+  uint64_t global_address(const std::string& name) {
+    if (!mod_) throw std::runtime_error("module unloaded");
+    hipDeviceptr_t gp = nullptr;
+    size_t gbytes = 0;
+    HIP_OK(hipModuleGetGlobal(&gp, &gbytes, mod_, name.c_str()));
+    return reinterpret_cast<uint64_t>(gp);
+  }
+  // bytes of a module global read back from the device (layout checks: the
+  // runtime table written into the image must be what the device sees)
+  py::bytes read_global(const std::string& name, size_t nbytes) {
+    if (!mod_) throw std::runtime_error("module unloaded");
+    hipDeviceptr_t gp = nullptr;
+    size_t gbytes = 0;
+    HIP_OK(hipModuleGetGlobal(&gp, &gbytes, mod_, name.c_str()));
+    if (nbytes > gbytes) throw std::invalid_argument("read past the global");
+    std::string out(nbytes, '\0');
+    {
+      py::gil_scoped_release rel;
+      HIP_OK(hipSetDevice(device_));
+      HIP_OK(hipMemcpyDtoH(&out[0], gp, nbytes));
+    }
+    return py::bytes(out);
+  }
   py::array_t<uint64_t> pointers() const {
     py::array_t<uint64_t> out(n_);
     std::memcpy(out.mutable_data(), ptrs_.data(), (size_t)n_ * 8);
@@ -271,6 +325,109 @@ class JitModule {
   hipModule_t mod_ = nullptr;
   std::vector<uint64_t> ptrs_;
 };
+
+// ---- glibc-exact math (glibc_math.h): self-check and device evaluation ----------------
+// The host build of the port against the host libm (what CPython calls), on
+// `n` arguments per function drawn to cover every branch of exp / log / pow
+// (tiny, near 1, large, subnormal results, over- / underflow).  Returns the
+// mismatch count per function and the first few mismatching arguments.
+py::dict glibc_math_selfcheck(int64_t n, uint64_t seed) {
+  std::mt19937_64 rng(seed);
+  std::uniform_real_distribution<double> U(0.0, 1.0);
+  auto bits = [&](uint64_t lo_exp, uint64_t hi_exp) {
+    const uint64_t e = lo_exp + rng() % (hi_exp - lo_exp + 1);
+    return fksd::gm::asd((e << 52) | (rng() & ((1ull << 52) - 1)));
+  };
+  auto same = [](double a, double b) { return fksd::gm::asu(a) == fksd::gm::asu(b); };
+  int64_t bad_exp = 0, bad_log = 0, bad_pow = 0;
+  std::vector<std::pair<double, double>> e1, e2, e3;
+  {
+    py::gil_scoped_release rel;
+    for (int64_t i = 0; i < n; ++i) {
+      const int c = (int)(rng() % 10);
+      double x;
+      if (c < 4) x = -745.2 + U(rng) * (709.8 + 745.2);
+      else if (c < 6) x = 2.0 * U(rng) - 1.0;
+      else if (c < 7) x = (rng() & 1 ? -1.0 : 1.0) * bits(0x3c0, 0x3fe);
+      else if (c < 9) x = (rng() & 1 ? -1.0 : 1.0) * bits(0x3c4, 0x40a);
+      else x = (rng() & 1) ? 700.0 + 10.0 * U(rng) : -760.0 + 60.0 * U(rng);
+      double o = 0.0;
+      const int st = fksd::gm::exp(x, o);
+      const double g = ::exp(x);
+      if (!same(o, g) || (st == 1) != std::isinf(g)) { if (bad_exp++ < 8) e1.push_back({x, 0.0}); }
+    }
+    for (int64_t i = 0; i < n; ++i) {
+      const int c = (int)(rng() % 10);
+      double x;
+      if (c < 3) x = bits(0, 0x7fe);
+      else if (c < 6) x = 1.0 + (U(rng) - 0.5) * 0.15;
+      else if (c < 8) x = 100.0 * U(rng);
+      else x = bits(1023 - 20, 1023 + 20);
+      if (!(x > 0.0)) x = 0.5;
+      double o = 0.0;
+      fksd::gm::log(x, o);
+      if (!same(o, ::log(x))) { if (bad_log++ < 8) e2.push_back({x, 0.0}); }
+    }
+    for (int64_t i = 0; i < n; ++i) {
+      const int cx = (int)(rng() % 10), cy = (int)(rng() % 10);
+      double x;
+      if (cx < 4) x = 1.0 + (U(rng) - 0.5);
+      else if (cx < 7) x = bits(0, 0x7fe);
+      else x = 1e4 * U(rng);
+      if (!(x > 0.0) || x == 1.0) x = 0.75;
+      double y;
+      if (cy < 3) y = 40.0 * U(rng) - 20.0;
+      else if (cy < 5) y = (double)((int64_t)(rng() % 81) - 40) * 0.5;
+      else if (cy < 7) y = 2000.0 * U(rng) - 1000.0;
+      else if (cy < 8) y = (rng() & 1 ? -1.0 : 1.0) * ((rng() & 1) ? bits(0x3b8, 0x3c4) : bits(0x43a, 0x444));
+      else {
+        const double lx = ::log(x);
+        y = lx != 0.0 ? (-760.0 + U(rng) * 1475.0) / lx : 3.0;
+      }
+      if (y == 0.0 || !std::isfinite(y)) y = 2.5;
+      double o = 0.0;
+      const int st = fksd::gm::pow(x, y, o);
+      const double g = ::pow(x, y);
+      if (!same(o, g) || (st == 1) != std::isinf(g)) { if (bad_pow++ < 8) e3.push_back({x, y}); }
+    }
+  }
+  py::list ex_exp, ex_log, ex_pow;
+  for (auto& v : e1) ex_exp.append(v.first);
+  for (auto& v : e2) ex_log.append(v.first);
+  for (auto& v : e3) ex_pow.append(py::make_tuple(v.first, v.second));
+  py::dict d;
+  d["n"] = n;
+  d["exp"] = bad_exp; d["log"] = bad_log; d["pow"] = bad_pow;
+  d["exp_examples"] = ex_exp; d["log_examples"] = ex_log; d["pow_examples"] = ex_pow;
+  return d;
+}
+
+// The device build on the MI355X: fn 0 exp(x), 1 log(x), 2 pow(x, y).  Returns
+// (status, result) per argument (tests/test_gpu_glibc_math.py: == host build).
+py::tuple gm_device_batch(int fn, py::array_t<double, py::array::c_style | py::array::forcecast> x,
+                          py::array_t<double, py::array::c_style | py::array::forcecast> y, int device) {
+  const int64_t n = (int64_t)x.size();
+  if (fn < 0 || fn > 2) throw std::invalid_argument("fn: 0 exp, 1 log, 2 pow");
+  if ((int64_t)y.size() != n) throw std::invalid_argument("x and y differ in length");
+  py::array_t<double> out(n);
+  py::array_t<int32_t> st(n);
+  if (n == 0) return py::make_tuple(st, out);
+  HIP_OK(hipSetDevice(device));
+  double *dx = nullptr, *dy = nullptr, *dout = nullptr;
+  int32_t* dst = nullptr;
+  HIP_OK(hipMalloc(&dx, n * 8));
+  HIP_OK(hipMalloc(&dy, n * 8));
+  HIP_OK(hipMalloc(&dout, n * 8));
+  HIP_OK(hipMalloc(&dst, n * 4));
+  HIP_OK(hipMemcpy(dx, x.data(), n * 8, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(dy, y.data(), n * 8, hipMemcpyHostToDevice));
+  HIP_OK(fksk::launch_gm_batch(fn, dx, dy, dout, dst, n));
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(out.mutable_data(), dout, n * 8, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(st.mutable_data(), dst, n * 4, hipMemcpyDeviceToHost));
+  for (void* p : {(void*)dx, (void*)dy, (void*)dout, (void*)dst}) (void)hipFree(p);
+  return py::make_tuple(st, out);
+}
 
 int device_count() {
   int n = 0;
@@ -315,26 +472,42 @@ PYBIND11_MODULE(_fks_hip, m) {
       .def("profile_native", &DeviceEngine::profile_native)
       .def("native_rt_table", &DeviceEngine::native_rt_table);
   py::class_<JitModule>(m, "JitModule")
-      .def(py::init<py::bytes, py::array_t<uint64_t, py::array::c_style | py::array::forcecast>, int, int>(),
-           py::arg("image"), py::arg("rt"), py::arg("n_programs"), py::arg("device") = 0)
-      .def("pointers", &JitModule::pointers);
+      .def(py::init<py::bytes, py::array_t<uint64_t, py::array::c_style | py::array::forcecast>, int, int, bool>(),
+           py::arg("image"), py::arg("rt"), py::arg("n_programs"), py::arg("device") = 0, py::arg("probe") = true)
+      .def("pointers", &JitModule::pointers)
+      .def("unload", &JitModule::unload)
+      .def("loaded", &JitModule::loaded)
+      .def("read_global", &JitModule::read_global)
+      .def("global_address", &JitModule::global_address);
   m.attr("JIT_VGPRS") = kJitVgprs;
   m.attr("JIT_SGPRS") = kJitSgprs;
   m.attr("WEIGHTS_PER_POLICY") = kWeights;
-  // host builds of the device math, for differential tests against glibc
-  m.def("dd_pow", [](double x, double y) { double o = 0; int s = fksd::dd_pow(x, y, o); return py::make_tuple(s, o); });
-  m.def("dd_exp", [](double x) { double o = 0; int s = fksd::dd_exp_d(x, o); return py::make_tuple(s, o); });
-  m.def("dd_log", [](double x) { double o = 0; int s = fksd::dd_log_d(x, o); return py::make_tuple(s, o); });
-  m.def("dd_pow_batch", [](py::array_t<double, py::array::c_style | py::array::forcecast> x,
-                           py::array_t<double, py::array::c_style | py::array::forcecast> y) {
+  // host builds of the device math (glibc_math.h), for differential tests against the libm CPython calls
+  m.def("gm_exp_batch", [](py::array_t<double, py::array::c_style | py::array::forcecast> x) {
     const py::ssize_t n = x.size();
     py::array_t<double> out(n);
     py::array_t<int32_t> st(n);
-    for (py::ssize_t i = 0; i < n; ++i) {
-      double o = 0;
-      st.mutable_data()[i] = fksd::dd_pow(x.data()[i], y.data()[i], o);
-      out.mutable_data()[i] = o;
-    }
+    for (py::ssize_t i = 0; i < n; ++i) st.mutable_data()[i] = fksd::gm::exp(x.data()[i], out.mutable_data()[i]);
     return py::make_tuple(st, out);
   });
+  m.def("gm_log_batch", [](py::array_t<double, py::array::c_style | py::array::forcecast> x) {
+    const py::ssize_t n = x.size();
+    py::array_t<double> out(n);
+    py::array_t<int32_t> st(n);
+    for (py::ssize_t i = 0; i < n; ++i) st.mutable_data()[i] = fksd::gm::log(x.data()[i], out.mutable_data()[i]);
+    return py::make_tuple(st, out);
+  });
+  m.def("gm_pow_batch", [](py::array_t<double, py::array::c_style | py::array::forcecast> x,
+                           py::array_t<double, py::array::c_style | py::array::forcecast> y) {
+    const py::ssize_t n = x.size();
+    if (y.size() != n) throw std::invalid_argument("x and y differ in length");
+    py::array_t<double> out(n);
+    py::array_t<int32_t> st(n);
+    for (py::ssize_t i = 0; i < n; ++i)
+      st.mutable_data()[i] = fksd::gm::pow(x.data()[i], y.data()[i], out.mutable_data()[i]);
+    return py::make_tuple(st, out);
+  });
+  m.def("glibc_math_selfcheck", &glibc_math_selfcheck, py::arg("n"), py::arg("seed") = 1);
+  m.def("gm_device_batch", &gm_device_batch, py::arg("fn"), py::arg("x"), py::arg("y"), py::arg("device") = 0);
+
 }

@@ -12,7 +12,7 @@
 
 #include "jit_env.h"
 #include "exc_codes.h"
-#include "dd_math.h"
+#include "glibc_math.h"
 
 namespace fksd {
 
@@ -110,8 +110,7 @@ __device__ __forceinline__ int d_float_pow_impl(double iv, double iw, PyN& r) {
   }
   if (iv == 1.0) { r = pf(neg ? -1.0 : 1.0); return EXC_NONE; }
   double ix;
-  const int st = dd_pow(iv, iw, ix);
-  if (st == 2) return EXC_UNSUPPORTED;
+  const int st = gm::pow(iv, iw, ix);   // glibc's pow, bit for bit (glibc_math.h)
   if (st == 1) return EXC_OVERFLOW;
   r = pf(neg ? -ix : ix);
   return EXC_NONE;
@@ -210,19 +209,19 @@ __device__ __forceinline__ int d_binop_impl(int op, const PyN& a, const PyN& b, 
       return d_float_pow(fv(a), fv(b), r);
     }
     case OP_LOGB: {
-      double num, den;
+      double num = 0.0, den = 1.0;
       for (int k = 0; k < 2; ++k) {
         const PyN& x = k == 0 ? a : b;
         double out;
         if (!x.fl) {
           if (x.b <= 0) return EXC_VALUE;
-          if (dd_log_d((double)x.b, out) == 2) return EXC_UNSUPPORTED;
+          gm::log((double)x.b, out);
         } else {
           const double v = __longlong_as_double(x.b);
           if (isnan(v)) out = v;
           else if (isinf(v)) { if (v > 0) out = v; else return EXC_VALUE; }
           else if (v <= 0.0) return EXC_VALUE;
-          else if (dd_log_d(v, out) == 2) return EXC_UNSUPPORTED;
+          else gm::log(v, out);
         }
         (k == 0 ? num : den) = out;
       }
@@ -304,13 +303,13 @@ __device__ __forceinline__ int d_unop_impl(int op, const PyN& a, PyN& r) {
       double out;
       if (!a.fl) {
         if (a.b <= 0) return EXC_VALUE;
-        if (dd_log_d((double)a.b, out) == 2) return EXC_UNSUPPORTED;
+        gm::log((double)a.b, out);
       } else {
         const double v = __longlong_as_double(a.b);
         if (isnan(v)) out = v;
         else if (isinf(v)) { if (v > 0) out = v; else return EXC_VALUE; }
         else if (v <= 0.0) return EXC_VALUE;
-        else if (dd_log_d(v, out) == 2) return EXC_UNSUPPORTED;
+        else gm::log(v, out);
       }
       r = pf(out); return EXC_NONE;
     }
@@ -319,9 +318,7 @@ __device__ __forceinline__ int d_unop_impl(int op, const PyN& a, PyN& r) {
       if (isnan(x)) { r = pf(x); return EXC_NONE; }
       if (isinf(x)) { r = pf(x > 0 ? x : 0.0); return EXC_NONE; }
       double out;
-      const int st = dd_exp_d(x, out);
-      if (st == 1) return EXC_OVERFLOW;
-      if (st == 2) return EXC_UNSUPPORTED;
+      if (gm::exp(x, out) == 1) return EXC_OVERFLOW;
       r = pf(out); return EXC_NONE;
     }
     case OP_SIN: case OP_COS: case OP_TAN:

@@ -325,6 +325,20 @@ __global__ __launch_bounds__(128, 1) void k_replay_native_duo(fksk::BuiltinArgs 
 __global__ __launch_bounds__(128, 1) void k_replay_native_duo_prof(fksk::BuiltinArgs a, RowNativeArgs nat) {
   replay_duo<true>(a.W, kernarg_workload(), a.gheap, a.out, nat, a.table, a.prof);
 }
+// glibc-exact exp / log / pow (glibc_math.h) on device, one argument per lane:
+// the device side of tests/test_gpu_glibc_math.py
+__global__ __launch_bounds__(256) void k_gm_batch(int fn, const double* x, const double* y, double* out, int32_t* st,
+                                                  int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double o = 0.0;
+  int s = 0;
+  if (fn == 0) s = gm::exp(x[i], o);
+  else if (fn == 1) s = gm::log(x[i], o);
+  else s = gm::pow(x[i], y[i], o);
+  out[i] = o;
+  st[i] = s;
+}
 #endif
 
 template <int NPASS, bool GHEAP>
@@ -492,12 +506,21 @@ hipError_t set_native_duo_attrs(int mx) {
   const hipError_t e = raise_lds(&k_replay_native_duo, mx);
   return e != hipSuccess ? e : raise_lds(&k_replay_native_duo_prof, mx);
 }
+int native_duo_blocks_per_cu(size_t lds) {
+  int n = 0;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_replay_native_duo, 128, lds) == hipSuccess ? n : -1;
+}
 int native_rows_waves_per_cu(size_t lds) {
   int n = 0;
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_replay_rows_native, 64, lds) == hipSuccess ? n : -1;
 }
 hipError_t native_rt_table(uint64_t* dev_out, hipStream_t s) {
   hipLaunchKernelGGL(k_native_rt_table, dim3(1), dim3(64), 0, s, dev_out);
+  return hipGetLastError();
+}
+hipError_t launch_gm_batch(int fn, const double* x, const double* y, double* out, int32_t* st, int64_t n) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gm_batch, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, fn, x, y, out, st, n);
   return hipGetLastError();
 }
 #endif

@@ -8,8 +8,8 @@
 // counters, exactly as the CPU VM does.  The virtual register file lives in
 // LDS behind the policy's event heap, lane-major ([reg][64 lanes] of 8 B: a
 // ds_read_b64 per operand, conflict-free), the int/float tags in one 64-bit
-// VGPR mask per lane.  exp/log/pow are the correctly rounded double-double
-// versions of dd_math.h; trigonometry defers to the host.
+// VGPR mask per lane.  exp/log/pow are glibc's own algorithms
+// (glibc_math.h, CPython's bits); trigonometry defers to the host.
 #pragma once
 
 #include "pyops_dev.h"

@@ -132,3 +132,83 @@ def measure_novel(dev, workload, n: int = 256, compile_batches: int = 4, seed: i
             "compile_s_per_64_median": round(float(np.median(t64)), 4) if t64 else None,
             "baseline_shapes": int(st.get("baseline_shapes", 0)), "llvm_shapes": int(st.get("llvm_shapes", 0)),
             "compared": int(cmp.sum()), "bit_identical": bool((tab[cmp] == vm[cmp]).all())}
+
+
+def _novel_worker(args):
+    n, seed = args
+    return novel_children(n, seed)
+
+
+def novel_children_parallel(n: int, seed: int = 0, workers: int = 8, exclude=()) -> List[CompiledPolicy]:
+    """`novel_children` generated in `workers` spawned processes (the offline
+    mutator + bytecode compiler run ~9 ms a program on one core); shapes are
+    deduplicated across workers, and the shortfall is made up serially."""
+    import concurrent.futures
+    import multiprocessing
+    from ..policy.native_codegen import shape_key
+    workers = max(1, min(workers, n // 64 or 1))
+    per = -(-n // workers) + 16
+    keys, out = set(exclude), []
+    if workers > 1:
+        with concurrent.futures.ProcessPoolExecutor(workers, mp_context=multiprocessing.get_context("spawn")) as ex:
+            parts = list(ex.map(_novel_worker, [(per, seed + 104729 * (w + 1)) for w in range(workers)]))
+    else:
+        parts = [novel_children(per, seed)]
+    for part in parts:
+        for p in part:
+            k = shape_key(p)
+            if k not in keys and len(out) < n:
+                keys.add(k)
+                out.append(p)
+    if len(out) < n:
+        out += novel_children(n - len(out), seed + 7, exclude=keys)
+    return out
+
+
+def measure_novel_large(dev, workload, n: int = 2048, seed: int = 0, compare: int = 128, cpu_threads: int = 0,
+                        workers: int = 8) -> dict:
+    """LLM-scale batch of `n` programs, every one a new shape, JIT included:
+    split over the device's slots, each chunk compiled (C++ generator, host
+    threads), loaded and launched while the previous chunks replay, with the
+    two-wave kernel's heap top sized for all `n` in flight.  The first
+    `compare` programs are checked against the CPU VM, row for row."""
+    import numpy as np
+    from ..engine import COLS
+    from ..ops import cpu_engine as ce
+    progs = novel_children_parallel(n, seed, workers, exclude=set(dev.native_compiler._shapes))
+    slots = max(1, dev.n_slots)
+    size = -(-n // slots)
+    chunks = [progs[i:i + size] for i in range(0, n, size)]
+    dev.set_options(native_inflight=n)
+    try:
+        t0 = time.perf_counter()
+        batches = [dev.submit_native(s, c) for s, c in enumerate(chunks)]
+        t_sub = time.perf_counter()
+        tabs = [dev.wait(s) for s in range(len(chunks))]
+        t1 = time.perf_counter()
+        info = dev.info()
+        # the same programs again: every shape cached (device time only)
+        for s, c in enumerate(chunks):
+            dev.submit_native(s, c)
+        tabs2 = [dev.wait(s) for s in range(len(chunks))]
+        t2 = time.perf_counter()
+    finally:
+        dev.set_options(native_inflight=0)
+    tab, tab2 = np.concatenate(tabs), np.concatenate(tabs2)
+    threads = cpu_threads or ce.default_threads()
+    sub = progs[:compare]
+    vm = ce.simulate_program_batch(workload, sub, threads=threads)
+    a, b = tab[:compare], vm
+    skip = (100, 101, 102, 103)
+    cmp = ~np.isin(a[:, COLS["exc"]].astype(int), skip) & ~np.isin(b[:, COLS["exc"]].astype(int), skip)
+    if not dev.options.get("trace_hash", True):
+        a, b = a[:, :COLS["trace_hash_hi"]], b[:, :COLS["trace_hash_hi"]]
+    return {"programs": n, "chunks": len(chunks), "new_shapes": int(sum(x.compiled for x in batches)),
+            "native": int(sum(x.ok.sum() for x in batches)),
+            "jit_s": round(sum(x.compile_s for x in batches), 4), "load_s": round(sum(x.load_s for x in batches), 4),
+            "submit_s": round(t_sub - t0, 4), "wall_s": round(t1 - t0, 4),
+            "evals_per_s_incl_jit": round(n / (t1 - t0), 1), "evals_per_s_cached": round(n / (t2 - t1), 1),
+            "duo_heap_top": info.get("native_duo_top_last"), "duo_programs_per_cu": info.get("native_duo_per_cu_last"),
+            "resident_capacity": int(info.get("native_duo_per_cu_last", 0)) * int(info.get("num_cus", 0)),
+            "repeat_identical": bool((tab == tab2).all()),
+            "compared": int(cmp.sum()), "bit_identical": bool((a[cmp] == b[cmp]).all())}

@@ -1,10 +1,9 @@
 """`evaluate()`: score policy programs on the fastest exact engine available.
 
-Routing per program (every path yields the reference's score bit-for-bit, with
-one documented exception: a device pow/exp/log result is correctly rounded, and
-where glibc -- what CPython calls -- rounds the other way (~0.08% of such calls,
-outside the narrow near-midpoint defer band) a program using them can score
-differently; docs/ARCHITECTURE.md "Exactness", parity unpinned there):
+Routing per program (every path yields the reference's score bit-for-bit; the
+device's `**`, math.exp / log / pow are glibc's own algorithms, so they return
+CPython's bits -- csrc/hip/glibc_math.h, checked at start-up by
+`hip_engine.glibc_math_ok`):
 
 1. compile to bytecode (`policy.compiler`); programs outside the native
    subset go straight to the object engine (CPython ``exec``, step 4);
@@ -14,7 +13,7 @@ differently; docs/ARCHITECTURE.md "Exactness", parity unpinned there):
    what the native backend declines, when the batch is large enough to fill
    the chip;
 3. native CPU VM (`ops.cpu_engine`): for no-GPU hosts, for programs the device
-   reports as EXC_UNSUPPORTED (bigint / complex / trig / near-tie math) or
+   reports as EXC_UNSUPPORTED (bigint / complex / trig) or
    EXC_BUDGET (per-call instruction budget), and for results whose exact-mean
    accumulator flagged `inexact`;
 4. object engine (`simulator.KubernetesSimulator` + ``exec``), which *is* the
@@ -285,7 +284,8 @@ class Evaluator:
         # 1) device: native code, then the bytecode VM
         pending = [i for i, p in enumerate(compiled) if p is not None]
         if self.device is not None:
-            dev_idx = [i for i in pending if compiled[i].device_ok]
+            dev_idx = [i for i in pending if compiled[i].device_ok
+                       and (self.device.math_exact or not compiled[i].uses_libm)]
             if dev_idx and native:
                 self._absorb_native(dev_idx, compiled, out, slot)
             dev_idx = [i for i in dev_idx if out[i] is None]

@@ -107,6 +107,8 @@ class SteadyStats:
     rejected: int = 0
     migrations: int = 0
     producer_cpu_s: float = 0.0
+    inflight_sum: float = 0.0        # programs in flight x seconds
+    inflight_n: float = 0.0          # seconds observed
     history: List[dict] = field(default_factory=list)
 
 
@@ -126,6 +128,10 @@ class SteadyStateSearch:
             dev.native_compiler.tierup_after = 0
         n_slots = dev.n_slots if dev is not None else 1
         self.slots = max(1, min(int(slots or n_slots), n_slots))
+        if dev is not None:
+            # the two-wave kernel sizes its LDS heap top so that every slot's batch
+            # stays resident at once (csrc/hip/engine_host.hip.h duo_top)
+            dev.set_options(native_inflight=self.batch * self.slots)
         from ..ops.cpu_engine import default_threads
         local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
         self.producers = int(producers or max(1, min(16, default_threads() // local - 1)))
@@ -207,6 +213,7 @@ class SteadyStateSearch:
         t_start = time.time()
         self._cpu0 = time.process_time()
         t_status = t_start
+        t_prev = t_start
         busy_since = None
         want_buffer = self.batch * (self.slots + 1)
         try:
@@ -317,8 +324,11 @@ class SteadyStateSearch:
                 want_stop = want_stop or global_best >= threshold or bool(wall_s and time.time() - t_start > wall_s)
                 if want_stop and not chan.active:
                     stop = True        # alone (or no migrations): nobody to agree with
-                # 6) status
+                # 6) status (time-weighted programs in flight, for the occupancy figure)
                 now = time.time()
+                self.stats.inflight_sum += sum(len(b.items) for b in batches if b is not None) * (now - t_prev)
+                self.stats.inflight_n += now - t_prev
+                t_prev = now
                 if now - t_status >= self.status_every_s:
                     t_status = now
                     self._status(now, t_start, busy_since, batches, ready, inflight_tasks, merged, global_best)
@@ -352,12 +362,24 @@ class SteadyStateSearch:
         wall = max(1e-9, now - t_start)
         busy = st.busy_s + (now - busy_since if busy_since is not None else 0.0)
         fs = self.fs
+        inflight = sum(len(b.items) for b in batches if b is not None)
+        # occupancy: programs in flight / programs the device holds resident at the
+        # current heap top (device_busy only says that *some* batch was in flight)
+        capacity = 0
+        dev = getattr(fs.evaluator, "device", None)
+        if dev is not None:
+            info = dev.info()
+            capacity = int(info.get("native_duo_per_cu_last", 0)) * int(info.get("num_cus", 0))
         rec = dict(kind="steady_final" if final else "steady_status", rank=fs.ctx.rank, wall_s=round(wall, 3),
                    evaluations=st.evaluations, evals_per_s=round(st.evaluations / wall, 2),
                    device_busy=round(busy / wall, 4),
                    new_shape_fraction=round(st.new_shapes / max(1, st.evaluations), 4),
                    native_fraction=round(st.native / max(1, st.evaluations), 4),
-                   inflight=sum(len(b.items) for b in batches if b is not None), queued=len(ready),
+                   inflight=inflight, inflight_mean=round(st.inflight_sum / max(1e-9, st.inflight_n), 1),
+                   resident_capacity=capacity,
+                   occupancy=round(inflight / capacity, 4) if capacity else None,
+                   occupancy_mean=round(st.inflight_sum / max(1e-9, st.inflight_n) / capacity, 4) if capacity else None,
+                   queued=len(ready),
                    producer_tasks=len(tasks), produced=st.produced,
                    producer_ms_per_child=round(1e3 * st.producer_cpu_s / max(1, st.produced), 3),
                    main_cpu_frac=round((time.process_time() - self._cpu0) / wall, 3), rejected=st.rejected, jit_s=round(st.jit_s, 3),

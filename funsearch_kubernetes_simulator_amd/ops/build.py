@@ -92,7 +92,7 @@ CPU_FLAGS = ["-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-f
 
 def _cpu_sources() -> List[Path]:
     return _deps("cpu/*.cpp", "cpu/*.hpp", "include/fks/*.hpp", "jit/*", "hip/jit_abi.h", "hip/pyops_dev.h",
-                 "hip/dd_math.h", "hip/jit_env.h", "hip/exc_codes.h")
+                 "hip/glibc_math.h", "hip/glibc_math_tables.inc", "hip/jit_env.h", "hip/exc_codes.h")
 
 
 def cpu_hash() -> str:
@@ -130,7 +130,7 @@ def _hip_flags() -> List[str]:
 
 
 def _hip_sources() -> List[Path]:
-    return _deps("hip/*.hip", "hip/*.h", "hip/*.cpp", "include/fks/*.hpp")
+    return _deps("hip/*.hip", "hip/*.h", "hip/*.inc", "hip/*.cpp", "include/fks/*.hpp")
 
 
 def hip_hash() -> str:

@@ -52,6 +52,38 @@ def native():
     return _mod
 
 
+_MATH_OK: Optional[bool] = None
+
+
+def glibc_math_ok(n: int = 200_000) -> bool:
+    """The device's exp / log / pow (csrc/hip/glibc_math.h, glibc's own FMA
+    algorithms and tables) equal this host's libm -- the one CPython calls --
+    on `n` arguments per function, and on a sample checked through Python's
+    `math` itself.  Checked once per process.  False (another libm build, a
+    host without FMA): programs that call them are kept off the device and
+    replayed by the CPU VM, which calls the host libm (`DeviceEvaluator`)."""
+    global _MATH_OK
+    if _MATH_OK is None:
+        import math
+        import random
+        m = native()
+        r = m.glibc_math_selfcheck(n, 7)
+        ok = r["exp"] == 0 and r["log"] == 0 and r["pow"] == 0
+        rng = random.Random(3)
+        xs = np.array([rng.uniform(-700, 700) for _ in range(2000)])
+        ys = np.array([rng.uniform(1e-3, 1e3) for _ in range(2000)])
+        zs = np.array([rng.uniform(-20, 20) for _ in range(2000)])
+        ok = ok and np.array_equal(m.gm_exp_batch(xs)[1], [math.exp(x) for x in xs]) \
+            and np.array_equal(m.gm_log_batch(ys)[1], [math.log(y) for y in ys]) \
+            and all(o == y ** z for o, y, z in zip(m.gm_pow_batch(ys, zs)[1], ys, zs) if y ** z != float("inf"))
+        if not ok:
+            import warnings
+            warnings.warn(f"device exp/log/pow differ from this host's libm ({r}); programs using them run on "
+                          "the CPU VM", RuntimeWarning)
+        _MATH_OK = bool(ok)
+    return _MATH_OK
+
+
 def device_available() -> bool:
     try:
         return native().device_count() > 0
@@ -218,6 +250,9 @@ class DeviceEvaluator:
         self._jit = None
         self._jit_lock = threading.Lock()
         self._native_post: Dict[int, Tuple[int, np.ndarray]] = {}   # slot -> (P, native row indices)
+        #: device exp / log / pow == host libm (else programs using them stay on the host)
+        self.math_exact = glibc_math_ok()
+        self._native_mods: Dict[int, tuple] = {}   # slot -> JIT modules its batch in flight calls into
 
     def info(self) -> dict:
         return dict(self._eng.info())
@@ -243,7 +278,15 @@ class DeviceEvaluator:
         get an EXC_UNSUPPORTED row from `wait`, so callers fall back per program.
         Returns the `NativeBatch` (compile time, cache hits, reasons)."""
         batch = self.native_compiler.prepare(progs)
+        if not self.math_exact:
+            for i, p in enumerate(progs):
+                if batch.ok[i] and p.uses_libm:
+                    batch.ok[i] = False
+                    batch.reasons[i] = "exp / log / pow: device math differs from this host's libm"
         idx = np.flatnonzero(batch.ok)
+        prev = self._native_mods.pop(slot, None)
+        if prev:    # a batch never waited for (the engine waits for it before restaging)
+            self.native_compiler.release(prev)
         dump = os.environ.get("FKS_DUMP_BATCHES")
         if dump and idx.size:
             # diagnostics: every native launch's program texts, written before the launch
@@ -252,17 +295,25 @@ class DeviceEvaluator:
                 f.write(json.dumps({"slot": slot, "t": time.time(), "P": int(idx.size),
                                     "codes": [progs[i].source for i in idx]}) + "\n")
         self._native_post[slot] = (len(progs), idx)
-        if idx.size:
-            self._eng.submit_native(slot, batch.fn[idx], batch.kc, batch.koff[idx])
+        try:
+            if idx.size:
+                self._eng.submit_native(slot, batch.fn[idx], batch.kc, batch.koff[idx])
+        except BaseException:
+            self.native_compiler.release(batch.modules)
+            raise
+        self._native_mods[slot] = batch.modules   # released once the batch is collected
         return batch
 
     def profile_native(self, progs: Sequence[CompiledPolicy]):
         """s_memtime phase-profiled native row-kernel launch: (table [P, 13], wave
         cycles [waves, 8] by ROW_PHASES); programs must all be native-compilable."""
         batch = self.native_compiler.prepare(progs)
-        if not batch.ok.all():
-            raise ValueError(f"not native: {batch.reasons}")
-        return self._eng.profile_native(batch.fn, batch.kc, batch.koff)
+        try:
+            if not batch.ok.all():
+                raise ValueError(f"not native: {batch.reasons}")
+            return self._eng.profile_native(batch.fn, batch.kc, batch.koff)
+        finally:
+            self.native_compiler.release(batch.modules)
 
     def evaluate_native(self, progs: Sequence[CompiledPolicy]) -> np.ndarray:
         if not progs:
@@ -313,8 +364,13 @@ class DeviceEvaluator:
         P, idx = post
         out = np.zeros((P, len(RESULT_COLUMNS)))
         out[:, 10] = 100.0   # EXC_UNSUPPORTED: not native -> the caller's next engine
-        if idx.size:
-            out[idx] = self._eng.wait(slot)
+        try:
+            if idx.size:
+                out[idx] = self._eng.wait(slot)
+        finally:
+            mods = self._native_mods.pop(slot, None)
+            if mods:
+                self.native_compiler.release(mods)
         return out
 
     def ready(self, slot: int) -> bool:

@@ -300,6 +300,18 @@ class NativeBatch:
     reasons: Dict[int, str] = field(default_factory=dict)
     compile_s: float = 0.0           # wall time spent compiling for this batch
     compiled: int = 0                # new shapes compiled for this batch
+    modules: Tuple[int, ...] = ()    # module ids the batch calls into (held until `release`)
+    load_s: float = 0.0              # of compile_s: module loads
+
+
+@dataclass
+class _ModRec:
+    """A loaded JIT module and the shapes that currently resolve into it."""
+    handle: object                   # _fks_hip.JitModule
+    shapes: set = field(default_factory=set)
+    refs: int = 0                    # batches in flight calling into it
+    last_use: int = 0                # prepare() sequence number of the last batch using it
+    tier: str = "baseline"
 
 
 class NativeCompiler:
@@ -319,9 +331,16 @@ class NativeCompiler:
         self._rt = np.asarray(engine.native_rt_table(), dtype=np.uint64)
         self.vgpr_cap = int(self._hip.JIT_VGPRS)
         self.sgpr_cap = int(self._hip.JIT_SGPRS)
-        self._shapes: Dict[str, Tuple[int, int]] = {}   # shape -> (module index, program index)
+        self._shapes: Dict[str, Tuple[int, int]] = {}   # shape -> (module id, program index)
+        self._ptr: Dict[str, int] = {}                  # shape -> device address of its code
         self._bad: Dict[str, str] = {}                  # shape -> reason it is not native
-        self._modules: List[CompiledModule] = []
+        self._modules: Dict[int, _ModRec] = {}         # live modules by id
+        self._next_mod = 0
+        self._seq = 0
+        # bounded module lifetime: beyond this many live modules the least recently
+        # used ones that no batch in flight calls into are unloaded (their shapes are
+        # recompiled if they come back -- the baseline tier takes ~0.2 ms a shape)
+        self.max_modules = int(os.environ.get("FKS_JIT_MAX_MODULES", "256"))
         self._lock = threading.Lock()
         self._inflight: Dict[str, threading.Event] = {}
         self._procs = threading.BoundedSemaphore(self.workers)
@@ -336,7 +355,9 @@ class NativeCompiler:
             self._baseline = BaselineJit(self._hip, self._rt, device)
         self.stats = {"modules": 0, "shapes": 0, "compile_s": 0.0, "rejected": 0, "hits": 0,
                       "baseline_shapes": 0, "llvm_shapes": 0, "baseline_s": 0.0, "llvm_s": 0.0, "load_s": 0.0,
-                      "disk_hits": 0, "tierup_queued": 0, "tierup_done": 0, "tierup_s": 0.0}
+                      "disk_hits": 0, "tierup_queued": 0, "tierup_done": 0, "tierup_s": 0.0,
+                      "live_modules": 0, "max_live_modules": 0, "retired_modules": 0, "evicted_shapes": 0,
+                      "unload_s": 0.0}
         # tier-up (auto tier): a baseline shape used in this many batches is
         # recompiled by the LLVM tier in the background (its code runs ~1.3x
         # faster on the device) and swapped in when ready; never on the
@@ -366,6 +387,7 @@ class NativeCompiler:
             for k in mine:
                 self._inflight[k] = threading.Event()
         t0 = time.perf_counter()
+        load0 = self.stats["load_s"]
         try:
             if mine:
                 self._compile_shapes(mine)
@@ -376,32 +398,123 @@ class NativeCompiler:
         for ev in others:
             ev.wait()
         dt = time.perf_counter() - t0
+        load_dt = self.stats["load_s"] - load0
         P = len(progs)
         fn = np.zeros(P, dtype=np.uint64)
         ok = np.zeros(P, dtype=bool)
         koff = np.zeros(P, dtype=np.int32)
         blocks, pos, reasons = [], 0, {}
+        for i, p in enumerate(progs):
+            kb = constant_block(p, self.budget)
+            koff[i] = pos
+            blocks.append(kb)
+            pos += len(kb)
+        used = set()
+        retry = {}
         with self._lock:
+            self._seq += 1
             for i, (k, p) in enumerate(zip(keys, progs)):
-                kb = constant_block(p, self.budget)
-                koff[i] = pos
-                blocks.append(kb)
-                pos += len(kb)
-                if k in self._shapes:
-                    mi, pi_ = self._shapes[k]
+                loc = self._shapes.get(k)
+                if loc is not None:
+                    used.add(loc[0])
                     # bit 0: the program opens with the template's feasibility
                     # prologue, so the kernels call it for feasible nodes only
-                    fn[i] = self._modules[mi].pointers[pi_] | (1 if _FEAS_SKIP and p.feasibility_prologue else 0)
+                    fn[i] = self._ptr[k] | (1 if _FEAS_SKIP and p.feasibility_prologue else 0)
                     ok[i] = True
+                elif k in self._bad:
+                    reasons[i] = self._bad[k]
                 else:
-                    reasons[i] = self._bad.get(k, "not compiled")
+                    retry[k] = p    # compiled, then retired by another thread before this batch held it
+            for mid in used:         # held until release(): never retired while a batch may call it
+                rec = self._modules[mid]
+                rec.refs += 1
+                rec.last_use = self._seq
             self.stats["hits"] += P - len(mine)
             up = self._tierup_candidates(keys, progs) if self.tierup_after else []
+        if retry:
+            # rare: recompile the retired shapes for this batch (their modules are gone)
+            sub = self.prepare([retry[k] for k in retry])
+            pos_of = {k: j for j, k in enumerate(retry)}
+            for i, k in enumerate(keys):
+                j = pos_of.get(k)
+                if j is None:
+                    continue
+                if sub.ok[j]:
+                    fn[i] = sub.fn[j] | (1 if _FEAS_SKIP and progs[i].feasibility_prologue else 0)
+                    ok[i] = True
+                else:
+                    reasons[i] = sub.reasons.get(j, "not compiled")
+            extra = sub.modules          # held by the inner prepare(): released with this batch
+            dt += sub.compile_s
+        else:
+            extra = ()
         self._reap_tierup()
         for k, p in up:
             self._tierup_futs.append(self._tierup_executor().submit(self._tierup, k, p))
+        self._retire()
         return NativeBatch(fn, np.concatenate(blocks) if blocks else np.zeros(1, np.int64), koff, ok, reasons, dt,
-                           len(mine))
+                           len(mine), tuple(sorted(used)) + tuple(extra), load_dt)
+
+    # -- module lifetime ---------------------------------------------------------------------
+    def release(self, modules: Sequence[int]) -> None:
+        """The batch that held `modules` (NativeBatch.modules) has completed."""
+        with self._lock:
+            for mid in modules:
+                rec = self._modules.get(mid)
+                if rec is not None:
+                    rec.refs -= 1
+        self._retire()
+
+    def _add_module(self, handle, tier: str) -> int:
+        """Register a loaded module (lock held); returns its id."""
+        mid = self._next_mod
+        self._next_mod += 1
+        self._modules[mid] = _ModRec(handle, tier=tier, last_use=self._seq)
+        self.stats["modules"] += 1
+        self.stats["live_modules"] = len(self._modules)
+        self.stats["max_live_modules"] = max(self.stats["max_live_modules"], len(self._modules))
+        return mid
+
+    def _map_shape(self, k: str, mid: int, idx: int, ptr: int) -> None:
+        """shape k -> program idx of module mid (lock held)."""
+        old = self._shapes.get(k)
+        if old is not None and old[0] in self._modules:
+            self._modules[old[0]].shapes.discard(k)
+        self._shapes[k] = (mid, idx)
+        self._ptr[k] = int(ptr)
+        self._modules[mid].shapes.add(k)
+
+    def _retire(self) -> None:
+        """Unload the least recently used modules no batch in flight calls
+        into, down to 3/4 of `max_modules`, once more than `max_modules` are
+        live.  Their shapes leave the cache (a later batch recompiles them).
+        No device-wide synchronisation: a module with no references has no
+        launch that could still call into it."""
+        if self.max_modules <= 0:
+            return
+        victims = []
+        with self._lock:
+            if len(self._modules) <= self.max_modules:
+                return
+            idle = sorted((rec.last_use, mid) for mid, rec in self._modules.items() if rec.refs <= 0)
+            excess = len(self._modules) - max(1, (3 * self.max_modules) // 4)
+            for _, mid in idle[:max(0, excess)]:
+                rec = self._modules.pop(mid)
+                for k in rec.shapes:
+                    if self._shapes.get(k, (None,))[0] == mid:
+                        del self._shapes[k]
+                        self._ptr.pop(k, None)
+                        self._tier_of.pop(k, None)
+                        self._uses.pop(k, None)
+                        self.stats["evicted_shapes"] += 1
+                victims.append(rec)
+            self.stats["retired_modules"] += len(victims)
+            self.stats["live_modules"] = len(self._modules)
+        t0 = time.perf_counter()
+        for rec in victims:
+            rec.handle.unload()
+        with self._lock:
+            self.stats["unload_s"] += time.perf_counter() - t0
 
     # -- background tier-up --------------------------------------------------------------
     def _tierup_candidates(self, keys, progs):
@@ -435,10 +548,11 @@ class NativeCompiler:
         mod.handle = self._hip.JitModule(mod.image, self._rt, mod.n, self.device)
         mod.pointers = np.asarray(mod.handle.pointers(), dtype=np.uint64)
         with self._lock:
-            mi = len(self._modules)
-            self._modules.append(mod)      # the baseline module stays loaded: batches in flight call it
-            self.stats["modules"] += 1
-            self._shapes[k] = (mi, 0)
+            if k not in self._shapes:     # retired meanwhile: nothing to upgrade
+                mod.handle.unload()
+                return False
+            mi = self._add_module(mod.handle, "llvm")   # the baseline module stays loaded: batches in flight call it
+            self._map_shape(k, mi, 0, int(mod.pointers[0]))
             self._tier_of[k] = "llvm"
             self.stats["tierup_done"] += 1
             self.stats["tierup_s"] += mod.compile_s
@@ -475,13 +589,13 @@ class NativeCompiler:
                 return exc
 
     def _compile_baseline(self, items):
-        """Baseline tier: generate every shape, load the batch as one module;
-        returns the (key, program, reason) the generator declined."""
-        from .gcnjit import compile_program
+        """Baseline tier: generate every shape (in parallel, C++ threads), load
+        the batch as one module; returns the (key, program, reason) the
+        generator declined."""
+        from .gcnjit import compile_many
         t0 = time.perf_counter()
         codes, keys, declined = [], [], []
-        for k, p in items:
-            code, why = compile_program(p)
+        for (k, p), (code, why) in zip(items, compile_many([p for _, p in items], self.workers)):
             if code is None:
                 declined.append((k, p, why))
             else:
@@ -492,15 +606,15 @@ class NativeCompiler:
             mod = self._baseline.load(codes, t1 - t0)
             t2 = time.perf_counter()
             with self._lock:
-                mi = len(self._modules)
-                self._modules.append(mod)
-                self.stats["modules"] += 1
+                mi = self._add_module(mod.handle, "baseline")
                 self.stats["compile_s"] += t2 - t0
                 self.stats["baseline_s"] += t1 - t0
                 self.stats["load_s"] += t2 - t1
+                self.stats["probed_loads"] = self.stats.get("probed_loads", 0) + int(mod.probed)
                 for j, k in enumerate(keys):
-                    self._shapes[k] = (mi, j)
+                    self._map_shape(k, mi, j, int(mod.pointers[j]))
                     self._tier_of[k] = "baseline"
+                    self._uses.pop(k, None)
                     self.stats["shapes"] += 1
                     self.stats["baseline_shapes"] += 1
         return declined
@@ -568,9 +682,7 @@ class NativeCompiler:
                 self.stats["llvm_s"] += mod.compile_s
                 self.stats["llvm_shapes"] += len(ch)
                 self.stats["disk_hits"] += int(mod.cached)
-                mi = len(self._modules)
-                self._modules.append(mod)
-                self.stats["modules"] += 1
+                mi = self._add_module(mod.handle, "llvm")
                 for j, (k, _) in enumerate(ch):
                     res = mod.resources[j]
                     why = "no resource record" if res is None else res.fits(self.vgpr_cap, self.sgpr_cap)
@@ -578,7 +690,7 @@ class NativeCompiler:
                         self._bad[k] = why
                         self.stats["rejected"] += 1
                     else:
-                        self._shapes[k] = (mi, j)
+                        self._map_shape(k, mi, j, int(mod.pointers[j]))
                         self._tier_of[k] = "llvm"
                         self.stats["shapes"] += 1
 

@@ -65,6 +65,10 @@ class Val:
     temp: bool = False
 
 
+#: operations CPython evaluates with libm (exp / log / pow: glibc_math.h on the device)
+_LIBM_OPS = frozenset({Op.POW, Op.LOG, Op.LOGB, Op.EXP, Op.MPOW})
+
+
 @dataclass
 class CompiledPolicy:
     """Bytecode + constant pool of one program."""
@@ -88,6 +92,11 @@ class CompiledPolicy:
         """False when the program uses functions the device interpreter routes
         back to the host (trigonometry: no correctly rounded device version)."""
         return "trig" not in self.features
+
+    @property
+    def uses_libm(self) -> bool:
+        """The program may call libm's exp / log / pow (`**`, math.exp / log / pow)."""
+        return "libm" in self.features
 
     @property
     def feasibility_prologue(self) -> bool:
@@ -152,6 +161,8 @@ class Compiler:
 
     # ------------------------------------------------------------------ emit
     def emit(self, op: Op, d: int = NO_REG, a: int = NO_REG, b: int = NO_REG, imm: int = 0) -> int:
+        if op in _LIBM_OPS:
+            self.features.add("libm")
         self.code.append([int(op), d, a, b, imm])
         return len(self.code) - 1
 

@@ -139,3 +139,62 @@ def test_concurrent_first_submits_share_one_compiler(default_workload):
         ok = out[k][:, 10] != Exc.UNSUPPORTED
         cpu = ce.simulate_program_batch(default_workload, batches[k])
         assert np.array_equal(out[k][ok], cpu[ok])
+
+
+@pytest.mark.parametrize("top", [63, 1023, -1])
+def test_duo_hbm_heap_tops_agree(dev, default_workload, top):
+    """The two-wave kernel with its heap mostly in the HBM slice (LDS top of
+    63 / 1,023 slots) and with the heap top sized for 2,048 programs in
+    flight: rows bit-identical to the CPU VM."""
+    progs = programs()[:24]
+    vm = ce.simulate_program_batch(default_workload, progs, threads=16)
+    opts = {"native_duo_top": top} if top >= 0 else {"native_inflight": 2048}
+    dev.set_options(**opts)
+    try:
+        nat = dev.evaluate_native(progs)
+        info = dev.info()
+    finally:
+        dev.set_options(native_duo_top=-1, native_inflight=0)
+    assert info["native_rows_last"] == 0, info
+    if top >= 0:
+        assert info["native_duo_top_last"] == top, info
+    else:
+        # as many programs resident as the registers allow (or all 2,048)
+        cap = info["native_duo_reg_cap"]
+        assert info["native_duo_per_cu_last"] >= min(cap, 2048 // info["num_cus"]), info
+    compared = 0
+    for i in range(len(progs)):
+        if int(nat[i, 10]) in (Exc.UNSUPPORTED, Exc.BUDGET) or int(vm[i, 10]) in (Exc.UNSUPPORTED, Exc.BUDGET):
+            continue
+        assert np.array_equal(nat[i], vm[i]), (top, i, nat[i], vm[i])
+        compared += 1
+    assert compared >= len(progs) - 4
+
+
+def test_module_retirement_bounds_live_modules(default_workload):
+    """Modules whose batches have completed are unloaded once more than
+    `max_modules` are live (no device-wide sync); their shapes leave the cache
+    and are recompiled when they come back, with identical rows.  Baseline
+    modules after the first of each skeleton size load without a probe kernel."""
+    from funsearch_kubernetes_simulator_amd.bench.programs import novel_children
+    from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
+    from funsearch_kubernetes_simulator_amd.ops.jit import NativeCompiler
+    d = he.DeviceEvaluator(default_workload)
+    d._jit = NativeCompiler(d._eng, d.device, budget=int(d.options["budget"]), tier="baseline")
+    nc = d.native_compiler
+    nc.max_modules = 3
+    progs = novel_children(32, seed=77)
+    batches = [progs[4 * k:4 * (k + 1)] for k in range(8)]
+    first = None
+    for k, b in enumerate(batches):
+        tab = d.evaluate_native(b)
+        if k == 0:
+            first = tab
+        assert nc.stats["live_modules"] <= 3, nc.stats
+    assert nc.stats["retired_modules"] >= 5 and nc.stats["evicted_shapes"] >= 20, nc.stats
+    assert nc.stats["probed_loads"] == 1, nc.stats          # later loads: no probe kernel, no copy
+    again = d.evaluate_native(batches[0])                    # evicted shapes: recompiled
+    assert np.array_equal(again, first)
+    cpu = ce.simulate_program_batch(default_workload, batches[0], threads=16)
+    ok = (first[:, 10] != Exc.UNSUPPORTED) & (cpu[:, 10] != Exc.UNSUPPORTED)
+    assert np.array_equal(first[ok], cpu[ok])
