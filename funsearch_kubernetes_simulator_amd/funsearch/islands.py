@@ -59,6 +59,19 @@ class IslandFunSearch:
         self.migrate_every = int(isl.get("migrate_every", 50))
         self.n_migrants = int(isl.get("migrants", 2))
         self.elastic = bool(isl.get("elastic", True))
+        # FunSearch-style island resets (off by default; the reference has one
+        # population): every `reset_every` generations the weakest
+        # `reset_fraction` of this rank's islands restart from the best program
+        # of a random surviving island, so the islands do not all converge on
+        # one lineage through migration
+        self.reset_every = int(isl.get("reset_every", 0))
+        self.reset_fraction = float(isl.get("reset_fraction", 0.5))
+        # migrants enter only if no equal-or-better member is too similar
+        # (the island's own dedup rule) and they beat its worst member
+        self.migrant_dedup = bool(isl.get("migrant_dedup", False))
+        import random as _random
+        self._reset_rng = _random.Random(int((self.config.get("llm") or {}).get("seed", 0)) * 31 + 7)
+        self.resets = 0
         # constant polish of island champions on the device (funsearch/polish.py)
         pol = self.config.get("polish") or {}
         self.polish_every = int(pol.get("every", 0))
@@ -177,6 +190,8 @@ class IslandFunSearch:
             s.population = sorted(elites + new, key=lambda x: x[1], reverse=True)[:s.population_size]
         for i in range(len(self.islands)):
             self.maybe_polish(i)
+        if self.reset_every and self.generation % self.reset_every == 0:
+            self.reset_weak_islands()
         if self.coupler is not None and self.coupler.due(self.generation):
             for rec in self.run_coupling():
                 self.inject_coupled(rec)
@@ -260,11 +275,39 @@ class IslandFunSearch:
         s = self.islands[li]
         known = {c for c, _ in s.population}
         for code, score in incoming:
-            if code not in known:
-                s.population.append((code, score))
-                if score > s.best_score:
-                    s.best_score, s.best_policy = score, code
+            if code in known:
+                continue
+            if self.migrant_dedup:
+                # replace only a worse member, never one the island already has in kind
+                full = len(s.population) >= s.population_size
+                if (full and score <= min(sc for _, sc in s.population)) or s._is_too_similar(code, score):
+                    continue
+            s.population.append((code, score))
+            known.add(code)
+            if score > s.best_score:
+                s.best_score, s.best_policy = score, code
         s.population = sorted(s.population, key=lambda x: x[1], reverse=True)[:s.population_size]
+
+    def reset_weak_islands(self) -> List[int]:
+        """FunSearch island reset: the weakest `reset_fraction` of this rank's
+        islands (by best score; ties: higher index first) are emptied and
+        re-seeded with the best program of a random surviving island.  Returns
+        the reset island indices (logged as an ``island_reset`` record)."""
+        k = len(self.islands)
+        n = int(k * self.reset_fraction)
+        if k < 2 or n < 1:
+            return []
+        order = sorted(range(k), key=lambda i: (self.islands[i].best_score, -i))
+        weak, keep = order[:n], order[n:]
+        for i in weak:
+            src = self.islands[self._reset_rng.choice(keep)]
+            s = self.islands[i]
+            s.population = [(src.best_policy, src.best_score)] if src.best_policy else list(src.population[:1])
+            s.best_policy, s.best_score = src.best_policy, src.best_score
+        self.resets += 1
+        self.log.write(kind="island_reset", rank=self.ctx.rank, generation=self.generation, reset=weak,
+                       bests=[round(s.best_score, 6) for s in self.islands])
+        return weak
 
     def absorb_migrants(self, glob) -> None:
         for li, inc in self.incoming_migrants(glob).items():

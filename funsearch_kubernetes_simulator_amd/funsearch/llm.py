@@ -12,10 +12,12 @@ unchanged with any of them:
   ``OPENROUTER_API_KEY`` / ``OPENAI_API_KEY`` environment variables (never from
   committed files).  The reference has no retries.
 * `MutationClient` -- deterministic, offline: parses the parent programs out of
-  the prompt and returns a mutated policy body (constant perturbation,
-  operator / comparison swaps, term insertion from a feature library, term
-  deletion, crossover of two parents).  Used for tests, benchmarks and
-  air-gapped runs.
+  the prompt and returns a mutated policy body: constant perturbation, term
+  insertion (a fixed library, or new terms from a feature grammar that covers
+  every template field), ast-level operator / aggregation swaps, wrapping a
+  subexpression (abs / min / max / square / power), subexpression crossover
+  between the two parents, statement deletion, line crossover.  Used for
+  tests, benchmarks and air-gapped runs.
 * `ScriptedClient` -- replays a fixed list of responses (tests).
 """
 
@@ -163,6 +165,95 @@ TERM_LIBRARY = [
 ]
 
 
+#: normalised (pod, node) features for freshly built terms (`_random_expr`):
+#: every template field appears in at least one, so a structural mutation can
+#: bring a field into a program that never used it
+FEATURES = [
+    "node.cpu_milli_left / max(1, node.cpu_milli_total)",
+    "node.memory_mib_left / max(1, node.memory_mib_total)",
+    "(node.cpu_milli_left - pod.cpu_milli) / max(1, node.cpu_milli_total)",
+    "(node.memory_mib_left - pod.memory_mib) / max(1, node.memory_mib_total)",
+    "pod.cpu_milli / max(1, node.cpu_milli_left)",
+    "pod.memory_mib / max(1, node.memory_mib_left)",
+    "node.gpu_left / max(1, len(node.gpus))",
+    "(node.gpu_left - pod.num_gpu) / max(1, len(node.gpus))",
+    "sum(g.gpu_milli_left for g in node.gpus) / max(1, 1000 * len(node.gpus))",
+    "(max(g.gpu_milli_left for g in node.gpus) if node.gpus else 0) / 1000",
+    "(min(g.gpu_milli_left for g in node.gpus) if node.gpus else 1000) / 1000",
+    "sum(1 for g in node.gpus if g.gpu_milli_left >= pod.gpu_milli) / max(1, len(node.gpus))",
+    "len([g for g in node.gpus if 0 < g.gpu_milli_left < g.gpu_milli_total]) / max(1, len(node.gpus))",
+    "sum(g.gpu_milli_left - pod.gpu_milli for g in node.gpus if g.gpu_milli_left >= pod.gpu_milli) / 1000",
+    "pod.gpu_milli / 1000",
+    "pod.num_gpu",
+    "min(node.cpu_milli_left / max(1, pod.cpu_milli), node.memory_mib_left / max(1, pod.memory_mib)) / 100",
+]
+
+#: names a moved subexpression may mention (anything else is a local of its parent)
+_FREE_OK = frozenset({"pod", "node", "math", "abs", "min", "max", "sum", "len", "int", "float", "round", "sorted"})
+_NUMERIC_FIELDS = frozenset({"cpu_milli", "memory_mib", "num_gpu", "gpu_milli", "cpu_milli_left", "memory_mib_left",
+                             "gpu_left", "cpu_milli_total", "memory_mib_total"})
+
+
+def _free_names(node: ast.AST) -> set:
+    """Names read in `node` that no comprehension inside it binds."""
+    bound, used = set(), set()
+    for n in ast.walk(node):
+        if isinstance(n, ast.comprehension):
+            for t in ast.walk(n.target):
+                if isinstance(t, ast.Name):
+                    bound.add(t.id)
+        elif isinstance(n, ast.Lambda):
+            bound.update(a.arg for a in n.args.args)
+        elif isinstance(n, ast.Name) and isinstance(n.ctx, ast.Load):
+            used.add(n.id)
+    return used - bound
+
+
+def _numeric_subexprs(tree: ast.AST, portable: bool) -> list:
+    """Expression nodes that hold a number and may be swapped for another
+    numeric expression: arithmetic, numeric literals, pod / node scalar fields,
+    abs / min / max / sum calls.  `portable`: only those that mention no
+    parent-local name (they may move into another program)."""
+    skip = set()
+    for n in ast.walk(tree):
+        if isinstance(n, ast.comprehension):
+            skip.update(id(x) for x in ast.walk(n.iter))     # keep `for g in node.gpus` intact
+        elif isinstance(n, (ast.Assign, ast.AugAssign)):
+            tgts = n.targets if isinstance(n, ast.Assign) else [n.target]
+            for t in tgts:
+                skip.update(id(x) for x in ast.walk(t))
+        elif isinstance(n, ast.Call):
+            skip.add(id(n.func))
+            skip.update(id(x) for x in ast.walk(n.func))
+    out = []
+    for n in ast.walk(tree):
+        if id(n) in skip:
+            continue
+        ok = (isinstance(n, (ast.BinOp, ast.UnaryOp))
+              or (isinstance(n, ast.Constant) and isinstance(n.value, (int, float)) and not isinstance(n.value, bool))
+              or (isinstance(n, ast.Attribute) and isinstance(n.value, ast.Name) and n.value.id in ("pod", "node")
+                  and n.attr in _NUMERIC_FIELDS)
+              or (isinstance(n, ast.Call) and isinstance(n.func, ast.Name) and n.func.id in ("abs", "min", "max", "sum")))
+        if ok and (not portable or _free_names(n) <= _FREE_OK):
+            out.append(n)
+    return out
+
+
+class _Replace(ast.NodeTransformer):
+    def __init__(self, target: ast.AST, new: ast.AST):
+        self.target, self.new = target, new
+
+    def generic_visit(self, node):
+        if node is self.target:
+            return self.new
+        return super().generic_visit(node)
+
+    def visit(self, node):
+        if node is self.target:
+            return self.new
+        return super().visit(node)
+
+
 @functools.lru_cache(maxsize=4096)   # parents repeat across thousands of children
 def _extract_body(program: str) -> Optional[str]:
     """The logic between ``score = 0.0`` and the final return of a
@@ -215,27 +306,137 @@ class MutationClient(BaseClient):
             self.calls += 1
             rng = random.Random(self.rng.random())
         bodies = [textwrap.dedent(b).strip("\n") for b in (_extract_body(p) for p in parents) if b]
+        other = None
         if not bodies:
             body = "score = 1000.0"
         elif len(bodies) >= 2 and rng.random() < 0.25:
             body = self._crossover(bodies[0], bodies[1], rng)
         else:
-            body = rng.choice(bodies)
+            k = rng.randrange(len(bodies))
+            body = bodies[k]
+            other = bodies[1 - k] if len(bodies) >= 2 else None
         for _ in range(1 + int(rng.random() < 0.5 * max(0.2, temperature))):
-            body = self._mutate(body, rng)
+            body = self._mutate(body, rng, other)
         return _response(self._indent(body))
 
     # -- operators ----------------------------------------------------------------------
-    def _mutate(self, body: str, rng: random.Random) -> str:
+    #: (cumulative probability, operator).  Structural operators (new terms from
+    #: the feature grammar, operator / aggregation swaps, subexpression crossover,
+    #: wrapping) change a program's shape; constant perturbations keep it.
+    OPERATORS = ((0.30, "constants"), (0.42, "library_term"), (0.57, "random_term"), (0.66, "swap_binop"),
+                 (0.74, "swap_aggregate"), (0.84, "subexpr_crossover"), (0.90, "wrap"), (0.96, "drop"),
+                 (1.00, "swap_comparison"))
+
+    def _mutate(self, body: str, rng: random.Random, other: Optional[str] = None) -> str:
         op = rng.random()
-        if op < 0.45:
+        name = next(n for p, n in self.OPERATORS if op < p)
+        self.last_op = name
+        if name == "constants":
             return self._perturb_constants(body, rng)
-        if op < 0.75:
+        if name == "library_term":
             term = rng.choice(TERM_LIBRARY).format(c=self._const(rng))
             return body.rstrip("\n") + "\n" + term
-        if op < 0.9:
+        if name == "random_term":
+            return body.rstrip("\n") + "\n" + self._random_term(rng)
+        if name == "drop":
             return self._drop_statement(body, rng)
-        return self._swap_comparison(body, rng)
+        if name == "swap_comparison":
+            return self._swap_comparison(body, rng)
+        out = self._structural(name, body, rng, other)
+        return out if out is not None else self._perturb_constants(body, rng)
+
+    # -- structural operators (ast) -------------------------------------------------------
+    def _random_expr(self, rng: random.Random, depth: int = 0) -> str:
+        r = rng.random()
+        if depth >= 2 or r < 0.45:
+            return f"({rng.choice(FEATURES)})"
+        a, b = self._random_expr(rng, depth + 1), self._random_expr(rng, depth + 1)
+        if r < 0.65:
+            return f"({a} {rng.choice(['+', '-', '*'])} {b})"
+        if r < 0.8:
+            return f"{rng.choice(['min', 'max'])}({a}, {b})"
+        if r < 0.9:
+            return f"abs({a} - {b})"
+        return f"({a}) ** 2"
+
+    def _random_term(self, rng: random.Random) -> str:
+        e = self._random_expr(rng)
+        c = self._const(rng)
+        form = rng.random()
+        if form < 0.45:
+            return f"score += {c} * {e}"
+        if form < 0.9:
+            return f"score -= {c} * {e}"
+        return f"if {e} > {round(rng.uniform(0, 1), 3)}:\n    score += {c}"
+
+    def _structural(self, name: str, body: str, rng: random.Random, other: Optional[str]) -> Optional[str]:
+        try:
+            tree = ast.parse(body)
+        except SyntaxError:
+            return None
+        if name == "swap_binop":
+            ops = [n for n in ast.walk(tree) if isinstance(n, ast.BinOp)
+                   and isinstance(n.op, (ast.Add, ast.Sub, ast.Mult, ast.Div))]
+            if not ops:
+                return None
+            n = rng.choice(ops)
+            swap = {ast.Add: ast.Sub, ast.Sub: ast.Add, ast.Mult: ast.Div, ast.Div: ast.Mult}
+            n.op = swap[type(n.op)]()
+            if isinstance(n.op, ast.Div):   # never divide by a possibly-zero right operand
+                n.right = ast.Call(ast.Name("max", ast.Load()), [ast.Constant(1), n.right], [])
+        elif name == "swap_aggregate":
+            calls = [n for n in ast.walk(tree) if isinstance(n, ast.Call) and isinstance(n.func, ast.Name)
+                     and n.func.id in ("min", "max", "sum") and not n.keywords]
+            if not calls:
+                return None
+            n = rng.choice(calls)
+            if len(n.args) == 1 and isinstance(n.args[0], ast.GeneratorExp):
+                n.func.id = rng.choice([f for f in ("min", "max", "sum") if f != n.func.id])
+                if n.func.id in ("min", "max"):   # an empty GPU list would raise: guard like the features do
+                    node = ast.IfExp(ast.Attribute(ast.Name("node", ast.Load()), "gpus", ast.Load()), n,
+                                     ast.Constant(0))
+                    tree = _Replace(n, node).visit(tree)
+            elif len(n.args) >= 2 and n.func.id in ("min", "max"):
+                n.func.id = "max" if n.func.id == "min" else "min"
+            else:
+                return None
+        elif name == "subexpr_crossover":
+            if not other:
+                return None
+            try:
+                donor = ast.parse(other)
+            except SyntaxError:
+                return None
+            targets = _numeric_subexprs(tree, portable=False)
+            pieces = [n for n in _numeric_subexprs(donor, portable=True) if not isinstance(n, ast.Constant)]
+            if not targets or not pieces:
+                return None
+            tree = _Replace(rng.choice(targets), rng.choice(pieces)).visit(tree)
+        elif name == "wrap":
+            targets = [n for n in _numeric_subexprs(tree, portable=False) if not isinstance(n, ast.Constant)]
+            if not targets:
+                return None
+            t = rng.choice(targets)
+            c = ast.Constant(float(self._const(rng)))
+            form = rng.randrange(4)
+            if form == 0:
+                new = ast.Call(ast.Name("abs", ast.Load()), [t], [])
+            elif form == 1:
+                new = ast.Call(ast.Name(rng.choice(["min", "max"]), ast.Load()), [t, c], [])
+            elif form == 2:
+                new = ast.BinOp(t, ast.Mult(), t)
+            else:
+                new = ast.BinOp(ast.Call(ast.Name("abs", ast.Load()), [t], []), ast.Pow(),
+                                ast.Constant(round(rng.uniform(0.3, 2.0), 2)))
+            tree = _Replace(t, new).visit(tree)
+        else:
+            return None
+        try:
+            out = ast.unparse(ast.fix_missing_locations(tree))
+            ast.parse(out)
+        except Exception:
+            return None
+        return out
 
     @staticmethod
     def _const(rng: random.Random) -> str:

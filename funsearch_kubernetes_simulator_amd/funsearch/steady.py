@@ -216,6 +216,7 @@ class SteadyStateSearch:
         t_prev = t_start
         busy_since = None
         want_buffer = self.batch * (self.slots + 1)
+        next_reset = ((start_gen // fs.reset_every) + 1) * fs.reset_every if fs.reset_every else 0
         try:
             while True:
                 progressed = False
@@ -312,6 +313,10 @@ class SteadyStateSearch:
                 fs.generation = g_min
                 for s, g in zip(islands, gens):
                     s.generation = start_gen + g
+                # island resets (islands.reset_every): at each multiple the slowest island passes
+                if fs.reset_every and g_min >= next_reset:
+                    fs.reset_weak_islands()
+                    next_reset = (g_min // fs.reset_every + 1) * fs.reset_every
                 # 5) migration: post async gathers; absorb finished ones (in order)
                 if chan.every:
                     if chan.post_due(g_min if not stop else -1, want_stop):
@@ -385,6 +390,7 @@ class SteadyStateSearch:
                    main_cpu_frac=round((time.process_time() - self._cpu0) / wall, 3), rejected=st.rejected, jit_s=round(st.jit_s, 3),
                    generation=fs.generation, best=round(fs.best[1], 6), best_global=round(best_global, 6),
                    islands=[round(s.best_score, 6) for s in fs.islands], migrations=st.migrations,
+                   resets=fs.resets, distinct_island_bests=len({s.best_policy for s in fs.islands}),
                    collective_wait_s=round(self.channel.wait_s, 4),
                    main_phase_s={k: round(v, 3) for k, v in self.phase.items()},
                    jit={k: (round(v, 3) if isinstance(v, float) else v)

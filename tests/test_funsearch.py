@@ -486,3 +486,58 @@ def test_pipelined_islands_native_declines_everything(tmp_path):
     assert fs.generation == 2
     assert ev.stats["device"] > 0 and ev.stats["device_native"] == 0
     assert set(ev.device.vm_slots) <= {0, 1} and len(set(ev.device.vm_slots)) == 2
+
+
+def test_structural_mutations_compile_and_diversify():
+    """The offline mutator's structural operators (feature-grammar terms,
+    ast operator / aggregation swaps, subexpression crossover, wrapping)
+    produce programs that compile and, unlike constant edits, new shapes."""
+    import random
+    from funsearch_kubernetes_simulator_amd.models.library import reference_policies
+    from funsearch_kubernetes_simulator_amd.policy.compiler import try_compile
+    from funsearch_kubernetes_simulator_amd.policy.native_codegen import shape_key
+    c = MutationClient(9)
+    parents = list(reference_policies().values()) + list(seed_policies().values())
+    rng = random.Random(2)
+    by_op, ok_by_op, shapes = {}, {}, set()
+    for _ in range(600):
+        pa = rng.sample(parents, 2)
+        prompt = PolicyTemplate.create_prompt_for_llm([(pa[0], 0.45), (pa[1], 0.44)], "fb")
+        body = c.chat.completions.create(model="m", messages=[{"role": "user", "content": prompt}]).choices[0].message.content
+        op = c.last_op
+        by_op[op] = by_op.get(op, 0) + 1
+        prog, _ = try_compile(PolicyTemplate.fill_template(body))
+        if prog is not None:
+            ok_by_op[op] = ok_by_op.get(op, 0) + 1
+            shapes.add(shape_key(prog))
+    structural = ("random_term", "swap_binop", "swap_aggregate", "subexpr_crossover", "wrap")
+    assert all(by_op.get(o, 0) > 0 for o in structural), by_op
+    assert sum(ok_by_op.values()) >= 0.9 * 600, (by_op, ok_by_op)
+    assert len(shapes) > 250       # constant-only edits would keep ~a dozen parent shapes
+
+
+def test_island_reset_and_migrant_dedup(tmp_path):
+    from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
+    cfg = _cfg(tmp_path)
+    cfg["islands"] = {"per_rank": 4, "migrate_every": 0, "migrants": 1, "reset_every": 1, "migrant_dedup": True}
+    fs = IslandFunSearch(cfg)
+    fs.initialize()
+    progs = [f"def priority_function(pod, node):\n    return {k} * node.cpu_milli_left + {k}\n" for k in range(4)]
+    for i, s in enumerate(fs.islands):
+        s.population = [(progs[i], 0.40 + 0.01 * i)]
+        s.best_policy, s.best_score = progs[i], 0.40 + 0.01 * i
+    weak = fs.reset_weak_islands()
+    assert sorted(weak) == [0, 1]
+    for i in weak:       # re-seeded with a surviving island's best
+        assert fs.islands[i].best_policy in progs[2:] and len(fs.islands[i].population) == 1
+    assert [s.best_policy for s in fs.islands[2:]] == progs[2:]
+    # dedup: a near-copy of a better member is refused, a worse-than-worst one too
+    s = fs.islands[3]
+    s.population = [(progs[3], 0.5)] + [(f"def priority_function(pod, node):\n    return {j}\n", 0.3)
+                                         for j in range(s.population_size - 1)]
+    fs.apply_migrants(3, [(progs[3].replace("3 *", "3.0 *"), 0.45), ("def priority_function(pod, node):\n"
+                                                                    "    return node.gpu_left\n", 0.1)])
+    assert len(s.population) == s.population_size and max(sc for _, sc in s.population) == 0.5
+    assert all(sc != 0.45 and sc != 0.1 for _, sc in s.population)
+    fs.apply_migrants(3, [("def priority_function(pod, node):\n    return node.memory_mib_left // 7 - 1\n", 0.44)])
+    assert 0.44 in [sc for _, sc in s.population]

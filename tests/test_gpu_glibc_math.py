@@ -32,13 +32,12 @@ def test_device_equals_host_build():
 def test_pow_heavy_program_native_equals_cpu_vm(default_workload):
     from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
     dev = he.DeviceEvaluator(default_workload)
-    body = ("def priority_function(pod, node):\n"
-            "    if node.cpu_milli_left < pod.cpu_milli or node.memory_mib_left < pod.memory_mib:\n"
-            "        return 0\n"
-            "    c = (node.cpu_milli_left / max(1, node.cpu_milli_total)) ** 1.37\n"
-            "    m = math.exp(-node.memory_mib_left / max(1.0, node.memory_mib_total * 1.9))\n"
-            "    g = math.log(1.0 + node.gpu_left + pod.cpu_milli / 997.0) ** 0.71\n"
-            "    return int(1000 * (c + m) * g * 7.3) + math.pow(2.0, g) * 3.1\n")
+    from funsearch_kubernetes_simulator_amd.policy.template import PolicyTemplate
+    body = PolicyTemplate.fill_template(
+        "c = (node.cpu_milli_left / max(1, node.cpu_milli_total)) ** 1.37\n"
+        "    m = math.exp(-node.memory_mib_left / max(1.0, node.memory_mib_total * 1.9))\n"
+        "    g = math.log(1.0 + node.gpu_left + pod.cpu_milli / 997.0) ** 0.71\n"
+        "    score = 1000 * (c + m) * g * 7.3 + math.pow(2.0, g) * 3.1")
     progs = [compile_policy(body.replace("1.37", str(1.37 + 0.013 * k))) for k in range(16)]
     nat = dev.evaluate_native(progs)
     vm = ce.simulate_program_batch(default_workload, progs, threads=16)
