@@ -44,8 +44,18 @@ struct DuoBox {
   uint32_t term;           // H: no more events
   int32_t h_exc, n_repush, n_dropped;
 };
+// Scoring-wave state kept in LDS between events (16 lanes): the mutable node
+// registers and waiting-class counters (16 int32 per lane) and the exact
+// accumulators (RowAcc, 32 B per lane).  Nothing of it is live across the
+// program call then: the JIT program may use every caller-saved VGPR below
+// kJitVgprs, so whatever the scoring wave keeps in registers across the call
+// must sit in the callee-saved blocks -- in registers this state pushed the
+// kernel to 169 VGPRs (2 waves/SIMD: 4 programs per CU); in LDS it stays at
+// the 128-VGPR floor (4 waves/SIMD: 8 programs per CU, 2,048 in flight).
+constexpr int kDuoNodeInts = 16;   // cpu_left, mem_left, gpu_left, -, gml[8], wcnt[4]
+constexpr size_t kDuoSBytes = (size_t)kRow * kDuoNodeInts * 4 + (size_t)kRow * 32;
 __host__ __device__ inline size_t duo_lds_bytes(int n_pods, int T) {
-  return rows_lds_bytes(n_pods, T, 1, true) + ((sizeof(DuoBox) + 15) & ~size_t(15));
+  return rows_lds_bytes(n_pods, T, 1, true) + ((sizeof(DuoBox) + 15) & ~size_t(15)) + kDuoSBytes;
 }
 
 __device__ __forceinline__ uint32_t duo_ld(FKS_LDS uint32_t* p) {
@@ -157,6 +167,9 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
   FKS_LDS int32_t* ntab = cls_lds + kRow * kRowClassSlots;
   FKS_LDS int64_t* kcp = reinterpret_cast<FKS_LDS int64_t*>(rowbase + rows_row_bytes(N, T));
   FKS_LDS DuoBox* box = reinterpret_cast<FKS_LDS DuoBox*>(reinterpret_cast<FKS_LDS char*>(lds) + rows_lds_bytes(N, T, 1, true));
+  FKS_LDS int32_t* sstate = reinterpret_cast<FKS_LDS int32_t*>(reinterpret_cast<FKS_LDS char*>(box) +
+                                                                ((sizeof(DuoBox) + 15) & ~size_t(15)));
+  FKS_LDS uint64_t* sacc = reinterpret_cast<FKS_LDS uint64_t*>(sstate + kRow * kDuoNodeInts);
 
   if (wave == 0) {
     if (lane < W.n_classes) cls_lds[lane] = *global_ptr(&W.class_value[lane]);
@@ -292,22 +305,49 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
   const uint64_t fne = *global_ptr(&nat.fn[p]);
   const ProgFn prog = prog_of(fne);
   const bool feas_pro = prog_feas(fne);   // call only for feasible nodes
-  NodeRegs<1> nr;
+  // this lane's node state and accumulators in LDS (kDuoSBytes above)
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  FKS_LDS v4i* my = reinterpret_cast<FKS_LDS v4i*>(sstate + jv * kDuoNodeInts);
+  FKS_LDS uint64_t* myacc = sacc + jv * 4;
   {
     const FKS_CONST DevWorkload* Wb = cold();
-    nr.cpu_left[0] = Wb->cpu_left0[jv];
-    nr.mem_left[0] = Wb->mem_left0[jv];
-    nr.gpu_left[0] = Wb->gpu_left0[jv];
-#pragma unroll
-    for (int g = 0; g < kGmax; ++g) nr.gml[0][g] = Wb->gml_left0[jv * kGmax + g];
+    v4i a = {Wb->cpu_left0[jv], Wb->mem_left0[jv], Wb->gpu_left0[jv], 0};
+    v4i g0 = {Wb->gml_left0[jv * kGmax + 0], Wb->gml_left0[jv * kGmax + 1], Wb->gml_left0[jv * kGmax + 2],
+              Wb->gml_left0[jv * kGmax + 3]};
+    v4i g1 = {Wb->gml_left0[jv * kGmax + 4], Wb->gml_left0[jv * kGmax + 5], Wb->gml_left0[jv * kGmax + 6],
+              Wb->gml_left0[jv * kGmax + 7]};
+    my[0] = a; my[1] = g0; my[2] = g1; my[3] = v4i{0, 0, 0, 0};
+    myacc[0] = 0; myacc[1] = 0; myacc[2] = 0; myacc[3] = 0;
   }
-  int32_t wcnt[kRowClassSlots];
-#pragma unroll
-  for (int sl = 0; sl < kRowClassSlots; ++sl) wcnt[sl] = 0;
+  const FKS_LDS int32_t* ncon = ntab + jv * kNodeConsts;
+  // node registers of this lane, fresh from LDS (constants from the node table)
+  auto load_nr = [&]() {
+    NodeRegs<1> r;
+    const v4i a = my[0], g0 = my[1], g1 = my[2];
+    r.cpu_left[0] = a.x; r.mem_left[0] = a.y; r.gpu_left[0] = a.z;
+    r.gml[0][0] = g0.x; r.gml[0][1] = g0.y; r.gml[0][2] = g0.z; r.gml[0][3] = g0.w;
+    r.gml[0][4] = g1.x; r.gml[0][5] = g1.y; r.gml[0][6] = g1.z; r.gml[0][7] = g1.w;
+    r.cpu_total[0] = ncon[0]; r.mem_total[0] = ncon[1]; r.ngpus[0] = ncon[2]; r.gmt1[0] = ncon[3];
+    return r;
+  };
+  auto store_nr = [&](const NodeRegs<1>& r) {
+    my[0] = v4i{r.cpu_left[0], r.mem_left[0], r.gpu_left[0], 0};
+    my[1] = v4i{r.gml[0][0], r.gml[0][1], r.gml[0][2], r.gml[0][3]};
+    my[2] = v4i{r.gml[0][4], r.gml[0][5], r.gml[0][6], r.gml[0][7]};
+  };
+  auto load_acc = [&]() {
+    RowAcc a;
+    a.lo = myacc[0]; a.hi = myacc[1];
+    a.count = (int32_t)(uint32_t)myacc[2]; a.inexact = (int32_t)(uint32_t)myacc[3];
+    return a;
+  };
+  auto store_acc = [&](const RowAcc& a) {
+    myacc[0] = a.lo; myacc[1] = a.hi;
+    myacc[2] = (uint64_t)(uint32_t)a.count; myacc[3] = (uint64_t)(uint32_t)a.inexact;
+  };
+  FKS_LDS int32_t* wcnt = sstate + jv * kDuoNodeInts + 12;   // waiting-class counters
   int32_t used_cpu = (int32_t)cold()->used_cpu0, used_mem = (int32_t)cold()->used_mem0;
   int32_t used_gcnt = (int32_t)cold()->used_gcnt0, used_gml = (int32_t)cold()->used_gmilli0;
-  RowAcc acc;
-  acc.init();
   int32_t processed = 0, next_fire = INT32_MAX;
   int ksnap = 0;
   double thr = cold()->thr_after_fire;
@@ -347,16 +387,17 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
     }
     if (!have) break;
     mark(0);
-    const uint64_t top = box->ev[k % kDuoRing];
+    // the event and its pod are wave-uniform: SGPRs, not VGPRs across the call
+    const uint64_t top = uniu64(box->ev[k % kDuoRing]);
     if (jv == 0) duo_st(&box->tail, k + 1);
     const int rank = (int)((top >> lb) & ((1ull << rb) - 1));
-    typedef int v4i __attribute__((ext_vector_type(4)));
     const v4i precv = *reinterpret_cast<const FKS_GLOBAL v4i*>(global_ptr(&W.pod[rank]));
     const int kind = (int)(top & 3);
     const int64_t t = (int64_t)(top >> tshift);
     PodView pod;
-    pod.cpu = precv.x; pod.mem = precv.y; pod.dur = precv.z;
-    pod.gmilli = precv.w & 0xFFFF; pod.ngpu = (precv.w >> 16) & 0xFF; pod.cls = (precv.w >> 24) & 0xFF;
+    const int pw = uni(precv.w);
+    pod.cpu = uni(precv.x); pod.mem = uni(precv.y); pod.dur = uni(precv.z);
+    pod.gmilli = pw & 0xFFFF; pod.ngpu = (pw >> 16) & 0xFF; pod.cls = (pw >> 24) & 0xFF;
     pod.ctime = t; pod.rank = rank;
     if constexpr (PROF) __builtin_amdgcn_s_waitcnt(0);
     mark(1);
@@ -365,28 +406,25 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
       const int node = (int)((top >> 2) & ((1u << nb) - 1));
       const int mask = (int)((top >> (2 + nb)) & 0xFF);
       if (jv == node) {
+        NodeRegs<1> nr = load_nr();
         nr.cpu_left[0] += pod.cpu;
         nr.mem_left[0] += pod.mem;
         nr.gpu_left[0] += pod.ngpu;
 #pragma unroll
         for (int g = 0; g < kGmax; ++g)
           if ((mask >> g) & 1) nr.gml[0][g] += pod.gmilli;
+        store_nr(nr);
       }
       used_cpu -= pod.cpu; used_mem -= pod.mem; used_gcnt -= pod.ngpu;
       used_gml -= pod.gmilli * __popc(mask);
       if (trace_hash) hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 1, (uint64_t)t);
       mark(4);
     } else {
-      {
-        const FKS_LDS int32_t* e = ntab + jv * kNodeConsts;
-        nr.cpu_total[0] = e[0];
-        nr.mem_total[0] = e[1];
-        nr.ngpus[0] = e[2];
-        nr.gmt1[0] = e[3];
-      }
       int lexc = EXC_NONE;
       int64_t s = 0;
-      if (node_valid && (!feas_pro || feasible<1>(0, nr, pod))) {
+      const NodeRegs<1> na = load_nr();   // call arguments; dead after the call
+      if (node_valid && (!feas_pro || feasible<1>(0, na, pod))) {
+        const NodeRegs<1>& nr = na;
         const int32_t* gl = nr.gml[0];
         int32_t gt[kGmax];
 #pragma unroll
@@ -397,6 +435,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
                  pod.gmilli | (pod.ngpu << 16), pod.ctime, pod.dur, kcp);
         if (s < 0) { lexc = (int)(-s); s = 0; }
       }
+      NodeRegs<1> nr = load_nr();         // re-read after the call (nothing kept across it)
       const uint32_t bad = row_ballot(lexc != EXC_NONE, 0);
       if (bad) {
         exc = row_read(lexc, 0, __ffs(bad) - 1);
@@ -408,17 +447,15 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
       mark(2);
       if (best_node < 0) {
         // failed placement: S keeps the metrics, H computes the repush
-        if (kind == kFresh && pod.ngpu > 0) {
-#pragma unroll
-          for (int sl = 0; sl < kRowClassSlots; ++sl)
-            if (sl == (pod.cls >> 4) && jv == (pod.cls & 15)) wcnt[sl] += 1;
-        }
+        if (kind == kFresh && pod.ngpu > 0 && jv == (pod.cls & 15)) wcnt[pod.cls >> 4] += 1;
         reply(DUO_FAIL, 0, k);   // H's first-deletion scan overlaps the fragmentation sum
         double frag = 0.0;
         int mcls = -1;
+        const v4i wc = *reinterpret_cast<FKS_LDS v4i*>(wcnt);
 #pragma unroll
         for (int sl = 0; sl < kRowClassSlots; ++sl) {
-          const uint32_t b = row_ballot(wcnt[sl] > 0, 0);
+          const int32_t w = sl == 0 ? wc.x : sl == 1 ? wc.y : sl == 2 ? wc.z : wc.w;
+          const uint32_t b = row_ballot(w > 0, 0);
           if (mcls < 0 && b) mcls = sl * kRow + __ffs(b) - 1;
         }
         if (mcls >= 0) {
@@ -433,7 +470,11 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
           const int64_t tg = cold()->tot_gmilli;
           frag = tg > 0 ? (double)stranded / (double)tg : 0.0;
         }
-        acc.add(4, frag, jv);
+        if (jv == 4) {
+          RowAcc acc = load_acc();
+          acc.add(4, frag, jv);
+          store_acc(acc);
+        }
         if (trace_hash) hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2) | 2, (uint64_t)t);
       } else {
         int gmask = 0, ok = 1;
@@ -457,14 +498,11 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
 #pragma unroll
           for (int g = 0; g < kGmax; ++g)
             if ((gmask >> g) & 1) nr.gml[0][g] -= pod.gmilli;
+          store_nr(nr);
         }
         used_cpu += pod.cpu; used_mem += pod.mem; used_gcnt += pod.ngpu;
         used_gml += pod.gmilli * __popc(gmask);
-        if (kind == kRetry && pod.ngpu > 0) {
-#pragma unroll
-          for (int sl = 0; sl < kRowClassSlots; ++sl)
-            if (sl == (pod.cls >> 4) && jv == (pod.cls & 15)) wcnt[sl] -= 1;
-        }
+        if (kind == kRetry && pod.ngpu > 0 && jv == (pod.cls & 15)) wcnt[pod.cls >> 4] -= 1;
         if (trace_hash)
           hsh = mix_event(hsh, ((uint64_t)(uint32_t)rank << 2), ((uint64_t)t << 8) ^ (uint64_t)best_node);
       }
@@ -478,7 +516,11 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
       const double r1 = Ws->tot_mem > 0 ? (double)used_mem / (double)Ws->tot_mem : 0.0;
       const double r2 = Ws->tot_gcnt > 0 ? (double)used_gcnt / (double)Ws->tot_gcnt : 0.0;
       const double r3 = Ws->tot_gmilli > 0 ? (double)used_gml / (double)Ws->tot_gmilli : 0.0;
-      acc.add(0, r0, jv); acc.add(1, r1, jv); acc.add(2, r2, jv); acc.add(3, r3, jv);
+      if (jv < 4) {
+        RowAcc acc = load_acc();
+        acc.add(0, r0, jv); acc.add(1, r1, jv); acc.add(2, r2, jv); acc.add(3, r3, jv);
+        store_acc(acc);
+      }
       ++ksnap;
       if (ksnap < Ws->n_fire) {
         next_fire = (int32_t)*global_ptr(&Ws->snap_fire[ksnap]);
@@ -508,6 +550,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
   const int n_repush = box->n_repush, n_dropped = box->n_dropped;
 
   // ---------------- result (replay_rows' write-back, fused evaluator)
+  const RowAcc acc = load_acc();
   const int64_t n_snap = row_read(acc.count, 0, 0);
   const int64_t n_frag = row_read(acc.count, 0, 4);
   const int inexact = row_ballot(jv < 5 && acc.inexact != 0, 0) != 0;

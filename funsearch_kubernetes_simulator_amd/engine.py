@@ -278,14 +278,14 @@ class Evaluator:
         return out
 
     def _evaluate_compiled(self, codes: Sequence[str], compiled: List[Optional[CompiledPolicy]],
-                           native: bool, slot: int = 0) -> List[EvalResult]:
+                           native: bool, slot: int = 0, host_only: bool = False) -> List[EvalResult]:
         n = len(codes)
         out: List[Optional[EvalResult]] = [None] * n
         # 1) device: native code, then the bytecode VM
         pending = [i for i, p in enumerate(compiled) if p is not None]
-        if self.device is not None:
-            dev_idx = [i for i in pending if compiled[i].device_ok
-                       and (self.device.math_exact or not compiled[i].uses_libm)]
+        if self.device is not None and not host_only:
+            exact = getattr(self.device, "math_exact", True)
+            dev_idx = [i for i in pending if compiled[i].device_ok and (exact or not compiled[i].uses_libm)]
             if dev_idx and native:
                 self._absorb_native(dev_idx, compiled, out, slot)
             dev_idx = [i for i in dev_idx if out[i] is None]
@@ -313,7 +313,11 @@ class Evaluator:
             if self._object_engine_ok():
                 budget_s = float(self.options.get("object_timeout_s", 600.0))
                 jobs = [(codes[i], self.workload, budget_s) for i in rest]
-                if len(rest) > 1 and self.object_workers > 1:
+                if host_only:
+                    # a worker thread (async fallback): the wall-clock budget needs a
+                    # process main thread, so the replays run in the spawned object pool
+                    results = list(self._object_pool().map(_object_worker, jobs))
+                elif len(rest) > 1 and self.object_workers > 1:
                     with ProcessPoolExecutor(max_workers=min(self.object_workers, len(rest))) as ex:
                         results = list(ex.map(_object_worker, jobs))
                 else:
@@ -385,7 +389,12 @@ class Evaluator:
             return self.device.ready(pend) if self.device is not None else True
         return not pend.native_idx or self.device.ready(pend.slot)
 
-    def collect(self, pend: "PendingPrograms") -> List[EvalResult]:
+    def collect(self, pend: "PendingPrograms", defer_fallback: bool = False) -> List[Optional[EvalResult]]:
+        """Results of a submitted batch.  Programs the device did not score
+        (declined, deferred) run on the host engines here -- or, with
+        `defer_fallback`, are left as None and listed in ``pend.fallback_idx``
+        for `fallback_async` (the steady-state dispatcher must not block on a
+        CPython replay)."""
         n = len(pend.codes)
         out: List[Optional[EvalResult]] = [None] * n
         if pend.native_idx:
@@ -397,6 +406,14 @@ class Evaluator:
                 out[i] = _row_to_result(row, "hip-native")
                 self.stats["device_native"] += 1
         rest = [i for i in range(n) if out[i] is None]
+        if rest and defer_fallback:
+            pend.fallback_idx = rest
+            if self.fault_rate > 0:
+                for i in range(n):
+                    if out[i] is not None and self._fault_rng.random() < self.fault_rate:
+                        out[i] = EvalResult(0.0, int(Exc.VALUE), "fault-injection")
+                        self.stats["faults"] = self.stats.get("faults", 0) + 1
+            return out
         if rest:
             sub = self._evaluate_compiled([pend.codes[i] for i in rest], [pend.compiled[i] for i in rest],
                                           native=False, slot=pend.slot)
@@ -408,6 +425,36 @@ class Evaluator:
                     out[i] = EvalResult(0.0, int(Exc.VALUE), "fault-injection")
                     self.stats["faults"] = self.stats.get("faults", 0) + 1
         return out  # type: ignore[return-value]
+
+    def fallback_async(self, pend: "PendingPrograms"):
+        """Score ``pend.fallback_idx`` on the host engines (CPU VM, then
+        CPython) in a worker thread; the future yields (indices, results)."""
+        idx = list(pend.fallback_idx)
+        codes = [pend.codes[i] for i in idx]
+        compiled = [pend.compiled[i] for i in idx]
+        with self._compile_lock:
+            if getattr(self, "_fallback_pool", None) is None:
+                from concurrent.futures import ThreadPoolExecutor
+                self._fallback_pool = ThreadPoolExecutor(max_workers=2, thread_name_prefix="fks-fallback")
+
+        def job():
+            res = self._evaluate_compiled(codes, compiled, native=False, host_only=True)
+            if self.fault_rate > 0:
+                for k in range(len(res)):
+                    if self._fault_rng.random() < self.fault_rate:
+                        res[k] = EvalResult(0.0, int(Exc.VALUE), "fault-injection")
+            return idx, res
+        return self._fallback_pool.submit(job)
+
+    def _object_pool(self):
+        """Persistent spawn pool for CPython replays started from worker threads."""
+        with self._compile_lock:
+            if getattr(self, "_obj_pool", None) is None:
+                import multiprocessing
+                self._obj_pool = ProcessPoolExecutor(max_workers=max(1, self.object_workers),
+                                                     mp_context=multiprocessing.get_context("spawn"))
+                atexit.register(self._obj_pool.shutdown, wait=False, cancel_futures=True)
+        return self._obj_pool
 
     def _absorb_native(self, idx, compiled, out, slot: int) -> None:
         batch = self.device.submit_native(slot, [compiled[i] for i in idx])
@@ -442,6 +489,7 @@ class PendingPrograms:
     new_shapes: int = 0
     t_launch: float = 0.0
     t_done: float = 0.0
+    fallback_idx: List[int] = field(default_factory=list)
 
 
 _default: Dict[str, Evaluator] = {}

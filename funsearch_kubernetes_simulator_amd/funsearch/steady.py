@@ -106,6 +106,7 @@ class SteadyStats:
     produced: int = 0
     rejected: int = 0
     migrations: int = 0
+    fallback: int = 0                # programs scored by the host engines (async)
     producer_cpu_s: float = 0.0
     inflight_sum: float = 0.0        # programs in flight x seconds
     inflight_n: float = 0.0          # seconds observed
@@ -132,6 +133,11 @@ class SteadyStateSearch:
             # the two-wave kernel sizes its LDS heap top so that every slot's batch
             # stays resident at once (csrc/hip/engine_host.hip.h duo_top)
             dev.set_options(native_inflight=self.batch * self.slots)
+            if not tierup:
+                # shapes the baseline generator declines (~0.1%) go to the host
+                # engines asynchronously instead of a ~0.2 s LLVM compile on the
+                # dispatcher thread
+                dev.native_compiler.tier = "baseline"
         from ..ops.cpu_engine import default_threads
         local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
         self.producers = int(producers or max(1, min(16, default_threads() // local - 1)))
@@ -205,6 +211,7 @@ class SteadyStateSearch:
             max_workers=self.producers, mp_context=ctx_mp, initializer=_producer_init,
             initargs=(llm_cfg, timeout_s, 1000 * ctx.rank + 1))
         inflight_tasks: List[concurrent.futures.Future] = []
+        fallbacks: list = []             # (batch items, future of the host-engine fallback)
         ready: List[tuple] = []          # produced children waiting for a batch
         batches: List[Optional[_Batch]] = [None] * self.slots
         # children requested per island: production stops at the island's target
@@ -279,13 +286,33 @@ class SteadyStateSearch:
                     if busy_since is None:
                         busy_since = time.time()
                     progressed = True
-                # 4) finished batches -> merge
+                # 4a) host-engine fallbacks that finished -> merge
+                still_fb = []
+                for items, fut in fallbacks:
+                    if not fut.done():
+                        still_fb.append((items, fut))
+                        continue
+                    idx, res = fut.result()
+                    t_m = time.perf_counter()
+                    for i, r in zip(idx, res):
+                        isl, code, _ = items[i]
+                        self._merge_one(islands[isl], code, r.score)
+                        merged[isl] += 1
+                    self.stats.fallback += len(idx)
+                    self.phase["merge"] += time.perf_counter() - t_m
+                    progressed = True
+                fallbacks = still_fb
+                # 4b) finished batches -> merge (programs the device did not score go
+                # to the host engines in a worker thread: the dispatcher never runs a
+                # CPU-VM or CPython replay itself)
                 for si in range(self.slots):
                     b = batches[si]
                     if b is None or not ev.ready(b.pend):
                         continue
                     t_ph = time.perf_counter()
-                    results = ev.collect(b.pend)
+                    results = ev.collect(b.pend, defer_fallback=True)
+                    if b.pend.fallback_idx:
+                        fallbacks.append((b.items, ev.fallback_async(b.pend)))
                     t_m = time.perf_counter()
                     self.phase["collect"] += t_m - t_ph
                     t_done = time.time()
@@ -294,6 +321,8 @@ class SteadyStateSearch:
                         self.stats.busy_s += t_done - busy_since
                         busy_since = None
                     for (isl, code, _), res in zip(b.items, results):
+                        if res is None:          # merged when its fallback completes
+                            continue
                         self._merge_one(islands[isl], code, res.score)
                         merged[isl] += 1
                         if res.engine == "hip-native":
@@ -339,7 +368,7 @@ class SteadyStateSearch:
                     self._status(now, t_start, busy_since, batches, ready, inflight_tasks, merged, global_best)
                 # 7) done?  (every child merged, or stopping; then every agreed gather finished)
                 all_launched = all(requested[i] >= target_children[i] for i in range(k))
-                idle = not inflight_tasks and all(b is None for b in batches)
+                idle = not inflight_tasks and all(b is None for b in batches) and not fallbacks
                 if idle and (stop or (all_launched and not ready)):
                     ready.clear()
                     due = chan.every and chan.next is not None and (
@@ -379,7 +408,7 @@ class SteadyStateSearch:
                    evaluations=st.evaluations, evals_per_s=round(st.evaluations / wall, 2),
                    device_busy=round(busy / wall, 4),
                    new_shape_fraction=round(st.new_shapes / max(1, st.evaluations), 4),
-                   native_fraction=round(st.native / max(1, st.evaluations), 4),
+                   native_fraction=round(st.native / max(1, st.evaluations), 4), host_fallback=st.fallback,
                    inflight=inflight, inflight_mean=round(st.inflight_sum / max(1e-9, st.inflight_n), 1),
                    resident_capacity=capacity,
                    occupancy=round(inflight / capacity, 4) if capacity else None,
