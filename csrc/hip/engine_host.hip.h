@@ -205,6 +205,20 @@ class DeviceEngine {
       W_.heap0p = dev_upload<uint64_t>(shifted, st, owned_);
       HIP_OK(hipStreamSynchronize(st));   // `shifted` dies with this scope
     }
+    {
+      // {cpu_total, mem_total, ngpus, GPU-milli total} per node slot (NodeRegs::c4, 256-node kernels)
+      py::array_t<int32_t, py::array::c_style | py::array::forcecast> ct(arr("cpu_total")), mt(arr("mem_total")),
+          ng(arr("ngpus")), gt(arr("gml_total"));
+      const py::ssize_t np = ct.size();
+      std::vector<int32_t> c4((size_t)np * 4);
+      for (py::ssize_t i = 0; i < np; ++i) {
+        c4[4 * i] = ct.data()[i];
+        c4[4 * i + 1] = mt.data()[i];
+        c4[4 * i + 2] = ng.data()[i];
+        c4[4 * i + 3] = gt.data()[i * kGmax];
+      }
+      W_.node_c4 = reinterpret_cast<const int4*>(dev_upload_vec(c4, owned_));
+    }
     W_.class_value = dev_upload<int32_t>(arr("class_value"), st, owned_);
     W_.snap_fire = dev_upload<int64_t>(arr("snap_fire"), st, owned_);
     W_.n_fire = (int32_t)arr("snap_fire").size();
@@ -225,6 +239,7 @@ class DeviceEngine {
     arch_ = prop.gcnArchName;
     heap_bytes_ = (size_t)lds_heap_entries(W_.n_pods) * sizeof(uint64_t);
     delmap_bytes_ = (size_t)lds_delmap_words(W_.n_pods) * 4;
+    W_.delmap_slots = lds_delmap_words(W_.n_pods) * 32;   // full bitmap unless a launch narrows it
     lds_heap_ok_ = heap_bytes_ + delmap_bytes_ <= kMaxLds;
     rows_ok_ = npass_ == 1 && W_.n_nodes <= kRow && W_.n_classes <= kRow * kRowClassSlots &&
                W_.n_pods <= kRowMaxHeap && W_.tot_cpu < (int64_t(1) << 31) && W_.tot_mem < (int64_t(1) << 31) &&
@@ -248,6 +263,7 @@ class DeviceEngine {
     if (o.contains("snapshot_interval")) W_.snapshot_interval = o["snapshot_interval"].cast<double>();
     if (o.contains("budget")) budget_ = o["budget"].cast<int64_t>();
     if (o.contains("heap_top")) heap_top_opt_ = o["heap_top"].cast<int>();   // -1: auto
+    if (o.contains("partial_delmap")) partial_delmap_off_ = !o["partial_delmap"].cast<bool>();   // A/B
     if (o.contains("trace_hash")) W_.trace_hash = o["trace_hash"].cast<bool>() ? 1 : 0;
     if (o.contains("check_invariants")) {
       const int64_t k = o["check_invariants"].cast<int64_t>();
@@ -731,10 +747,22 @@ class DeviceEngine {
     return P > 2 * num_cus_;
   }
 
+  // Heap slots the wave kernels' LDS deletion bitmap covers.  256-node
+  // clusters (NPASS 4) keep only the first kPartialDelmap slots' bits with an
+  // HBM heap: the first DELETION in heap-array order sits near the root
+  // (deletion times are close, creation times spread over the trace), and
+  // WaveHeapT::first_deletion reads the keys beyond; the full bitmap of a
+  // 65,536-pod trace (8 KiB) would take most of a 16-policies-per-CU LDS share.
+  static constexpr int kPartialDelmap = 4096;
+  int delmap_slots(bool g) const {
+    const int full = lds_delmap_words(W_.n_pods) * 32;
+    return (g && npass_ >= 4 && !partial_delmap_off_) ? std::min(full, kPartialDelmap) : full;
+  }
   size_t lds_bytes(bool g, int top, int nregs) const {
     const size_t vregs = (size_t)nregs * 64 * 8;
     const size_t inv = (size_t)(W_.inv_words + kWeightWords) * 8;
-    return inv + (g ? delmap_bytes_ + (size_t)top * 8 + vregs : heap_bytes_ + delmap_bytes_ + vregs);
+    const size_t dm = (size_t)delmap_slots(g) / 8;
+    return inv + (g ? dm + (size_t)top * 8 + vregs : heap_bytes_ + delmap_bytes_ + vregs);
   }
 
   // HBM-heap launches keep the top 2^L - 1 heap slots in LDS, as many levels as
@@ -745,7 +773,7 @@ class DeviceEngine {
     // (NPASS 4: 3 waves/SIMD, FKS_NP4_WAVES; NPASS 2: 3)
     const size_t per_cu = vm ? kVmPoliciesPerCu : (npass_ >= 4 ? 4 * FKS_NP4_WAVES : npass_ == 2 ? 12 : kPoliciesPerCu);
     const size_t budget = kMaxLds / per_cu;
-    const size_t fixed = delmap_bytes_ + (size_t)nregs * 64 * 8 + (size_t)(W_.inv_words + kWeightWords) * 8;
+    const size_t fixed = (size_t)delmap_slots(true) / 8 + (size_t)nregs * 64 * 8 + (size_t)(W_.inv_words + kWeightWords) * 8;
     int T = 0;
     while (T < entries && fixed + (size_t)(2 * T + 1) * 8 <= budget) T = 2 * T + 1;
     return std::min(T, entries);
@@ -754,6 +782,7 @@ class DeviceEngine {
   DevWorkload launch_workload(bool g, int nregs, bool vm) const {
     DevWorkload Wl = W_;
     Wl.heap_top = g ? heap_top_for(nregs, vm) : 0;
+    Wl.delmap_slots = delmap_slots(g);
     return Wl;
   }
 
@@ -1032,6 +1061,7 @@ class DeviceEngine {
   std::string heap_mode_ = "auto";
   int64_t budget_ = 0;
   int heap_top_opt_ = -1;
+  bool partial_delmap_off_ = false;
   std::vector<void*> owned_;
 };
 

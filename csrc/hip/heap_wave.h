@@ -40,7 +40,8 @@ struct WaveHeapT {
   FKS_GLOBAL uint64_t* h;   // keys (slots >= T), the policy's HBM slice
   FKS_LDS uint64_t* top;    // LDS copy of slots [0, T)
   int T;
-  FKS_LDS uint32_t* delmap; // bit p set <=> slot p holds a deletion
+  FKS_LDS uint32_t* delmap; // bit p set <=> slot p (< M) holds a deletion
+  int M;              // slots the bitmap covers (a multiple of 32; >= n: all of them)
   int lb;             // low (payload) bits below the (time, rank) compare key
   int lane;           // this lane's id, refreshed (opaquely) per event by the caller
   uint64_t* gtop;     // FLAT: generic addresses of top / h (bind())
@@ -72,6 +73,7 @@ struct WaveHeapT {
   }
 
   __device__ __forceinline__ void mark(int pos, uint64_t v) const {
+    if (pos >= M) return;   // beyond the bitmap: first_deletion reads the keys themselves
     const uint32_t bit = 1u << (pos & 31);
     if ((v & 3) == kDelKind) __hip_atomic_fetch_or(&delmap[pos >> 5], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     else __hip_atomic_fetch_and(&delmap[pos >> 5], ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -173,19 +175,27 @@ struct WaveHeapT {
     if (lane == 0) { st(aJ, item); mark(aJ, item); }
   }
 
-  // index of the first DELETION in h[0, n), or -1
+  // index of the first DELETION in h[0, n), or -1: the bitmap for slots below
+  // M, then (rarely: a deletion usually sits near the root, its time being
+  // close) the keys themselves, 64 slots per step
   __device__ int first_deletion(int n) const {
-    const int words = (n + 31) >> 5;
+    const int nb = n < M ? n : M;
+    const int words = (nb + 31) >> 5;
     for (int base = 0; base < words; base += kWave) {
       const int wi = base + lane;
       uint32_t w = wi < words ? delmap[wi] : 0u;
-      if (wi == words - 1 && (n & 31)) w &= (1u << (n & 31)) - 1;   // stale bits past the end
+      if (wi == words - 1 && (nb & 31)) w &= (1u << (nb & 31)) - 1;   // stale bits past the end
       const uint64_t b = ballot(w != 0);
       if (b) {
         const int fl = first_lane(b);
         const uint32_t fw = (uint32_t)readlane((int)w, fl);
         return ((base + fl) << 5) + (__ffs(fw) - 1);
       }
+    }
+    for (int base = nb; base < n; base += kWave) {
+      const int i = base + lane;
+      const uint64_t b = ballot(i < n && (ld(i) & 3) == (uint64_t)kDelKind);
+      if (b) return base + first_lane(b);
     }
     return -1;
   }

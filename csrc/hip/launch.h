@@ -14,7 +14,7 @@
 // waves per SIMD of the 256-node (NPASS 4) wave kernels; the host sizes their
 // LDS share to match (build knob for A/B runs)
 #ifndef FKS_NP4_WAVES
-#define FKS_NP4_WAVES 3     // one GPU-milli total per node keeps them <= 168 VGPRs
+#define FKS_NP4_WAVES 4     // packed GPU milli + node constants on demand: <= 128 VGPRs
 #endif
 
 namespace fksk {

@@ -102,6 +102,7 @@ __global__ __launch_bounds__(64) void k_test_heap(const uint64_t* init, int n0, 
   hp.top = lds_ptr(lds);
   hp.T = 1 << 30;   // all slots in LDS
   hp.delmap = reinterpret_cast<FKS_LDS uint32_t*>(lds_ptr(lds) + 4096);
+  hp.M = 1 << 30;   // the bitmap covers every slot
   hp.lb = lb;
   hp.lane = lane;
   for (int i = lane; i < n0; i += 64) lds[i] = init[i];

@@ -62,6 +62,8 @@ struct DevWorkload {
   int32_t inv_words;          // LDS u64 words reserved for the invariant check (0: off)
   int32_t trace_hash;         // 1: fold every event into DevResult.hash (cross-engine trace check)
   const uint64_t* heap0p;     // initial heap shifted by one slot (row kernel layout: address = slot + 1)
+  const int4* node_c4;        // [64*NPASS] {cpu_total, mem_total, ngpus, gml_total of GPU 0} per node slot
+  int32_t delmap_slots;       // wave kernels: heap slots the LDS deletion bitmap covers (WaveHeapT::M)
   // Row-kernel composite scorer (scorers.hip.h composite_row): host-verified
   // reciprocals RN(1/d) of the node-constant divisors max(cpu_total, 1),
   // max(mem_total, 1), max(ngpus, 1) ([node][3]) and of 1000 (z1000), valid
@@ -110,12 +112,47 @@ __host__ __device__ inline int lds_vreg_offset(int n_pods) {
 // instead of kGmax -- 28 VGPRs on 256-node clusters, the difference between 2
 // and 3 waves per SIMD there.  gt(ps, j) is the per-GPU view (0 past ngpus,
 // like the zero padding of the host table).
+// On 256-node clusters (NPASS = 4) the per-GPU milli left of two GPUs share
+// one register (16-bit halves; the host refuses GPU milli totals >= 2^16
+// there): 16 VGPRs instead of 32 for the four node slots.  Updates are plain
+// 32-bit adds of the shifted delta -- a GPU never holds less than it gives
+// back or more than its total, so a half never borrows from or carries into
+// the other.
 template <int NPASS>
 struct NodeRegs {
+  static constexpr bool kPack = NPASS >= 4;
+  static constexpr int kGW = kPack ? kGmax / 2 : kGmax;
   int32_t cpu_left[NPASS], mem_left[NPASS], gpu_left[NPASS];
-  int32_t cpu_total[NPASS], mem_total[NPASS], ngpus[NPASS];
-  int32_t gml[NPASS][kGmax], gmt1[NPASS];
-  __device__ __forceinline__ int32_t gt(int ps, int j) const { return j < ngpus[ps] ? gmt1[ps] : 0; }
+  int32_t gw[NPASS][kGW];
+  // node constants: registers, or (kPack) re-read from the workload's int4
+  // table {cpu_total, mem_total, ngpus, gmt1} where used -- 16 VGPRs less
+  // through the pop / push phases, which need none of them
+  static constexpr int kCR = kPack ? 1 : NPASS;
+  int32_t cpu_total[kCR], mem_total[kCR], ngpus[kCR], gmt1[kCR];
+  const int4* cst;   // kPack: DevWorkload::node_c4, [slot * 64 + lane]
+  __device__ __forceinline__ int4 c4(int ps) const { return cst[ps * kWave + lane_id()]; }
+  __device__ __forceinline__ int32_t ctot(int ps) const { if constexpr (kPack) return c4(ps).x; else return cpu_total[ps]; }
+  __device__ __forceinline__ int32_t mtot(int ps) const { if constexpr (kPack) return c4(ps).y; else return mem_total[ps]; }
+  __device__ __forceinline__ int32_t ngp(int ps) const { if constexpr (kPack) return c4(ps).z; else return ngpus[ps]; }
+  __device__ __forceinline__ int32_t gmt(int ps) const { if constexpr (kPack) return c4(ps).w; else return gmt1[ps]; }
+  __device__ __forceinline__ int32_t gt(int ps, int j) const { return j < ngp(ps) ? gmt(ps) : 0; }
+  // GPU j's milli left on node slot ps
+  __device__ __forceinline__ int32_t g(int ps, int j) const {
+    if constexpr (kPack) return (int32_t)(((uint32_t)gw[ps][j >> 1] >> ((j & 1) * 16)) & 0xFFFFu);
+    else return gw[ps][j];
+  }
+  __device__ __forceinline__ void g_add(int ps, int j, int32_t d) {
+    if constexpr (kPack) gw[ps][j >> 1] += (int32_t)((uint32_t)d << ((j & 1) * 16));
+    else gw[ps][j] += d;
+  }
+  __device__ __forceinline__ void g_init(int ps, int j, int32_t v) {
+    if constexpr (kPack) {
+      if (j & 1) gw[ps][j >> 1] |= (int32_t)((uint32_t)v << 16);
+      else gw[ps][j >> 1] = v;
+    } else {
+      gw[ps][j] = v;
+    }
+  }
 };
 
 struct PodView {
@@ -161,17 +198,17 @@ enum Phase { PH_POP = 0, PH_DELETE = 1, PH_SCORE = 2, PH_FAIL = 3, PH_COMMIT = 4
 template <int NPASS>
 __device__ __forceinline__ int pick_gpus(const NodeRegs<NPASS>& nr, int ps, int gm, int need, bool first_fit,
                                          int& ok) {
-  const int ng = nr.ngpus[ps];
+  const int ng = nr.ngp(ps);
   int cnt = 0;
 #pragma unroll
-  for (int j = 0; j < kGmax; ++j) cnt += (j < ng && nr.gml[ps][j] >= gm);
+  for (int j = 0; j < kGmax; ++j) cnt += (j < ng && nr.g(ps, j) >= gm);
   ok = cnt >= need;
   int mask = 0;
   if (need == 1 && !first_fit) {
     int best = -1, bv = 0;
 #pragma unroll
     for (int j = 0; j < kGmax; ++j) {
-      const int l = nr.gml[ps][j];
+      const int l = nr.g(ps, j);
       if (j < ng && l >= gm && (best < 0 || l < bv)) { best = j; bv = l; }
     }
     mask = best >= 0 ? (1 << best) : 0;
@@ -179,13 +216,13 @@ __device__ __forceinline__ int pick_gpus(const NodeRegs<NPASS>& nr, int ps, int 
   }
 #pragma unroll
   for (int j = 0; j < kGmax; ++j) {
-    const bool vj = j < ng && nr.gml[ps][j] >= gm;
+    const bool vj = j < ng && nr.g(ps, j) >= gm;
     int r = 0;
 #pragma unroll
     for (int i = 0; i < kGmax; ++i) {
-      const bool vi = i < ng && nr.gml[ps][i] >= gm;
+      const bool vi = i < ng && nr.g(ps, i) >= gm;
       r += first_fit ? (vi && i < j)
-                     : (vi && (nr.gml[ps][i] < nr.gml[ps][j] || (nr.gml[ps][i] == nr.gml[ps][j] && i < j)));
+                     : (vi && (nr.g(ps, i) < nr.g(ps, j) || (nr.g(ps, i) == nr.g(ps, j) && i < j)));
     }
     if (vj && r < need) mask |= 1 << j;
   }
@@ -230,13 +267,13 @@ __device__ bool invariants_hold(const DevWorkload& W, const Heap& heap, int n, c
     if (node >= W.n_nodes) continue;
     const FKS_LDS int32_t* row = inv + node * kInvCols;
     const int32_t cl = nr.cpu_left[ps], ml = nr.mem_left[ps], gl = nr.gpu_left[ps];
-    bad |= cl < 0 || cl > nr.cpu_total[ps] || row[0] + cl != nr.cpu_total[ps];
-    bad |= ml < 0 || ml > nr.mem_total[ps] || row[1] + ml != nr.mem_total[ps];
-    bad |= gl < 0 || gl > nr.ngpus[ps] || row[2] + gl != nr.ngpus[ps];
+    bad |= cl < 0 || cl > nr.ctot(ps) || row[0] + cl != nr.ctot(ps);
+    bad |= ml < 0 || ml > nr.mtot(ps) || row[1] + ml != nr.mtot(ps);
+    bad |= gl < 0 || gl > nr.ngp(ps) || row[2] + gl != nr.ngp(ps);
 #pragma unroll
     for (int j = 0; j < kGmax; ++j)
-      if (j < nr.ngpus[ps]) {
-        const int32_t l = nr.gml[ps][j], t = nr.gt(ps, j);
+      if (j < nr.ngp(ps)) {
+        const int32_t l = nr.g(ps, j), t = nr.gt(ps, j);
         bad |= l < 0 || l > t || row[3 + j] + l != t;
       }
   }
@@ -272,23 +309,27 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
   heap.bind();
   heap.T = T;
   heap.delmap = delmap;
+  heap.M = W.delmap_slots;
   heap.lb = lb;
   for (int i = lane; i < N; i += kWave) heap.st(i, W.heap0[i]);
-  for (int i = lane; i < lds_delmap_words(N); i += kWave) heap.delmap[i] = 0u;
+  for (int i = lane; i < (W.delmap_slots >> 5); i += kWave) heap.delmap[i] = 0u;
 
   NodeRegs<NPASS> nr;
+  nr.cst = W.node_c4;
 #pragma unroll
   for (int ps = 0; ps < NPASS; ++ps) {
     const int node = ps * kWave + lane;
     nr.cpu_left[ps] = W.cpu_left0[node];
     nr.mem_left[ps] = W.mem_left0[node];
     nr.gpu_left[ps] = W.gpu_left0[node];
-    nr.cpu_total[ps] = W.cpu_total[node];
-    nr.mem_total[ps] = W.mem_total[node];
-    nr.ngpus[ps] = W.ngpus[node];
+    if constexpr (!NodeRegs<NPASS>::kPack) {
+      nr.cpu_total[ps] = W.cpu_total[node];
+      nr.mem_total[ps] = W.mem_total[node];
+      nr.ngpus[ps] = W.ngpus[node];
+      nr.gmt1[ps] = W.gml_total[node * kGmax];
+    }
 #pragma unroll
-    for (int j = 0; j < kGmax; ++j) nr.gml[ps][j] = W.gml_left0[node * kGmax + j];
-    nr.gmt1[ps] = W.gml_total[node * kGmax];
+    for (int j = 0; j < kGmax; ++j) nr.g_init(ps, j, W.gml_left0[node * kGmax + j]);
   }
   // waiting histogram over gpu_milli classes: class k -> lane k%64, slot k/64
   constexpr int KP = 4;  // up to 256 classes
@@ -323,8 +364,15 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
       int ol = lane;
       asm volatile("" : "+v"(ol));
       heap.lane = ol;
+      if constexpr (!NodeRegs<NPASS>::kPack) {
 #pragma unroll
-      for (int ps = 0; ps < NPASS; ++ps) asm volatile("" : "+v"(nr.ngpus[ps]));
+        for (int ps = 0; ps < NPASS; ++ps) asm volatile("" : "+v"(nr.ngpus[ps]));
+      } else {
+        // re-derived per event (uniform, opaque): the constant loads are not hoisted out of the loop
+        const int4* c = reinterpret_cast<const int4*>(uniu64(reinterpret_cast<uint64_t>(nr.cst)));
+        asm volatile("" : "+s"(c));
+        nr.cst = c;
+      }
     }
     // ---------------- pop (pod record load issued first, consumed after the sift)
     const uint64_t top = uniu64(heap.ld_u(0));
@@ -355,7 +403,7 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
           nr.gpu_left[ps] += pod.ngpu;
 #pragma unroll
           for (int j = 0; j < kGmax; ++j)
-            if ((mask >> j) & 1) nr.gml[ps][j] += pod.gmilli;
+            if ((mask >> j) & 1) nr.g_add(ps, j, pod.gmilli);
         }
       }
       used_cpu -= pod.cpu; used_mem -= pod.mem; used_gcnt -= pod.ngpu;
@@ -424,8 +472,8 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
           for (int ps = 0; ps < NPASS; ++ps)
 #pragma unroll
             for (int j = 0; j < kGmax; ++j) {
-              const int l = nr.gml[ps][j];
-              if (j < nr.ngpus[ps] && 0 < l && l < m) stranded += l;
+              const int l = nr.g(ps, j);
+              if (j < nr.ngp(ps) && 0 < l && l < m) stranded += l;
             }
           stranded = wave_sum_i64(stranded);
           const int64_t tg = Wc->tot_gmilli;
@@ -481,7 +529,7 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
             nr.gpu_left[ps] -= pod.ngpu;
 #pragma unroll
             for (int j = 0; j < kGmax; ++j)
-              if ((gmask >> j) & 1) nr.gml[ps][j] -= pod.gmilli;
+              if ((gmask >> j) & 1) nr.g_add(ps, j, -pod.gmilli);
           }
         }
         used_cpu += pod.cpu; used_mem += pod.mem; used_gcnt += pod.ngpu;

@@ -325,15 +325,15 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
     NodeRegs<1> r;
     const v4i a = my[0], g0 = my[1], g1 = my[2];
     r.cpu_left[0] = a.x; r.mem_left[0] = a.y; r.gpu_left[0] = a.z;
-    r.gml[0][0] = g0.x; r.gml[0][1] = g0.y; r.gml[0][2] = g0.z; r.gml[0][3] = g0.w;
-    r.gml[0][4] = g1.x; r.gml[0][5] = g1.y; r.gml[0][6] = g1.z; r.gml[0][7] = g1.w;
+    r.gw[0][0] = g0.x; r.gw[0][1] = g0.y; r.gw[0][2] = g0.z; r.gw[0][3] = g0.w;
+    r.gw[0][4] = g1.x; r.gw[0][5] = g1.y; r.gw[0][6] = g1.z; r.gw[0][7] = g1.w;
     r.cpu_total[0] = ncon[0]; r.mem_total[0] = ncon[1]; r.ngpus[0] = ncon[2]; r.gmt1[0] = ncon[3];
     return r;
   };
   auto store_nr = [&](const NodeRegs<1>& r) {
     my[0] = v4i{r.cpu_left[0], r.mem_left[0], r.gpu_left[0], 0};
-    my[1] = v4i{r.gml[0][0], r.gml[0][1], r.gml[0][2], r.gml[0][3]};
-    my[2] = v4i{r.gml[0][4], r.gml[0][5], r.gml[0][6], r.gml[0][7]};
+    my[1] = v4i{r.gw[0][0], r.gw[0][1], r.gw[0][2], r.gw[0][3]};
+    my[2] = v4i{r.gw[0][4], r.gw[0][5], r.gw[0][6], r.gw[0][7]};
   };
   auto load_acc = [&]() {
     RowAcc a;
@@ -412,7 +412,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
         nr.gpu_left[0] += pod.ngpu;
 #pragma unroll
         for (int g = 0; g < kGmax; ++g)
-          if ((mask >> g) & 1) nr.gml[0][g] += pod.gmilli;
+          if ((mask >> g) & 1) nr.g_add(0, g, pod.gmilli);
         store_nr(nr);
       }
       used_cpu -= pod.cpu; used_mem -= pod.mem; used_gcnt -= pod.ngpu;
@@ -425,7 +425,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
       const NodeRegs<1> na = load_nr();   // call arguments; dead after the call
       if (node_valid && (!feas_pro || feasible<1>(0, na, pod))) {
         const NodeRegs<1>& nr = na;
-        const int32_t* gl = nr.gml[0];
+        const int32_t* gl = nr.gw[0];   // NPASS 1: unpacked
         int32_t gt[kGmax];
 #pragma unroll
         for (int g = 0; g < kGmax; ++g) gt[g] = nr.gt(0, g);
@@ -463,7 +463,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
           int64_t stranded = 0;
 #pragma unroll
           for (int g = 0; g < kGmax; ++g) {
-            const int l = nr.gml[0][g];
+            const int l = nr.g(0, g);
             if (g < nr.ngpus[0] && 0 < l && l < mv) stranded += l;
           }
           stranded = row_sum_i64(node_valid ? stranded : 0);
@@ -497,7 +497,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
           nr.gpu_left[0] -= pod.ngpu;
 #pragma unroll
           for (int g = 0; g < kGmax; ++g)
-            if ((gmask >> g) & 1) nr.gml[0][g] -= pod.gmilli;
+            if ((gmask >> g) & 1) nr.g_add(0, g, -pod.gmilli);
           store_nr(nr);
         }
         used_cpu += pod.cpu; used_mem += pod.mem; used_gcnt += pod.ngpu;

@@ -74,11 +74,13 @@ __device__ __forceinline__ Slot policy_slot(const DevWorkload& W, uint64_t* ghea
   s.inv = reinterpret_cast<FKS_LDS int32_t*>(lds0);
   s.w = reinterpret_cast<FKS_LDS double*>(lds0 + W.inv_words);
   if (GHEAP) {
+    // the deletion bitmap covers the first W.delmap_slots slots (a multiple of 64)
+    const int dw = W.delmap_slots >> 5;
     s.h = global_ptr(gheap + (size_t)p * lds_heap_entries(N));
     s.delmap = reinterpret_cast<FKS_LDS uint32_t*>(lds);
-    s.top = lds + lds_delmap_words(N) / 2;
+    s.top = lds + dw / 2;
     s.T = W.heap_top;
-    s.vregs = lds_raw + W.inv_words + kWeights + lds_delmap_words(N) / 2 + W.heap_top;
+    s.vregs = lds_raw + W.inv_words + kWeights + dw / 2 + W.heap_top;
   } else {
     s.h = global_ptr(gheap);   // never dereferenced: T covers the whole heap
     s.top = lds;
@@ -264,12 +266,14 @@ struct NativeScorerDev {
   template <int NPASS>
   __device__ int64_t score(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, int& exc) {
     const int node = ps * kWave + lane_id();
-    const int32_t* gl = nr.gml[ps];
-    int32_t gt[kGmax];
+    int32_t gl[kGmax], gt[kGmax];
 #pragma unroll
-    for (int g = 0; g < kGmax; ++g) gt[g] = nr.gt(ps, g);
-    const int64_t r = fn(nr.cpu_left[ps], nr.cpu_total[ps], nr.mem_left[ps], nr.mem_total[ps],
-                         pack_gpu_ng(nr.gpu_left[ps], nr.ngpus[ps]), gl[0], gl[1], gl[2], gl[3], gl[4], gl[5], gl[6], gl[7], gt[0], gt[1], gt[2], gt[3],
+    for (int g = 0; g < kGmax; ++g) {
+      gl[g] = nr.g(ps, g);
+      gt[g] = nr.gt(ps, g);
+    }
+    const int64_t r = fn(nr.cpu_left[ps], nr.ctot(ps), nr.mem_left[ps], nr.mtot(ps),
+                         pack_gpu_ng(nr.gpu_left[ps], nr.ngp(ps)), gl[0], gl[1], gl[2], gl[3], gl[4], gl[5], gl[6], gl[7], gt[0], gt[1], gt[2], gt[3],
                          gt[4], gt[5], gt[6], gt[7], gmem + (size_t)node * kGmax, pod.cpu, pod.mem,
                          pod.gmilli | (pod.ngpu << 16), pod.ctime, pod.dur, kc);
     if (r < 0) { exc = (int)(-r); return 0; }

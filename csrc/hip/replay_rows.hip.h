@@ -542,7 +542,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
     nr.gpu_left[0] = Wb->gpu_left0[jv];
 #pragma unroll
     for (int g = 0; g < kGmax; ++g) {
-      nr.gml[0][g] = Wb->gml_left0[jv * kGmax + g];
+      nr.g_init(0, g, Wb->gml_left0[jv * kGmax + g]);
     }
 #pragma unroll
     for (int k = 0; k < kRowClassSlots / 2; ++k) wcp[k] = 0u;
@@ -600,7 +600,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
           nr.gpu_left[0] += pod.ngpu;
 #pragma unroll
           for (int g = 0; g < kGmax; ++g)
-            if ((mask >> g) & 1) nr.gml[0][g] += pod.gmilli;
+            if ((mask >> g) & 1) nr.g_add(0, g, pod.gmilli);
         }
         if (cold()->trace_hash) rcs[0] = mix_event(rcs[0], ((uint64_t)(uint32_t)rank << 2) | 1, (uint64_t)t);
         prof.mark(PH_DELETE);
@@ -619,7 +619,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
           // the program holds the template's feasibility prologue itself; one
           // that opens with it is not called for nodes feasible() rejects
           if (node_valid && (!feas_pro || feasible<1>(0, nr, pod))) {
-            const int32_t* gl = nr.gml[0];
+            const int32_t* gl = nr.gw[0];   // NPASS 1: unpacked
             int32_t gt[kGmax];
 #pragma unroll
             for (int g = 0; g < kGmax; ++g) gt[g] = nr.gt(0, g);
@@ -680,7 +680,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
             int32_t stranded = 0;   // the cluster's GPU milli total < 2^31 (host-checked)
 #pragma unroll
             for (int g = 0; g < kGmax; ++g) {
-              const int l = nr.gml[0][g];
+              const int l = nr.g(0, g);
               if (0 < l && l < mv) stranded += l;   // GPUs past ngpus hold 0 milli (host padding)
             }
             stranded = row_sum_i32(node_valid ? stranded : 0);
@@ -718,7 +718,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
             nr.gpu_left[0] -= pod.ngpu;
 #pragma unroll
             for (int g = 0; g < kGmax; ++g)
-              if ((gmask >> g) & 1) nr.gml[0][g] -= pod.gmilli;
+              if ((gmask >> g) & 1) nr.g_add(0, g, -pod.gmilli);
           }
           if (kind == kRetry && pod.ngpu > 0) {
 #pragma unroll
@@ -749,7 +749,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
         // n_nodes and GPUs past ngpus hold 0): no per-event used counters
         int32_t gl_sum = 0;
 #pragma unroll
-        for (int g = 0; g < kGmax; ++g) gl_sum += nr.gml[0][g];
+        for (int g = 0; g < kGmax; ++g) gl_sum += nr.g(0, g);
         const int32_t used_cpu = (int32_t)Ws->tot_cpu - row_sum_i32(nr.cpu_left[0]);
         const int32_t used_mem = (int32_t)Ws->tot_mem - row_sum_i32(nr.mem_left[0]);
         const int32_t used_gcnt = (int32_t)Ws->tot_gcnt - row_sum_i32(nr.gpu_left[0]);

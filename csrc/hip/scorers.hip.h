@@ -41,7 +41,7 @@ __device__ __forceinline__ bool feasible(int ps, const NodeRegs<NPASS>& nr, cons
   if (pod.ngpu > 0) {
     int avail = 0;
 #pragma unroll
-    for (int j = 0; j < kGmax; ++j) avail += (j < nr.ngpus[ps] && nr.gml[ps][j] >= pod.gmilli);
+    for (int j = 0; j < kGmax; ++j) avail += (j < nr.ngp(ps) && nr.g(ps, j) >= pod.gmilli);
     if (avail < pod.ngpu) return false;
   }
   return true;
@@ -109,10 +109,10 @@ struct BuiltinScorerDev {
         const int64_t rc = (int64_t)nr.cpu_left[ps] - pod.cpu;
         const int64_t rm = (int64_t)nr.mem_left[ps] - pod.mem;
         const int64_t rg = (int64_t)nr.gpu_left[ps] - pod.ngpu;
-        if (nr.cpu_total[ps] == 0 || nr.mem_total[ps] == 0) { exc = EXC_ZERO_DIVISION; return 0; }
-        const double nc = (double)rc / (double)nr.cpu_total[ps];
-        const double nm = (double)rm / (double)nr.mem_total[ps];
-        const int gd = nr.ngpus[ps] > 1 ? nr.ngpus[ps] : 1;
+        if (nr.ctot(ps) == 0 || nr.mtot(ps) == 0) { exc = EXC_ZERO_DIVISION; return 0; }
+        const double nc = (double)rc / (double)nr.ctot(ps);
+        const double nm = (double)rm / (double)nr.mtot(ps);
+        const int gd = nr.ngp(ps) > 1 ? nr.ngp(ps) : 1;
         const double ng = (double)rg / (double)gd;
         const double t = nc * 0.33 + nm * 0.33;
         const double nrm = t + ng * 0.34;
@@ -147,11 +147,11 @@ struct BuiltinScorerDev {
   // held live across the node loop.
   template <int NPASS, class WP>
   __device__ static double composite(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, WP w) {
-    const int ng = nr.ngpus[ps];
+    const int ng = nr.ngp(ps);
     const bool gpod = pod.ngpu > 0;
     // 32-bit temporaries: GPU milli totals < 2^20 (prepare_device_workload),
     // so sums over <= 8 GPUs cannot overflow; differences widen where formed
-    const int32_t ct = nr.cpu_total[ps], mt = nr.mem_total[ps];
+    const int32_t ct = nr.ctot(ps), mt = nr.mtot(ps);
     const int32_t cl = nr.cpu_left[ps], ml = nr.mem_left[ps];
     const double cpu_u = (double)((int64_t)ct - cl) / (double)(ct > 1 ? ct : 1);
     const double mem_u = (double)((int64_t)mt - ml) / (double)(mt > 1 ? mt : 1);
@@ -159,7 +159,7 @@ struct BuiltinScorerDev {
 #pragma unroll
     for (int j = 0; j < kGmax; ++j) {
       if (j < ng) {
-        const int32_t l = nr.gml[ps][j];
+        const int32_t l = nr.g(ps, j);
         free_m += l;
         idle += (l == nr.gt(ps, j));
         gmax = (j == 0 || l > gmax) ? l : gmax;
@@ -208,9 +208,9 @@ struct BuiltinScorerDev {
   template <int NPASS, class WP>
   __device__ static double composite_fast(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, WP w,
                                           const double* z, double zcap) {
-    const int ng = nr.ngpus[ps];
+    const int ng = nr.ngp(ps);
     const bool gpod = pod.ngpu > 0;
-    const int32_t ct = nr.cpu_total[ps], mt = nr.mem_total[ps];
+    const int32_t ct = nr.ctot(ps), mt = nr.mtot(ps);
     const int32_t cl = nr.cpu_left[ps], ml = nr.mem_left[ps];
     // the host's verified reciprocals (DeviceEngine::prepare_recips): numerators in [0, total]
     const double cpu_u = div_by_recip((double)(ct - cl), (double)(ct > 1 ? ct : 1), z[0]);
@@ -219,7 +219,7 @@ struct BuiltinScorerDev {
 #pragma unroll
     for (int j = 0; j < kGmax; ++j) {
       if (j < ng) {
-        const int32_t l = nr.gml[ps][j];
+        const int32_t l = nr.g(ps, j);
         free_m += l;
         idle += (l == nr.gt(ps, j));
         gmax = (j == 0 || l > gmax) ? l : gmax;
@@ -280,7 +280,7 @@ struct BuiltinScorerDev {
 #pragma unroll
     for (int j = 0; j < kGmax; ++j) {
       if (j < ng) {
-        const int32_t l = nr.gml[0][j];
+        const int32_t l = nr.g(0, j);
         free_m += l;
         idle += (l == nr.gmt1[0]);
         gmax = (j == 0 || l > gmax) ? l : gmax;
@@ -314,9 +314,9 @@ struct BuiltinScorerDev {
 
   template <int NPASS>
   __device__ static void features(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, double* f) {
-    const int ng = nr.ngpus[ps];
-    const int64_t cpu_tot = nr.cpu_total[ps] > 1 ? nr.cpu_total[ps] : 1;
-    const int64_t mem_tot = nr.mem_total[ps] > 1 ? nr.mem_total[ps] : 1;
+    const int ng = nr.ngp(ps);
+    const int64_t cpu_tot = nr.ctot(ps) > 1 ? nr.ctot(ps) : 1;
+    const int64_t mem_tot = nr.mtot(ps) > 1 ? nr.mtot(ps) : 1;
     const int ngd = ng > 1 ? ng : 1;
     f[0] = 1.0;
     const double rc = (double)((int64_t)nr.cpu_left[ps] - pod.cpu) / (double)cpu_tot;
@@ -329,7 +329,7 @@ struct BuiltinScorerDev {
 #pragma unroll
     for (int j = 0; j < kGmax; ++j) {
       if (j < ng) {
-        const int32_t l = nr.gml[ps][j];
+        const int32_t l = nr.g(ps, j);
         free_m += l;
         idle += (l == nr.gt(ps, j));
         part += (0 < l && l < nr.gt(ps, j));
@@ -345,7 +345,7 @@ struct BuiltinScorerDev {
     f[8] = (double)part / (double)ngd;
     f[9] = (pod.ngpu == 0 && ng > 0) ? 1.0 : 0.0;
     f[10] = best < 0 ? 0.0 : (double)best / 1000.0;
-    f[11] = (double)nr.cpu_total[ps] / 100000.0;
+    f[11] = (double)nr.ctot(ps) / 100000.0;
   }
 };
 

@@ -96,10 +96,10 @@ struct VmScorerDev {
     // (score() is out of line, so `nr` arrives through memory)
     int32_t gml[kGmax], gmt[kGmax];
 #pragma unroll
-    for (int j = 0; j < kGmax; ++j) { gml[j] = nr.gml[ps][j]; gmt[j] = nr.gt(ps, j); }
-    const int ngp = nr.ngpus[ps];
-    const int64_t n_cpu_left = nr.cpu_left[ps], n_cpu_total = nr.cpu_total[ps];
-    const int64_t n_mem_left = nr.mem_left[ps], n_mem_total = nr.mem_total[ps], n_gpu_left = nr.gpu_left[ps];
+    for (int j = 0; j < kGmax; ++j) { gml[j] = nr.g(ps, j); gmt[j] = nr.gt(ps, j); }
+    const int ngp = nr.ngp(ps);
+    const int64_t n_cpu_left = nr.cpu_left[ps], n_cpu_total = nr.ctot(ps);
+    const int64_t n_mem_left = nr.mem_left[ps], n_mem_total = nr.mtot(ps), n_gpu_left = nr.gpu_left[ps];
     const int64_t p_cpu = pod.cpu, p_mem = pod.mem, p_ngpu = pod.ngpu, p_gmilli = pod.gmilli;
     const int64_t p_ctime = pod.ctime, p_dur = pod.dur;
 

@@ -151,6 +151,9 @@ def prepare_device_workload(w: Workload, snapshot_interval: float = 0.05) -> Dic
             or p.pod_ngpu.max(initial=0) >= 2 ** 8 or p.pod_ngpu.min(initial=0) < 0:
         raise UnsupportedWorkload("gpu request outside the packed pod record")
     npass = 1 if N <= 64 else (2 if N <= 128 else 4)
+    if npass == 4 and c.gpu_milli_total.size and c.gpu_milli_total.max() >= 2 ** 16:
+        # > 128 nodes: two GPUs' milli left share a register (16-bit halves, NodeRegs::kPack)
+        raise UnsupportedWorkload("GPU milli totals >= 2^16 on a > 128-node cluster")
     NP = 64 * npass
 
     def pad(a, dtype):
