@@ -365,23 +365,49 @@ class Evaluator:
                         slot: int, count_errors: bool = True) -> "PendingPrograms":
         """`submit_programs` for programs whose bytecode was produced elsewhere
         (the steady-state search compiles in its producer processes)."""
-        pend = PendingPrograms(list(codes), slot)
+        return self.launch_prepared(self.prepare_compiled(codes, compiled, count_errors), slot)
+
+    def prepare_compiled(self, codes: Sequence[str], compiled: Sequence[Optional[CompiledPolicy]],
+                         count_errors: bool = True) -> "PendingPrograms":
+        """The compile half of `submit_compiled`, callable from a worker thread:
+        JIT-compiles and loads the batch's native shapes (held until the batch
+        is collected or `discard_prepared`).  `launch_prepared` starts it."""
+        pend = PendingPrograms(list(codes), -1)
         pend.compiled = list(compiled)
         if count_errors:
-            self.stats["compile_errors"] += sum(p is None for p in pend.compiled)
+            with self._compile_lock:
+                self.stats["compile_errors"] += sum(p is None for p in pend.compiled)
         if self.device is not None and self.native:
             idx = [i for i, p in enumerate(pend.compiled) if p is not None and p.device_ok]
             if idx:
                 t0 = time.perf_counter()
-                batch = self.device.submit_native(slot, [pend.compiled[i] for i in idx])
+                batch = self.device.prepare_native([pend.compiled[i] for i in idx])
+                pend.prepared = batch
+                pend.native_idx = idx
                 pend.jit_s = batch.compile_s
                 pend.new_shapes = batch.compiled
-                pend.native_idx = idx
-                pend.t_launch = time.perf_counter()
-                self.stats["jit_s"] += batch.compile_s
-                self.stats["jit_shapes"] += batch.compiled
-                pend.submit_s = pend.t_launch - t0
+                pend.submit_s = time.perf_counter() - t0
+                with self._compile_lock:
+                    self.stats["jit_s"] += batch.compile_s
+                    self.stats["jit_shapes"] += batch.compiled
         return pend
+
+    def launch_prepared(self, pend: "PendingPrograms", slot: int) -> "PendingPrograms":
+        """Launch a `prepare_compiled` batch on device slot `slot` (main thread)."""
+        pend.slot = slot
+        if pend.native_idx:
+            t0 = time.perf_counter()
+            self.device.submit_native(slot, [pend.compiled[i] for i in pend.native_idx], pend.prepared)
+            pend.prepared = None
+            pend.t_launch = time.perf_counter()
+            pend.submit_s += pend.t_launch - t0
+        return pend
+
+    def discard_prepared(self, pend: "PendingPrograms") -> None:
+        """Give back the modules of a prepared batch that will not be launched."""
+        if pend.prepared is not None:
+            self.device.release_native(pend.prepared)
+            pend.prepared = None
 
     def ready(self, pend) -> bool:
         """Slot index (family batches) or `PendingPrograms`: finished?"""
@@ -487,6 +513,7 @@ class PendingPrograms:
     jit_s: float = 0.0
     submit_s: float = 0.0
     new_shapes: int = 0
+    prepared: object = None          # NativeBatch compiled ahead, not launched yet
     t_launch: float = 0.0
     t_done: float = 0.0
     fallback_idx: List[int] = field(default_factory=list)

@@ -225,6 +225,7 @@ def _numeric_subexprs(tree: ast.AST, portable: bool) -> list:
         elif isinstance(n, ast.Call):
             skip.add(id(n.func))
             skip.update(id(x) for x in ast.walk(n.func))
+    scopes = _scope_sets(tree) if portable else None
     out = []
     for n in ast.walk(tree):
         if id(n) in skip:
@@ -234,24 +235,57 @@ def _numeric_subexprs(tree: ast.AST, portable: bool) -> list:
               or (isinstance(n, ast.Attribute) and isinstance(n.value, ast.Name) and n.value.id in ("pod", "node")
                   and n.attr in _NUMERIC_FIELDS)
               or (isinstance(n, ast.Call) and isinstance(n.func, ast.Name) and n.func.id in ("abs", "min", "max", "sum")))
-        if ok and (not portable or _free_names(n) <= _FREE_OK):
+        if ok and portable:
+            used, bound = scopes[id(n)]
+            ok = used - bound <= _FREE_OK
+        if ok:
             out.append(n)
     return out
 
 
-class _Replace(ast.NodeTransformer):
-    def __init__(self, target: ast.AST, new: ast.AST):
-        self.target, self.new = target, new
+def _scope_sets(tree: ast.AST) -> dict:
+    """id(node) -> (names read, names bound by comprehensions / lambdas) over
+    the node's subtree, in one bottom-up pass (`_free_names` of every node
+    without re-walking each subtree)."""
+    memo = {}
 
-    def generic_visit(self, node):
-        if node is self.target:
-            return self.new
-        return super().generic_visit(node)
+    def rec(n):
+        used, bound = set(), set()
+        t = type(n)
+        if t is ast.Name:
+            if type(n.ctx) is ast.Load:
+                used.add(n.id)
+        elif t is ast.comprehension:
+            bound.update(x.id for x in ast.walk(n.target) if isinstance(x, ast.Name))
+        elif t is ast.Lambda:
+            bound.update(a.arg for a in n.args.args)
+        for c in ast.iter_child_nodes(n):
+            u, b = rec(c)
+            used |= u
+            bound |= b
+        memo[id(n)] = (used, bound)
+        return used, bound
 
-    def visit(self, node):
-        if node is self.target:
-            return self.new
-        return super().visit(node)
+    rec(tree)
+    return memo
+
+
+def _replace(tree: ast.AST, target: ast.AST, new: ast.AST) -> ast.AST:
+    """`tree` with the (single) occurrence of node `target` swapped for `new`."""
+    if tree is target:
+        return new
+    for parent in ast.walk(tree):
+        for f in parent._fields:
+            v = getattr(parent, f, None)
+            if v is target:
+                setattr(parent, f, new)
+                return tree
+            if type(v) is list:
+                for i, x in enumerate(v):
+                    if x is target:
+                        v[i] = new
+                        return tree
+    return tree
 
 
 @functools.lru_cache(maxsize=4096)   # parents repeat across thousands of children
@@ -395,7 +429,7 @@ class MutationClient(BaseClient):
                 if n.func.id in ("min", "max"):   # an empty GPU list would raise: guard like the features do
                     node = ast.IfExp(ast.Attribute(ast.Name("node", ast.Load()), "gpus", ast.Load()), n,
                                      ast.Constant(0))
-                    tree = _Replace(n, node).visit(tree)
+                    tree = _replace(tree, n, node)
             elif len(n.args) >= 2 and n.func.id in ("min", "max"):
                 n.func.id = "max" if n.func.id == "min" else "min"
             else:
@@ -411,7 +445,7 @@ class MutationClient(BaseClient):
             pieces = [n for n in _numeric_subexprs(donor, portable=True) if not isinstance(n, ast.Constant)]
             if not targets or not pieces:
                 return None
-            tree = _Replace(rng.choice(targets), rng.choice(pieces)).visit(tree)
+            tree = _replace(tree, rng.choice(targets), rng.choice(pieces))
         elif name == "wrap":
             targets = [n for n in _numeric_subexprs(tree, portable=False) if not isinstance(n, ast.Constant)]
             if not targets:
@@ -428,11 +462,11 @@ class MutationClient(BaseClient):
             else:
                 new = ast.BinOp(ast.Call(ast.Name("abs", ast.Load()), [t], []), ast.Pow(),
                                 ast.Constant(round(rng.uniform(0.3, 2.0), 2)))
-            tree = _Replace(t, new).visit(tree)
+            tree = _replace(tree, t, new)
         else:
             return None
         try:
-            out = ast.unparse(ast.fix_missing_locations(tree))
+            out = ast.unparse(tree)             # unparse needs no source locations
             ast.parse(out)
         except Exception:
             return None

@@ -12,9 +12,10 @@ flight on one GPU:
   fill, sandbox validation and bytecode compile, all off the main process;
   parents are sampled from each island's population *at submission time*;
 * **dispatcher** -- the main thread packs ready children into batches of up to
-  ``batch`` programs and launches them on free HIP slots (up to ``slots``
-  batches in flight), JIT-compiling new shapes with the baseline tier
-  (`ops/gcnjit.py`, ~0.2 ms per program) right before the launch;
+  ``batch`` programs; a stager thread JIT-compiles their new shapes with the
+  baseline tier (`ops/gcnjit.py`, ~0.2 ms per program) and loads the modules
+  up to ``ahead`` batches before a slot frees, and the main thread launches a
+  staged batch the moment a HIP slot is free (up to ``slots`` in flight);
 * **merge** -- results land per batch and merge into their island one by one
   with the reference's rules (dedup by difflib ratio against equal-or-better
   members, keep the top ``population_size``): a steady-state GA instead of
@@ -37,6 +38,7 @@ evals/s, device busy fraction, new-shape fraction, best per island).
 
 from __future__ import annotations
 
+import collections
 import concurrent.futures
 import multiprocessing
 import os
@@ -118,9 +120,11 @@ class SteadyStateSearch:
     distributed context, log and checkpoint settings)."""
 
     def __init__(self, fs, batch: int = 256, slots: Optional[int] = None, producers: int = 0,
-                 task_size: int = 8, status_every_s: float = 5.0, tierup: bool = False):
+                 task_size: int = 8, status_every_s: float = 5.0, tierup: bool = False, ahead: int = 2):
         self.fs = fs
         self.batch = int(batch)
+        #: batches compiled and loaded ahead of a free slot (the stager thread)
+        self.ahead = max(1, int(ahead))
         dev = getattr(fs.evaluator, "device", None)
         if dev is not None and not tierup:
             # background LLVM recompiles of hot shapes compete with the producer
@@ -212,6 +216,8 @@ class SteadyStateSearch:
             initargs=(llm_cfg, timeout_s, 1000 * ctx.rank + 1))
         inflight_tasks: List[concurrent.futures.Future] = []
         fallbacks: list = []             # (batch items, future of the host-engine fallback)
+        staged: collections.deque = collections.deque()   # (batch items, future of prepare_compiled)
+        stager = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="fks-stage")
         ready: List[tuple] = []          # produced children waiting for a batch
         batches: List[Optional[_Batch]] = [None] * self.slots
         # children requested per island: production stops at the island's target
@@ -222,14 +228,14 @@ class SteadyStateSearch:
         t_status = t_start
         t_prev = t_start
         busy_since = None
-        want_buffer = self.batch * (self.slots + 1)
+        want_buffer = self.batch * (self.slots + self.ahead + 1)
         next_reset = ((start_gen // fs.reset_every) + 1) * fs.reset_every if fs.reset_every else 0
         try:
             while True:
                 progressed = False
                 # 1) keep producers busy (children from the islands' CURRENT elites)
                 queued = len(ready) + sum(len(b.items) for b in batches if b is not None) + \
-                    self.task_size * len(inflight_tasks)
+                    sum(len(t) for t, _ in staged) + self.task_size * len(inflight_tasks)
                 while (not stop and queued < want_buffer + self.task_size * self.producers
                        and len(inflight_tasks) < 2 * self.producers):
                     cands = [i for i in range(k) if requested[i] < target_children[i]]
@@ -267,17 +273,27 @@ class SteadyStateSearch:
                     else:
                         still.append(f)
                 inflight_tasks = still
-                # 3) launch full batches on free slots (a partial one when nothing else is coming)
-                for si in range(self.slots):
-                    if batches[si] is not None or not ready:
-                        continue
+                # 3a) stage the next batches: JIT compile + module loads on the stager
+                # thread while the slots are busy, so a freed slot relaunches at once
+                # (a partial batch when nothing else is coming)
+                while ready and len(staged) < self.ahead:
                     tail = not inflight_tasks and all(requested[i] >= target_children[i] for i in range(k))
-                    if len(ready) < self.batch and not (tail or stop or all(b is None for b in batches)):
-                        continue
+                    if len(ready) < self.batch and not (
+                            tail or stop or (all(b is None for b in batches) and not staged)):
+                        break
                     take, ready = ready[:self.batch], ready[self.batch:]
+                    staged.append((take, stager.submit(ev.prepare_compiled, [c for _, c, _ in take],
+                                                       [p for _, _, p in take])))
+                    progressed = True
+                # 3b) launch staged batches (in order) on free slots
+                for si in range(self.slots):
+                    if batches[si] is not None or not staged or not staged[0][1].done():
+                        continue
+                    take, fut = staged.popleft()
+                    pend = fut.result()
                     with roctx_range(f"steady.launch slot {si} ({len(take)} programs)"):
                         t_ph = time.perf_counter()
-                        pend = ev.submit_compiled([c for _, c, _ in take], [p for _, _, p in take], slot=si)
+                        ev.launch_prepared(pend, si)
                         self.phase["submit"] += time.perf_counter() - t_ph
                     b = _Batch(si, take, pend, time.time(), pend.new_shapes, pend.jit_s)
                     batches[si] = b
@@ -368,7 +384,8 @@ class SteadyStateSearch:
                     self._status(now, t_start, busy_since, batches, ready, inflight_tasks, merged, global_best)
                 # 7) done?  (every child merged, or stopping; then every agreed gather finished)
                 all_launched = all(requested[i] >= target_children[i] for i in range(k))
-                idle = not inflight_tasks and all(b is None for b in batches) and not fallbacks
+                idle = (not inflight_tasks and all(b is None for b in batches) and not fallbacks
+                        and not staged)
                 if idle and (stop or (all_launched and not ready)):
                     ready.clear()
                     due = chan.every and chan.next is not None and (
@@ -382,6 +399,10 @@ class SteadyStateSearch:
                     time.sleep(0.0005)
         finally:
             pool.shutdown(wait=False, cancel_futures=True)
+            stager.shutdown(wait=True, cancel_futures=True)
+            for _, fut in staged:        # compiled but never launched: give the modules back
+                if fut.done() and not fut.cancelled() and fut.exception() is None:
+                    ev.discard_prepared(fut.result())
         now = time.time()
         rec = self._status(now, t_start, busy_since, batches, ready, inflight_tasks, merged, global_best, final=True)
         if fs.ck_dir:

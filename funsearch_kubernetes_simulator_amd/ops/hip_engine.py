@@ -275,17 +275,31 @@ class DeviceEvaluator:
                                                budget=int(self.options.get("budget") or DEFAULT_CALL_BUDGET))
         return self._jit
 
-    def submit_native(self, slot: int, progs: Sequence[CompiledPolicy]):
-        """Compile (shape-cached) and launch one k_replay_native wave per program on
-        `slot`.  Programs the native backend cannot take (codegen / register limits)
-        get an EXC_UNSUPPORTED row from `wait`, so callers fall back per program.
-        Returns the `NativeBatch` (compile time, cache hits, reasons)."""
+    def prepare_native(self, progs: Sequence[CompiledPolicy]):
+        """The compile half of `submit_native` (any thread): JIT-compile and load
+        the shapes `progs` need and hold their modules.  The `NativeBatch` is then
+        launched with `submit_native(slot, progs, batch)` or handed back with
+        `release_native(batch)`."""
         batch = self.native_compiler.prepare(progs)
         if not self.math_exact:
             for i, p in enumerate(progs):
                 if batch.ok[i] and p.uses_libm:
                     batch.ok[i] = False
                     batch.reasons[i] = "exp / log / pow: device math differs from this host's libm"
+        return batch
+
+    def release_native(self, batch) -> None:
+        """A prepared batch that will not be launched."""
+        self.native_compiler.release(batch.modules)
+
+    def submit_native(self, slot: int, progs: Sequence[CompiledPolicy], batch=None):
+        """Compile (shape-cached) and launch one k_replay_native wave per program on
+        `slot`.  Programs the native backend cannot take (codegen / register limits)
+        get an EXC_UNSUPPORTED row from `wait`, so callers fall back per program.
+        `batch`: the result of `prepare_native(progs)` (compiled ahead on another
+        thread).  Returns the `NativeBatch` (compile time, cache hits, reasons)."""
+        if batch is None:
+            batch = self.prepare_native(progs)
         idx = np.flatnonzero(batch.ok)
         prev = self._native_mods.pop(slot, None)
         if prev:    # a batch never waited for (the engine waits for it before restaging)

@@ -39,6 +39,11 @@ from .bytecode import (GPU_FIELDS, MAX_REGS, NO_REG, NODE_FIELDS, NODE_NGPUS, PO
                        TAG_INT, Exc, Op, pack_insn)
 
 
+#: AST node types that never matter to the analysis passes (see `_index_tree`)
+_LEAF_NODES = frozenset(c for base in (ast.expr_context, ast.operator, ast.unaryop, ast.cmpop, ast.boolop)
+                        for c in base.__subclasses__())
+
+
 class CompileError(Exception):
     """The program uses a construct outside the native subset."""
 
@@ -136,7 +141,8 @@ class Compiler:
         self.free: List[int] = list(range(MAX_REGS - 1, -1, -1))
         self.features = set()
         self.globals: Dict[str, Val] = {}
-        self._walk_memo: Dict[int, tuple] = {}
+        self._order: list = []
+        self._span: Dict[int, tuple] = {}
         self.scope = _Scope()
         self.pod_name = self.node_name = None
         self.loop_depth = 0
@@ -265,15 +271,14 @@ class Compiler:
         rest in LDS, so hot temporaries and loop variables get the fast file.
         A pure renaming: both VMs execute the same instructions."""
         from collections import Counter
-        uses: Counter = Counter()
-        for op, d, a, b, imm in self.code:
-            for r in (d, a, b) + ((imm,) if op in self._IMM_REG_OPS else ()):
-                if r != NO_REG:
-                    uses[r] += 1
+        imm_ops = self._IMM_REG_OPS
+        uses = Counter(r for op, d, a, b, imm in self.code
+                       for r in ((d, a, b, imm) if op in imm_ops else (d, a, b)))
+        uses.pop(NO_REG, None)
         order = sorted(uses, key=lambda r: (-uses[r], r))
         perm = {r: i for i, r in enumerate(order)}
-        m = lambda r: NO_REG if r == NO_REG else perm[r]
-        self.code = [(op, m(d), m(a), m(b), m(imm) if op in self._IMM_REG_OPS else imm)
+        perm[NO_REG] = NO_REG
+        self.code = [(op, perm[d], perm[a], perm[b], perm[imm] if op in imm_ops else imm)
                      for op, d, a, b, imm in self.code]
 
     def _fold_constant(self, node: ast.AST):
@@ -289,38 +294,57 @@ class Compiler:
                 raise CompileError("module-level constant must be a literal expression")
         return value
 
+    #: constructs the compiler rejects anywhere inside the policy function
+    _BANNED = frozenset((ast.Global, ast.Nonlocal, ast.FunctionDef, ast.AsyncFunctionDef,
+                         ast.ClassDef, ast.With, ast.Try, ast.Raise, ast.Assert, ast.Delete,
+                         ast.Yield, ast.YieldFrom, ast.Await, ast.NamedExpr, ast.Starred,
+                         ast.DictComp, ast.SetComp, ast.Dict, ast.Set, ast.JoinedStr))
+
     def _check_names(self, fn: ast.FunctionDef) -> None:
+        self._index_tree(fn)
         reserved = {self.pod_name, self.node_name, "math", "operator"} | SAFE_BUILTINS
+        banned, Name, Store = self._BANNED, ast.Name, ast.Store
         for node in self._walk(fn):
-            if isinstance(node, ast.Name) and isinstance(node.ctx, ast.Store) and node.id in reserved:
+            t = type(node)
+            if t is Name and type(node.ctx) is Store and node.id in reserved:
                 raise CompileError(f"assignment to reserved name {node.id}")
-            if isinstance(node, (ast.Global, ast.Nonlocal, ast.FunctionDef, ast.AsyncFunctionDef,
-                                 ast.ClassDef, ast.With, ast.Try, ast.Raise, ast.Assert, ast.Delete,
-                                 ast.Yield, ast.YieldFrom, ast.Await, ast.NamedExpr, ast.Starred,
-                                 ast.DictComp, ast.SetComp, ast.Dict, ast.Set, ast.JoinedStr)):
-                if node is not fn:
-                    raise CompileError(f"unsupported construct {type(node).__name__}")
+            if t in banned and node is not fn:
+                raise CompileError(f"unsupported construct {t.__name__}")
 
     # ------------------------------------------------------------------ analysis
+    def _index_tree(self, root) -> None:
+        """One pre-order pass over the function: every subtree is then a slice
+        of `self._order`.  The analysis passes re-walk the same statements
+        (kind planning runs three rounds, the unbound analysis nests per
+        statement); walking them afresh each time was over half of compile
+        time, and a per-subtree memo still paid O(size x depth).  Operator and
+        load/store context nodes carry nothing the passes look at and are left
+        out (they are a third of a typical tree)."""
+        order, span, AST, leaf = [], {}, ast.AST, _LEAF_NODES
+
+        def visit(n):
+            i = len(order)
+            order.append(n)
+            for f in n._fields:
+                v = getattr(n, f, None)
+                if type(v) is list:
+                    for x in v:
+                        if isinstance(x, AST) and type(x) not in leaf:
+                            visit(x)
+                elif isinstance(v, AST) and type(v) not in leaf:
+                    visit(v)
+            span[id(n)] = (n, i, len(order))
+
+        visit(root)
+        self._order, self._span = order, span
+
     def _walk(self, node) -> list:
-        """`ast.walk(node)` as a list, memoised per subtree: the analysis passes
-        re-walk the same statements (kind planning runs three rounds, the unbound
-        analysis nests per statement), which made walking ~55% of compile time.
-        The node is kept in the entry so an id() cannot be reused while cached."""
-        hit = self._walk_memo.get(id(node))
-        if hit is None or hit[0] is not node:
-            out, i = [node], 0
-            while i < len(out):                 # breadth-first, the order of ast.walk
-                n = out[i]
-                i += 1
-                for f in n._fields:
-                    v = getattr(n, f, None)
-                    if isinstance(v, ast.AST):
-                        out.append(v)
-                    elif isinstance(v, list):
-                        out.extend(x for x in v if isinstance(x, ast.AST))
-            hit = self._walk_memo[id(node)] = (node, out)
-        return hit[1]
+        """The nodes of `node`'s subtree in pre-order: `ast.walk` up to order,
+        without operator and context nodes."""
+        hit = self._span.get(id(node))
+        if hit is not None and hit[0] is node:
+            return self._order[hit[1]:hit[2]]
+        return list(ast.walk(node))
 
     @staticmethod
     def _assigned_names(body) -> set:
@@ -334,17 +358,20 @@ class Compiler:
     def _plan_kinds(self, body) -> None:
         """Fix each local's kind from its assignments (a name must keep one kind)."""
         self.kinds: Dict[str, str] = {}
+        kinds = (ast.Assign, ast.AnnAssign, ast.AugAssign, ast.For)
+        sites = [node for stmt in body for node in self._walk(stmt) if type(node) in kinds]
         for _ in range(3):
-            for stmt in body:
-                for node in self._walk(stmt):
-                    if isinstance(node, (ast.Assign, ast.AnnAssign)):
-                        targets = node.targets if isinstance(node, ast.Assign) else [node.target]
-                        for t in targets:
-                            self._plan_target(t, node.value)
-                    elif isinstance(node, ast.AugAssign):
-                        self._plan_set(node.target, NUM)
-                    elif isinstance(node, ast.For):
-                        self._plan_for(node)
+            for node in sites:
+                t = type(node)
+                if t is ast.Assign:
+                    for tgt in node.targets:
+                        self._plan_target(tgt, node.value)
+                elif t is ast.AnnAssign:
+                    self._plan_target(node.target, node.value)
+                elif t is ast.AugAssign:
+                    self._plan_set(node.target, NUM)
+                else:
+                    self._plan_for(node)
 
     def _plan_set(self, target, kind) -> None:
         if not isinstance(target, ast.Name):

@@ -31,6 +31,11 @@ from contextlib import contextmanager
 from typing import Any, Dict
 
 
+#: node types without children that the structure check never inspects
+_LEAF_NODES = frozenset(c for base in (ast.expr_context, ast.operator, ast.unaryop, ast.cmpop, ast.boolop)
+                        for c in base.__subclasses__())
+
+
 class SafeExecutor:
     ALLOWED_BUILTINS = {
         "abs", "min", "max", "sum", "len", "range", "enumerate",
@@ -58,16 +63,35 @@ class SafeExecutor:
             tree = ast.parse(code)
         except SyntaxError as exc:
             raise ValueError(f"Syntax error in generated code: {exc}")
-        for node in ast.walk(tree):
-            if isinstance(node, (ast.Import, ast.ImportFrom)):
+        allowed = self._allowed_calls()
+        queue, i = [tree], 0
+        while i < len(queue):                   # breadth-first: ast.walk's order
+            node = queue[i]
+            i += 1
+            t = type(node)
+            if t is ast.Call:
+                if type(node.func) is ast.Name and node.func.id not in allowed:
+                    raise ValueError(f"Function {node.func.id} not allowed")
+            elif t is ast.Attribute:
+                if node.attr.startswith("__"):
+                    raise ValueError(f"Access to {node.attr} not allowed")
+            elif t is ast.Import or t is ast.ImportFrom:
                 raise ValueError("Import statements not allowed")
-            if isinstance(node, ast.Attribute) and node.attr.startswith("__"):
-                raise ValueError(f"Access to {node.attr} not allowed")
-            if isinstance(node, ast.Call) and isinstance(node.func, ast.Name):
-                name = node.func.id
-                if name not in self.ALLOWED_BUILTINS and not self._is_allowed_function_call(name):
-                    raise ValueError(f"Function {name} not allowed")
+            for f in node._fields:
+                v = getattr(node, f, None)
+                if type(v) is list:
+                    queue.extend(x for x in v if isinstance(x, ast.AST) and type(x) not in _LEAF_NODES)
+                elif isinstance(v, ast.AST) and type(v) not in _LEAF_NODES:
+                    queue.append(v)
         return True
+
+    def _allowed_calls(self) -> frozenset:
+        key = (frozenset(self.ALLOWED_BUILTINS), tuple((m, tuple(n)) for m, n in self.ALLOWED_MODULES.items()))
+        if getattr(self, "_allowed_key", None) != key:
+            self._allowed_key = key
+            self._allowed = frozenset(self.ALLOWED_BUILTINS).union(
+                *(set(names) for names in self.ALLOWED_MODULES.values()))
+        return self._allowed
 
     def validate_code_content(self, code: str) -> bool:
         lowered = code.lower()

@@ -437,15 +437,23 @@ class _DecliningDevice:
                 raise RuntimeError(f"slot busy: wait() for its batch first (slot {slot})")
             self.busy[slot] = payload
 
-    def submit_native(self, slot, progs):
+    def prepare_native(self, progs):
         import numpy as np
         from funsearch_kubernetes_simulator_amd.ops.jit import NativeBatch
+        n = len(progs)
+        return NativeBatch(np.zeros(n, np.uint64), np.zeros(1, np.int64), np.zeros(n, np.int32),
+                           np.zeros(n, bool), {i: "declined" for i in range(n)}, 0.0, 0)
+
+    def release_native(self, batch):
+        pass
+
+    def submit_native(self, slot, progs, batch=None):
+        import numpy as np
         n = len(progs)
         tab = np.zeros((n, 13))
         tab[:, 10] = 100.0                                   # EXC_UNSUPPORTED: not native
         self._take(slot, tab)
-        return NativeBatch(np.zeros(n, np.uint64), np.zeros(1, np.int64), np.zeros(n, np.int32),
-                           np.zeros(n, bool), {i: "declined" for i in range(n)}, 0.0, 0)
+        return batch if batch is not None else self.prepare_native(progs)
 
     def ready(self, slot):
         return True

@@ -65,6 +65,23 @@ def test_steady_single_rank(tmp_path):
     assert (tmp_path / "ck" / "islands_rank0.json").exists()
 
 
+def test_steady_stager_depths(tmp_path):
+    """Batches compiled ahead on the stager thread (``ahead`` 1 and 3, small
+    batches so several are staged at once): every child is still evaluated
+    exactly once and merged."""
+    from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
+    for ahead in (1, 3):
+        cfg = _cfg(tmp_path / f"a{ahead}", gens=2)
+        cfg["islands"]["steady"].update(batch=3, ahead=ahead)
+        fs = IslandFunSearch(cfg)
+        fs.run(2)
+        st = fs.steady.stats
+        assert fs.steady.ahead == ahead
+        assert st.produced == 2 * 2 * 4 and st.evaluations == st.produced - st.rejected
+        assert st.batches >= st.evaluations // 3
+        assert fs.generation == 2
+
+
 def test_steady_early_stop_single_rank(tmp_path):
     from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
     fs = IslandFunSearch(_cfg(tmp_path, gens=50, threshold=0.0))
