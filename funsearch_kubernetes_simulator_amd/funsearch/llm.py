@@ -162,6 +162,20 @@ TERM_LIBRARY = [
     "if node.cpu_milli_left > pod.cpu_milli * 2 and node.memory_mib_left > pod.memory_mib * 2:\n    score += {c}",
     "score += {c} * min(node.cpu_milli_left - pod.cpu_milli, node.memory_mib_left - pod.memory_mib) / "
     "max(node.cpu_milli_total, node.memory_mib_total)",
+    # piecewise utilisation (a free fraction that counts only below / above a load level)
+    "if node.cpu_milli_left > 0.3 * node.cpu_milli_total:\n    score += {c} * node.cpu_milli_left / max(1, node.cpu_milli_total)",
+    "if node.memory_mib_left > 0.3 * node.memory_mib_total:\n    score += {c} * node.memory_mib_left / max(1, node.memory_mib_total)",
+    "if pod.num_gpu > 0 and len(node.gpus) > 0:\n    score += {c} * sum(g.gpu_milli_left for g in node.gpus) / "
+    "max(1, sum(g.gpu_milli_total for g in node.gpus))",
+    "if node.cpu_milli_left < 0.1 * node.cpu_milli_total or node.memory_mib_left < 0.1 * node.memory_mib_total:\n"
+    "    score -= {c}",
+    # GPU fragmentation: spread of the per-GPU free compute, partially used GPUs left behind
+    "if pod.num_gpu > 0 and len(node.gpus) > 0:\n    score -= {c} * (max(g.gpu_milli_left for g in node.gpus) - "
+    "min(g.gpu_milli_left for g in node.gpus)) / 1000",
+    "score -= {c} * sum(1 for g in node.gpus if 0 < g.gpu_milli_left - pod.gpu_milli < 200) / max(1, len(node.gpus))",
+    # node scale and the balance of what the pod leaves behind
+    "score += {c} * min(1.0, node.cpu_milli_total / 100000)",
+    "score -= {c} * abs(node.cpu_milli_left / max(1, node.memory_mib_left) - pod.cpu_milli / max(1, pod.memory_mib)) / 100",
 ]
 
 
@@ -186,6 +200,9 @@ FEATURES = [
     "pod.gpu_milli / 1000",
     "pod.num_gpu",
     "min(node.cpu_milli_left / max(1, pod.cpu_milli), node.memory_mib_left / max(1, pod.memory_mib)) / 100",
+    "(1.0 if node.cpu_milli_left < 0.3 * node.cpu_milli_total else 0.0)",
+    "(1.0 if node.memory_mib_left < 0.3 * node.memory_mib_total else 0.0)",
+    "(1.0 if node.gpu_left == len(node.gpus) else 0.0)",
 ]
 
 #: names a moved subexpression may mention (anything else is a local of its parent)

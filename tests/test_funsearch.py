@@ -549,3 +549,21 @@ def test_island_reset_and_migrant_dedup(tmp_path):
     assert all(sc != 0.45 and sc != 0.1 for _, sc in s.population)
     fs.apply_migrants(3, [("def priority_function(pod, node):\n    return node.memory_mib_left // 7 - 1\n", 0.44)])
     assert 0.44 in [sc for _, sc in s.population]
+
+
+def test_mutator_library_terms_compile_for_the_device():
+    """Every term and feature the offline mutator can insert passes the
+    sandbox and compiles to device bytecode (a term that does not would only
+    ever produce rejected children)."""
+    from funsearch_kubernetes_simulator_amd.funsearch.llm import FEATURES, TERM_LIBRARY
+    from funsearch_kubernetes_simulator_amd.policy.compiler import try_compile
+    from funsearch_kubernetes_simulator_amd.policy.sandbox import SafeExecutor
+    from funsearch_kubernetes_simulator_amd.policy.template import PolicyTemplate
+    ex = SafeExecutor()
+    bodies = ["score = 0.0\n" + t.format(c=1.5) for t in TERM_LIBRARY]
+    bodies += [f"score = 0.0\nscore += 2.0 * ({f})" for f in FEATURES]
+    for body in bodies:
+        code = PolicyTemplate.fill_template("    " + body.replace("\n", "\n    "))
+        assert ex.validate(code)
+        prog, err = try_compile(code)
+        assert prog is not None and prog.device_ok, (body, err)
