@@ -358,7 +358,7 @@ PYBIND11_MODULE(_fks_cpu, m) {
     out["words"] = np_of(r.words);
     out["relocs"] = np_of(r.relocs);
     out["n_insns"] = r.n_insns; out["vgprs"] = r.vgprs; out["sgprs"] = r.sgprs; out["calls"] = r.calls;
-    out["vregs"] = r.vregs; out["tagged"] = r.tagged; out["mir"] = r.mir;
+    out["vregs"] = r.vregs; out["tagged"] = r.tagged; out["mir"] = r.mir; out["spills"] = r.spills;
     return out;
   }, py::arg("code"), py::arg("ctag"), py::arg("is_lit"), py::arg("iconst"), py::arg("fconst"));
   // A batch of programs on `threads` host threads (the generator is
@@ -417,7 +417,7 @@ PYBIND11_MODULE(_fks_cpu, m) {
       d["words"] = np_of(r.words);
       d["relocs"] = np_of(r.relocs);
       d["n_insns"] = r.n_insns; d["vgprs"] = r.vgprs; d["sgprs"] = r.sgprs; d["calls"] = r.calls;
-      d["vregs"] = r.vregs; d["tagged"] = r.tagged; d["mir"] = r.mir;
+      d["vregs"] = r.vregs; d["tagged"] = r.tagged; d["mir"] = r.mir; d["spills"] = r.spills;
       out.append(d);
     }
     return out;
@@ -463,6 +463,9 @@ PYBIND11_MODULE(_fks_cpu, m) {
     return py::make_tuple(py::bytes(img), offs);
   }, py::arg("skeleton"), py::arg("arena_off"), py::arg("arena_vaddr"), py::arg("capacity"), py::arg("rt_vaddr"),
      py::arg("rt_off"), py::arg("rt_vals"), py::arg("words"), py::arg("relocs"), py::arg("align") = 256);
+  // test hook: at most `pairs` VGPR pairs for virtual registers (0: no cap),
+  // which sends ordinary programs down the spill path
+  m.def("gcn_set_pair_cap", [](int pairs) { fks::gcnapi::set_pair_cap(pairs); });
   m.def("gcn_listing", [](py::bytes code, std::vector<uint8_t> ctag, std::vector<uint8_t> is_lit,
                           std::vector<int64_t> iconst, std::vector<double> fconst) {
     const std::string c = code;

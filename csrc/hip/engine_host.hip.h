@@ -236,6 +236,16 @@ class DeviceEngine {
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, device_));
     num_cus_ = prop.multiProcessorCount;
+    // the native kernels call JIT code through function pointers (dynamic
+    // stack): a baseline function's spill slots and a runtime call's save area
+    // (csrc/jit) sit on that per-lane stack, next to the runtime library's frames
+    {
+      size_t st = 0;
+      if (hipDeviceGetLimit(&st, hipLimitStackSize) == hipSuccess && st < kJitStackBytes)
+        (void)hipDeviceSetLimit(hipLimitStackSize, kJitStackBytes);
+      if (hipDeviceGetLimit(&st, hipLimitStackSize) == hipSuccess) stack_bytes_ = st;
+      (void)hipGetLastError();
+    }
     arch_ = prop.gcnArchName;
     heap_bytes_ = (size_t)lds_heap_entries(W_.n_pods) * sizeof(uint64_t);
     delmap_bytes_ = (size_t)lds_delmap_words(W_.n_pods) * 4;
@@ -244,7 +254,8 @@ class DeviceEngine {
     rows_ok_ = npass_ == 1 && W_.n_nodes <= kRow && W_.n_classes <= kRow * kRowClassSlots &&
                W_.n_pods <= kRowMaxHeap && W_.tot_cpu < (int64_t(1) << 31) && W_.tot_mem < (int64_t(1) << 31) &&
                W_.tot_gcnt < (int64_t(1) << 31) && W_.tot_gmilli < (int64_t(1) << 31) &&   // int32 row totals
-               max_class_pods_ < (1 << 16);   // 16-bit waiting-class counters
+               max_class_pods_ < (1 << 16) &&    // 16-bit waiting-class counters
+               max_gpu_milli_ < (1 << 16);       // 16-bit GPU milli halves (NodeRegs<1, true>)
     set_attrs();
   }
 
@@ -575,6 +586,7 @@ class DeviceEngine {
     d["cap_recips"] = W_.cap_recip[1] != 0.0;
     d["frag_recip"] = W_.z_tg != 0.0;
     d["row_composite_waves"] = comp_waves_;
+    d["stack_bytes"] = (int64_t)stack_bytes_;
     d["row_flat"] = row_flat_;
     d["native_rows_last"] = last_native_rows_;
     d["native_waves_last"] = last_native_waves_;
@@ -621,6 +633,10 @@ class DeviceEngine {
       if ((pw >> 16) & 0xFF) ++per_class[pw >> 24];
     }
     max_class_pods_ = *std::max_element(per_class.begin(), per_class.end());
+    {   // row kernels pack two GPUs' milli left per register (16-bit halves)
+      const auto gt = i32("gml_total");
+      max_gpu_milli_ = gt.size() ? *std::max_element(gt.data(), gt.data() + gt.size()) : 0;
+    }
     for (int n = 0; n < nn; ++n) {
       const int32_t a = ct.data()[n], b = mt.data()[n];
       ok = ok && 0 <= cl.data()[n] && cl.data()[n] <= a && 0 <= ml.data()[n] && ml.data()[n] <= b;
@@ -1053,6 +1069,9 @@ class DeviceEngine {
   int last_native_rows_ = 0, last_native_waves_ = 0;
   size_t row_min_lds_ = 0;
   int32_t max_class_pods_ = 0;   // most GPU pods of one gpu_milli class (row kernel: < 2^16)
+  int32_t max_gpu_milli_ = 0;    // largest per-GPU milli total (row kernel: < 2^16)
+  static constexpr size_t kJitStackBytes = 2048;   // per-lane stack of the native kernels
+  size_t stack_bytes_ = 0;
   bool row_flat_ = true;  // composite row kernel: flat heap accesses (false: exec-masked ds / global)
   int comp_waves_ = 5;   // composite row kernel: 4 or 5 waves per SIMD (row_composite_waves)
   mutable std::vector<std::pair<int, int>> row_layout_cache_ = std::vector<std::pair<int, int>>(8, {0, 0});

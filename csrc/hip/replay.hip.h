@@ -112,29 +112,30 @@ __host__ __device__ inline int lds_vreg_offset(int n_pods) {
 // instead of kGmax -- 28 VGPRs on 256-node clusters, the difference between 2
 // and 3 waves per SIMD there.  gt(ps, j) is the per-GPU view (0 past ngpus,
 // like the zero padding of the host table).
-// On 256-node clusters (NPASS = 4) the per-GPU milli left of two GPUs share
-// one register (16-bit halves; the host refuses GPU milli totals >= 2^16
-// there): 16 VGPRs instead of 32 for the four node slots.  Updates are plain
-// 32-bit adds of the shifted delta -- a GPU never holds less than it gives
-// back or more than its total, so a half never borrows from or carries into
-// the other.
-template <int NPASS>
+// GP (on 256-node clusters, NPASS = 4, and in the row kernels) packs the
+// per-GPU milli left of two GPUs into one register (16-bit halves; the host
+// refuses GPU milli totals >= 2^16 there): 16 VGPRs instead of 32 for the four
+// node slots, 4 instead of 8 per row lane.  Updates are plain 32-bit adds of
+// the shifted delta -- a GPU never holds less than it gives back or more than
+// its total, so a half never borrows from or carries into the other.
+template <int NPASS, bool GP = (NPASS >= 4)>
 struct NodeRegs {
-  static constexpr bool kPack = NPASS >= 4;
+  static constexpr bool kPack = GP;
+  static constexpr bool kCst = NPASS >= 4;   // node constants re-read from `cst`
   static constexpr int kGW = kPack ? kGmax / 2 : kGmax;
   int32_t cpu_left[NPASS], mem_left[NPASS], gpu_left[NPASS];
   int32_t gw[NPASS][kGW];
-  // node constants: registers, or (kPack) re-read from the workload's int4
+  // node constants: registers, or (kCst) re-read from the workload's int4
   // table {cpu_total, mem_total, ngpus, gmt1} where used -- 16 VGPRs less
   // through the pop / push phases, which need none of them
-  static constexpr int kCR = kPack ? 1 : NPASS;
+  static constexpr int kCR = kCst ? 1 : NPASS;
   int32_t cpu_total[kCR], mem_total[kCR], ngpus[kCR], gmt1[kCR];
-  const int4* cst;   // kPack: DevWorkload::node_c4, [slot * 64 + lane]
+  const int4* cst;   // kCst: DevWorkload::node_c4, [slot * 64 + lane]
   __device__ __forceinline__ int4 c4(int ps) const { return cst[ps * kWave + lane_id()]; }
-  __device__ __forceinline__ int32_t ctot(int ps) const { if constexpr (kPack) return c4(ps).x; else return cpu_total[ps]; }
-  __device__ __forceinline__ int32_t mtot(int ps) const { if constexpr (kPack) return c4(ps).y; else return mem_total[ps]; }
-  __device__ __forceinline__ int32_t ngp(int ps) const { if constexpr (kPack) return c4(ps).z; else return ngpus[ps]; }
-  __device__ __forceinline__ int32_t gmt(int ps) const { if constexpr (kPack) return c4(ps).w; else return gmt1[ps]; }
+  __device__ __forceinline__ int32_t ctot(int ps) const { if constexpr (kCst) return c4(ps).x; else return cpu_total[ps]; }
+  __device__ __forceinline__ int32_t mtot(int ps) const { if constexpr (kCst) return c4(ps).y; else return mem_total[ps]; }
+  __device__ __forceinline__ int32_t ngp(int ps) const { if constexpr (kCst) return c4(ps).z; else return ngpus[ps]; }
+  __device__ __forceinline__ int32_t gmt(int ps) const { if constexpr (kCst) return c4(ps).w; else return gmt1[ps]; }
   __device__ __forceinline__ int32_t gt(int ps, int j) const { return j < ngp(ps) ? gmt(ps) : 0; }
   // GPU j's milli left on node slot ps
   __device__ __forceinline__ int32_t g(int ps, int j) const {
@@ -195,8 +196,8 @@ enum Phase { PH_POP = 0, PH_DELETE = 1, PH_SCORE = 2, PH_FAIL = 3, PH_COMMIT = 4
 
 // GPU pick on one node (lane-local): mask of the `need` tightest-fitting
 // eligible GPUs (stable: ties by index) or the first `need` eligible GPUs.
-template <int NPASS>
-__device__ __forceinline__ int pick_gpus(const NodeRegs<NPASS>& nr, int ps, int gm, int need, bool first_fit,
+template <int NPASS, bool GP>
+__device__ __forceinline__ int pick_gpus(const NodeRegs<NPASS, GP>& nr, int ps, int gm, int need, bool first_fit,
                                          int& ok) {
   const int ng = nr.ngp(ps);
   int cnt = 0;
@@ -238,8 +239,8 @@ __device__ __forceinline__ int pick_gpus(const NodeRegs<NPASS>& nr, int ps, int 
 constexpr int kInvCols = 3 + kGmax;   // cpu, mem, gpu count, per-GPU milli
 __host__ __device__ inline int inv_words_for(int npass) { return (kWave * npass * kInvCols * 4 + 7) / 8; }
 
-template <int NPASS, class Heap>
-__device__ bool invariants_hold(const DevWorkload& W, const Heap& heap, int n, const NodeRegs<NPASS>& nr,
+template <int NPASS, class Heap, bool GP>
+__device__ bool invariants_hold(const DevWorkload& W, const Heap& heap, int n, const NodeRegs<NPASS, GP>& nr,
                                 FKS_LDS int32_t* inv, int lane) {
   for (int i = lane; i < kWave * NPASS * kInvCols; i += kWave) inv[i] = 0;
   __syncthreads();
@@ -322,7 +323,7 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
     nr.cpu_left[ps] = W.cpu_left0[node];
     nr.mem_left[ps] = W.mem_left0[node];
     nr.gpu_left[ps] = W.gpu_left0[node];
-    if constexpr (!NodeRegs<NPASS>::kPack) {
+    if constexpr (!NodeRegs<NPASS>::kCst) {
       nr.cpu_total[ps] = W.cpu_total[node];
       nr.mem_total[ps] = W.mem_total[node];
       nr.ngpus[ps] = W.ngpus[node];
@@ -364,7 +365,7 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
       int ol = lane;
       asm volatile("" : "+v"(ol));
       heap.lane = ol;
-      if constexpr (!NodeRegs<NPASS>::kPack) {
+      if constexpr (!NodeRegs<NPASS>::kCst) {
 #pragma unroll
         for (int ps = 0; ps < NPASS; ++ps) asm volatile("" : "+v"(nr.ngpus[ps]));
       } else {

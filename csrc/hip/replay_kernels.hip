@@ -263,8 +263,8 @@ struct NativeScorerDev {
   ProgFn fn;
   const int64_t* gmem;   // [node][kGmax] GPU memory MiB
   KcPtr kc;              // the policy's [budget, constants...], staged in LDS
-  template <int NPASS>
-  __device__ int64_t score(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, int& exc) {
+  template <int NPASS, bool GP>
+  __device__ int64_t score(int ps, const NodeRegs<NPASS, GP>& nr, const PodView& pod, int& exc) {
     const int node = ps * kWave + lane_id();
     int32_t gl[kGmax], gt[kGmax];
 #pragma unroll

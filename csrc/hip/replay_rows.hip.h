@@ -480,7 +480,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
   // per-policy state (row-uniform except the node registers / lane-owned slots)
   int p = claim();
   int family = FAM;
-  NodeRegs<1> nr;
+  NodeRegs<1, !kNative> nr;   // builtin families: two GPUs per register (host: GPU milli totals < 2^16)
   auto load_consts = [&]() {
     const FKS_LDS int32_t* e = ntab + jv * kNodeConsts;
     nr.cpu_total[0] = e[0];

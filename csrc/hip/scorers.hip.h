@@ -35,8 +35,8 @@ __device__ __forceinline__ double trunc_score_f(double s, int& exc) {
   return v > 1.0 ? v : 1.0;
 }
 
-template <int NPASS>
-__device__ __forceinline__ bool feasible(int ps, const NodeRegs<NPASS>& nr, const PodView& pod) {
+template <int NPASS, bool GP>
+__device__ __forceinline__ bool feasible(int ps, const NodeRegs<NPASS, GP>& nr, const PodView& pod) {
   if (pod.cpu > nr.cpu_left[ps] || pod.mem > nr.mem_left[ps] || pod.ngpu > nr.gpu_left[ps]) return false;
   if (pod.ngpu > 0) {
     int avail = 0;
@@ -70,8 +70,8 @@ struct BuiltinScorerDev {
     wp = p;
   }
 
-  template <int NPASS>
-  __device__ int64_t score(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, int& exc) const {
+  template <int NPASS, bool GP>
+  __device__ int64_t score(int ps, const NodeRegs<NPASS, GP>& nr, const PodView& pod, int& exc) const {
     if (!feasible<NPASS>(ps, nr, pod)) return 0;
     // weights are re-read (scalar-cache hits) at every call rather than held in
     // SGPRs across the event loop: the opaque pointer stops the compiler from
@@ -99,8 +99,8 @@ struct BuiltinScorerDev {
   // The family formulas on an already-loaded weight vector (shared with the
   // 4-policies-per-wave row kernel, replay_rows.hip.h, whose weights come
   // from LDS).  The caller has checked feasibility.
-  template <int NPASS, class WP>
-  __device__ static int64_t score_weights(int family, WP w, int ps, const NodeRegs<NPASS>& nr,
+  template <int NPASS, class WP, bool GP>
+  __device__ static int64_t score_weights(int family, WP w, int ps, const NodeRegs<NPASS, GP>& nr,
                                           const PodView& pod, int& exc) {
     switch (FAM >= 0 ? FAM : family) {
       case FAM_FIRST_FIT:
@@ -145,8 +145,8 @@ struct BuiltinScorerDev {
   // the weighted terms are accumulated as they are produced (same order and
   // rounding as `score += w_k * (f_k)`), so no 16-double feature vector is
   // held live across the node loop.
-  template <int NPASS, class WP>
-  __device__ static double composite(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, WP w) {
+  template <int NPASS, class WP, bool GP>
+  __device__ static double composite(int ps, const NodeRegs<NPASS, GP>& nr, const PodView& pod, WP w) {
     const int ng = nr.ngp(ps);
     const bool gpod = pod.ngpu > 0;
     // 32-bit temporaries: GPU milli totals < 2^20 (prepare_device_workload),
@@ -205,8 +205,8 @@ struct BuiltinScorerDev {
   // 0.001 is RN(1/1000); the host's fast_div check covers [0, 2^21)) and the
   // host-verified node / GPU-capacity reciprocals, read per node pass from the
   // workload's tables (no registers held across passes).
-  template <int NPASS, class WP>
-  __device__ static double composite_fast(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, WP w,
+  template <int NPASS, class WP, bool GP>
+  __device__ static double composite_fast(int ps, const NodeRegs<NPASS, GP>& nr, const PodView& pod, WP w,
                                           const double* z, double zcap) {
     const int ng = nr.ngp(ps);
     const bool gpod = pod.ngpu > 0;
@@ -267,8 +267,8 @@ struct BuiltinScorerDev {
     double zcap;         // RN(1 / max(gpu_left * gmilli_total, 1)) when fast_cap, else 0
     double dc, dm, dg;   // max(cpu_total, 1), max(mem_total, 1), max(ngpus, 1) as doubles
   };
-  template <class WP>
-  __device__ static double composite_row(const NodeRegs<1>& nr, const PodView& pod, WP w, const RowRecip& rz) {
+  template <class WP, bool GP>
+  __device__ static double composite_row(const NodeRegs<1, GP>& nr, const PodView& pod, WP w, const RowRecip& rz) {
     const int ng = nr.ngpus[0];
     const bool gpod = pod.ngpu > 0;
     const int32_t ct = nr.cpu_total[0], mt = nr.mem_total[0];
@@ -312,8 +312,8 @@ struct BuiltinScorerDev {
     return s;
   }
 
-  template <int NPASS>
-  __device__ static void features(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, double* f) {
+  template <int NPASS, bool GP>
+  __device__ static void features(int ps, const NodeRegs<NPASS, GP>& nr, const PodView& pod, double* f) {
     const int ng = nr.ngp(ps);
     const int64_t cpu_tot = nr.ctot(ps) > 1 ? nr.ctot(ps) : 1;
     const int64_t mem_tot = nr.mtot(ps) > 1 ? nr.mtot(ps) : 1;

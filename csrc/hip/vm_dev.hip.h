@@ -64,8 +64,8 @@ struct VmScorerDev {
     vregs = vreg_base;
   }
 
-  template <int NPASS>
-  __device__ int64_t score(int ps, const NodeRegs<NPASS>& nr, const PodView& pod, int& exc) {
+  template <int NPASS, bool GP>
+  __device__ int64_t score(int ps, const NodeRegs<NPASS, GP>& nr, const PodView& pod, int& exc) {
     const int lane = lane_id();
     const int node = ps * kWave + lane;
     int off = 0;

@@ -28,11 +28,14 @@ struct Result {
   std::string reason;
   std::vector<uint32_t> words;      // machine code (position independent except relocs)
   std::vector<uint32_t> relocs;     // triples: lo literal word, hi literal word, byte offset of the PC
-  int n_insns = 0, vgprs = 0, sgprs = 0, calls = 0, vregs = 0, tagged = 0, mir = 0;
+  int n_insns = 0, vgprs = 0, sgprs = 0, calls = 0, vregs = 0, tagged = 0, mir = 0, spills = 0;
 };
 
 // bytecode -> gfx950 machine code (never throws: failures come back as !ok + reason)
 Result compile(const ProgramDesc& p);
+
+// Test hook: cap the VGPR pairs for virtual registers (0: none) -> forces spills.
+void set_pair_cap(int pairs);
 
 // Human-readable listing of the generated machine-instruction stream (debugging).
 std::string listing(const ProgramDesc& p);

@@ -25,9 +25,14 @@
 //    iteration budget (EXC_BUDGET), so every loop ends;
 //  * exceptions are "soft" per lane, exactly as the C++ codegen: the first
 //    exception is kept, the lane keeps running until the next RET / back edge;
-//  * anything the baseline tier does not lower (an unknown opcode, register
-//    pressure) throws CodegenError and the program goes to the LLVM tier or
-//    the VMs.
+//  * register pressure beyond the caller-saved pairs: the virtual registers
+//    with the highest interference per use live in per-lane scratch slots at
+//    [s32, s32 + 8k); every instruction that touches one reloads it into a
+//    reserved pair first and stores it back after (a runtime call's save area
+//    starts above the slots);
+//  * anything the baseline tier does not lower (an unknown opcode, more than
+//    kMaxSpills spilled registers) throws CodegenError and the program goes to
+//    the LLVM tier or the VMs.
 #pragma once
 
 #include <array>
@@ -61,8 +66,16 @@ struct ProgIn {
 };
 
 struct GenStats {
-  int vregs = 0, vgprs_used = 0, sgprs_used = 0, calls = 0, tagged = 0;
+  int vregs = 0, vgprs_used = 0, sgprs_used = 0, calls = 0, tagged = 0, spills = 0;
 };
+
+// Test hook: at most this many VGPR pairs for virtual registers (0: no cap),
+// so CPU tests can force the spill path on ordinary programs.
+inline int& pair_cap() {
+  static int cap = 0;
+  return cap;
+}
+constexpr int kMaxSpills = 16;   // 128 B of scratch per lane
 
 class Codegen {
  public:
@@ -83,6 +96,7 @@ class Codegen {
       st->tagged = n_tagged_;
       st->vgprs_used = max_vgpr_ + 1;
       st->sgprs_used = max_sgpr_ + 1;
+      st->spills = __builtin_popcountll(spilled_);
     }
     return F_;
   }
@@ -114,6 +128,12 @@ class Codegen {
   std::vector<int> free_spairs_;
   std::vector<int> ctl_spairs_;           // SGPR pairs held by open control frames
   int max_vgpr_ = 0, max_sgpr_ = 0;
+  // ---- spills: registers in scratch slots, reloaded per instruction
+  uint64_t spilled_ = 0;
+  std::array<int, kMaxRegs> slot_{};      // byte offset of a spilled register's slot
+  std::array<int, kMaxRegs> map_{};       // reload pair of a spilled register in the current instruction (-1)
+  int rl_[4] = {-1, -1, -1, -1};          // reload pairs (operands a, b, imm and the destination)
+  int m_tmp_ = -1;                        // pair for writes outside an instruction (bools, zero init)
 
   struct Frame {
     bool loop;
@@ -429,27 +449,73 @@ class Codegen {
     v_spill_ = take_single();
     // colour virtual registers (most-constrained first)
     base_.fill(-1);
-    std::vector<int> order;
+    map_.fill(-1);
+    slot_.fill(-1);
+    std::vector<int> regs;
     for (int r = 0; r < kMaxRegs; ++r)
-      if (used >> r & 1) order.push_back(r);
-    n_vregs_ = (int)order.size();
-    std::sort(order.begin(), order.end(),
-              [&](int a, int b) { return __builtin_popcountll(adj[a]) > __builtin_popcountll(adj[b]); });
-    std::vector<int> colour_base;   // colour -> VGPR pair
-    std::vector<int> colour(kMaxRegs, -1);
-    for (int r : order) {
-      std::vector<char> busy(colour_base.size(), 0);
-      for (int q = 0; q < kMaxRegs; ++q)
-        if ((adj[r] >> q & 1) && colour[q] >= 0) busy[(size_t)colour[q]] = 1;
-      int c = -1;
-      for (size_t k = 0; k < busy.size(); ++k)
-        if (!busy[k]) { c = (int)k; break; }
-      if (c < 0) {
-        colour_base.push_back(take_pair());
-        c = (int)colour_base.size() - 1;
+      if (used >> r & 1) regs.push_back(r);
+    n_vregs_ = (int)regs.size();
+    if (pair_cap() > 0 && (int)pairs.size() > pair_cap()) pairs.resize((size_t)pair_cap() + 5);
+    // colours for the registers outside `spill` from `pool`; false: not enough pairs
+    auto colour_with = [&](uint64_t spill, const std::vector<int>& pool, size_t cap) {
+      std::vector<int> order;
+      for (int r : regs)
+        if (!(spill >> r & 1)) order.push_back(r);
+      std::stable_sort(order.begin(), order.end(),
+                       [&](int a, int b) { return __builtin_popcountll(adj[a]) > __builtin_popcountll(adj[b]); });
+      std::vector<int> colour(kMaxRegs, -1);
+      size_t n_col = 0;
+      for (int r : order) {
+        std::vector<char> busy(n_col, 0);
+        for (int q = 0; q < kMaxRegs; ++q)
+          if ((adj[r] >> q & 1) && colour[q] >= 0) busy[(size_t)colour[q]] = 1;
+        int c = -1;
+        for (size_t k = 0; k < busy.size(); ++k)
+          if (!busy[k]) { c = (int)k; break; }
+        if (c < 0) {
+          if (n_col >= std::min(cap, pool.size())) return false;
+          c = (int)n_col++;
+        }
+        colour[r] = c;
       }
-      colour[r] = c;
-      base_[r] = colour_base[(size_t)c];
+      for (int r : order) base_[r] = pool[(size_t)colour[r]];
+      for (size_t k = 0; k < n_col; ++k) max_vgpr_ = std::max(max_vgpr_, pool[k] + 1);
+      return true;
+    };
+    const size_t cap0 = pair_cap() > 0 ? (size_t)pair_cap() : pairs.size();
+    if (!colour_with(0, pairs, cap0)) {
+      // spill: reserve the reload pairs, then move registers to scratch -- most
+      // interference per static use first -- until the rest colour
+      if (pairs.size() < 6) throw CodegenError("out of VGPR pairs");
+      std::vector<int> pool(pairs.begin(), pairs.end());
+      for (int k = 0; k < 4; ++k) rl_[k] = pool[(size_t)k];
+      m_tmp_ = pool[4];
+      for (int k = 0; k < 5; ++k) max_vgpr_ = std::max(max_vgpr_, pool[(size_t)k] + 1);
+      pool.erase(pool.begin(), pool.begin() + 5);
+      std::array<int, kMaxRegs> nuse{};
+      for (int pc = 0; pc < n_; ++pc) {
+        const uint64_t ud = uses(pc) | defs(pc);
+        for (int r = 0; r < kMaxRegs; ++r) nuse[r] += (int)(ud >> r & 1);
+      }
+      // (control-flow instructions are safe too: labels inside ELSE / ENDIF /
+      // LOOP_EXIT precede no register access, IF / LOOP_TEST read their
+      // condition right after the reload, LOOP_BEGIN places the loop head
+      // before the next instruction's reloads)
+      std::vector<int> cand(regs);
+      std::stable_sort(cand.begin(), cand.end(), [&](int a, int b) {
+        return (int64_t)__builtin_popcountll(adj[a]) * (1 + nuse[b]) > (int64_t)__builtin_popcountll(adj[b]) * (1 + nuse[a]);
+      });
+      const size_t cap1 = pair_cap() > 0 ? (size_t)pair_cap() : pool.size();
+      bool ok = false;
+      for (int r : cand) {
+        if (__builtin_popcountll(spilled_) >= kMaxSpills) break;
+        slot_[r] = 8 * __builtin_popcountll(spilled_);
+        spilled_ |= 1ull << r;
+        base_.fill(-1);
+        if (colour_with(spilled_, pool, cap1)) { ok = true; break; }
+      }
+      if (!ok) throw CodegenError("out of VGPR pairs");
+      F_.spill_bytes = 8 * __builtin_popcountll(spilled_);
     }
     // SGPR pairs: s[24:25] and s[28:29] are macro scratch; s30-s33 ABI; callee-saved ones untouched
     free_spairs_ = {0, 2, 4, 6, 8, 10, 12, 14, 16, 18, 20, 22, 26, 40, 42, 44, 46, 56, 58, 60, 62, 72, 74, 76, 78,
@@ -511,8 +577,53 @@ class Codegen {
   void materialize(int r) {
     if (!(pend_ >> r & 1)) return;
     pend_ &= ~(1ull << r);
+    if (spilled_ >> r & 1) {   // into the register's reload pair (if mapped) and its slot
+      const int p = map_[r] >= 0 ? map_[r] : m_tmp_;
+      e(mk(V_CNDMASK_B32, v(p), ic(0), ic(1), s(bm_pair_[bm_of_[r]])));
+      e(mk(V_MOV_B32, v(p + 1), ic(0)));
+      spill_store(r, p);
+      return;
+    }
     e(mk(V_CNDMASK_B32, R(r), ic(0), ic(1), s(bm_pair_[bm_of_[r]])));
     e(mk(V_MOV_B32, Rh(r), ic(0)));
+  }
+  // scratch slot of spilled register r <-> VGPR pair p (active lanes)
+  void spill_store(int r, int p) {
+    for (int h = 0; h < 2; ++h) {
+      MI st = mk(SCRATCH_STORE_DWORD, NONE, NONE, s(32), v(p + h));
+      st.imm = slot_[r] + 4 * h;
+      e(st);
+    }
+  }
+  void spill_load(int r, int p) {
+    for (int h = 0; h < 2; ++h) {
+      MI ld = mk(SCRATCH_LOAD_DWORD, v(p + h), NONE, s(32));
+      ld.imm = slot_[r] + 4 * h;
+      e(ld);
+    }
+  }
+  // before instruction pc: its spilled operands (and destination: partial
+  // writes keep the inactive lanes' value) in reload pairs
+  void spill_in(int pc) {
+    const uint64_t need = (uses(pc) | defs(pc)) & spilled_;
+    if (!need) return;
+    int k = 0;
+    for (int r = 0; r < kMaxRegs; ++r)
+      if (need >> r & 1) {
+        if (k >= 4) throw CodegenError("internal: more than four spilled registers in one instruction");
+        map_[r] = rl_[k++];
+        spill_load(r, map_[r]);
+      }
+    e(mkimm(S_WAITCNT, 0x0F70));   // vmcnt(0)
+  }
+  // after it: the destination back to its slot (a bool still only in its
+  // mask is stored when it is materialised)
+  void spill_out(int pc) {
+    if (!spilled_) return;
+    const uint64_t dd = defs(pc) & spilled_;
+    for (int r = 0; r < kMaxRegs; ++r)
+      if ((dd >> r & 1) && !(pend_ >> r & 1) && map_[r] >= 0) spill_store(r, map_[r]);
+    map_.fill(-1);
   }
   void materialize_live(uint64_t live) {
     for (int r = 0; r < kMaxRegs; ++r)
@@ -535,6 +646,10 @@ class Codegen {
     bm_of_[r] = (int8_t)slot;
   }
   uint16_t R(int r) const {
+    if (spilled_ >> r & 1) {
+      if (map_[r] < 0) throw CodegenError("spilled register used outside its instruction");
+      return v(map_[r]);
+    }
     if (base_[r] < 0) throw CodegenError("register without a home");
     return v(base_[r]);
   }
@@ -690,6 +805,8 @@ class Codegen {
     for (int r = 0; r < kMaxRegs; ++r)
       if ((live >> r & 1) && base_[r] >= 0) bases.insert(base_[r]);
     for (int b : bases) { out.push_back(b); out.push_back(b + 1); }
+    for (int r = 0; r < kMaxRegs; ++r)   // spilled operands reloaded for this instruction
+      if (map_[r] >= 0) { out.push_back(map_[r]); out.push_back(map_[r] + 1); }
     std::sort(out.begin(), out.end());
     out.erase(std::unique(out.begin(), out.end()), out.end());
     return out;
@@ -785,8 +902,15 @@ class Codegen {
       e(mkimm(S_WAITCNT, 0xC07F));
       e(mk(V_MOV_B32, v(v_bud_), T(0)));
     }
-    for (int r = 0; r < kMaxRegs; ++r)
-      if ((live_in_[0] >> r & 1) && base_[r] >= 0) e(mk(V_MOV_B64, R(r), ic(0)));
+    for (int r = 0; r < kMaxRegs; ++r) {
+      if (!(live_in_[0] >> r & 1)) continue;
+      if (spilled_ >> r & 1) {
+        e(mk(V_MOV_B64, v(m_tmp_), ic(0)));
+        spill_store(r, m_tmp_);
+      } else if (base_[r] >= 0) {
+        e(mk(V_MOV_B64, R(r), ic(0)));
+      }
+    }
     const int l_end = label();
     for (int pc = 0; pc < n_; ++pc) {
       auto it = label_at_pc_.find(pc);
@@ -797,7 +921,9 @@ class Codegen {
       // their EXEC frames (an ENDIF after a then-branch that always returns
       // is unreached by flow, yet the IF branches to it)
       if (!reached_[pc] && !structural(P_.code[pc].op)) continue;
+      spill_in(pc);
       emit_op(pc);
+      spill_out(pc);
     }
     if (!frames_.empty()) throw CodegenError("unbalanced control flow");
     // epilogue: v[0:1] = exc ? -exc : out
@@ -864,7 +990,7 @@ class Codegen {
           set_tag_static(d, false);
           break;
         }
-        if (base_[d] != base_[a]) e(mk(V_MOV_B64, R(d), R(a)));
+        if (R(d) != R(a)) e(mk(V_MOV_B64, R(d), R(a)));
         copy_tag(d, a, ta);
         bm_of_[d] = bm_of_[a];
         break;
@@ -973,7 +1099,7 @@ class Codegen {
       case OP_NEG: case OP_ABS:
         if (ta == TY_IF) { rtcall(1, in.op, pc, d, a, ta); break; }
         if (ta == TY_F) {
-          if (base_[d] != base_[a]) e(mk(V_MOV_B32, R(d), R(a)));
+          if (R(d) != R(a)) e(mk(V_MOV_B32, R(d), R(a)));
           if (in.op == OP_NEG) e(mklit(V_XOR_B32, Rh(d), 0x80000000u, Rh(a)));
           else e(mklit(V_AND_B32, Rh(d), 0x7FFFFFFFu, Rh(a)));
           set_tag_static(d, true);
@@ -996,7 +1122,7 @@ class Codegen {
       case OP_INT: case OP_ROUND:
         if (ta == TY_IF) { rtcall(1, in.op, pc, d, a, ta); break; }
         if (ta == TY_I) {
-          if (base_[d] != base_[a]) e(mk(V_MOV_B64, R(d), R(a)));
+          if (R(d) != R(a)) e(mk(V_MOV_B64, R(d), R(a)));
           set_tag_static(d, false);
           break;
         }
@@ -1028,7 +1154,7 @@ class Codegen {
             pend_ |= 1ull << d;
           } else {
             pend_ &= ~(1ull << d);
-            if (base_[d] != base_[a]) e(mk(V_MOV_B64, R(d), R(a)));
+            if (R(d) != R(a)) e(mk(V_MOV_B64, R(d), R(a)));
           }
           bm_of_[d] = bm_of_[a];
           set_tag_static(d, false);

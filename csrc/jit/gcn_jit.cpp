@@ -76,6 +76,7 @@ Result compile(const ProgramDesc& p) {
     r.calls = st.calls;
     r.vregs = st.vregs;
     r.tagged = st.tagged;
+    r.spills = st.spills;
     r.mir = (int)f.mi.size();
     r.ok = true;
   } catch (const std::exception& e) {
@@ -84,6 +85,8 @@ Result compile(const ProgramDesc& p) {
   }
   return r;
 }
+
+void set_pair_cap(int pairs) { gcn::pair_cap() = pairs < 0 ? 0 : pairs; }
 
 std::string listing(const ProgramDesc& p) {
   std::ostringstream os;

@@ -22,6 +22,7 @@ struct Func {
   std::vector<MI> mi;
   std::vector<CallInfo> calls;
   int n_labels = 0;
+  int spill_bytes = 0;          // per-lane scratch [s32, s32 + spill_bytes): spilled registers
   MacroRegs mr;
   int new_label() { return n_labels++; }
 };
@@ -99,7 +100,7 @@ inline void expand(const Func& f, std::vector<MI>& out, int& next_label) {
         out.push_back(mkimm(S_CBRANCH_EXECZ, skip));
         MI sav = mk(S_OR_SAVEEXEC_B64, s(r.sc), ic(-1));
         out.push_back(sav);
-        int off = 0;
+        int off = f.spill_bytes;   // the save area sits above the spill slots
         for (int g : c.vgprs) {
           MI st = mk(SCRATCH_STORE_DWORD, NONE, NONE, s(32), v(g));
           st.imm = off; off += 4;
@@ -157,7 +158,7 @@ inline void expand(const Func& f, std::vector<MI>& out, int& next_label) {
         out.push_back(mk(V_MOV_B32, (uint16_t)(c.res + 1), v(1)));
         out.push_back(mk(V_MOV_B32, c.resy, v(2)));
         out.push_back(mk(S_OR_SAVEEXEC_B64, s(r.sc), ic(-1)));
-        off = 0;
+        off = f.spill_bytes;
         for (int g : c.vgprs) {
           MI ldv = mk(SCRATCH_LOAD_DWORD, v(g), NONE, s(32));
           ldv.imm = off; off += 4;

@@ -278,7 +278,8 @@ class Evaluator:
         return out
 
     def _evaluate_compiled(self, codes: Sequence[str], compiled: List[Optional[CompiledPolicy]],
-                           native: bool, slot: int = 0, host_only: bool = False) -> List[EvalResult]:
+                           native: bool, slot: int = 0, host_only: bool = False,
+                           object_ok: bool = True) -> List[EvalResult]:
         n = len(codes)
         out: List[Optional[EvalResult]] = [None] * n
         # 1) device: native code, then the bytecode VM
@@ -309,6 +310,13 @@ class Evaluator:
                 self.stats["cpu_vm"] += 1
         # 3) object engine (exact by construction)
         rest = [i for i in range(n) if out[i] is None]
+        if rest and not object_ok:
+            # the caller sheds what only CPython can score (bigint / complex
+            # intermediates): engine "shed", never a score
+            for i in rest:
+                out[i] = EvalResult(0.0, int(Exc.UNSUPPORTED), "shed")
+                self.stats["shed"] = self.stats.get("shed", 0) + 1
+            rest = []
         if rest:
             if self._object_engine_ok():
                 budget_s = float(self.options.get("object_timeout_s", 600.0))
@@ -452,9 +460,10 @@ class Evaluator:
                     self.stats["faults"] = self.stats.get("faults", 0) + 1
         return out  # type: ignore[return-value]
 
-    def fallback_async(self, pend: "PendingPrograms"):
+    def fallback_async(self, pend: "PendingPrograms", object_ok: bool = True):
         """Score ``pend.fallback_idx`` on the host engines (CPU VM, then
-        CPython) in a worker thread; the future yields (indices, results)."""
+        CPython unless `object_ok` is False) in a worker thread; the future
+        yields (indices, results)."""
         idx = list(pend.fallback_idx)
         codes = [pend.codes[i] for i in idx]
         compiled = [pend.compiled[i] for i in idx]
@@ -464,7 +473,7 @@ class Evaluator:
                 self._fallback_pool = ThreadPoolExecutor(max_workers=2, thread_name_prefix="fks-fallback")
 
         def job():
-            res = self._evaluate_compiled(codes, compiled, native=False, host_only=True)
+            res = self._evaluate_compiled(codes, compiled, native=False, host_only=True, object_ok=object_ok)
             if self.fault_rate > 0:
                 for k in range(len(res)):
                     if self._fault_rng.random() < self.fault_rate:

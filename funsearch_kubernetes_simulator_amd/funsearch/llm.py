@@ -366,9 +366,47 @@ class MutationClient(BaseClient):
             k = rng.randrange(len(bodies))
             body = bodies[k]
             other = bodies[1 - k] if len(bodies) >= 2 else None
+        if len(body) > self.max_body_chars:
+            # bloat control: a parent grown past the size of LLM-written policies
+            # loses random score terms first (children of ever-growing parents
+            # cost the producers, the JIT's registers and the host fallbacks)
+            body = self._prune(body, rng, int(0.8 * self.max_body_chars))
         for _ in range(1 + int(rng.random() < 0.5 * max(0.2, temperature))):
             body = self._mutate(body, rng, other)
         return _response(self._indent(body))
+
+    #: body size (characters) past which a parent is pruned before mutation; the
+    #: longest LLM-found champion bodies in data/policies are ~2,300 characters
+    max_body_chars = 3000
+
+    @staticmethod
+    def _score_only(stmt: ast.stmt) -> bool:
+        """A statement that only updates ``score`` (droppable without leaving a
+        later read of a name it defined)."""
+        def upd(s):
+            if isinstance(s, ast.AugAssign):
+                return isinstance(s.target, ast.Name) and s.target.id == "score"
+            if isinstance(s, ast.Assign):
+                return len(s.targets) == 1 and isinstance(s.targets[0], ast.Name) and s.targets[0].id == "score"
+            if isinstance(s, ast.If):
+                return all(upd(x) for x in s.body + s.orelse)
+            return False
+        return upd(stmt)
+
+    def _prune(self, body: str, rng: random.Random, limit: int) -> str:
+        try:
+            tree = ast.parse(body)
+        except SyntaxError:
+            return body
+        size = len(body)
+        while size > limit:
+            cands = [i for i, st in enumerate(tree.body) if i > 0 and self._score_only(st)]
+            if not cands:
+                break
+            i = rng.choice(cands)
+            size -= len(ast.unparse(tree.body[i])) + 1
+            del tree.body[i]
+        return ast.unparse(tree)
 
     # -- operators ----------------------------------------------------------------------
     #: (cumulative probability, operator).  Structural operators (new terms from

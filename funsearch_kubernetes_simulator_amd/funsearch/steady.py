@@ -109,6 +109,8 @@ class SteadyStats:
     rejected: int = 0
     migrations: int = 0
     fallback: int = 0                # programs scored by the host engines (async)
+    shed: int = 0                    # children only CPython could score, not evaluated (host_object off)
+    abandoned: int = 0               # host fallbacks still queued when the run stopped
     producer_cpu_s: float = 0.0
     inflight_sum: float = 0.0        # programs in flight x seconds
     inflight_n: float = 0.0          # seconds observed
@@ -120,8 +122,14 @@ class SteadyStateSearch:
     distributed context, log and checkpoint settings)."""
 
     def __init__(self, fs, batch: int = 256, slots: Optional[int] = None, producers: int = 0,
-                 task_size: int = 8, status_every_s: float = 5.0, tierup: bool = False, ahead: int = 2):
+                 task_size: int = 8, status_every_s: float = 5.0, tierup: bool = False, ahead: int = 2,
+                 host_object: bool = False):
         self.fs = fs
+        #: children only CPython can score (bigint / complex intermediates, ~1% of
+        #: mutated programs, ~3 s each on one core) go to the object engine only
+        #: when True; else they are shed (counted, never merged) -- the search
+        #: loses ~1% of its children instead of its host cores
+        self.host_object = bool(host_object)
         self.batch = int(batch)
         #: batches compiled and loaded ahead of a free slot (the stager thread)
         self.ahead = max(1, int(ahead))
@@ -215,7 +223,7 @@ class SteadyStateSearch:
             max_workers=self.producers, mp_context=ctx_mp, initializer=_producer_init,
             initargs=(llm_cfg, timeout_s, 1000 * ctx.rank + 1))
         inflight_tasks: List[concurrent.futures.Future] = []
-        fallbacks: list = []             # (batch items, future of the host-engine fallback)
+        fallbacks: list = []             # (batch items, future of the host-engine fallback, programs)
         staged: collections.deque = collections.deque()   # (batch items, future of prepare_compiled)
         stager = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="fks-stage")
         ready: List[tuple] = []          # produced children waiting for a batch
@@ -304,16 +312,21 @@ class SteadyStateSearch:
                     progressed = True
                 # 4a) host-engine fallbacks that finished -> merge
                 still_fb = []
-                for items, fut in fallbacks:
+                for items, fut, nfb in fallbacks:
                     if not fut.done():
-                        still_fb.append((items, fut))
+                        still_fb.append((items, fut, nfb))
+                        continue
+                    if fut.cancelled():
                         continue
                     idx, res = fut.result()
                     t_m = time.perf_counter()
                     for i, r in zip(idx, res):
                         isl, code, _ = items[i]
-                        self._merge_one(islands[isl], code, r.score)
                         merged[isl] += 1
+                        if r.engine == "shed":
+                            self.stats.shed += 1
+                            continue
+                        self._merge_one(islands[isl], code, r.score)
                     self.stats.fallback += len(idx)
                     self.phase["merge"] += time.perf_counter() - t_m
                     progressed = True
@@ -328,7 +341,8 @@ class SteadyStateSearch:
                     t_ph = time.perf_counter()
                     results = ev.collect(b.pend, defer_fallback=True)
                     if b.pend.fallback_idx:
-                        fallbacks.append((b.items, ev.fallback_async(b.pend)))
+                        fallbacks.append((b.items, ev.fallback_async(b.pend, object_ok=self.host_object),
+                                          len(b.pend.fallback_idx)))
                     t_m = time.perf_counter()
                     self.phase["collect"] += t_m - t_ph
                     t_done = time.time()
@@ -382,6 +396,16 @@ class SteadyStateSearch:
                 if now - t_status >= self.status_every_s:
                     t_status = now
                     self._status(now, t_start, busy_since, batches, ready, inflight_tasks, merged, global_best)
+                # stopping: host fallbacks not started yet are abandoned (a CPU-VM
+                # replay of a large program takes seconds of a core)
+                if stop and fallbacks and all(b is None for b in batches) and not staged:
+                    kept = []
+                    for items, fut, nfb in fallbacks:
+                        if fut.cancel():
+                            self.stats.abandoned += nfb
+                        else:
+                            kept.append((items, fut, nfb))
+                    fallbacks = kept
                 # 7) done?  (every child merged, or stopping; then every agreed gather finished)
                 all_launched = all(requested[i] >= target_children[i] for i in range(k))
                 idle = (not inflight_tasks and all(b is None for b in batches) and not fallbacks
@@ -430,6 +454,7 @@ class SteadyStateSearch:
                    device_busy=round(busy / wall, 4),
                    new_shape_fraction=round(st.new_shapes / max(1, st.evaluations), 4),
                    native_fraction=round(st.native / max(1, st.evaluations), 4), host_fallback=st.fallback,
+                   shed=st.shed, abandoned=st.abandoned,
                    inflight=inflight, inflight_mean=round(st.inflight_sum / max(1e-9, st.inflight_n), 1),
                    resident_capacity=capacity,
                    occupancy=round(inflight / capacity, 4) if capacity else None,
@@ -448,7 +473,8 @@ class SteadyStateSearch:
                                      or {}).items()},
                    collective_wait_frac=round(self.channel.wait_s / wall, 5),
                    engines={k: v for k, v in fs.evaluator.stats.items() if k in
-                            ("device_native", "device", "cpu_vm", "object", "compile_errors", "jit_shapes")})
+                            ("device_native", "device", "cpu_vm", "object", "shed", "compile_errors", "jit_shapes",
+                             "native_timeout", "native_invariant")})
         fs.log.write(**rec)
         st.history.append(rec)
         if fs.verbose and fs.ctx.is_main and not final:

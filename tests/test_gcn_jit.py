@@ -279,3 +279,53 @@ def test_per_lane_pods_several_rows_in_one_call(corpus):
             if ref in (-100, -101) or emu[n] in (-100, -101):
                 continue
             assert emu[n] == ref, (p.source[-300:], n, pod, (k, v), emu[n])
+
+
+@pytest.mark.parametrize("cap", [2, 3])
+def test_spilled_registers_equal_cpu_vm(corpus, cap):
+    """Register pressure beyond the pairs: with the pool capped at `cap` pairs
+    ordinary programs spill virtual registers to per-lane scratch slots
+    (reloaded per instruction, stored back after, the runtime calls' save area
+    above the slots).  Emulated single events stay equal to the VM."""
+    m = ce.native()
+    rng = random.Random(17 + cap)
+    progs = corpus[::3] + [compile_policy("def priority_function(pod, node):\n    " + b + "\n") for b in (
+        "s = 0.0\n    if pod.cpu_milli > 30000:\n        s = int(pod.cpu_milli * 0.05)\n    s = max(1, s)\n"
+        "    if node.cpu_milli_left > pod.cpu_milli * 2:\n        s += 54.111\n    return max(1, int(s))",
+        "x = node.cpu_milli_left ** 0.5 + (node.memory_mib_left % 7) // 2\n    return x",
+        "g = sorted(node.gpus, key=lambda g: g.gpu_milli_left)[:2]\n    t = 0\n"
+        "    for q in g:\n        t += q.gpu_milli_left\n    return t + len(g) * 3",
+        "a = node.cpu_milli_left; b = node.memory_mib_left; c = node.gpu_left; d = pod.cpu_milli\n"
+        "    e = a * 2 + b; f = b - c * 3; g2 = (a + d) / max(1, b); h = e * f - g2\n"
+        "    return a + b + c + d + e + f + g2 + h")]
+    m.gcn_set_pair_cap(cap)
+    try:
+        spilled = 0
+        for p in progs:
+            info = m.gcn_compile(p.code, list(map(int, p.ctag)), gcnjit.literal_mask(p).tolist(),
+                                 list(map(int, p.iconst)), list(map(float, p.fconst)))
+            if not info["ok"]:
+                assert "VGPR" in info["reason"] or "spilled register" in info["reason"], info["reason"]
+                continue
+            spilled += info["spills"] > 0
+            kc = constant_block(p, 1 << 16).tolist()
+            for _ in range(4):
+                node, gl, gt, gm, pod = _random_event(rng)
+                emu = m.gcn_emu_event(p.code, list(map(int, p.ctag)), gcnjit.literal_mask(p).tolist(),
+                                      list(map(int, p.iconst)), list(map(float, p.fconst)), kc, node, gl, gt, gm, pod)
+                podd = dict(cpu_milli=pod[0], memory_mib=pod[1], num_gpu=pod[2], gpu_milli=pod[3],
+                            creation_time=pod[4], duration_time=pod[5])
+                for n in range(16):
+                    nd = dict(cpu_milli_left=node[6 * n], cpu_milli_total=node[6 * n + 1],
+                              memory_mib_left=node[6 * n + 2], memory_mib_total=node[6 * n + 3],
+                              gpu_left=node[6 * n + 4])
+                    ng = node[6 * n + 5]
+                    k, v = m.score_program_once(p.code, list(p.fconst), list(p.iconst), list(p.ctag), podd, nd,
+                                                gl[8 * n:8 * n + ng], gt[8 * n:8 * n + ng], gm[8 * n:8 * n + ng])
+                    ref = _finish(k, v)
+                    if ref in (-100, -101) or emu[n] in (-100, -101):
+                        continue
+                    assert emu[n] == ref, (p.source[-300:], n, (k, v), emu[n], info["spills"])
+        assert spilled >= len(progs) // 4, (spilled, len(progs))
+    finally:
+        m.gcn_set_pair_cap(0)

@@ -71,3 +71,27 @@ def test_novel_batch_measurement_is_exact(default_workload):
     rec = measure_novel(dev, default_workload, n=64, compile_batches=1, seed=5, cpu_threads=16)
     assert rec["new_shapes"] == 64 and rec["native"] == 64 and rec["bit_identical"], rec
     assert rec["compared"] >= 60 and rec["compile_s_per_64_median"] < 1.0
+
+
+@pytest.mark.parametrize("cap", [2, 3])
+def test_spilled_registers_equal_cpu_vm(default_workload, cap):
+    """Baseline code with virtual registers in per-lane scratch slots (the pool
+    capped at `cap` pairs forces the spill path on ordinary programs): full
+    device replays bit-identical to the CPU VM, runtime calls included (their
+    save area sits above the slots on the kernel's stack)."""
+    from funsearch_kubernetes_simulator_amd.bench.programs import mutation_children
+    from funsearch_kubernetes_simulator_amd.ops import gcnjit
+    m = ce.native()
+    progs = programs()[:24] + mutation_children(24, seed=29)
+    m.gcn_set_pair_cap(cap)
+    try:
+        codes = [(p, gcnjit.compile_program(p)[0]) for p in progs]
+        spilled = [p for p, c in codes if c is not None and c.info["spills"] > 0]
+        assert len(spilled) >= 8, len(spilled)
+        dev = _dev(default_workload, "baseline")
+        assert dev.info()["stack_bytes"] >= 2048
+        nat = dev.evaluate_native(spilled)
+    finally:
+        m.gcn_set_pair_cap(0)
+    vm = ce.simulate_program_batch(default_workload, spilled, threads=16)
+    assert _assert_equal_rows(nat, vm, spilled) >= len(spilled) - 2

@@ -134,3 +134,20 @@ def test_steady_two_gloo_ranks_agree_on_stop(tmp_path):
     outs = _two_ranks(tmp_path, cfg, 36000)
     assert outs[0]["migrations"] == outs[1]["migrations"] <= 4
     assert all(o["evaluations"] < 40 * 4 for o in outs)
+
+
+def test_host_fallback_sheds_object_engine_programs():
+    """A program only CPython can score (an int64 overflow -> bigint in the
+    replay) is shed, not replayed, when the caller turns the object engine
+    off (steady `host_object: false`); with it on, CPython scores it."""
+    from funsearch_kubernetes_simulator_amd.engine import Evaluator
+    from funsearch_kubernetes_simulator_amd.policy.template import PolicyTemplate
+    code = PolicyTemplate.fill_template(
+        "    score = node.cpu_milli_left * node.memory_mib_left * node.cpu_milli_total * node.memory_mib_total\n"
+        "    score = score * 1000000 / 10 ** 30")
+    ev = Evaluator(device="cpu")
+    prog = ev.compile_batch([code])
+    shed = ev._evaluate_compiled([code], prog, native=False, host_only=True, object_ok=False)[0]
+    assert shed.engine == "shed" and ev.stats["shed"] == 1
+    full = ev._evaluate_compiled([code], prog, native=False, host_only=True, object_ok=True)[0]
+    assert full.engine == "object" and full.exc == 0 and full.score > 0
