@@ -88,6 +88,18 @@ def _produce(task):
 
 
 @dataclass
+class _Polish:
+    """A constant-polish batch: literal settings of one island champion (one
+    shape: one JIT compile, then data only; funsearch/polish.py)."""
+    island: int
+    code: str
+    prog: object                   # the champion's CompiledPolicy
+    base: float
+    cands: list                    # {constant-pool index: value} per variant
+    progs: Optional[list] = None   # the variants' CompiledPolicy (until staged)
+
+
+@dataclass
 class _Batch:
     slot: int
     items: list                    # [(island, code, prog)]
@@ -95,6 +107,7 @@ class _Batch:
     t_launch: float
     new_shapes: int = 0
     jit_s: float = 0.0
+    polish: Optional[_Polish] = None
 
 
 @dataclass
@@ -112,6 +125,9 @@ class SteadyStats:
     shed: int = 0                    # children only CPython could score, not evaluated (host_object off)
     abandoned: int = 0               # host fallbacks still queued when the run stopped
     producer_cpu_s: float = 0.0
+    polish_batches: int = 0          # constant-polish batches (variants of an island champion)
+    polish_evals: int = 0            # their device evaluations (not children)
+    polish_improved: int = 0         # polished champions re-entered as children
     inflight_sum: float = 0.0        # programs in flight x seconds
     inflight_n: float = 0.0          # seconds observed
     history: List[dict] = field(default_factory=list)
@@ -133,6 +149,11 @@ class SteadyStateSearch:
         self.batch = int(batch)
         #: batches compiled and loaded ahead of a free slot (the stager thread)
         self.ahead = max(1, int(ahead))
+        #: constant polish of island champions as device batches (the islands'
+        #: ``polish`` config: every / variants; 0 = off)
+        self.polish_every = int(getattr(fs, "polish_every", 0) or 0)
+        self.polish_variants = int(getattr(fs, "polish_variants", 512) or 512)
+        self._polish_count: dict = {}
         dev = getattr(fs.evaluator, "device", None)
         if dev is not None and not tierup:
             # background LLVM recompiles of hot shapes compete with the producer
@@ -193,6 +214,65 @@ class SteadyStateSearch:
                 fs.save_checkpoint()
         return bool(results)
 
+    def _polish_job(self, merged, start_gen, polish_next) -> Optional[_Polish]:
+        """The next due constant polish (round robin over the islands): variants
+        of the island champion's literals, one (1 + lambda) round per polish with
+        the step size cycling through the schedule of funsearch/polish.py."""
+        from ..policy.bytecode import TAG_FLOAT
+        from ..policy.compiler import try_compile
+        from .polish import _perturb, tunable_literals, with_values
+        fs = self.fs
+        gens = self._gen_of(merged)
+        for i in range(len(gens)):
+            g = start_gen + gens[i]
+            if g < polish_next[i]:
+                continue
+            polish_next[i] = g + self.polish_every
+            s = fs.islands[i]
+            if not s.population:
+                continue
+            code, score = max(s.population, key=lambda x: x[1])
+            if not fs.polish_repeat and code in fs._polished:
+                continue
+            fs._polished.add(code)
+            prog, _ = try_compile(code)
+            if prog is None or not prog.device_ok:
+                continue
+            tune = tunable_literals(prog)
+            if not tune:
+                continue
+            base = {prog.literals[j][0]: (prog.fconst[prog.literals[j][0]] if prog.ctag[prog.literals[j][0]] == TAG_FLOAT
+                                          else prog.iconst[prog.literals[j][0]]) for j in range(len(prog.literals))}
+            n_done = self._polish_count.get(i, 0)
+            self._polish_count[i] = n_done + 1
+            sigma = 0.35 * (0.6 ** (n_done % 3))
+            rng = random.Random(hash((fs.ctx.rank, i, g)) & 0xFFFFFFFF)
+            cands = [_perturb(prog, base, tune, sigma, rng) for _ in range(self.polish_variants)]
+            return _Polish(i, code, prog, score, cands, [with_values(prog, v) for v in cands])
+        return None
+
+    def _polish_done(self, job: _Polish, results, ready: list) -> None:
+        """Best variant better than the champion -> its rewritten text enters the
+        island as an ordinary child (re-scored exactly, merged by the usual rules)."""
+        from ..policy.compiler import try_compile
+        from .polish import rewrite_source
+        st = self.stats
+        st.polish_batches += 1
+        st.polish_evals += sum(r is not None for r in results)
+        self.fs.evaluations += sum(r is not None for r in results)
+        scores = [r.score if r is not None and r.exc == 0 else -1.0 for r in results]
+        j = max(range(len(scores)), key=scores.__getitem__) if scores else -1
+        rec = dict(kind="steady_polish", rank=self.fs.ctx.rank, island=job.island, base=round(job.base, 6),
+                   best=round(scores[j], 6) if j >= 0 else None, variants=len(results))
+        if j >= 0 and scores[j] > job.base:
+            text = rewrite_source(job.prog, job.cands[j])
+            prog, _ = try_compile(text)
+            if prog is not None:
+                ready.insert(0, (job.island, text, prog))
+                st.polish_improved += 1
+                rec["improved"] = True
+        self.fs.log.write(**rec)
+
     def _gen_of(self, merged: List[int]) -> List[int]:
         return [m // max(1, s.policies_per_generation) for m, s in zip(merged, self.fs.islands)]
 
@@ -224,7 +304,8 @@ class SteadyStateSearch:
             initargs=(llm_cfg, timeout_s, 1000 * ctx.rank + 1))
         inflight_tasks: List[concurrent.futures.Future] = []
         fallbacks: list = []             # (batch items, future of the host-engine fallback, programs)
-        staged: collections.deque = collections.deque()   # (batch items, future of prepare_compiled)
+        polish_next = [start_gen + self.polish_every] * k   # generation of each island's next polish
+        staged: collections.deque = collections.deque()   # (batch items, future of prepare_compiled, polish job)
         stager = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="fks-stage")
         ready: List[tuple] = []          # produced children waiting for a batch
         batches: List[Optional[_Batch]] = [None] * self.slots
@@ -243,7 +324,7 @@ class SteadyStateSearch:
                 progressed = False
                 # 1) keep producers busy (children from the islands' CURRENT elites)
                 queued = len(ready) + sum(len(b.items) for b in batches if b is not None) + \
-                    sum(len(t) for t, _ in staged) + self.task_size * len(inflight_tasks)
+                    sum(len(t) for t, _, pj in staged if pj is None) + self.task_size * len(inflight_tasks)
                 while (not stop and queued < want_buffer + self.task_size * self.producers
                        and len(inflight_tasks) < 2 * self.producers):
                     cands = [i for i in range(k) if requested[i] < target_children[i]]
@@ -283,7 +364,16 @@ class SteadyStateSearch:
                 inflight_tasks = still
                 # 3a) stage the next batches: JIT compile + module loads on the stager
                 # thread while the slots are busy, so a freed slot relaunches at once
-                # (a partial batch when nothing else is coming)
+                # (a partial batch when nothing else is coming); a due constant polish
+                # of an island champion goes first
+                if self.polish_every and not stop and len(staged) < self.ahead:
+                    job = self._polish_job(merged, start_gen, polish_next)
+                    if job is not None:
+                        items = [(job.island, job.code, pv) for pv in job.progs]
+                        staged.append((items, stager.submit(ev.prepare_compiled, [job.code] * len(items),
+                                                            job.progs, False), job))
+                        job.progs = None
+                        progressed = True
                 while ready and len(staged) < self.ahead:
                     tail = not inflight_tasks and all(requested[i] >= target_children[i] for i in range(k))
                     if len(ready) < self.batch and not (
@@ -291,19 +381,19 @@ class SteadyStateSearch:
                         break
                     take, ready = ready[:self.batch], ready[self.batch:]
                     staged.append((take, stager.submit(ev.prepare_compiled, [c for _, c, _ in take],
-                                                       [p for _, _, p in take])))
+                                                       [p for _, _, p in take]), None))
                     progressed = True
                 # 3b) launch staged batches (in order) on free slots
                 for si in range(self.slots):
                     if batches[si] is not None or not staged or not staged[0][1].done():
                         continue
-                    take, fut = staged.popleft()
+                    take, fut, pjob = staged.popleft()
                     pend = fut.result()
                     with roctx_range(f"steady.launch slot {si} ({len(take)} programs)"):
                         t_ph = time.perf_counter()
                         ev.launch_prepared(pend, si)
                         self.phase["submit"] += time.perf_counter() - t_ph
-                    b = _Batch(si, take, pend, time.time(), pend.new_shapes, pend.jit_s)
+                    b = _Batch(si, take, pend, time.time(), pend.new_shapes, pend.jit_s, pjob)
                     batches[si] = b
                     self.stats.jit_s += pend.jit_s
                     self.stats.new_shapes += pend.new_shapes
@@ -339,7 +429,19 @@ class SteadyStateSearch:
                     if b is None or not ev.ready(b.pend):
                         continue
                     t_ph = time.perf_counter()
-                    results = ev.collect(b.pend, defer_fallback=True)
+                    # (no device: a polish batch is scored here, on the host engines)
+                    results = ev.collect(b.pend, defer_fallback=b.polish is None or ev.device is not None)
+                    if b.polish is not None:
+                        # declined variants are not replayed on the host: the polish
+                        # takes the best device-scored setting
+                        batches[si] = None
+                        if busy_since is not None and all(x is None for x in batches):
+                            self.stats.busy_s += time.time() - busy_since
+                            busy_since = None
+                        self._polish_done(b.polish, results, ready)
+                        self.phase["collect"] += time.perf_counter() - t_ph
+                        progressed = True
+                        continue
                     if b.pend.fallback_idx:
                         fallbacks.append((b.items, ev.fallback_async(b.pend, object_ok=self.host_object),
                                           len(b.pend.fallback_idx)))
@@ -424,7 +526,7 @@ class SteadyStateSearch:
         finally:
             pool.shutdown(wait=False, cancel_futures=True)
             stager.shutdown(wait=True, cancel_futures=True)
-            for _, fut in staged:        # compiled but never launched: give the modules back
+            for _, fut, _pj in staged:   # compiled but never launched: give the modules back
                 if fut.done() and not fut.cancelled() and fut.exception() is None:
                     ev.discard_prepared(fut.result())
         now = time.time()
@@ -454,7 +556,8 @@ class SteadyStateSearch:
                    device_busy=round(busy / wall, 4),
                    new_shape_fraction=round(st.new_shapes / max(1, st.evaluations), 4),
                    native_fraction=round(st.native / max(1, st.evaluations), 4), host_fallback=st.fallback,
-                   shed=st.shed, abandoned=st.abandoned,
+                   shed=st.shed, abandoned=st.abandoned, polish_batches=st.polish_batches,
+                   polish_evals=st.polish_evals, polish_improved=st.polish_improved,
                    inflight=inflight, inflight_mean=round(st.inflight_sum / max(1e-9, st.inflight_n), 1),
                    resident_capacity=capacity,
                    occupancy=round(inflight / capacity, 4) if capacity else None,

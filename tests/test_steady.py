@@ -151,3 +151,22 @@ def test_host_fallback_sheds_object_engine_programs():
     assert shed.engine == "shed" and ev.stats["shed"] == 1
     full = ev._evaluate_compiled([code], prog, native=False, host_only=True, object_ok=True)[0]
     assert full.engine == "object" and full.exc == 0 and full.score > 0
+
+
+def test_steady_constant_polish_batches(tmp_path):
+    """Constant polish in steady mode: due island champions get a batch of
+    literal variants (one shape), and a better setting re-enters the island as
+    an ordinary child; children accounting is unaffected by the variants."""
+    from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
+    cfg = _cfg(tmp_path, gens=4)
+    cfg["polish"] = {"every": 1, "variants": 8, "repeat": True}
+    fs = IslandFunSearch(cfg)
+    fs.run(4)
+    st = fs.steady.stats
+    assert st.polish_batches > 0 and st.polish_evals == 8 * st.polish_batches
+    assert st.evaluations == st.produced - st.rejected + st.polish_improved
+    recs = [json.loads(l) for l in open(tmp_path / "log.jsonl")]
+    pol = [r for r in recs if r["kind"] == "steady_polish"]
+    assert len(pol) == st.polish_batches and all(r["variants"] == 8 for r in pol)
+    fin = [r for r in recs if r["kind"] == "steady_final"][-1]
+    assert fin["polish_batches"] == st.polish_batches
