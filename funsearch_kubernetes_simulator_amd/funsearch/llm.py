@@ -377,7 +377,7 @@ class MutationClient(BaseClient):
 
     #: body size (characters) past which a parent is pruned before mutation; the
     #: longest LLM-found champion bodies in data/policies are ~2,300 characters
-    max_body_chars = 3000
+    max_body_chars = 2400
 
     @staticmethod
     def _score_only(stmt: ast.stmt) -> bool:

@@ -219,10 +219,13 @@ class Compiler:
 
     # ------------------------------------------------------------------ top level
     def compile(self) -> CompiledPolicy:
-        try:
-            tree = ast.parse(self.source)
-        except SyntaxError as exc:
-            raise CompileError(f"syntax error: {exc}")
+        from .sandbox import take_parsed
+        tree = take_parsed(self.source)   # the validator's parse of this very string
+        if tree is None:
+            try:
+                tree = ast.parse(self.source)
+            except SyntaxError as exc:
+                raise CompileError(f"syntax error: {exc}")
         fn = None
         for stmt in tree.body:
             if isinstance(stmt, ast.FunctionDef) and stmt.name == "priority_function":
