@@ -1,0 +1,49 @@
+"""Compact timeline of a steady-state run's status records.
+
+    python tools/steady_summary.py STEADY_LOG_OR_METRICS_JSONL [--final-only]
+
+One line per `steady_status` (and the `steady_final`): wall time, evaluations,
+evals/s, programs in flight (time-weighted mean), queued children, producer
+tasks and CPU ms per child, host fallbacks / shed children, polish batches,
+best score, distinct island bests, generation, main-thread phase seconds,
+module-load seconds and the device-busy fraction; then the final record in
+full.  Used for the profiles/r4_config3_steady_*.txt summaries.
+"""
+
+from __future__ import annotations
+
+import json
+import sys
+
+
+def main() -> None:
+    path = sys.argv[1]
+    final_only = "--final-only" in sys.argv
+    last = None
+    for line in open(path):
+        line = line.strip()
+        if not line.startswith("{"):
+            continue
+        try:
+            r = json.loads(line)
+        except ValueError:
+            continue
+        if r.get("kind") not in ("steady_status", "steady_final"):
+            continue
+        last = r
+        if final_only and r["kind"] != "steady_final":
+            continue
+        ph = {k: round(v, 1) for k, v in r.get("main_phase_s", {}).items()}
+        print(f"{r['wall_s']:8.1f}s evals {r['evaluations']:7d} {r['evals_per_s']:8.1f}/s "
+              f"inflight~{r.get('inflight_mean', 0):6.0f} queued {r.get('queued', 0):4d} "
+              f"tasks {r.get('producer_tasks', 0):2d} ms/child {r.get('producer_ms_per_child', 0):5.2f} "
+              f"fallback {r.get('host_fallback', 0)} shed {r.get('shed', 0)} "
+              f"polish {r.get('polish_batches', 0)}/{r.get('polish_improved', 0)} "
+              f"best {r['best']:.6f} distinct {r.get('distinct_island_bests', 0)} gen {r['generation']} "
+              f"phases {ph} load_s {r.get('jit', {}).get('load_s')} busy {r.get('device_busy')}")
+    if last is not None:
+        print(json.dumps(last))
+
+
+if __name__ == "__main__":
+    main()
