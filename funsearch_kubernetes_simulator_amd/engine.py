@@ -470,7 +470,19 @@ class Evaluator:
         with self._compile_lock:
             if getattr(self, "_fallback_pool", None) is None:
                 from concurrent.futures import ThreadPoolExecutor
-                self._fallback_pool = ThreadPoolExecutor(max_workers=2, thread_name_prefix="fks-fallback")
+                nice = int(getattr(self, "fallback_nice", 0))
+
+                def lower_priority():
+                    # a host fallback (a CPU-VM replay: seconds of a core for a large
+                    # program) yields the cores to the threads that keep the GPU fed;
+                    # nice is per thread on Linux and the VM's worker threads inherit it
+                    if nice > 0 and hasattr(os, "setpriority") and hasattr(threading, "get_native_id"):
+                        try:
+                            os.setpriority(os.PRIO_PROCESS, threading.get_native_id(), nice)
+                        except OSError:
+                            pass
+                self._fallback_pool = ThreadPoolExecutor(max_workers=2, thread_name_prefix="fks-fallback",
+                                                         initializer=lower_priority)
 
         def job():
             res = self._evaluate_compiled(codes, compiled, native=False, host_only=True, object_ok=object_ok)

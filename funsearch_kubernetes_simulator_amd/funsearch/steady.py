@@ -160,6 +160,8 @@ class SteadyStateSearch:
             # processes for the host's cores and with the batches' module loads;
             # at steady state almost every shape is evaluated once or twice
             dev.native_compiler.tierup_after = 0
+        # host fallbacks run at low priority: the producers come first
+        fs.evaluator.fallback_nice = 15
         n_slots = dev.n_slots if dev is not None else 1
         self.slots = max(1, min(int(slots or n_slots), n_slots))
         if dev is not None:
