@@ -36,6 +36,7 @@
 #pragma once
 
 #include <array>
+#include <cstdlib>
 #include <map>
 #include <set>
 #include <stdexcept>
@@ -89,6 +90,7 @@ class Codegen {
     liveness();
     simt_liveness();
     layout_registers();
+    arg_liveness();
     emit_all();
     if (st) {
       st->vregs = n_vregs_;
@@ -588,19 +590,15 @@ class Codegen {
     e(mk(V_MOV_B32, Rh(r), ic(0)));
   }
   // scratch slot of spilled register r <-> VGPR pair p (active lanes)
-  void spill_store(int r, int p) {
-    for (int h = 0; h < 2; ++h) {
-      MI st = mk(SCRATCH_STORE_DWORD, NONE, NONE, s(32), v(p + h));
-      st.imm = slot_[r] + 4 * h;
-      e(st);
-    }
+  void spill_store(int r, int p) {   // pairs are even-aligned: one 64-bit access
+    MI st = mk(SCRATCH_STORE_DWORDX2, NONE, NONE, s(32), v(p));
+    st.imm = slot_[r];
+    e(st);
   }
   void spill_load(int r, int p) {
-    for (int h = 0; h < 2; ++h) {
-      MI ld = mk(SCRATCH_LOAD_DWORD, v(p + h), NONE, s(32));
-      ld.imm = slot_[r] + 4 * h;
-      e(ld);
-    }
+    MI ld = mk(SCRATCH_LOAD_DWORDX2, v(p), NONE, s(32));
+    ld.imm = slot_[r];
+    e(ld);
   }
   // before instruction pc: its spilled operands (and destination: partial
   // writes keep the inactive lanes' value) in reload pairs
@@ -780,15 +778,47 @@ class Codegen {
         if (b >= 0) { out.push_back(b); out.push_back(b + 1); }
     return out;
   }
+  // Argument VGPRs are read only by NODE / GLIST_ALL / GLIST_LEN / GPU / POD
+  // instructions; past the last such read (a read inside a loop counts up to
+  // the loop's exit) a class of them is dead and a runtime call need not save
+  // it.  The code is structured and emitted in pc order, so this pc bound is
+  // exact for the wave (SIMT) as well.
+  enum ArgClass { AC_NODE, AC_GL, AC_GMEM, AC_POD, AC_N };
+  std::array<int, AC_N> arg_last_{};
+  void arg_liveness() {
+    arg_last_.fill(-1);
+    std::vector<std::pair<int, int>> loops;   // (LOOP_BEGIN pc, LOOP_EXIT pc)
+    std::vector<int> open;
+    for (int pc = 0; pc < n_; ++pc) {
+      const Insn& in = P_.code[pc];
+      if (in.op == OP_LOOP_BEGIN) open.push_back(pc);
+      else if (in.op == OP_LOOP_EXIT && !open.empty()) { loops.push_back({open.back(), pc}); open.pop_back(); }
+    }
+    auto mark = [&](int cls, int pc) {
+      int end = pc;
+      for (const auto& l : loops)
+        if (l.first <= pc && pc <= l.second) end = std::max(end, l.second);
+      arg_last_[cls] = std::max(arg_last_[cls], end);
+    };
+    static const bool save_all = std::getenv("FKS_JIT_SAVE_ALL_ARGS") != nullptr;   // A/B knob
+    if (save_all) { arg_last_.fill(n_); return; }
+    for (int pc = 0; pc < n_; ++pc) {
+      const Insn& in = P_.code[pc];
+      if (in.op == OP_NODE || in.op == OP_GLIST_ALL || in.op == OP_GLIST_LEN) mark(AC_NODE, pc);
+      if (in.op == OP_GPU) mark(in.imm == 0 || in.imm == 1 ? AC_GL : AC_GMEM, pc);
+      if (in.op == OP_GPU) mark(AC_NODE, pc);   // (GPU j exists: the count in v4)
+      if (in.op == OP_POD) mark(AC_POD, pc);
+    }
+  }
   std::vector<int> live_vgprs(int pc, int d) const {
     std::vector<int> out;
-    if (use_node_ || use_gl_ || use_gmem_)
+    if ((use_node_ || use_gl_ || use_gmem_) && arg_last_[AC_NODE] > pc)
       for (int g = 0; g <= 4; ++g) out.push_back(g);
-    if (use_gl_)
+    if (use_gl_ && arg_last_[AC_GL] > pc)
       for (int g = 5; g <= 20; ++g) out.push_back(g);
-    if (use_gmem_) { out.push_back(21); out.push_back(22); }
+    if (use_gmem_ && arg_last_[AC_GMEM] > pc) { out.push_back(21); out.push_back(22); }
     for (int f = 0; f < 6; ++f)   // pod arguments the program still reads
-      if (pod_s_[f] >= 0) {
+      if (pod_s_[f] >= 0 && arg_last_[AC_POD] > pc) {
         out.push_back(pod_s_[f]);
         if (f == 4) out.push_back(pod_s_[f] + 1);
       }

@@ -295,11 +295,22 @@ struct Emu {
           std::memcpy(&x, reinterpret_cast<const void*>(a), 8);
           w64v(m.d, l, x);
         }); break;
-        case SCRATCH_LOAD_DWORD: case SCRATCH_STORE_DWORD: lanes([&](int l) {
+        case SCRATCH_LOAD_DWORD: case SCRATCH_STORE_DWORD: case SCRATCH_LOAD_DWORDX2: case SCRATCH_STORE_DWORDX2:
+        case SCRATCH_LOAD_DWORDX4: lanes([&](int l) {
+          const int n = (m.op == SCRATCH_LOAD_DWORDX4) ? 4
+                        : (m.op == SCRATCH_LOAD_DWORDX2 || m.op == SCRATCH_STORE_DWORDX2) ? 2 : 1;
           const size_t a = (size_t)sg[m.s1] + (size_t)m.imm;
-          if (scratch[l].size() < a + 4) scratch[l].resize(a + 64);
-          if (m.op == SCRATCH_STORE_DWORD) { const uint32_t x = r32(m.s2, l, m.lit); std::memcpy(scratch[l].data() + a, &x, 4); }
-          else { uint32_t x; std::memcpy(&x, scratch[l].data() + a, 4); w32(m.d, l, x); }
+          if (scratch[l].size() < a + 4 * n) scratch[l].resize(a + 4 * n + 64);
+          for (int k = 0; k < n; ++k) {
+            if (m.op == SCRATCH_STORE_DWORD || m.op == SCRATCH_STORE_DWORDX2) {
+              const uint32_t x = r32((uint16_t)(m.s2 + k), l, m.lit);
+              std::memcpy(scratch[l].data() + a + 4 * k, &x, 4);
+            } else {
+              uint32_t x;
+              std::memcpy(&x, scratch[l].data() + a + 4 * k, 4);
+              w32((uint16_t)(m.d + k), l, x);
+            }
+          }
         }); break;
         // ---- macros
         case M_FDIV64: lanes([&](int l) { w64v(m.d, l, dbits(rf(m.s0, l, m.lit) / rf(m.s1, l, m.lit))); }); break;

@@ -329,3 +329,37 @@ def test_spilled_registers_equal_cpu_vm(corpus, cap):
         assert spilled >= len(progs) // 4, (spilled, len(progs))
     finally:
         m.gcn_set_pair_cap(0)
+
+
+@have_mc
+def test_spilled_code_round_trips_through_llvm_mc(corpus):
+    """Spill slots and the runtime calls' paired saves / quad restores encode
+    as the assembler does (scratch_*_dwordx2 / _dwordx4 at s32 offsets)."""
+    m = ce.native()
+    m.gcn_set_pair_cap(2)
+    try:
+        done = 0
+        for p in corpus[::4]:
+            code, _ = gcnjit.compile_program(p)
+            if code is None or code.info["spills"] == 0:
+                continue
+            words = code.words.copy()
+            for lo, hi, _ in code.relocs.reshape(-1, 3):
+                words[int(lo)], words[int(hi)] = 0x12345678, 0xFFFFF000
+            raw = words.tobytes()
+            dis = subprocess.run([MC, "-disassemble", "-triple=amdgcn-amd-amdhsa", "-mcpu=gfx950"],
+                                 input=" ".join(f"0x{b:02x}" for b in raw), capture_output=True, text=True)
+            assert dis.returncode == 0 and not dis.stderr.strip(), dis.stderr[:2000]
+            asm = "\n".join(ln.strip() for ln in dis.stdout.splitlines() if ln.strip() and not ln.strip().startswith("."))
+            assert "scratch_load_dwordx2" in asm and "scratch_store_dwordx2" in asm
+            re = subprocess.run([MC, "-triple=amdgcn-amd-amdhsa", "-mcpu=gfx950", "-show-encoding"], input=asm,
+                                capture_output=True, text=True)
+            out = bytearray()
+            for line in re.stdout.splitlines():
+                if "encoding: [" in line:
+                    out += bytes(int(x, 16) for x in line.split("encoding: [")[1].rstrip("]").split(","))
+            assert bytes(out) == raw
+            done += 1
+        assert done >= 3
+    finally:
+        m.gcn_set_pair_cap(0)
