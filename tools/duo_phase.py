@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--programs", type=int, default=48)
     ap.add_argument("--tier", default="auto", choices=["auto", "baseline", "llvm"],
                     help="JIT tier of the programs (ops/jit.py)")
+    ap.add_argument("--ck", default="", help="also: children of this evolved population (tools/population_bench.py)")
     a = ap.parse_args()
     from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
     from funsearch_kubernetes_simulator_amd.ops.jit import NativeCompiler
@@ -38,6 +39,10 @@ def main():
     sets = {"first_fit": [compile_policy(reference_policies()["first_fit"])],
             "funsearch_4901": [compile_policy(reference_policies()["funsearch_4901"])],
             "children": mutation_children(a.programs, 0)}
+    if a.ck:
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from population_bench import _programs
+        sets["population"] = _programs(a.ck, a.programs, 7)
     for name, progs in sets.items():
         dev.profile_native(progs)   # compile + warm
         tab, prof = dev.profile_native(progs)
