@@ -229,35 +229,53 @@ def _free_names(node: ast.AST) -> set:
 def _numeric_subexprs(tree: ast.AST, portable: bool) -> list:
     """Expression nodes that hold a number and may be swapped for another
     numeric expression: arithmetic, numeric literals, pod / node scalar fields,
-    abs / min / max / sum calls.  `portable`: only those that mention no
-    parent-local name (they may move into another program)."""
-    skip = set()
-    for n in ast.walk(tree):
-        if isinstance(n, ast.comprehension):
-            skip.update(id(x) for x in ast.walk(n.iter))     # keep `for g in node.gpus` intact
-        elif isinstance(n, (ast.Assign, ast.AugAssign)):
-            tgts = n.targets if isinstance(n, ast.Assign) else [n.target]
-            for t in tgts:
-                skip.update(id(x) for x in ast.walk(t))
-        elif isinstance(n, ast.Call):
-            skip.add(id(n.func))
-            skip.update(id(x) for x in ast.walk(n.func))
-    scopes = _scope_sets(tree) if portable else None
+    abs / min / max / sum calls -- never inside a comprehension's iterable
+    (keeps `for g in node.gpus` intact), an assignment target or a called
+    name.  `portable`: only those that mention no parent-local name (they may
+    move into another program).  One pass, pre-order."""
     out = []
-    for n in ast.walk(tree):
-        if id(n) in skip:
-            continue
-        ok = (isinstance(n, (ast.BinOp, ast.UnaryOp))
-              or (isinstance(n, ast.Constant) and isinstance(n.value, (int, float)) and not isinstance(n.value, bool))
-              or (isinstance(n, ast.Attribute) and isinstance(n.value, ast.Name) and n.value.id in ("pod", "node")
-                  and n.attr in _NUMERIC_FIELDS)
-              or (isinstance(n, ast.Call) and isinstance(n.func, ast.Name) and n.func.id in ("abs", "min", "max", "sum")))
-        if ok and portable:
-            used, bound = scopes[id(n)]
-            ok = used - bound <= _FREE_OK
+    Name, Load, Constant, Attribute, Call = ast.Name, ast.Load, ast.Constant, ast.Attribute, ast.Call
+    arith = (ast.BinOp, ast.UnaryOp)
+
+    def visit(n, skipped):
+        # returns (names read, names bound) of the subtree when `portable`
+        used, bound = (set(), set()) if portable else (None, None)
+        t = type(n)
+        ok = False
+        if not skipped:
+            ok = (t in arith
+                  or (t is Constant and isinstance(n.value, (int, float)) and not isinstance(n.value, bool))
+                  or (t is Attribute and type(n.value) is Name and n.value.id in ("pod", "node")
+                      and n.attr in _NUMERIC_FIELDS)
+                  or (t is Call and type(n.func) is Name and n.func.id in ("abs", "min", "max", "sum")))
         if ok:
+            slot = len(out)
             out.append(n)
-    return out
+        if portable:
+            if t is Name:
+                if type(n.ctx) is Load:
+                    used.add(n.id)
+            elif t is ast.comprehension:
+                bound.update(x.id for x in ast.walk(n.target) if isinstance(x, ast.Name))
+            elif t is ast.Lambda:
+                bound.update(a.arg for a in n.args.args)
+        for f in n._fields:
+            v = getattr(n, f, None)
+            kids = v if type(v) is list else (v,)
+            sk = skipped or (t is ast.comprehension and f == "iter") or (t is Call and f == "func") \
+                or (t is ast.Assign and f == "targets") or (t is ast.AugAssign and f == "target")
+            for c in kids:
+                if isinstance(c, ast.AST):
+                    u, bd = visit(c, sk)
+                    if portable:
+                        used |= u
+                        bound |= bd
+        if ok and portable and not (used - bound <= _FREE_OK):
+            out[slot] = None
+        return used, bound
+
+    visit(tree, False)
+    return [n for n in out if n is not None]
 
 
 def _scope_sets(tree: ast.AST) -> dict:
@@ -394,19 +412,29 @@ class MutationClient(BaseClient):
         return upd(stmt)
 
     def _prune(self, body: str, rng: random.Random, limit: int) -> str:
+        """Drop random score-only top-level statements until the body is at most
+        `limit` characters; removes their source lines, so the rest of the text
+        is kept verbatim (no unparse)."""
         try:
             tree = ast.parse(body)
         except SyntaxError:
             return body
-        size = len(body)
-        while size > limit:
-            cands = [i for i, st in enumerate(tree.body) if i > 0 and self._score_only(st)]
-            if not cands:
-                break
-            i = rng.choice(cands)
-            size -= len(ast.unparse(tree.body[i])) + 1
-            del tree.body[i]
-        return ast.unparse(tree)
+        lines = body.split("\n")
+        line_of = {}
+        for i, st in enumerate(tree.body):
+            for ln in range(st.lineno, (st.end_lineno or st.lineno) + 1):
+                line_of.setdefault(ln, []).append(i)
+        cands = [i for i, st in enumerate(tree.body)
+                 if i > 0 and self._score_only(st)
+                 and all(line_of[ln] == [i] for ln in range(st.lineno, (st.end_lineno or st.lineno) + 1))]
+        drop, size = set(), len(body)
+        while size > limit and cands:
+            i = cands.pop(rng.randrange(len(cands)))
+            st = tree.body[i]
+            for ln in range(st.lineno, (st.end_lineno or st.lineno) + 1):
+                drop.add(ln)
+                size -= len(lines[ln - 1]) + 1
+        return "\n".join(l for k, l in enumerate(lines, 1) if k not in drop)
 
     # -- operators ----------------------------------------------------------------------
     #: (cumulative probability, operator).  Structural operators (new terms from
