@@ -567,3 +567,63 @@ def test_mutator_library_terms_compile_for_the_device():
         assert ex.validate(code)
         prog, err = try_compile(code)
         assert prog is not None and prog.device_ok, (body, err)
+
+
+def test_mutator_prunes_bloated_parents_by_lines():
+    """Bloat control: a parent body past the cap loses random score-only
+    top-level statements (their source lines, the rest verbatim) until it fits;
+    the first statement, statements sharing a line and non-score statements
+    stay."""
+    import ast
+    import random
+    from funsearch_kubernetes_simulator_amd.funsearch.llm import MutationClient
+    head = "x = node.cpu_milli_left / max(1, node.cpu_milli_total)\nscore = 0.0\n"
+    terms = "".join(f"score += {i}.5 * x * (node.memory_mib_left / max(1, node.memory_mib_total))\n" for i in range(60))
+    body = head + "a = 1; score += a\n" + terms + "if x > 0.5:\n    score -= 3.0\n"
+    mc = MutationClient(0)
+    out = mc._prune(body, random.Random(4), 1500)
+    assert len(out) <= 1500 and len(out) < len(body)
+    tree = ast.parse(out)
+    assert out.split("\n")[0] == head.split("\n")[0]          # first statement kept verbatim
+    assert "a = 1; score += a" in out                          # shared line kept
+    kept = [ln for ln in out.split("\n") if ln.startswith("score += ")]
+    assert all(ln in body.split("\n") for ln in kept)          # surviving lines verbatim
+    assert isinstance(tree.body[0], ast.Assign)
+
+
+def test_numeric_subexprs_match_naive_definition():
+    """The one-pass candidate search equals the definition: numeric nodes not
+    inside a comprehension iterable, an assignment target or a called name;
+    `portable` ones read no parent-local name."""
+    import ast
+    from funsearch_kubernetes_simulator_amd.funsearch import llm
+    from funsearch_kubernetes_simulator_amd.models.library import reference_policies, seed_policies
+
+    def naive(tree, portable):
+        skip = set()
+        for n in ast.walk(tree):
+            if isinstance(n, ast.comprehension):
+                skip.update(id(x) for x in ast.walk(n.iter))
+            elif isinstance(n, (ast.Assign, ast.AugAssign)):
+                for t in (n.targets if isinstance(n, ast.Assign) else [n.target]):
+                    skip.update(id(x) for x in ast.walk(t))
+            elif isinstance(n, ast.Call):
+                skip.update(id(x) for x in ast.walk(n.func))
+        out = []
+        for n in ast.walk(tree):
+            if id(n) in skip:
+                continue
+            ok = (isinstance(n, (ast.BinOp, ast.UnaryOp))
+                  or (isinstance(n, ast.Constant) and isinstance(n.value, (int, float)) and not isinstance(n.value, bool))
+                  or (isinstance(n, ast.Attribute) and isinstance(n.value, ast.Name) and n.value.id in ("pod", "node")
+                      and n.attr in llm._NUMERIC_FIELDS)
+                  or (isinstance(n, ast.Call) and isinstance(n.func, ast.Name)
+                      and n.func.id in ("abs", "min", "max", "sum")))
+            if ok and (not portable or llm._free_names(n) <= llm._FREE_OK):
+                out.append(id(n))
+        return sorted(out)
+
+    for code in list(reference_policies().values()) + list(seed_policies().values()):
+        tree = ast.parse(code)
+        for portable in (False, True):
+            assert sorted(id(n) for n in llm._numeric_subexprs(tree, portable)) == naive(tree, portable)
