@@ -71,9 +71,10 @@ def _producer_init(llm_cfg: dict, timeout_s: int, seed: int) -> None:
 
 def _produce(task):
     """(island, elites [(code, score)], n) -> [(island, code, CompiledPolicy | None)]."""
-    from ..policy.compiler import try_compile
+    from ..policy.compiler import same_shape_child, try_compile
     island, elites, n = task
     gen, rng = _W["gen"], _W["rng"]
+    pcache = _W.setdefault("parents", {})   # parent text -> CompiledPolicy (elites repeat)
     t0 = time.process_time()
     out = []
     for _ in range(n):
@@ -82,7 +83,21 @@ def _produce(task):
         if not code:             # LLM / validation failure: the child slot is spent
             out.append((island, None, None))
             continue
-        prog, _ = try_compile(code)
+        prog = None
+        # a constant-only mutation keeps its parent's shape: bytecode reused
+        for pc, _ in parents:
+            pp = pcache.get(pc)
+            if pp is None:
+                if len(pcache) > 256:
+                    pcache.clear()
+                pp = pcache[pc] = try_compile(pc)[0] or False
+            if pp:
+                prog = same_shape_child(pp, code)
+                if prog is not None:
+                    _W["reused"] = _W.get("reused", 0) + 1
+                    break
+        if prog is None:
+            prog, _ = try_compile(code)
         out.append((island, code, prog))
     return out, time.process_time() - t0
 

@@ -1514,6 +1514,77 @@ def compile_policy(source: str) -> CompiledPolicy:
     return Compiler(source).compile()
 
 
+_NUM_TOKEN = None
+
+
+def same_shape_child(parent: CompiledPolicy, child: str) -> Optional[CompiledPolicy]:
+    """`child` compiled without the compiler when it is `parent.source` with only
+    the digits of numeric literals changed (an offline mutator's constant
+    perturbation): the parent's bytecode with the child's literal values and
+    spans.  Exact by construction -- same token stream, every changed token a
+    literal of the same int / float kind; anything else (a changed non-literal
+    digit, a literal the token scan does not see, a kind change) returns None
+    and the caller compiles."""
+    import re
+    global _NUM_TOKEN
+    if _NUM_TOKEN is None:
+        _NUM_TOKEN = re.compile(r"(?<![\w.])(\d+\.\d+|\d+)(?![\w.])")
+    src = parent.source
+    if len(child) > 2 * len(src) + 64:
+        return None
+    tp = [(m.start(), m.end()) for m in _NUM_TOKEN.finditer(src)]
+    tc = [(m.start(), m.end()) for m in _NUM_TOKEN.finditer(child)]
+    if len(tp) != len(tc):
+        return None
+    # text between the tokens must be identical
+    prev_p = prev_c = 0
+    for (ps, pe), (cs, ce) in zip(tp, tc):
+        if src[prev_p:ps] != child[prev_c:cs]:
+            return None
+        prev_p, prev_c = pe, ce
+    if src[prev_p:] != child[prev_c:]:
+        return None
+    # literal spans of the parent -> token positions
+    starts = [0]
+    for line in src.split("\n"):
+        starts.append(starts[-1] + len(line) + 1)
+    lit_at = {}
+    for idx, ln, col, eln, ecol in parent.literals:
+        if ln != eln:
+            return None
+        lit_at[starts[ln - 1] + col] = (idx, starts[ln - 1] + ecol)
+    cstarts = [0]
+    for line in child.split("\n"):
+        cstarts.append(cstarts[-1] + len(line) + 1)
+    f, i = list(parent.fconst), list(parent.iconst)
+    lits, seen = [], 0
+    line_c = 0
+    for (ps, pe), (cs, ce) in zip(tp, tc):
+        hit = lit_at.get(ps)
+        ptxt, ctxt = src[ps:pe], child[cs:ce]
+        if hit is None or hit[1] != pe:
+            if ptxt != ctxt:
+                return None        # a changed digit outside a literal the compiler saw
+            continue
+        idx = hit[0]
+        seen += 1
+        is_float = "." in ctxt
+        if is_float != (parent.ctag[idx] == TAG_FLOAT):
+            return None
+        if is_float:
+            f[idx] = float(ctxt)
+        else:
+            i[idx] = int(ctxt)
+        while cstarts[line_c + 1] <= cs:
+            line_c += 1
+        lits.append((idx, line_c + 1, cs - cstarts[line_c], line_c + 1, ce - cstarts[line_c]))
+    if seen != len(parent.literals):
+        return None
+    span = {lt[0]: lt for lt in lits}
+    return CompiledPolicy(parent.code, f, i, list(parent.ctag), parent.nregs, child, parent.features,
+                          [span[lt[0]] for lt in parent.literals])   # the compiler's order
+
+
 def try_compile(source: str) -> Tuple[Optional[CompiledPolicy], Optional[str]]:
     try:
         return compile_policy(source), None

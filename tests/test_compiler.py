@@ -196,3 +196,37 @@ def test_feasibility_prologue_detection():
     # two definitions: the compiler takes the last one, the fast path declines and the AST path decides
     twice = prog + "\ndef priority_function(pod, node):\n    return 7\n"
     assert not starts_with_feasibility_prologue(twice)
+
+
+def test_same_shape_child_equals_full_compile():
+    """A constant-only mutation reuses its parent's bytecode: the result equals
+    compiling the child from scratch (code, constants, kinds, literal spans);
+    any other change is refused."""
+    import random
+    from funsearch_kubernetes_simulator_amd.funsearch.llm import MutationClient
+    from funsearch_kubernetes_simulator_amd.models.library import reference_policies
+    from funsearch_kubernetes_simulator_amd.policy.compiler import same_shape_child, try_compile
+    from funsearch_kubernetes_simulator_amd.policy.template import PolicyTemplate
+    mc = MutationClient(0)
+    rng = random.Random(3)
+    parents = [PolicyTemplate.fill_template(
+        "    score = 0.0\n    a = node.cpu_milli_left / max(1, node.cpu_milli_total)\n"
+        "    if a > 0.25:\n        score += 17 * a - 2.5\n    score -= 0.125 * abs(pod.cpu_milli - 300)\n"
+        "    # tuned 2 times\n    return max(1, int(score * 1000))")] + list(reference_policies().values())
+    hits = 0
+    for code in parents:
+        p, _ = try_compile(code)
+        for _ in range(20):
+            child = mc._perturb_constants(code, rng)
+            fast = same_shape_child(p, child)
+            if fast is None:
+                continue
+            full, _ = try_compile(child)
+            for k in ("code", "fconst", "iconst", "ctag", "literals", "nregs", "features", "source"):
+                assert getattr(fast, k) == getattr(full, k), k
+            hits += 1
+    assert hits >= 20
+    p, _ = try_compile(parents[0])
+    assert same_shape_child(p, parents[0].replace("17 * a", "17.0 * a")) is None        # int -> float literal
+    assert same_shape_child(p, parents[0].replace("tuned 2 times", "tuned 3 times")) is None   # comment digit
+    assert same_shape_child(p, parents[0].replace("score += 17", "score -= 17")) is None  # operator
