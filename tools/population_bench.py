@@ -46,6 +46,10 @@ def _programs(path: str, n: int, seed: int):
     pop.sort(key=lambda x: -x[1])
     elites = pop[:8]
     steady._producer_init({"backend": "mutation", "seed": seed}, 3, 1)
+    # deterministic children (the producer seeds from its pid): the same programs
+    # in every variant's process
+    steady._W["rng"] = random.Random(seed)
+    steady._W["gen"].llm_client.rng = random.Random(seed + 1)
     random.seed(seed)
     out = []
     while len(out) < n:
