@@ -75,8 +75,11 @@ for step in "$@"; do
       args=""
       [ "$script" != "$val" ] && args=${val#*:}
       base=$(basename "$script" .py)
-      timeout -k 10 900 python -u "$script" $args > "$O/py_$base.txt" 2>&1 || die "py $script" "$O/py_$base.txt"
-      tail -5 "$O/py_$base.txt" | cut -c1-400 ;;
+      out="$O/py_$base.txt"
+      n=2
+      while [ -e "$out" ]; do out="$O/py_${base}_$n.txt"; n=$((n + 1)); done   # repeated steps keep their output
+      timeout -k 10 900 python -u "$script" $args > "$out" 2>&1 || die "py $script" "$out"
+      tail -5 "$out" | cut -c1-400 ;;
     *)
       die "unknown step $step" ;;
   esac
