@@ -36,7 +36,6 @@
 #pragma once
 
 #include <array>
-#include <cstdlib>
 #include <map>
 #include <set>
 #include <stdexcept>
@@ -590,15 +589,19 @@ class Codegen {
     e(mk(V_MOV_B32, Rh(r), ic(0)));
   }
   // scratch slot of spilled register r <-> VGPR pair p (active lanes)
-  void spill_store(int r, int p) {   // pairs are even-aligned: one 64-bit access
-    MI st = mk(SCRATCH_STORE_DWORDX2, NONE, NONE, s(32), v(p));
-    st.imm = slot_[r];
-    e(st);
+  void spill_store(int r, int p) {   // dword accesses (scratch is swizzled per lane in dwords)
+    for (int h = 0; h < 2; ++h) {
+      MI st = mk(SCRATCH_STORE_DWORD, NONE, NONE, s(32), v(p + h));
+      st.imm = slot_[r] + 4 * h;
+      e(st);
+    }
   }
   void spill_load(int r, int p) {
-    MI ld = mk(SCRATCH_LOAD_DWORDX2, v(p), NONE, s(32));
-    ld.imm = slot_[r];
-    e(ld);
+    for (int h = 0; h < 2; ++h) {
+      MI ld = mk(SCRATCH_LOAD_DWORD, v(p + h), NONE, s(32));
+      ld.imm = slot_[r] + 4 * h;
+      e(ld);
+    }
   }
   // before instruction pc: its spilled operands (and destination: partial
   // writes keep the inactive lanes' value) in reload pairs
@@ -800,8 +803,6 @@ class Codegen {
         if (l.first <= pc && pc <= l.second) end = std::max(end, l.second);
       arg_last_[cls] = std::max(arg_last_[cls], end);
     };
-    static const bool save_all = std::getenv("FKS_JIT_SAVE_ALL_ARGS") != nullptr;   // A/B knob
-    if (save_all) { arg_last_.fill(n_); return; }
     for (int pc = 0; pc < n_; ++pc) {
       const Insn& in = P_.code[pc];
       if (in.op == OP_NODE || in.op == OP_GLIST_ALL || in.op == OP_GLIST_LEN) mark(AC_NODE, pc);

@@ -1,7 +1,6 @@
 // Macro expansion, gfx950 hazard padding, branch resolution and encoding of a
 // baseline-JIT function (gcn_isa.hpp).
 #pragma once
-#include <cstdlib>
 
 #include <algorithm>
 #include <unordered_map>
@@ -53,16 +52,6 @@ inline MI mklit(Opc op, uint16_t d, uint32_t lit, uint16_t s1 = NONE) {
 }
 
 // ---- macro expansion -------------------------------------------------------------------
-// sorted VGPR indices -> (first, count) runs of consecutive registers
-inline std::vector<std::pair<int, int>> save_runs(const std::vector<int>& regs) {
-  std::vector<std::pair<int, int>> runs;
-  for (int g : regs) {
-    if (!runs.empty() && runs.back().first + runs.back().second == g) ++runs.back().second;
-    else runs.push_back({g, 1});
-  }
-  return runs;
-}
-
 inline void expand(const Func& f, std::vector<MI>& out, int& next_label) {
   const MacroRegs& r = f.mr;
   auto X = [&](int i) { return v(r.x[i]); };
@@ -112,22 +101,13 @@ inline void expand(const Func& f, std::vector<MI>& out, int& next_label) {
         MI sav = mk(S_OR_SAVEEXEC_B64, s(r.sc), ic(-1));
         out.push_back(sav);
         int off = f.spill_bytes;   // the save area sits above the spill slots
-        // live VGPRs in runs: an even-aligned pair is one 64-bit store (wider
-        // stores would need a wait state before the argument moves overwrite
-        // their data registers); the restore loads four at a time
-        static const bool narrow = std::getenv("FKS_JIT_NARROW_SAVES") != nullptr;   // A/B knob: dword saves
-        std::vector<std::pair<int, int>> runs = save_runs(c.vgprs);
-        if (narrow) {
-          runs.clear();
-          for (int g : c.vgprs) runs.push_back({g, 1});
-        }
-        for (const auto& r : runs) {
-          for (int k = 0; k < r.second;) {
-            const int g = r.first + k, n = (r.second - k >= 2 && (g & 1) == 0) ? 2 : 1;
-            MI st = mk(n == 2 ? SCRATCH_STORE_DWORDX2 : SCRATCH_STORE_DWORD, NONE, NONE, s(32), v(g));
-            st.imm = off; off += 4 * n; k += n;
-            out.push_back(st);
-          }
+        // one dword per live VGPR: scratch is swizzled per lane in dwords, and
+        // paired / quad accesses measured ~9% slower on evolved populations
+        // (tools/population_bench.py, profiles/r4_jit_rtcall_save_ab.txt)
+        for (int g : c.vgprs) {
+          MI st = mk(SCRATCH_STORE_DWORD, NONE, NONE, s(32), v(g));
+          st.imm = off; off += 4;
+          out.push_back(st);
         }
         int lane = 0;
         for (int sg : c.sgprs) {
@@ -182,15 +162,10 @@ inline void expand(const Func& f, std::vector<MI>& out, int& next_label) {
         out.push_back(mk(V_MOV_B32, c.resy, v(2)));
         out.push_back(mk(S_OR_SAVEEXEC_B64, s(r.sc), ic(-1)));
         off = f.spill_bytes;
-        for (const auto& r : runs) {
-          for (int k = 0; k < r.second;) {
-            const int g = r.first + k;
-            const int n = (g & 1) ? 1 : (r.second - k >= 4 ? 4 : r.second - k >= 2 ? 2 : 1);
-            MI ldv = mk(n == 4 ? SCRATCH_LOAD_DWORDX4 : n == 2 ? SCRATCH_LOAD_DWORDX2 : SCRATCH_LOAD_DWORD, v(g),
-                        NONE, s(32));
-            ldv.imm = off; off += 4 * n; k += n;
-            out.push_back(ldv);
-          }
+        for (int g : c.vgprs) {
+          MI ldv = mk(SCRATCH_LOAD_DWORD, v(g), NONE, s(32));
+          ldv.imm = off; off += 4;
+          out.push_back(ldv);
         }
         {
           MI ldv = mk(SCRATCH_LOAD_DWORD, c.spill_vgpr, NONE, s(32));

@@ -333,8 +333,8 @@ def test_spilled_registers_equal_cpu_vm(corpus, cap):
 
 @have_mc
 def test_spilled_code_round_trips_through_llvm_mc(corpus):
-    """Spill slots and the runtime calls' paired saves / quad restores encode
-    as the assembler does (scratch_*_dwordx2 / _dwordx4 at s32 offsets)."""
+    """Spill slots and the runtime calls' saves and restores encode
+    as the assembler does (scratch_*_dword at s32 offsets)."""
     m = ce.native()
     m.gcn_set_pair_cap(2)
     try:
@@ -351,7 +351,7 @@ def test_spilled_code_round_trips_through_llvm_mc(corpus):
                                  input=" ".join(f"0x{b:02x}" for b in raw), capture_output=True, text=True)
             assert dis.returncode == 0 and not dis.stderr.strip(), dis.stderr[:2000]
             asm = "\n".join(ln.strip() for ln in dis.stdout.splitlines() if ln.strip() and not ln.strip().startswith("."))
-            assert "scratch_load_dwordx2" in asm and "scratch_store_dwordx2" in asm
+            assert "scratch_load_dword" in asm and "scratch_store_dword" in asm
             re = subprocess.run([MC, "-triple=amdgcn-amd-amdhsa", "-mcpu=gfx950", "-show-encoding"], input=asm,
                                 capture_output=True, text=True)
             out = bytearray()
