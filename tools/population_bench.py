@@ -65,6 +65,18 @@ def child(args) -> None:
     progs = _programs(args.ck, args.children, args.seed)
     dev = DeviceEvaluator(load_default_workload())
     dev.set_options(native_inflight=args.batch)
+    if args.rows:
+        dev.set_options(native_rows=args.rows)   # programs per wave (four: k_replay_rows_native)
+    if args.polish:
+        # constant variants of one shape (a steady-mode polish batch)
+        from funsearch_kubernetes_simulator_amd.funsearch.polish import _perturb, tunable_literals, with_values
+        import random
+        rng = random.Random(args.seed)
+        base_p = progs[0]
+        tune = tunable_literals(base_p)
+        vals = {base_p.literals[j][0]: (base_p.fconst[base_p.literals[j][0]] if base_p.ctag[base_p.literals[j][0]] == 1
+                                        else base_p.iconst[base_p.literals[j][0]]) for j in range(len(base_p.literals))}
+        progs = [with_values(base_p, _perturb(base_p, vals, tune, 0.35, rng)) for _ in range(len(progs))]
     dev.native_compiler.tier = "baseline"
     t0 = time.perf_counter()
     for i in range(0, len(progs), args.batch):
@@ -77,7 +89,8 @@ def child(args) -> None:
         dt = time.perf_counter() - t0
         best = dt if best is None else min(best, dt)
     tab = np.concatenate(rows)
-    print(json.dumps({"variant": args.name, "programs": len(progs), "batch": args.batch,
+    print(json.dumps({"variant": args.name, "rows": args.rows, "polish": args.polish, "programs": len(progs),
+                      "batch": args.batch,
                       "first_pass_s": round(first, 3), "cached_s": round(best, 3),
                       "cached_evals_per_s": round(len(progs) / best, 1),
                       "exc_rows": int((tab[:, 10] != 0).sum()), "mean_events": float(tab[:, 8].mean()),
@@ -95,6 +108,8 @@ def main() -> None:
     ap.add_argument("--variant", action="append", default=[], help="NAME=ENV1=V1,ENV2=V2 (empty: no change)")
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--name", default="base")
+    ap.add_argument("--rows", type=int, default=0, help="native programs per wave (0: the two-wave kernel)")
+    ap.add_argument("--polish", action="store_true", help="constant variants of one program instead of children")
     args = ap.parse_args()
     if args.child:
         child(args)
@@ -107,7 +122,7 @@ def main() -> None:
             env[k] = v
         cmd = [sys.executable, "-u", os.path.abspath(__file__), "--child", "--name", name, "--ck", args.ck,
                "--children", str(args.children), "--batch", str(args.batch), "--reps", str(args.reps),
-               "--seed", str(args.seed)]
+               "--seed", str(args.seed), "--rows", str(args.rows)] + (["--polish"] if args.polish else [])
         r = subprocess.run(cmd, env=env, timeout=600)
         if r.returncode != 0:
             sys.exit(r.returncode)
