@@ -474,7 +474,9 @@ class MutationClient(BaseClient):
             return f"{rng.choice(['min', 'max'])}({a}, {b})"
         if r < 0.9:
             return f"abs({a} - {b})"
-        return f"({a}) ** 2"
+        # a square as a product: `x ** 2` is a libm pow call per node on the device
+        # (and for CPython), x * x one multiply
+        return f"({a}) * ({a})"
 
     def _random_term(self, rng: random.Random) -> str:
         e = self._random_expr(rng)
@@ -535,7 +537,8 @@ class MutationClient(BaseClient):
                 return None
             t = rng.choice(targets)
             c = ast.Constant(float(self._const(rng)))
-            form = rng.randrange(4)
+            u = rng.random()   # abs / min-max / square 30% each, a fractional power 10%
+            form = 0 if u < 0.3 else 1 if u < 0.6 else 2 if u < 0.9 else 3
             if form == 0:
                 new = ast.Call(ast.Name("abs", ast.Load()), [t], [])
             elif form == 1:
