@@ -146,6 +146,11 @@ class Compiler:
         self.scope = _Scope()
         self.pod_name = self.node_name = None
         self.loop_depth = 0
+        # common subexpressions (see `expr`): text -> register holding the value
+        self._cse: Dict[str, Val] = {}
+        self._cse_memo: Dict[int, tuple] = {}
+        self._cond = 0                      # > 0: inside a branch (no new cache entries)
+        self._lines: Optional[List[str]] = None
 
     # ------------------------------------------------------------------ regs
     def alloc(self) -> int:
@@ -629,6 +634,7 @@ class Compiler:
         t = self.truth(s.test)
         at_if = self.emit(Op.IF, a=t.reg)
         self.release(t)
+        self._cond += 1
         self.block(s.body)
         if s.orelse:
             at_else = self.emit(Op.ELSE)
@@ -639,6 +645,7 @@ class Compiler:
         else:
             at_end = self.emit(Op.ENDIF)
             self.patch(at_if, at_end)
+        self._cond -= 1
 
     def _loop(self, header, body_fn, step_fn=None) -> None:
         """Masked loop skeleton: BEGIN; test: header() -> cond; TEST; body; CONT; step; NEXT; EXIT."""
@@ -854,7 +861,93 @@ class Compiler:
         m = getattr(self, "e_" + type(e).__name__, None)
         if m is None:
             raise CompileError(f"unsupported expression {type(e).__name__}")
-        return m(e)
+        key = self._cse_key(e)
+        if key is not None:
+            hit = self._cse.get(key)
+            if hit is not None:
+                return hit
+        v = m(e)
+        if key is not None and v.kind == NUM and v.temp and not self._cond and not self.loop_depth \
+                and len(self._cse) < self.CSE_MAX:
+            v.temp = False                  # held for the rest of the function
+            self._cse[key] = v
+        return v
+
+    #: cached values per program (each holds a register to the end)
+    CSE_MAX = 16
+    _CSE_NODES = (ast.BinOp, ast.UnaryOp, ast.Compare, ast.BoolOp, ast.IfExp, ast.Call, ast.Attribute,
+                  ast.Subscript, ast.GeneratorExp, ast.ListComp, ast.comprehension, ast.Lambda, ast.Name,
+                  ast.Constant, ast.Slice, ast.arguments, ast.arg, ast.keyword)
+
+    def _cse_key(self, e) -> Optional[str]:
+        """Common-subexpression elimination for what is invariant within a call:
+        an expression that reads only pod / node fields (and names it binds
+        itself, as a comprehension does), calls only the pure builtins and
+        `math` functions, and holds no numeric literal other than int 0 / 1.
+        The first evaluation of such an expression at an unconditional point of
+        the function (not in a branch, loop or conditional operand) keeps its
+        register; later occurrences with the same source text reuse it.  Exact:
+        the value cannot change within the call, and if the first evaluation
+        raises, the call ends there as in CPython.  Literal-free, so a
+        program's bytecode never depends on its tunable constants (constant
+        polish and `same_shape_child` change values, not shapes).  None: not
+        eligible."""
+        if not isinstance(e, (ast.BinOp, ast.UnaryOp, ast.Compare, ast.BoolOp, ast.IfExp, ast.Call,
+                              ast.Subscript)):
+            return None
+        ok, used, bound, size, has_call = self._cse_info(e)
+        if not ok or size < 4 and not has_call:
+            return None
+        if not (used - bound) <= {self.pod_name, self.node_name, "math"} | SAFE_BUILTINS:
+            return None
+        if e.lineno != e.end_lineno:
+            return None
+        if self._lines is None:
+            self._lines = self.source.split("\n")
+        line = self._lines[e.lineno - 1]
+        if not line.isascii():
+            return None                     # (offsets are UTF-8 bytes)
+        return line[e.col_offset:e.end_col_offset]
+
+    def _cse_info(self, e) -> tuple:
+        """(eligible, names read, names bound, nodes, has a call) of a subtree, memoised."""
+        hit = self._cse_memo.get(id(e))
+        if hit is not None and hit[0] is e:
+            return hit[1]
+        t = type(e)
+        ok = isinstance(e, self._CSE_NODES)
+        used, bound, size, has_call = set(), set(), 1, t is ast.Call or t is ast.GeneratorExp or t is ast.ListComp
+        if t is ast.Constant:
+            ok = type(e.value) is int and e.value in (0, 1)
+        elif t is ast.Name:
+            if type(e.ctx) is ast.Load:
+                used.add(e.id)
+            else:
+                bound.add(e.id)             # a comprehension target
+        elif t is ast.arg:
+            bound.add(e.arg)
+        elif t is ast.Call and not (isinstance(e.func, ast.Name) and e.func.id in SAFE_BUILTINS
+                                    or isinstance(e.func, ast.Attribute) and isinstance(e.func.value, ast.Name)
+                                    and e.func.value.id == "math"):
+            ok = False
+        if ok:
+            for f in e._fields:
+                v = getattr(e, f, None)
+                for c in (v if type(v) is list else (v,)):
+                    if isinstance(c, ast.AST) and type(c) not in _LEAF_NODES:
+                        cok, cu, cb, cs, cc = self._cse_info(c)
+                        if not cok:
+                            ok = False
+                            break
+                        used |= cu
+                        bound |= cb
+                        size += cs
+                        has_call = has_call or cc
+                if not ok:
+                    break
+        res = (ok, used, bound, size, has_call)
+        self._cse_memo[id(e)] = (e, res)
+        return res
 
     def e_Constant(self, e: ast.Constant) -> Val:
         if isinstance(e.value, (bool, int, float)):
@@ -928,6 +1021,7 @@ class Compiler:
         self.emit(Op.MOV, r.reg, first.reg)
         self.release(first)
         ifs = []
+        self._cond += 1
         for v in e.values[1:]:
             t = self.tmp()
             self.emit(Op.TRUTH, t.reg, r.reg)
@@ -938,6 +1032,7 @@ class Compiler:
             nv = self.num(v)
             self.emit(Op.MOV, r.reg, nv.reg)
             self.release(nv)
+        self._cond -= 1
         for at in reversed(ifs):
             self.patch(at, self.emit(Op.ENDIF))
         return r
@@ -956,6 +1051,8 @@ class Compiler:
             left = right
             if i < len(e.ops) - 1:
                 ifs.append(self.emit(Op.IF, a=r.reg))
+                self._cond += 1             # the rest of a chain is conditional
+        self._cond -= len(ifs)
         self.release(left)
         for at in reversed(ifs):
             self.patch(at, self.emit(Op.ENDIF))
@@ -965,6 +1062,7 @@ class Compiler:
         t = self.truth(e.test)
         at_if = self.emit(Op.IF, a=t.reg)
         self.release(t)
+        self._cond += 1
         a = self.expr(e.body)
         r = self.tmp(a.kind)
         self.emit(Op.MOV, r.reg, a.reg)
@@ -972,6 +1070,7 @@ class Compiler:
         at_else = self.emit(Op.ELSE)
         self.patch(at_if, at_else)
         b = self.expr(e.orelse)
+        self._cond -= 1
         if b.kind != r.kind:
             raise CompileError("conditional expression mixes kinds")
         self.emit(Op.MOV, r.reg, b.reg)
@@ -1575,6 +1674,8 @@ def same_shape_child(parent: CompiledPolicy, child: str) -> Optional[CompiledPol
             f[idx] = float(ctxt)
         else:
             i[idx] = int(ctxt)
+            if ptxt != ctxt and (parent.iconst[idx] in (0, 1) or i[idx] in (0, 1)):
+                return None        # int 0 / 1 decide common-subexpression eligibility (Compiler._cse_key)
         while cstarts[line_c + 1] <= cs:
             line_c += 1
         lits.append((idx, line_c + 1, cs - cstarts[line_c], line_c + 1, ce - cstarts[line_c]))
