@@ -120,7 +120,9 @@ __device__ void pop_reinsert64(const RowHeap& hp, int n, uint64_t last, int j, u
 
 // PROF: s_memtime phase split (diagnostics build), per wave into
 // prof_out[16 * blockIdx.x + 8 * wave + phase] (H: pop, ring, sift, wait, push;
-// S: wait, pod, score, verdict, delete, eval)
+// S: wait, pod, score, verdict, delete, eval, args, call; `score` is the
+// argmax after the call, `args` the node-state load, `call` the feasibility
+// test, argument set-up and the program call)
 template <bool PROF = false>
 __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64_t* gheap, DevResult* out,
                            RowNativeArgs nat, double* table, uint64_t* prof_out = nullptr) {
@@ -423,6 +425,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
       int lexc = EXC_NONE;
       int64_t s = 0;
       const NodeRegs<1> na = load_nr();   // call arguments; dead after the call
+      mark(6);
       if (node_valid && (!feas_pro || feasible<1>(0, na, pod))) {
         const NodeRegs<1>& nr = na;
         const int32_t* gl = nr.gw[0];   // NPASS 1: unpacked
@@ -435,6 +438,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
                  pod.gmilli | (pod.ngpu << 16), pod.ctime, pod.dur, kcp);
         if (s < 0) { lexc = (int)(-s); s = 0; }
       }
+      mark(7);
       NodeRegs<1> nr = load_nr();         // re-read after the call (nothing kept across it)
       const uint32_t bad = row_ballot(lexc != EXC_NONE, 0);
       if (bad) {

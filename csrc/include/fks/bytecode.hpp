@@ -42,6 +42,8 @@ static_assert(sizeof(Insn) == 8, "Insn must be 8 bytes");
 constexpr int kMaxRegs = 64;
 constexpr int kNoReg = 255;
 constexpr int kMaxListLen = 15;
+// imm of GLIST_GET / LT / ADD in the compiler's GPU-list loop skeletons (policy/bytecode.py LOOP_INDEX)
+constexpr int32_t kLoopIndex = 1;
 
 enum Op : uint8_t {
   OP_NOP = 0,

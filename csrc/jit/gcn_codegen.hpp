@@ -85,6 +85,7 @@ class Codegen {
     if (n_ <= 0) throw CodegenError("empty program");
     if (P_.n_const + 1 > 256) throw CodegenError("constant block larger than the LDS staging area");
     analyse_flow();
+    list_facts();
     infer_types();
     liveness();
     simt_liveness();
@@ -109,6 +110,11 @@ class Codegen {
   // ---- flow
   std::vector<int> brk_t_, cont_t_;
   std::vector<std::array<int, 2>> succ_;
+  // ---- GPU-list facts per pc entry: registers holding node.gpus unchanged on
+  // every path (all_in_), and elements of such lists read by a kLoopIndex GET
+  // in the current iteration (uni_in_: the loop counter, equal in every lane
+  // still in the loop)
+  std::vector<uint64_t> all_in_, uni_in_;
   // ---- types: per pc entry state
   std::vector<std::array<uint8_t, kMaxRegs>> ty_;
   std::vector<char> reached_;
@@ -128,6 +134,7 @@ class Codegen {
   int s_entry_ = -1, s_dead_ = -1, ST_[3] = {-1, -1, -1}, S_LIT_ = -1;
   std::vector<int> free_spairs_;
   std::vector<int> ctl_spairs_;           // SGPR pairs held by open control frames
+  std::vector<int> held_spairs_;          // SGPR pairs an instruction keeps across its own runtime call
   int max_vgpr_ = 0, max_sgpr_ = 0;
   // ---- spills: registers in scratch slots, reloaded per instruction
   uint64_t spilled_ = 0;
@@ -222,6 +229,51 @@ class Codegen {
         if (t != -1 && (t < 0 || t >= n_)) throw CodegenError("jump target out of range");
       succ_[pc] = sc;
     }
+  }
+
+  // Forward must-analyses over the CFG (meet = intersection).  A lane follows
+  // one CFG path, so "on every path" holds per lane.  uni_in_ is cleared at
+  // every LOOP_CONT / LOOP_EXIT: an element is uniform only inside the
+  // iteration that read it (after the loop, lanes hold different last GPUs).
+  template <class F>
+  void must_solve(std::vector<uint64_t>& st, F transfer) {
+    st.assign(n_, ~0ull);
+    std::vector<char> seen(n_, 0);
+    st[0] = 0;
+    seen[0] = 1;
+    std::vector<int> work{0};
+    while (!work.empty()) {
+      const int pc = work.back();
+      work.pop_back();
+      const uint64_t out = transfer(pc, st[pc]);
+      for (int t : succ_[pc]) {
+        if (t < 0) continue;
+        const uint64_t nw = seen[t] ? (st[t] & out) : out;
+        if (!seen[t] || nw != st[t]) {
+          st[t] = nw;
+          seen[t] = 1;
+          work.push_back(t);
+        }
+      }
+    }
+  }
+  void list_facts() {
+    must_solve(all_in_, [&](int pc, uint64_t s) {
+      const Insn& in = P_.code[pc];
+      if (!defines(in.op) || in.d == kNoReg) return s;
+      const uint64_t bit = 1ull << in.d;
+      if (in.op == OP_GLIST_ALL || (in.op == OP_MOV && in.a != kNoReg && (s >> in.a & 1))) return s | bit;
+      return s & ~bit;
+    });
+    must_solve(uni_in_, [&](int pc, uint64_t s) {
+      const Insn& in = P_.code[pc];
+      if (in.op == OP_LOOP_CONT || in.op == OP_LOOP_EXIT) return (uint64_t)0;
+      if (!defines(in.op) || in.d == kNoReg) return s;
+      const uint64_t bit = 1ull << in.d;
+      if (in.op == OP_GLIST_GET && in.imm == kLoopIndex && in.a != kNoReg && (all_in_[pc] >> in.a & 1))
+        return s | bit;
+      return s & ~bit;
+    });
   }
 
   static uint8_t result_type(uint8_t op, uint8_t ta, uint8_t tb, uint8_t ct) {
@@ -776,6 +828,7 @@ class Codegen {
   // SGPR pairs live across a runtime call
   std::vector<int> live_sgprs() const {
     std::vector<int> out = {30, 31, s_entry_, s_entry_ + 1, s_dead_, s_dead_ + 1};
+    for (int b : held_spairs_) { out.push_back(b); out.push_back(b + 1); }
     for (const Frame& fr : frames_)
       for (int b : {fr.s_save, fr.s_else, fr.s_entry, fr.s_brk, fr.s_cont})
         if (b >= 0) { out.push_back(b); out.push_back(b + 1); }
@@ -1063,7 +1116,7 @@ class Codegen {
         set_tag_static(d, false);
         break;
       }
-      case OP_GPU: emit_gpu(in, ta); break;
+      case OP_GPU: emit_gpu(in, ta, (uni_in_[pc] >> a & 1) != 0); break;
       case OP_GLIST_ALL:
         e(mk(V_LSHRREV_B32, T(1), ic(16), v(4)));                 // n
         e(mk(V_LSHLREV_B32, Th(1), ic(2), T(1)));                 // 4n
@@ -1080,7 +1133,23 @@ class Codegen {
         e(mk(V_MOV_B32, Rh(d), ic(0)));
         set_tag_static(d, false);
         break;
-      case OP_GLIST_GET: emit_glist_get(in, tb); break;
+      case OP_GLIST_GET:
+        if (in.imm == kLoopIndex && tb == TY_I) {
+          // the compiler's loop counter: 0 <= b < len(a), no checks
+          if (all_in_[pc] >> a & 1) {   // node.gpus: element b is GPU b
+            if (R(d) != R(b)) e(mk(V_MOV_B64, R(d), R(b)));
+          } else {
+            e(mk(V_LSHLREV_B32, Th(1), ic(2), R(b)));
+            e(mk(V_ADD_U32, Th(1), ic(4), Th(1)));
+            e(mk(V_LSHRREV_B64, T(2), Th(1), R(a)));
+            e(mk(V_AND_B32, R(d), ic(15), T(2)));
+            e(mk(V_MOV_B32, Rh(d), ic(0)));
+          }
+          set_tag_static(d, false);
+          break;
+        }
+        emit_glist_get(in, tb);
+        break;
       case OP_GLIST_SLICE: emit_glist_slice(in, st); break;
       case OP_GLIST_NEW:
         e(mk(V_MOV_B64, R(d), ic(0)));
@@ -1089,6 +1158,13 @@ class Codegen {
       case OP_GLIST_APPEND: emit_glist_append(in); break;
       case OP_GLIST_INSERT: emit_glist_insert(in, st); break;
       case OP_ADD: case OP_SUB: case OP_MUL:
+        if (in.op == OP_ADD && in.imm == kLoopIndex && ta == TY_I && tb == TY_I) {
+          // loop counter step: counter + 1 <= 15, no overflow; the high half stays 0
+          e(mk(V_ADD_U32, R(d), R(a), R(b)));
+          if (R(d) != R(a)) e(mk(V_MOV_B32, Rh(d), ic(0)));
+          set_tag_static(d, false);
+          break;
+        }
         if (ta == TY_IF || tb == TY_IF) { rtcall(0, in.op, pc, d, a, ta, b, tb); break; }
         if (ta == TY_I && tb == TY_I) { emit_int_arith(in); break; }
         {
@@ -1122,6 +1198,10 @@ class Codegen {
         rtcall(0, in.op, pc, d, a, ta, b, tb);
         break;
       case OP_POW: case OP_LOGB: case OP_MPOW:
+        if (in.op == OP_POW && ta == TY_F && tb == TY_I && in.imm >= 1 && in.imm <= 3) {
+          emit_small_pow(in, pc);
+          break;
+        }
         rtcall(0, in.op, pc, d, a, ta, b, tb);
         break;
       case OP_SQRT: case OP_LOG: case OP_EXP: case OP_SIN: case OP_COS: case OP_TAN:
@@ -1211,7 +1291,10 @@ class Codegen {
         }
         break;
       case OP_LT: case OP_LE: case OP_GT: case OP_GE: case OP_EQ: case OP_NE:
-        emit_compare(in.op, a, ta, b, tb, ST(0));
+        if (in.op == OP_LT && in.imm == kLoopIndex && ta == TY_I && tb == TY_I)
+          cmp(V_CMP_LT_I32, ST(0), R(a), R(b));   // counter < length, both in [0, 15]
+        else
+          emit_compare(in.op, a, ta, b, tb, ST(0));
         set_bool(d, ST(0));
         break;
       case OP_MIN2: case OP_MAX2: emit_minmax(in, ta, tb); break;
@@ -1433,10 +1516,106 @@ class Codegen {
     set_tag_static(d, false);
   }
 
+  // ---- float ** k for a literal k in {1, 2, 3} (bytecode POW imm = k):
+  // glibc's pow is within 0.52 ULP of the exact power, so where the exact
+  // value x**k (as hi + residual, error-free products) lies within 0.4375 ULP
+  // of hi = fl(x**k) -- every neighbour of hi is then over 0.56 ULP away --
+  // pow returns hi.  hi must be normal, not a power of two (an exact value
+  // just below one sits in the finer binade) and well above the underflow
+  // range (exact error terms).  Other lanes call the runtime pow as before.
+  void small_pow_mask(int k, uint16_t x, uint16_t mask) {
+    // mask = lanes whose x ** k is hi (hi into T(0), residual into T(1))
+    auto normal_far = [&](uint16_t h, uint16_t out) {
+      e(mklit(S_MOV_B32, s(S_LIT_), 0x108u));                      // -normal | +normal
+      cmp(V_CMP_CLASS_F64, out, h, s(S_LIT_));
+      e(mk(V_BFE_U32, Th(2), (uint16_t)(h + 1), ic(20), ic(11)));    // biased exponent
+      e(mklit(S_MOV_B32, s(S_LIT_), 123u));
+      cmp(V_CMP_GT_U32, ST(2), Th(2), s(S_LIT_));
+      e(mk(S_AND_B64, out, out, ST(2)));
+    };
+    if (k == 1) {
+      normal_far(x, mask);
+      e(mklit(V_AND_B32, T(2), 0xFFFFFu, (uint16_t)(x + 1)));
+      e(mk(V_OR_B32, T(2), T(2), x));
+      cmp(V_CMP_NE_U32, ST(1), ic(0), T(2));
+      e(mk(S_AND_B64, mask, mask, ST(1)));
+      return;
+    }
+    e(mk(V_MUL_F64, T(0), x, x));                                    // h2
+    if (k == 2) {
+      MI f = mk(V_FMA_F64, T(1), x, x, T(0)); f.neg = 4; e(f);      // x*x - h2 (exact)
+    } else {
+      normal_far(T(0), mask);                                        // h2 normal, far from underflow
+      MI f = mk(V_FMA_F64, T(1), x, x, T(0)); f.neg = 4; e(f);      // l2
+      e(mk(V_MUL_F64, T(2), T(0), x));                               // h3
+      MI g = mk(V_FMA_F64, T(0), T(0), x, T(2)); g.neg = 4; e(g);   // e3 = h2*x - h3 (exact)
+      e(mk(V_FMA_F64, T(1), T(1), x, T(0)));                         // residual = l2*x + e3
+      e(mk(V_MOV_B64, T(0), T(2)));                                  // hi = h3
+    }
+    normal_far(T(0), k == 2 ? mask : ST(1));
+    if (k == 3) e(mk(S_AND_B64, mask, mask, ST(1)));
+    // hi's mantissa nonzero
+    e(mklit(V_AND_B32, T(2), 0xFFFFFu, Th(0)));
+    e(mk(V_OR_B32, T(2), T(2), T(0)));
+    cmp(V_CMP_NE_U32, ST(1), ic(0), T(2));
+    e(mk(S_AND_B64, mask, mask, ST(1)));
+    // |residual| <= 1.75 * 2^(eb - 1077) = 0.4375 ulp(hi): bits ((eb - 54) << 20 | 0xC0000, 0)
+    e(mk(V_BFE_U32, Th(2), Th(0), ic(20), ic(11)));
+    e(mk(V_LSHLREV_B32, Th(2), ic(20), Th(2)));
+    e(mklit(V_ADD_U32, Th(2), (uint32_t)(0xC0000 - (54 << 20)), Th(2)));
+    e(mk(V_MOV_B32, T(2), ic(0)));
+    cmp(V_CMP_LE_F64, ST(1), T(1), T(2), 1);
+    e(mk(S_AND_B64, mask, mask, ST(1)));
+  }
+  void emit_small_pow(const Insn& in, int pc) {
+    const int d = in.d, a = in.a, b = in.b, k = in.imm;
+    materialize_live(slive_out_[pc] | live_out_[pc]);   // both paths of the branch below see the same state
+    const int P = take_spair(), Q = take_spair();
+    held_spairs_ = {P, Q};
+    small_pow_mask(k, R(a), s(P));
+    // the other lanes: the runtime pow (inactive lanes' registers survive the call)
+    e(mk(S_ANDN2_B64, ST(0), EXEC, s(P)));
+    e(mk(S_AND_SAVEEXEC_B64, s(Q), ST(0)));
+    const int skip = label();
+    e(mkimm(S_CBRANCH_EXECZ, skip));
+    rtcall(0, OP_POW, pc, d, a, TY_F, b, TY_I);
+    place(skip);
+    e(mk(S_MOV_B64, EXEC, s(Q)));
+    held_spairs_.clear();
+    // fast lanes: hi (recomputed from x, which those lanes kept)
+    uint16_t hi = R(a);
+    if (k >= 2) {
+      e(mk(V_MUL_F64, T(0), R(a), R(a)));
+      if (k == 3) e(mk(V_MUL_F64, T(0), T(0), R(a)));
+      hi = T(0);
+    }
+    e(mk(V_CNDMASK_B32, R(d), R(d), hi, s(P)));
+    e(mk(V_CNDMASK_B32, Rh(d), Rh(d), (uint16_t)(hi + 1), s(P)));
+    set_tag_static(d, true);
+    give_spair(Q);
+    give_spair(P);
+  }
+
   // ---- node.gpus[j].field
-  void emit_gpu(const Insn& in, uint8_t ta) {
+  void emit_gpu(const Insn& in, uint8_t ta, bool uniform) {
     (void)ta;
     const int d = in.d, a = in.a;
+    if (uniform && (in.imm == 0 || in.imm == 1)) {
+      // j is the same in every active lane: one indexed move (GPR index mode)
+      // instead of a 3-level v_cndmask tree; j & 7 keeps an empty-exec read in range
+      const int base = in.imm == 0 ? 5 : 13;
+      e(mk(V_READFIRSTLANE_B32, s(S_LIT_), R(a)));
+      e(mk(S_AND_B32, s(S_LIT_), s(S_LIT_), ic(7)));
+      MI on = mk(S_SET_GPR_IDX_ON, NONE, s(S_LIT_));
+      on.s1 = 1;   // the mode field: index SRC0
+      e(on);
+      e(mkimm(S_NOP, 0));
+      e(mk(V_MOV_B32, R(d), v(base)));
+      e(mkimm(S_SET_GPR_IDX_OFF, 0));
+      e(mk(V_ASHRREV_I32, Rh(d), ic(31), R(d)));
+      set_tag_static(d, false);
+      return;
+    }
     e(mk(V_AND_B32, T(1), ic(15), R(a)));   // j
     if (in.imm == 0 || in.imm == 1) {
       const int base = in.imm == 0 ? 5 : 13;

@@ -24,6 +24,7 @@ struct Emu {
   uint32_t vg[256][kW];
   uint32_t sg[128];
   bool scc = false;
+  int gidx = -1;   // GPR index mode (SRC0) offset, -1: off
   std::vector<uint8_t> lds;
   std::vector<uint8_t> scratch[kW];
   int64_t steps = 0;
@@ -108,6 +109,8 @@ struct Emu {
         for (uint64_t b = ex; b; b &= b - 1) fn(__builtin_ctzll(b));
       };
       auto jump = [&](int lab) { next = (size_t)label_at[(size_t)lab]; };
+      if (gidx >= 0 && is_valu(m.op) && m.op != V_MOV_B32)
+        throw std::logic_error("emu: VALU other than v_mov_b32 in GPR index mode");
       switch (m.op) {
         case LABEL: case S_NOP: case S_WAITCNT: break;
         case S_ENDPGM: throw std::logic_error("emu: s_endpgm in a function");
@@ -141,12 +144,24 @@ struct Emu {
         case S_ADDC_U32: { const uint64_t x = (uint64_t)r32(m.s0, 0, m.lit) + r32(m.s1, 0, m.lit) + (scc ? 1 : 0); sg[m.d] = (uint32_t)x; scc = x >> 32; break; }
         case S_SUB_U32: { const uint32_t a = r32(m.s0, 0, m.lit), b = r32(m.s1, 0, m.lit); sg[m.d] = a - b; scc = b > a; break; }
         case S_ADD_I32: { const int64_t x = (int64_t)(int32_t)r32(m.s0, 0, m.lit) + (int32_t)r32(m.s1, 0, m.lit); sg[m.d] = (uint32_t)x; scc = x != (int32_t)x; break; }
+        case S_SET_GPR_IDX_ON:
+          if (m.s1 != 1) throw std::logic_error("emu: GPR index mode other than SRC0");
+          gidx = (int)(sg[m.s0] & 0xFF);
+          break;
+        case S_SET_GPR_IDX_OFF: gidx = -1; break;
         case S_CMP_EQ_U32: scc = r32(m.s0, 0, m.lit) == r32(m.s1, 0, m.lit); break;
         case S_CMP_LG_U32: scc = r32(m.s0, 0, m.lit) != r32(m.s1, 0, m.lit); break;
         case S_CMP_EQ_U64: scc = r64(m.s0, 0, m.lit) == r64(m.s1, 0, m.lit); break;
         case S_CMP_LG_U64: scc = r64(m.s0, 0, m.lit) != r64(m.s1, 0, m.lit); break;
         // ---- VALU
-        case V_MOV_B32: lanes([&](int l) { w32(m.d, l, r32(m.s0, l, m.lit)); }); break;
+        case V_MOV_B32:
+          if (gidx >= 0) {
+            if (m.s0 < 256 || m.s0 - 256 + gidx >= 256) throw std::logic_error("emu: indexed move out of range");
+            lanes([&](int l) { w32(m.d, l, vg[m.s0 - 256 + gidx][l]); });
+          } else {
+            lanes([&](int l) { w32(m.d, l, r32(m.s0, l, m.lit)); });
+          }
+          break;
         case V_MOV_B64: lanes([&](int l) { w64v(m.d, l, r64(m.s0, l, m.lit)); }); break;
         case V_NOT_B32: lanes([&](int l) { w32(m.d, l, ~r32(m.s0, l, m.lit)); }); break;
         case V_READFIRSTLANE_B32: {

@@ -224,7 +224,7 @@ inline void encode_one(const MI& m, std::vector<uint32_t>& out) {
       else if (oi.fmt == VOP2) op3 = 0x100 + op;
       uint32_t w0 = 0xD0000000u | op3 << 16;
       if (oi.fmt == VOPC) {
-        w0 |= f8(m.sd);
+        w0 |= f8(m.sd) | (uint32_t)(m.abs & 3) << 8;   // VOP3A: sdst in the vdst field, abs still encoded
       } else {
         const uint32_t dst = m.d == NONE ? 0u : (is_v(m.d) ? (uint32_t)vidx(m.d) : (uint32_t)m.d);
         w0 |= dst;

@@ -82,6 +82,13 @@ TAG_INT, TAG_FLOAT = 0, 1
 MAX_REGS = 64
 NO_REG = 255
 MAX_LIST_LEN = 15
+#: `imm` of GLIST_GET / LT / ADD in the compiler's own GPU-list loop skeletons
+#: (hidden list snapshot, length and counter): the counter runs 0 .. len-1, so
+#: the GET is in range, the LT compares two ints in [0, 15] and the ADD is
+#: counter + 1 <= 15.  Interpreters ignore it (their checks pass anyway); the
+#: baseline JIT drops the checks, and when the list is ``node.gpus`` unchanged
+#: indexes the GPU fields with the counter (uniform across the lanes in the loop).
+LOOP_INDEX = 1
 
 
 class Exc(enum.IntEnum):

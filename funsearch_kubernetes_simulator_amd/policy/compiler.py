@@ -35,7 +35,7 @@ import struct
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
-from .bytecode import (GPU_FIELDS, MAX_REGS, NO_REG, NODE_FIELDS, NODE_NGPUS, POD_FIELDS, TAG_FLOAT,
+from .bytecode import (GPU_FIELDS, LOOP_INDEX, MAX_REGS, NO_REG, NODE_FIELDS, NODE_NGPUS, POD_FIELDS, TAG_FLOAT,
                        TAG_INT, Exc, Op, pack_insn)
 
 
@@ -704,14 +704,14 @@ class Compiler:
 
         def header():
             c = self.tmp()
-            self.emit(Op.LT, c.reg, idx.reg, n.reg)
+            self.emit(Op.LT, c.reg, idx.reg, n.reg, LOOP_INDEX)
             return c
 
         def body_fn():
             g = self.var_val(target.id, GPU) if isinstance(target, ast.Name) else None
             if g is None:
                 raise CompileError("loop target must be a name")
-            self.emit(Op.GLIST_GET, g.reg, src.reg, idx.reg)
+            self.emit(Op.GLIST_GET, g.reg, src.reg, idx.reg, LOOP_INDEX)
             self.mark_defined(target.id)
             if idx_target is not None:
                 iv = self.var_val(idx_target.id, NUM)
@@ -720,7 +720,7 @@ class Compiler:
             self.block(body)
 
         def step():
-            self.emit(Op.ADD, idx.reg, idx.reg, one.reg)
+            self.emit(Op.ADD, idx.reg, idx.reg, one.reg, LOOP_INDEX)
 
         self._loop(header, body_fn, step)
         for v in (src, n, idx, one):
@@ -873,8 +873,12 @@ class Compiler:
             self._cse[key] = v
         return v
 
-    #: cached values per program (each holds a register to the end)
-    CSE_MAX = 16
+    #: cached values per program (each holds a register to the end).  Off: on
+    #: an evolved population (data/populations/config3_steady_r4_islands.json,
+    #: 512 children) 16 held values made the baseline JIT decline 371 programs
+    #: for VGPR pressure (4: 154; 0: 2) -- a declined program replays on the
+    #: device VM at a fraction of native speed, far more than the saved work
+    CSE_MAX = 0
     _CSE_NODES = (ast.BinOp, ast.UnaryOp, ast.Compare, ast.BoolOp, ast.IfExp, ast.Call, ast.Attribute,
                   ast.Subscript, ast.GeneratorExp, ast.ListComp, ast.comprehension, ast.Lambda, ast.Name,
                   ast.Constant, ast.Slice, ast.arguments, ast.arg, ast.keyword)
@@ -994,9 +998,18 @@ class Compiler:
         if op is None:
             raise CompileError(f"unsupported operator {type(e.op).__name__}")
         a = self.num(e.left)
-        b = self.num(e.right)
-        d = self.tmp()
-        self.emit(op, d.reg, a.reg, b.reg)
+        r = e.right
+        if op == Op.POW and isinstance(r, ast.Constant) and type(r.value) is int and r.value in (1, 2, 3):
+            # x ** 1 / 2 / 3: the exponent is part of the code (not a tunable
+            # literal) and named in imm, so the baseline JIT can inline the
+            # power (POW semantics unchanged; interpreters ignore imm)
+            b = self.load_const(r.value)
+            d = self.tmp()
+            self.emit(op, d.reg, a.reg, b.reg, r.value)
+        else:
+            b = self.num(r)
+            d = self.tmp()
+            self.emit(op, d.reg, a.reg, b.reg)
         self.release(a)
         self.release(b)
         return d
@@ -1189,14 +1202,14 @@ class Compiler:
 
                 def header():
                     c = self.tmp()
-                    self.emit(Op.LT, c.reg, idx.reg, n.reg)
+                    self.emit(Op.LT, c.reg, idx.reg, n.reg, LOOP_INDEX)
                     return c
 
                 def body_fn():
-                    self.emit(Op.GLIST_GET, elem.reg, src.reg, idx.reg)
+                    self.emit(Op.GLIST_GET, elem.reg, src.reg, idx.reg, LOOP_INDEX)
                     body()
 
-                self._loop(header, body_fn, lambda: self.emit(Op.ADD, idx.reg, idx.reg, one.reg))
+                self._loop(header, body_fn, lambda: self.emit(Op.ADD, idx.reg, idx.reg, one.reg, LOOP_INDEX))
                 for v in (src, n, idx, one):
                     self.release(v)
             else:

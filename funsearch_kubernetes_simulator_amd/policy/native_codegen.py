@@ -40,6 +40,7 @@ Control-flow mapping (bytecode pcs become labels):
 from __future__ import annotations
 
 import hashlib
+import math
 import struct
 from typing import Dict, List, Sequence, Tuple
 
@@ -87,10 +88,23 @@ class CodegenError(ValueError):
     """The bytecode has a shape the native backend does not lower."""
 
 
+def data_literal(tag: int, fval: float, ival: int) -> bool:
+    """A source literal kept as run-time data (read from the constant block):
+    the values constant polish tunes (funsearch/polish.py tunable_literals) --
+    ints of magnitude >= 2, finite nonzero floats.  0, +-1, 0.0 and non-finite
+    literals are compiled in as immediates instead (no dependent LDS read per
+    use) and, like compiler-generated constants, are part of the shape key."""
+    if tag == TAG_FLOAT:
+        return fval != 0.0 and math.isfinite(fval)
+    return abs(int(ival)) >= 2
+
+
 def _literal_slots(prog: CompiledPolicy) -> set:
-    """Pool entries that hold source literals (the data of a shape); the rest
-    are compiler-generated (loop start / step, ...) and fixed by the code."""
-    return {int(lit[0]) for lit in getattr(prog, "literals", ()) or ()}
+    """Pool entries read from the constant block at run time (the data of a
+    shape); the rest -- compiler-generated constants (loop start / step, ...)
+    and the literals data_literal() pins -- are immediates in the code."""
+    return {k for k in (int(lit[0]) for lit in getattr(prog, "literals", ()) or ())
+            if data_literal(int(prog.ctag[k]), float(prog.fconst[k]), int(prog.iconst[k]))}
 
 
 def _all_list_at(code, flow) -> List[set]:
@@ -153,7 +167,8 @@ def shape_key(prog: CompiledPolicy) -> str:
     data (read from the constant block), so programs that differ only in them
     share a shape; compiler-generated constants are immediates in the code and
     part of the key."""
-    h = hashlib.sha1(prog.code)
+    h = hashlib.sha1(b"imm-literals-1")
+    h.update(prog.code)
     h.update(bytes(prog.ctag))
     h.update(repr(_inline_constants(prog)).encode())
     return h.hexdigest()

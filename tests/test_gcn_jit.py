@@ -160,25 +160,14 @@ def test_single_events_equal_cpu_vm_on_random_states(corpus):
                 assert emu[n] == ref, (p.source[-300:], n, pod, node[6 * n:6 * n + 6], (k, v), emu[n])
 
 
-def test_dynamic_types_runtime_calls_and_lists():
-    """Programs whose registers change type at run time (runtime-library calls,
-    tag bits), GPU-list slicing / insertion / sorting, and exceptions."""
-    bodies = [
-        "s = 0.0\n    if pod.cpu_milli > 30000:\n        s = int(pod.cpu_milli * 0.05)\n    s = max(1, s)\n"
-        "    if node.cpu_milli_left > pod.cpu_milli * 2:\n        s += 54.111\n    return max(1, int(s))",
-        "x = node.cpu_milli_left ** 0.5 + (node.memory_mib_left % 7) // 2\n    return x",
-        "g = sorted(node.gpus, key=lambda g: g.gpu_milli_left)[:2]\n    t = 0\n"
-        "    for q in g:\n        t += q.gpu_milli_left\n    return t + len(g) * 3",
-        "v = node.cpu_milli_left / (node.gpu_left - 1)\n    return v",
-        "a = [g for g in node.gpus if g.gpu_milli_left > 100]\n    return max(1, len(a) * 100 - node.gpus[0].gpu_milli_left)",
-        "r = round(node.memory_mib_left / 3.0) + abs(pod.cpu_milli - node.cpu_milli_left)\n    return -r if r % 2 else r",
-    ]
+def _check_bodies(bodies, seed, events=8):
+    """Each body as a program: one emulated wave per random event == the VM per node."""
     m = ce.native()
-    rng = random.Random(11)
+    rng = random.Random(seed)
     for body in bodies:
         p = compile_policy("def priority_function(pod, node):\n    " + body + "\n")
         kc = constant_block(p, 1 << 16).tolist()
-        for _ in range(8):
+        for _ in range(events):
             node, gl, gt, gm, pod = _random_event(rng)
             emu = m.gcn_emu_event(p.code, list(map(int, p.ctag)), gcnjit.literal_mask(p).tolist(),
                                   list(map(int, p.iconst)), list(map(float, p.fconst)), kc, node, gl, gt, gm, pod)
@@ -194,6 +183,118 @@ def test_dynamic_types_runtime_calls_and_lists():
                 if ref in (-100, -101) or emu[n] in (-100, -101):
                     continue
                 assert emu[n] == ref, (body, n, (k, v), emu[n])
+
+
+GPU_LOOP_BODIES = [
+    # node.gpus loops: counter-indexed GPU fields (GPR index mode), unchecked GETs
+    "c = 0\n    for gpu in node.gpus:\n        if gpu.gpu_milli_left >= pod.gpu_milli:\n            c += 1\n"
+    "    return c * 10 + 1",
+    "return sum(g.gpu_milli_left for g in node.gpus) + 3 * len([g for g in node.gpus if g.gpu_milli_total > 0])",
+    "return max(g.gpu_milli_total - g.gpu_milli_left for g in node.gpus)",
+    "t = 0\n    for i, g in enumerate(node.gpus):\n        t += i * g.gpu_milli_left + g.memory_mib_left % 7\n    return t",
+    # the outer element inside an inner loop, and after its loop (per-lane last GPU)
+    "t = 0\n    for g in node.gpus:\n        for h in node.gpus:\n            if h.gpu_milli_left > g.gpu_milli_left:\n"
+    "                t += g.gpu_milli_total - h.gpu_milli_left\n    return t",
+    "t = 1\n    g = node.gpus[0]\n    for g in node.gpus:\n        t += 1\n    return t * 1000 + g.gpu_milli_left",
+    # the loop variable reassigned in the body; loops over other lists
+    "t = 0\n    for g in node.gpus:\n        if g.gpu_milli_left < 500:\n            g = node.gpus[0]\n"
+    "        t += g.gpu_milli_left\n    return t",
+    "a = [g for g in node.gpus if g.gpu_milli_left > 100]\n    t = 0\n    for g in a:\n"
+    "        t += g.gpu_milli_total - g.gpu_milli_left\n    return t + len(a)",
+    "gs = node.gpus\n    if pod.num_gpu > 1:\n        gs = gs[1:]\n    t = 0\n    for g in gs:\n"
+    "        t += g.gpu_milli_left\n    return t",
+    "t = 0\n    for g in node.gpus:\n        if g.gpu_milli_left == 0:\n            continue\n        if t > 1500:\n"
+    "            break\n        t += g.gpu_milli_left\n    return t",
+    "s = sorted(node.gpus, key=lambda g: -g.gpu_milli_left)\n    return s[0].gpu_milli_left * 2 + s[-1].gpu_milli_total",
+]
+
+
+SMALL_POW_BODIES = [
+    "x = node.cpu_milli_left / node.cpu_milli_total\n    return (x ** 2 + x ** 3 - x ** 1) * 1e6",
+    "x = (node.memory_mib_left - pod.memory_mib) / 7.0\n    return x ** 3 + x ** 2 * 3.5 + (x - 1) ** 1",
+    "x = (pod.cpu_milli - node.cpu_milli_left) * 1e-300\n    return (x ** 2) * 1e300 + (x * 1e150) ** 3",
+    "x = 0.0 if node.gpu_left == 0 else node.cpu_milli_left / node.gpu_left\n    return x ** 2 - node.cpu_milli_left ** 2 / 1e3",
+    "x = float(2 ** (node.gpu_left + 1))\n    return x ** 2 + x ** 3 + x ** 1",
+    "x = node.cpu_milli_left * 1e200\n    return min(x ** 2, 1e300) + min(x ** 3, 1e308)",
+]
+
+
+def test_small_integer_powers_equal_cpu_vm():
+    """float ** 1 / 2 / 3 inlined by the JIT (glibc pow's 0.52-ULP bound:
+    lanes near a rounding boundary, zeros, powers of two, underflow and
+    overflow take the runtime pow) == the VM, which runs glibc's pow."""
+    _check_bodies(SMALL_POW_BODIES, seed=31, events=12)
+
+
+def test_gpu_list_loops_equal_cpu_vm():
+    """The compiler's GPU-list loop skeletons (bytecode LOOP_INDEX): unchecked
+    gets, 32-bit counters and, for node.gpus, fields read with the counter in
+    GPR index mode -- and the cases that must not take that path (outer
+    element in an inner loop, after the loop, reassigned, other lists)."""
+    _check_bodies(GPU_LOOP_BODIES, seed=21)
+
+
+@have_mc
+def test_node_gpus_loop_indexes_fields_uniformly():
+    p = compile_policy("def priority_function(pod, node):\n    " + GPU_LOOP_BODIES[0] + "\n")
+    code, why = gcnjit.compile_program(p)
+    assert code is not None, why
+    txt = " ".join(f"0x{b:02x}" for b in code.words.tobytes())
+    dis = subprocess.run([MC, "-disassemble", "-triple=amdgcn-amd-amdhsa", "-mcpu=gfx950"], input=txt,
+                         capture_output=True, text=True).stdout
+    assert dis.count("s_set_gpr_idx_on") == 1 and dis.count("s_set_gpr_idx_off") == 1
+    assert "v_cmp_lt_i32" in dis
+
+
+def test_evolved_population_compiles_natively():
+    """Register pressure on real evolved programs (a steady-mode population:
+    long, bloated bodies): the baseline JIT takes nearly all of them (a decline
+    sends a program to the device VM)."""
+    import json
+    pops = os.path.join(os.path.dirname(__file__), "..", "data", "populations")
+    codes = []
+
+    def walk(o):
+        if isinstance(o, dict):
+            if isinstance(o.get("code"), str):
+                codes.append(o["code"])
+            for v in o.values():
+                walk(v)
+        elif isinstance(o, list):
+            if len(o) == 2 and isinstance(o[0], str) and isinstance(o[1], (int, float)):
+                codes.append(o[0])   # [code, score] members
+            else:
+                for v in o:
+                    walk(v)
+    for name in ("config3_steady_r4_islands.json", "config3_steady_r4f_islands.json"):
+        walk(json.load(open(os.path.join(pops, name))))
+    codes = sorted(set(codes))
+    assert len(codes) >= 48
+    declined = []
+    for src in codes:
+        p = compile_policy(src)
+        if not p.device_ok:
+            continue
+        code, why = gcnjit.compile_program(p)
+        if code is None:
+            declined.append(why)
+    assert len(declined) <= len(codes) // 32, declined
+
+
+def test_dynamic_types_runtime_calls_and_lists():
+    """Programs whose registers change type at run time (runtime-library calls,
+    tag bits), GPU-list slicing / insertion / sorting, and exceptions."""
+    bodies = [
+        "s = 0.0\n    if pod.cpu_milli > 30000:\n        s = int(pod.cpu_milli * 0.05)\n    s = max(1, s)\n"
+        "    if node.cpu_milli_left > pod.cpu_milli * 2:\n        s += 54.111\n    return max(1, int(s))",
+        "x = node.cpu_milli_left ** 0.5 + (node.memory_mib_left % 7) // 2\n    return x",
+        "g = sorted(node.gpus, key=lambda g: g.gpu_milli_left)[:2]\n    t = 0\n"
+        "    for q in g:\n        t += q.gpu_milli_left\n    return t + len(g) * 3",
+        "v = node.cpu_milli_left / (node.gpu_left - 1)\n    return v",
+        "a = [g for g in node.gpus if g.gpu_milli_left > 100]\n    return max(1, len(a) * 100 - node.gpus[0].gpu_milli_left)",
+        "r = round(node.memory_mib_left / 3.0) + abs(pod.cpu_milli - node.cpu_milli_left)\n    return -r if r % 2 else r",
+    ]
+    _check_bodies(bodies, seed=11)
 
 
 def test_skeleton_layout_and_relocations():

@@ -21,7 +21,33 @@ from funsearch_kubernetes_simulator_amd.models.library import reference_policies
 from funsearch_kubernetes_simulator_amd.policy.compiler import compile_policy  # noqa: E402
 
 H = ("pop", "ring", "sift", "wait", "push")
-S = ("wait", "pod", "score", "verdict", "delete", "eval")
+S = ("wait", "pod", "argmax", "verdict", "delete", "eval", "args", "call")
+
+
+_FEAS = """def priority_function(pod, node):
+    if (pod.cpu_milli > node.cpu_milli_left or
+        pod.memory_mib > node.memory_mib_left or
+        pod.num_gpu > node.gpu_left):
+        return 0
+    if pod.num_gpu > 0:
+        available_gpus = 0
+        for gpu in node.gpus:
+            if gpu.gpu_milli_left >= pod.gpu_milli:
+                available_gpus += 1
+        if available_gpus < pod.num_gpu:
+            return 0
+"""
+_ALL_ARGS = _FEAS + """    s = node.cpu_milli_left + node.cpu_milli_total + node.memory_mib_left + node.memory_mib_total
+    s += node.gpu_left + pod.cpu_milli + pod.memory_mib + pod.num_gpu + pod.gpu_milli
+    for gpu in node.gpus:
+        s += gpu.gpu_milli_left + gpu.gpu_milli_total
+    return s
+"""
+
+_POW4 = _FEAS + """    a = node.cpu_milli_left ** 0.5 + node.memory_mib_left ** 1.5
+    b = (pod.cpu_milli + 1) ** 0.25 + math.exp(-node.cpu_milli_left / node.cpu_milli_total)
+    return a + b
+"""
 
 
 def main():
@@ -38,7 +64,11 @@ def main():
     dev._jit.tierup_after = 0
     sets = {"first_fit": [compile_policy(reference_policies()["first_fit"])],
             "funsearch_4901": [compile_policy(reference_policies()["funsearch_4901"])],
-            "children": mutation_children(a.programs, 0)}
+            "children": mutation_children(a.programs, 0),
+            # call-cost probes (feasibility prologue + body): one that reads
+            # every argument once, one with four libm calls
+            "all_args": [compile_policy(_ALL_ARGS)],
+            "pow4": [compile_policy(_POW4)]}
     if a.ck:
         sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
         from population_bench import _programs
@@ -48,6 +78,9 @@ def main():
         tab, prof = dev.profile_native(progs)
         prof = prof.reshape(len(progs), 2, 8)
         ev = float(tab[:, 8].sum())
+        if ev == 0:   # not replayed natively (e.g. declined): nothing to split
+            print(json.dumps({"set": name, "events": 0, "exc": tab[:, 10].tolist()}), flush=True)
+            continue
         rec = {"set": name, "tier": a.tier, "P": len(progs), "events": int(ev),
                "heap_wave": {H[i]: round(float(prof[:, 0, i].sum()) / ev, 1) for i in range(len(H))},
                "score_wave": {S[i]: round(float(prof[:, 1, i].sum()) / ev, 1) for i in range(len(S))}}

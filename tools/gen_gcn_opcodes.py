@@ -51,9 +51,11 @@ FORMS = [
     ("S_CMP_LG_U32", "SOPC", "s_cmp_lg_u32 s1, s2"),
     ("S_CMP_EQ_U64", "SOPC", "s_cmp_eq_u64 s[2:3], s[4:5]"),
     ("S_CMP_LG_U64", "SOPC", "s_cmp_lg_u64 s[2:3], s[4:5]"),
+    ("S_SET_GPR_IDX_ON", "SOPC", "s_set_gpr_idx_on s2, gpr_idx(SRC0)"),
     # SOPP
     ("S_NOP", "SOPP", "s_nop 1"),
     ("S_ENDPGM", "SOPP", "s_endpgm"),
+    ("S_SET_GPR_IDX_OFF", "SOPP", "s_set_gpr_idx_off"),
     ("S_BRANCH", "SOPP", "s_branch 5"),
     ("S_CBRANCH_SCC0", "SOPP", "s_cbranch_scc0 5"),
     ("S_CBRANCH_SCC1", "SOPP", "s_cbranch_scc1 5"),
