@@ -488,6 +488,12 @@ PYBIND11_MODULE(_fks_cpu, m) {
     p.n_const = ctag.size();
     return gcnapi::emu_event(p, kc, node, gl, gt, gmem, pod);
   });
+  m.def("gcn_emu_profile", [](bool on) { gcnapi::emu_profile(on); });
+  m.def("gcn_emu_profile_counts", []() {
+    py::dict d;
+    for (const auto& kv : gcnapi::emu_profile_counts()) d[py::str(kv.first)] = kv.second;
+    return d;
+  });
   m.def("gcn_emu_batch", [](const Workload& w, std::vector<py::bytes> codes, std::vector<std::vector<uint8_t>> ctags,
                             std::vector<std::vector<uint8_t>> lits, std::vector<std::vector<int64_t>> iconsts,
                             std::vector<std::vector<double>> fconsts, std::vector<std::vector<int64_t>> kcs,

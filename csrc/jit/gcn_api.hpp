@@ -43,6 +43,11 @@ std::string listing(const ProgramDesc& p);
 // Full replays with each program's generated code run on the wave64 emulator
 // as the scorer (CPU validation of the generator); kc[i] is program i's
 // constant block [budget, constants...].
+// Dynamic instruction counts of emulated replays (emu_simulate_batch) per
+// opcode name, collected while enabled (enabling resets them).
+void emu_profile(bool on);
+std::vector<std::pair<std::string, int64_t>> emu_profile_counts();
+
 std::vector<SimResult> emu_simulate_batch(const Workload& w, const std::vector<ProgramDesc>& progs,
                                           const std::vector<std::vector<int64_t>>& kc, const SimOptions& o,
                                           int threads);

@@ -170,7 +170,10 @@ class Codegen {
     if (in.op == OP_LOOP_BEGIN || in.op == OP_LOOP_EXIT || in.op == OP_CONST || in.op == OP_POD ||
         in.op == OP_NODE || in.op == OP_RAISE)
       return 0;
-    if (in.a != kNoReg) u |= 1ull << in.a;
+    // node.gpus itself is not read by its length or a loop-counter get (all_in_)
+    const bool all_list_read = (in.op == OP_GLIST_LEN || (in.op == OP_GLIST_GET && in.imm == kLoopIndex)) &&
+                               in.a != kNoReg && !all_in_.empty() && (all_in_[pc] >> in.a & 1);
+    if (in.a != kNoReg && !all_list_read) u |= 1ull << in.a;
     if (in.b != kNoReg) u |= 1ull << in.b;
     if ((in.op == OP_GLIST_SLICE || in.op == OP_GLIST_INSERT) && in.imm != kNoReg) u |= 1ull << in.imm;
     return u;
@@ -746,20 +749,34 @@ class Codegen {
     else e(mklit(V_MOV_B32, d, x));
   }
   // exc = (exc == 0 && lanes(mask)) ? code : exc
+  // Raising lanes record their code and leave EXEC at once (s_dead_), so every
+  // active lane has no exception yet and a raise is one v_cndmask: codes >= 100
+  // are held as code - 44 (56-59, inline constants) and mapped back in the
+  // epilogue.  Every EXEC restore excludes s_dead_.
+  static int exc_internal(int code) { return code >= 100 ? code - 44 : code; }
+  void kill_vcc() {
+    e(mk(S_OR_B64, s(s_dead_), s(s_dead_), VCC));
+    e(mk(S_ANDN2_B64, EXEC, EXEC, VCC));
+  }
   void soft_raise(uint16_t mask, int code) {
-    cmp(V_CMP_EQ_U32, ST(2), ic(0), v(v_exc_));
-    e(mk(S_AND_B64, VCC, ST(2), mask));
-    if (ic(code) != NONE) e(mk(V_CNDMASK_B32, v(v_exc_), v(v_exc_), ic(code), VCC));
+    const int c = exc_internal(code);
+    e(mk(S_AND_B64, VCC, EXEC, mask));
+    if (ic(c) != NONE) e(mk(V_CNDMASK_B32, v(v_exc_), v(v_exc_), ic(c), VCC));
     else {
-      vmov32(Th(2), (uint32_t)code);
+      vmov32(Th(2), (uint32_t)c);
       e(mk(V_CNDMASK_B32, v(v_exc_), v(v_exc_), Th(2), VCC));
     }
+    kill_vcc();
   }
-  // same with the code in a VGPR
+  // same with the (external) code in a VGPR
   void soft_raise_v(uint16_t mask, uint16_t code_v) {
-    cmp(V_CMP_EQ_U32, ST(2), ic(0), v(v_exc_));
-    e(mk(S_AND_B64, VCC, ST(2), mask));
-    e(mk(V_CNDMASK_B32, v(v_exc_), v(v_exc_), code_v, VCC));
+    e(mklit(S_MOV_B32, s(S_LIT_), 100u));
+    cmp(V_CMP_GE_U32, ST(2), code_v, s(S_LIT_));
+    e(mklit(V_ADD_U32, Th(2), (uint32_t)-44, code_v));
+    e(mk(V_CNDMASK_B32, Th(2), code_v, Th(2), ST(2)));
+    e(mk(S_AND_B64, VCC, EXEC, mask));
+    e(mk(V_CNDMASK_B32, v(v_exc_), v(v_exc_), Th(2), VCC));
+    kill_vcc();
   }
   // lanes where register r holds a float -> SGPR pair
   void tag_mask(int r, uint16_t dst) {
@@ -1013,6 +1030,9 @@ class Codegen {
     // epilogue: v[0:1] = exc ? -exc : out
     place(l_end);
     e(mk(S_MOV_B64, EXEC, s(s_entry_)));
+    cmp(V_CMP_GE_U32, ST(0), v(v_exc_), ic(56));                  // internal code -> EXC_*
+    e(mk(V_ADD_U32, T(1), ic(44), v(v_exc_)));
+    e(mk(V_CNDMASK_B32, v(v_exc_), v(v_exc_), T(1), ST(0)));
     cmp(V_CMP_NE_U32, ST(0), ic(0), v(v_exc_));
     e(mk(V_SUB_U32, T(0), ic(0), v(v_exc_)));
     e(mk(V_CNDMASK_B32, v(0), v(v_out_), T(0), ST(0)));
@@ -1040,13 +1060,22 @@ class Codegen {
     uint16_t mask_a = NONE;
     if (exec_change) {
       if (in.op == OP_IF || in.op == OP_LOOP_TEST) mask_a = truth(a, ta, ST(0));
-      if (mask_a != NONE && mask_a != ST(0)) { e(mk(S_MOV_B64, ST(0), mask_a)); mask_a = ST(0); }
+      // (a bool's mask pair survives the materialisation below: used in place)
       materialize_live(slive_out_[pc] | live_out_[pc]);
       bm_clear();
     } else if (defines(in.op) && d != kNoReg && !via_mask) {
       // (NOT / TRUTH read their operand's mask first and set d's state themselves)
       if (!(in.op == OP_MOV || in.op == OP_POS)) bm_of_[d] = -1;
       if (!((in.op == OP_MOV || in.op == OP_POS) && (pend_ >> a & 1))) pend_ &= ~(1ull << d);
+    }
+    // a side-effect-free definition nothing reads (e.g. node.gpus built for a
+    // len() or a counter-indexed loop) emits nothing
+    if (d != kNoReg && !(live_out_[pc] >> d & 1) &&
+        (in.op == OP_CONST || in.op == OP_MOV || in.op == OP_POS || in.op == OP_POD || in.op == OP_NODE ||
+         in.op == OP_GLIST_ALL || in.op == OP_GLIST_LEN || (in.op == OP_GPU && in.imm <= 1))) {
+      pend_ &= ~(1ull << d);
+      bm_of_[d] = -1;
+      return;
     }
     switch (in.op) {
       case OP_NOP: break;
@@ -1129,7 +1158,8 @@ class Codegen {
         set_tag_static(d, false);
         break;
       case OP_GLIST_LEN:
-        e(mk(V_AND_B32, R(d), ic(15), R(a)));
+        if (all_in_[pc] >> a & 1) e(mk(V_LSHRREV_B32, R(d), ic(16), v(4)));   // len(node.gpus): the GPU count
+        else e(mk(V_AND_B32, R(d), ic(15), R(a)));
         e(mk(V_MOV_B32, Rh(d), ic(0)));
         set_tag_static(d, false);
         break;
@@ -1308,11 +1338,11 @@ class Codegen {
         if (t <= pc || t >= n_) throw CodegenError("bad IF target");
         if (P_.code[t].op == OP_ELSE) {
           fr.s_else = take_spair();
-          e(mk(S_ANDN2_B64, s(fr.s_else), EXEC, ST(0)));
+          e(mk(S_ANDN2_B64, s(fr.s_else), EXEC, mask_a));
         } else if (P_.code[t].op != OP_ENDIF) {
           throw CodegenError("IF target is neither ELSE nor ENDIF");
         }
-        e(mk(S_AND_SAVEEXEC_B64, s(fr.s_save), ST(0)));
+        e(mk(S_AND_SAVEEXEC_B64, s(fr.s_save), mask_a));
         e(mkimm(S_CBRANCH_EXECZ, label_for_pc(t)));
         frames_.push_back(fr);
         break;
@@ -1367,14 +1397,9 @@ class Codegen {
         Frame* l = innermost_loop();
         if (!l || frames_.back().pc != l->pc) throw CodegenError("LOOP_NEXT not at loop level");
         if (in.imm != l->pc + 1) throw CodegenError("loop back edge not to the loop head");
-        cmp(V_CMP_NE_U32, ST(0), ic(0), v(v_exc_));
-        e(mk(S_OR_B64, s(s_dead_), s(s_dead_), ST(0)));
-        e(mk(S_ANDN2_B64, EXEC, EXEC, ST(0)));
         e(mk(V_SUB_U32, v(v_bud_), v(v_bud_), ic(1)));
         cmp(V_CMP_LT_I32, ST(0), v(v_bud_), ic(0));
-        soft_raise(ST(0), EXC_BUDGET);
-        e(mk(S_OR_B64, s(s_dead_), s(s_dead_), ST(0)));
-        e(mk(S_ANDN2_B64, EXEC, EXEC, ST(0)));
+        soft_raise(ST(0), EXC_BUDGET);   // (lanes that raised in the body left EXEC already)
         e(mkimm(S_CBRANCH_EXECNZ, l->l_head));
         if (pc + 1 >= n_ || P_.code[pc + 1].op != OP_LOOP_EXIT) e(mkimm(S_BRANCH, label_for_pc(l_exit_of(pc))));
         break;
@@ -1580,7 +1605,7 @@ class Codegen {
     e(mkimm(S_CBRANCH_EXECZ, skip));
     rtcall(0, OP_POW, pc, d, a, TY_F, b, TY_I);
     place(skip);
-    e(mk(S_MOV_B64, EXEC, s(Q)));
+    e(mk(S_ANDN2_B64, EXEC, s(Q), s(s_dead_)));   // lanes the runtime pow raised in stay out
     held_spairs_.clear();
     // fast lanes: hi (recomputed from x, which those lanes kept)
     uint16_t hi = R(a);

@@ -25,6 +25,7 @@ struct Emu {
   uint32_t sg[128];
   bool scc = false;
   int gidx = -1;   // GPR index mode (SRC0) offset, -1: off
+  int64_t* hist = nullptr;   // executed instructions per opcode (profiling), or null
   std::vector<uint8_t> lds;
   std::vector<uint8_t> scratch[kW];
   int64_t steps = 0;
@@ -103,6 +104,7 @@ struct Emu {
       if (pc >= f.mi.size()) throw std::logic_error("emu: ran off the end");
       if (++steps > max_steps) throw std::runtime_error("emu: step limit");
       const MI& m = f.mi[pc];
+      if (hist) ++hist[m.op];
       const uint64_t ex = exec();
       size_t next = pc + 1;
       auto lanes = [&](auto fn) {

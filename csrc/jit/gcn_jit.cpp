@@ -4,6 +4,7 @@
 // runtime-library host build it emulates (pyops_dev.h under FKS_HOST_JIT)
 // defines HIP-style attribute macros.
 #include <chrono>
+#include <mutex>
 #include <cstring>
 #include <sstream>
 #include <string>
@@ -178,6 +179,26 @@ struct EmuScorer {
 
 }  // namespace
 
+namespace {
+std::mutex g_prof_mu;
+std::vector<int64_t> g_prof;
+bool g_prof_on = false;
+}  // namespace
+
+void emu_profile(bool on) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  g_prof.assign((size_t)gcn::NUM_OPC, 0);
+  g_prof_on = on;
+}
+
+std::vector<std::pair<std::string, int64_t>> emu_profile_counts() {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  std::vector<std::pair<std::string, int64_t>> out;
+  for (size_t i = 0; i < g_prof.size(); ++i)
+    if (g_prof[i]) out.emplace_back(gcn::info((gcn::Opc)i).name, g_prof[i]);
+  return out;
+}
+
 std::vector<SimResult> emu_simulate_batch(const Workload& w, const std::vector<ProgramDesc>& progs,
                                           const std::vector<std::vector<int64_t>>& kc, const SimOptions& o,
                                           int threads) {
@@ -197,6 +218,11 @@ std::vector<SimResult> emu_simulate_batch(const Workload& w, const std::vector<P
   parallel_for(P, threads, [&](int64_t i) {
     try {
       auto emu = std::make_unique<gcn::Emu>();
+      std::vector<int64_t> hist;
+      if (g_prof_on) {
+        hist.assign((size_t)gcn::NUM_OPC, 0);
+        emu->hist = hist.data();
+      }
       const std::vector<int64_t>& k = kc[(size_t)i];
       emu->lds.resize(k.size() * 8 + 64, 0);
       std::memcpy(emu->lds.data(), k.data(), k.size() * 8);
@@ -204,6 +230,10 @@ std::vector<SimResult> emu_simulate_batch(const Workload& w, const std::vector<P
       SimResult r = simulate(w, sc, o);
       if (r.exc == EXC_NONE && sc.exc) r.exc = sc.exc;
       out[(size_t)i] = std::move(r);
+      if (!hist.empty()) {
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        for (size_t j = 0; j < hist.size() && j < g_prof.size(); ++j) g_prof[j] += hist[j];
+      }
     } catch (const std::exception& e) {
       errs[(size_t)i] = e.what();
     }

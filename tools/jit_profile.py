@@ -1,0 +1,55 @@
+"""Dynamic instruction mix of baseline-JIT code (ops/gcnjit.py) over full
+replays on the wave64 emulator: executed wave instructions per opcode, per
+replayed event, for a program set (the reference seeds, offline-mutation
+children, or children of an evolved population).  Shows where the scoring
+wave's call time goes without a GPU.
+
+    python tools/jit_profile.py --set children --programs 24
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--set", default="children", choices=["children", "reference", "population"])
+    ap.add_argument("--programs", type=int, default=24)
+    ap.add_argument("--ck", default="data/populations/config3_steady_r4_islands.json")
+    ap.add_argument("--top", type=int, default=30)
+    a = ap.parse_args()
+    from funsearch_kubernetes_simulator_amd.core import load_default_workload
+    from funsearch_kubernetes_simulator_amd.ops import cpu_engine as ce
+    from funsearch_kubernetes_simulator_amd.ops import gcnjit
+    from funsearch_kubernetes_simulator_amd.policy.compiler import compile_policy
+    if a.set == "children":
+        from funsearch_kubernetes_simulator_amd.bench.programs import mutation_children
+        progs = mutation_children(a.programs, 0)
+    elif a.set == "reference":
+        from funsearch_kubernetes_simulator_amd.models.library import reference_policies
+        progs = [compile_policy(s) for s in reference_policies().values()]
+    else:
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from population_bench import _programs
+        progs = _programs(a.ck, a.programs, 7)
+    progs = [p for p in progs if gcnjit.compile_program(p)[0] is not None]
+    w = load_default_workload()
+    budget = 1 << 16
+    ce.native().gcn_emu_profile(True)
+    tab = gcnjit.emulate_programs(w, progs, budget, ce.SimOptions(budget=budget))
+    counts = ce.native().gcn_emu_profile_counts()
+    ce.native().gcn_emu_profile(False)
+    events = float(tab[:, 8].sum())
+    total = sum(v for k, v in counts.items() if k != "LABEL")
+    rows = sorted(((k, v) for k, v in counts.items() if k != "LABEL"), key=lambda kv: -kv[1])
+    print(json.dumps({"set": a.set, "programs": len(progs), "events": int(events),
+                      "insns_per_event": round(total / events, 1)}))
+    for k, v in rows[:a.top]:
+        print(f"{k:28s} {v / events:9.2f} per event  {100.0 * v / total:5.1f}%")
+
+
+if __name__ == "__main__":
+    main()
