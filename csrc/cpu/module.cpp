@@ -355,6 +355,7 @@ PYBIND11_MODULE(_fks_cpu, m) {
     py::dict out;
     out["ok"] = r.ok;
     out["reason"] = r.reason;
+    out["elided"] = r.elided;
     out["words"] = np_of(r.words);
     out["relocs"] = np_of(r.relocs);
     out["n_insns"] = r.n_insns; out["vgprs"] = r.vgprs; out["sgprs"] = r.sgprs; out["calls"] = r.calls;
@@ -370,12 +371,18 @@ PYBIND11_MODULE(_fks_cpu, m) {
       std::vector<uint8_t> ctag, is_lit;
       std::vector<int64_t> iconst;
       std::vector<double> fconst;
+      int elide_lo = 0, elide_hi = 0;
     };
     const size_t n = progs.size();
     std::vector<Owned> own(n);
     for (size_t i = 0; i < n; ++i) {
       py::tuple t = progs[i].cast<py::tuple>();
-      if (t.size() != 5) throw std::invalid_argument("program tuple: (code, ctag, is_lit, iconst, fconst)");
+      if (t.size() != 5 && t.size() != 7)
+        throw std::invalid_argument("program tuple: (code, ctag, is_lit, iconst, fconst[, elide_lo, elide_hi])");
+      if (t.size() == 7) {
+        own[i].elide_lo = t[5].cast<int>();
+        own[i].elide_hi = t[6].cast<int>();
+      }
       own[i].code = t[0].cast<std::string>();
       auto ct = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>(t[1]);
       auto il = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>(t[2]);
@@ -400,6 +407,8 @@ PYBIND11_MODULE(_fks_cpu, m) {
           p.ctag = own[i].ctag.data(); p.is_lit = own[i].is_lit.data();
           p.iconst = own[i].iconst.data(); p.fconst = own[i].fconst.data();
           p.n_const = own[i].ctag.size();
+          p.elide_lo = own[i].elide_lo;
+          p.elide_hi = own[i].elide_hi;
           res[i] = gcnapi::compile(p);
         }
       };
@@ -414,6 +423,7 @@ PYBIND11_MODULE(_fks_cpu, m) {
       py::dict d;
       d["ok"] = r.ok;
       d["reason"] = r.reason;
+      d["elided"] = r.elided;
       d["words"] = np_of(r.words);
       d["relocs"] = np_of(r.relocs);
       d["n_insns"] = r.n_insns; d["vgprs"] = r.vgprs; d["sgprs"] = r.sgprs; d["calls"] = r.calls;
@@ -479,15 +489,19 @@ PYBIND11_MODULE(_fks_cpu, m) {
   m.def("gcn_emu_event", [](py::bytes code, std::vector<uint8_t> ctag, std::vector<uint8_t> is_lit,
                             std::vector<int64_t> iconst, std::vector<double> fconst, std::vector<int64_t> kc,
                             std::vector<int64_t> node, std::vector<int32_t> gl, std::vector<int32_t> gt,
-                            std::vector<int64_t> gmem, std::vector<int64_t> pod) {
+                            std::vector<int64_t> gmem, std::vector<int64_t> pod, int elide_lo, int elide_hi) {
     const std::string c = code;
     gcnapi::ProgramDesc p;
     p.code = reinterpret_cast<const uint8_t*>(c.data());
     p.code_bytes = c.size();
     p.ctag = ctag.data(); p.is_lit = is_lit.data(); p.iconst = iconst.data(); p.fconst = fconst.data();
     p.n_const = ctag.size();
+    p.elide_lo = elide_lo;
+    p.elide_hi = elide_hi;
     return gcnapi::emu_event(p, kc, node, gl, gt, gmem, pod);
-  });
+  }, py::arg("code"), py::arg("ctag"), py::arg("is_lit"), py::arg("iconst"), py::arg("fconst"), py::arg("kc"),
+     py::arg("node"), py::arg("gl"), py::arg("gt"), py::arg("gmem"), py::arg("pod"), py::arg("elide_lo") = 0,
+     py::arg("elide_hi") = 0);
   m.def("gcn_emu_profile", [](bool on) { gcnapi::emu_profile(on); });
   m.def("gcn_emu_profile_counts", []() {
     py::dict d;

@@ -21,6 +21,7 @@ struct ProgramDesc {
   const int64_t* iconst = nullptr;
   const double* fconst = nullptr;
   size_t n_const = 0;
+  int elide_lo = 0, elide_hi = 0;   // bytecode range of a kernel-checked feasibility prologue (0, 0: none)
 };
 
 struct Result {
@@ -29,6 +30,7 @@ struct Result {
   std::vector<uint32_t> words;      // machine code (position independent except relocs)
   std::vector<uint32_t> relocs;     // triples: lo literal word, hi literal word, byte offset of the PC
   int n_insns = 0, vgprs = 0, sgprs = 0, calls = 0, vregs = 0, tagged = 0, mir = 0, spills = 0;
+  bool elided = false;              // compiled without the prologue (ProgramDesc elide range)
 };
 
 // bytecode -> gfx950 machine code (never throws: failures come back as !ok + reason)

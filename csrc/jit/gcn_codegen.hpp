@@ -63,6 +63,10 @@ struct ProgIn {
   const int64_t* iconst = nullptr;
   const double* fconst = nullptr;
   int n_const = 0;
+  // [elide_lo, elide_hi): the template's feasibility prologue, compiled out
+  // when every caller calls only for nodes its own feasible() accepts (the
+  // prologue then falls through with no effect); 0, 0: none
+  int elide_lo = 0, elide_hi = 0;
 };
 
 struct GenStats {
@@ -79,15 +83,32 @@ constexpr int kMaxSpills = 16;   // 128 B of scratch per lane
 
 class Codegen {
  public:
-  explicit Codegen(const ProgIn& p) : P_(p), n_(p.n) {}
+  explicit Codegen(const ProgIn& p) : P_(p), n_(p.n) {
+    if (p.elide_lo >= 0 && p.elide_lo < p.elide_hi && p.elide_hi <= p.n) {
+      own_code_.assign(p.code, p.code + p.n);
+      for (int pc = p.elide_lo; pc < p.elide_hi; ++pc) {
+        if (defines(own_code_[(size_t)pc].op) && own_code_[(size_t)pc].d != kNoReg)
+          elided_defs_ |= 1ull << own_code_[(size_t)pc].d;
+        own_code_[(size_t)pc] = Insn{};   // OP_NOP
+        own_code_[(size_t)pc].op = OP_NOP;
+        own_code_[(size_t)pc].d = own_code_[(size_t)pc].a = own_code_[(size_t)pc].b = kNoReg;
+      }
+      P_.code = own_code_.data();
+    }
+  }
 
   Func run(GenStats* st = nullptr) {
     if (n_ <= 0) throw CodegenError("empty program");
     if (P_.n_const + 1 > 256) throw CodegenError("constant block larger than the LDS staging area");
     analyse_flow();
     list_facts();
+    value_facts();
     infer_types();
     liveness();
+    // a value the elided prologue would have computed (e.g. its GPU count)
+    // must not be read afterwards: the caller then compiles the whole program
+    if (elided_defs_ && P_.elide_hi < n_ && (live_in_[(size_t)P_.elide_hi] & elided_defs_))
+      throw CodegenError("elided prologue defines a value the body reads");
     simt_liveness();
     layout_registers();
     arg_liveness();
@@ -104,7 +125,9 @@ class Codegen {
   }
 
  private:
-  const ProgIn& P_;
+  ProgIn P_;
+  std::vector<Insn> own_code_;   // the bytecode with the elided prologue as NOPs
+  uint64_t elided_defs_ = 0;     // registers the elided prologue defined
   int n_;
   Func F_;
   // ---- flow
@@ -115,6 +138,22 @@ class Codegen {
   // in the current iteration (uni_in_: the loop counter, equal in every lane
   // still in the loop)
   std::vector<uint64_t> all_in_, uni_in_;
+  // ---- value facts per pc entry (every path, per lane): ints with |x| < 2^31
+  // (i32_in_) / |x| <= 2^53 (ex_in_), and small non-negative constants (kin_:
+  // value 0-15, or -1) -- overflow / exactness checks and list indexing they make moot
+  std::vector<uint64_t> i32_in_, ex_in_, acc_in_;
+  std::vector<std::array<int8_t, kMaxRegs>> kin_;
+  int cur_pc_ = -1;
+  bool i32(int r) const { return cur_pc_ >= 0 && r != kNoReg && (i32_in_[cur_pc_] >> r & 1); }
+  bool exact(int r) const { return cur_pc_ >= 0 && r != kNoReg && (ex_in_[cur_pc_] >> r & 1); }
+  bool acc(int r) const { return cur_pc_ >= 0 && r != kNoReg && (acc_in_[cur_pc_] >> r & 1); }
+  // Loop iterations per call are capped at kJitLoopCap (more -> EXC_BUDGET, the
+  // next engine decides), so a static ADD / SUB runs at most 2 * cap + 1 times
+  // a call; with at most kAccSites of them, a value built from int32 terms by
+  // ADD / SUB with an int32 operand stays below 1024 * (2^21 + 1) * 2^31 < 2^63.
+  static constexpr uint32_t kJitLoopCap = 1u << 20;
+  static constexpr int kAccSites = 1024;
+  int kval(int r) const { return cur_pc_ >= 0 && r != kNoReg ? kin_[cur_pc_][r] : -1; }
   // ---- types: per pc entry state
   std::vector<std::array<uint8_t, kMaxRegs>> ty_;
   std::vector<char> reached_;
@@ -268,15 +307,136 @@ class Codegen {
       if (in.op == OP_GLIST_ALL || (in.op == OP_MOV && in.a != kNoReg && (s >> in.a & 1))) return s | bit;
       return s & ~bit;
     });
+    // the loop (LOOP_BEGIN pc) each pc belongs to, and the registers the
+    // counter-indexed GETs of each loop define: they stop being uniform at
+    // that loop's LOOP_CONT / LOOP_EXIT (an inner loop keeps an outer element)
+    std::vector<int> loop_of(n_, -1);
+    std::map<int, uint64_t> gen_of;
+    {
+      std::vector<int> stk;
+      for (int pc = 0; pc < n_; ++pc) {
+        const Insn& in = P_.code[pc];
+        if (in.op == OP_LOOP_BEGIN) stk.push_back(pc);
+        loop_of[pc] = stk.empty() ? -1 : stk.back();
+        if (in.op == OP_LOOP_EXIT && !stk.empty()) stk.pop_back();
+        if (in.op == OP_GLIST_GET && in.imm == kLoopIndex && in.d != kNoReg && loop_of[pc] >= 0)
+          gen_of[loop_of[pc]] |= 1ull << in.d;
+      }
+    }
     must_solve(uni_in_, [&](int pc, uint64_t s) {
       const Insn& in = P_.code[pc];
-      if (in.op == OP_LOOP_CONT || in.op == OP_LOOP_EXIT) return (uint64_t)0;
+      if (in.op == OP_LOOP_CONT || in.op == OP_LOOP_EXIT) {
+        const auto it = gen_of.find(loop_of[pc]);
+        return it == gen_of.end() ? s : (s & ~it->second);
+      }
       if (!defines(in.op) || in.d == kNoReg) return s;
       const uint64_t bit = 1ull << in.d;
       if (in.op == OP_GLIST_GET && in.imm == kLoopIndex && in.a != kNoReg && (all_in_[pc] >> in.a & 1))
         return s | bit;
       return s & ~bit;
     });
+  }
+
+  void value_facts() {
+    // constants compiled into the code only: a data literal (is_lit) takes
+    // other values in other programs of the same shape
+    auto fixed_int = [&](int k) { return k >= 0 && k < P_.n_const && !P_.is_lit[k] && P_.ctag[k] != TAG_FLOAT; };
+    auto small_k = [&](int k) { return fixed_int(k) && P_.iconst[k] > -(1ll << 31) && P_.iconst[k] < (1ll << 31); };
+    auto is_bool_op = [](uint8_t op) {
+      return op == OP_LT || op == OP_LE || op == OP_GT || op == OP_GE || op == OP_EQ || op == OP_NE ||
+             op == OP_NOT || op == OP_TRUTH || op == OP_ISINT;
+    };
+    // does the definition at pc give an int with |x| < 2^31 (i: i32 facts on entry)?
+    auto i32_def = [&](const Insn& in, uint64_t i) {
+      switch (in.op) {
+        case OP_CONST: return small_k(in.imm);
+        case OP_MOV: case OP_POS: return (i >> in.a & 1) != 0;
+        case OP_NODE: case OP_GLIST_LEN: case OP_GLIST_GET: return true;   // int32 argument fields / [0, 15]
+        case OP_POD: return in.imm >= 0 && in.imm <= 3;                     // creation / duration: int64
+        case OP_GPU: return in.imm == 0 || in.imm == 1;                     // GPU memory: int64
+        case OP_MIN2: case OP_MAX2: return (i >> in.a & 1) && (i >> in.b & 1);
+        default: return is_bool_op(in.op);
+      }
+    };
+    must_solve(i32_in_, [&](int pc, uint64_t st) {
+      const Insn& in = P_.code[pc];
+      if (!defines(in.op) || in.d == kNoReg) return st;
+      const uint64_t bit = 1ull << in.d;
+      return i32_def(in, st) ? (st | bit) : (st & ~bit);
+    });
+    must_solve(ex_in_, [&](int pc, uint64_t st) {
+      const Insn& in = P_.code[pc];
+      if (!defines(in.op) || in.d == kNoReg) return st;
+      const uint64_t bit = 1ull << in.d;
+      const uint64_t i = i32_in_[pc];
+      bool r = i32_def(in, i);
+      switch (in.op) {
+        case OP_MOV: case OP_POS: r = r || (st >> in.a & 1); break;
+        case OP_ADD: case OP_SUB: r = r || ((i >> in.a & 1) && (i >> in.b & 1)); break;   // |x| < 2^32
+        case OP_NEG: case OP_ABS: r = r || (i >> in.a & 1); break;
+        case OP_MIN2: case OP_MAX2: r = r || ((st >> in.a & 1) && (st >> in.b & 1)); break;
+        case OP_CONST:
+          r = r || (fixed_int(in.imm) && P_.iconst[in.imm] >= -(1ll << 53) && P_.iconst[in.imm] <= (1ll << 53));
+          break;
+        default: break;
+      }
+      return r ? (st | bit) : (st & ~bit);
+    });
+    int add_sites = 0;
+    for (int pc = 0; pc < n_; ++pc)
+      if (P_.code[pc].op == OP_ADD || P_.code[pc].op == OP_SUB) ++add_sites;
+    must_solve(acc_in_, [&](int pc, uint64_t st) {
+      const Insn& in = P_.code[pc];
+      if (!defines(in.op) || in.d == kNoReg) return st;
+      const uint64_t bit = 1ull << in.d;
+      const uint64_t i = i32_in_[pc];
+      bool r = i32_def(in, i);
+      if (add_sites <= kAccSites) {
+        switch (in.op) {
+          case OP_MOV: case OP_POS: case OP_NEG: case OP_ABS: r = r || (st >> in.a & 1); break;
+          case OP_ADD: case OP_SUB:
+            r = r || ((st >> in.a & 1) && (i >> in.b & 1)) || ((i >> in.a & 1) && (st >> in.b & 1));
+            break;
+          case OP_MIN2: case OP_MAX2: r = r || ((st >> in.a & 1) && (st >> in.b & 1)); break;
+          default: break;
+        }
+      }
+      return r ? (st | bit) : (st & ~bit);
+    });
+    // small constants: per register 0-15, -1 unknown, -2 not reached yet
+    kin_.assign(n_, {});
+    for (auto& a : kin_) a.fill(-2);
+    kin_[0].fill(-1);
+    std::vector<char> seen(n_, 0);
+    seen[0] = 1;
+    std::vector<int> work{0};
+    while (!work.empty()) {
+      const int pc = work.back();
+      work.pop_back();
+      std::array<int8_t, kMaxRegs> out = kin_[pc];
+      const Insn& in = P_.code[pc];
+      if (defines(in.op) && in.d != kNoReg) {
+        int8_t v = -1;
+        if (in.op == OP_CONST && fixed_int(in.imm) && P_.iconst[in.imm] >= 0 && P_.iconst[in.imm] <= 15)
+          v = (int8_t)P_.iconst[in.imm];
+        else if ((in.op == OP_MOV || in.op == OP_POS) && in.a != kNoReg)
+          v = kin_[pc][in.a];
+        else if (in.op == OP_GLIST_GET && in.a != kNoReg && in.b != kNoReg && (all_in_[pc] >> in.a & 1) &&
+                 kin_[pc][in.b] >= 0)
+          v = kin_[pc][in.b];   // node.gpus[k] is GPU k (lanes with k >= len raised)
+        out[in.d] = v < 0 ? -1 : v;
+      }
+      for (int t : succ_[pc]) {
+        if (t < 0) continue;
+        bool changed = !seen[t];
+        for (int r = 0; r < kMaxRegs; ++r) {
+          const int8_t nv = !seen[t] ? out[r] : (kin_[t][r] == out[r] ? out[r] : (int8_t)-1);
+          if (nv != kin_[t][r]) { kin_[t][r] = nv; changed = true; }
+        }
+        seen[t] = 1;
+        if (changed) work.push_back(t);
+      }
+    }
   }
 
   static uint8_t result_type(uint8_t op, uint8_t ta, uint8_t tb, uint8_t ct) {
@@ -602,6 +762,7 @@ class Codegen {
   // the first instruction that touches their destination, or at any label /
   // branch / call (so every control-flow merge starts with nothing pending).
   std::vector<uint16_t> lds_pending_;
+  uint8_t cur_bc_ = 255;   // bytecode opcode being lowered (MI::bc)
   void e(const MI& m) {
     if (!lds_pending_.empty()) {
       bool need = m.op == LABEL || is_branch(m.op) || m.op == S_SETPC_B64 || m.op == M_RTCALL || m.op == S_WAITCNT;
@@ -610,10 +771,14 @@ class Codegen {
           if (c != NONE && c + 1 >= b && c <= b + 1) need = true;
       if (need) {
         lds_pending_.clear();
-        if (m.op != S_WAITCNT) F_.mi.push_back(mkimm(S_WAITCNT, 0xC07F));
+        if (m.op != S_WAITCNT) {
+          F_.mi.push_back(mkimm(S_WAITCNT, 0xC07F));
+          F_.mi.back().bc = cur_bc_;
+        }
       }
     }
     F_.mi.push_back(m);
+    F_.mi.back().bc = cur_bc_;
     if (m.op == DS_READ_B64) lds_pending_.push_back(m.d);
   }
   // Bool-mask cache: a register that holds a 0 / 1 produced in the current
@@ -825,6 +990,10 @@ class Codegen {
   // f64 value of register r (type t) -> operand code of a pair
   uint16_t as_f64(int r, uint8_t t, int tmp) {
     if (t == TY_F) return R(r);
+    if (t == TY_I && i32(r)) {   // exact from the low dword
+      e(mk(V_CVT_F64_I32, T(tmp), R(r)));
+      return T(tmp);
+    }
     e(mk(M_CVT_F64_I64, T(tmp), R(r)));
     if (t == TY_I) return T(tmp);
     tag_mask(r, ST(1));
@@ -1001,7 +1170,7 @@ class Codegen {
       ld.imm = 0;
       e(ld);
       e(mkimm(S_WAITCNT, 0xC07F));
-      e(mk(V_MOV_B32, v(v_bud_), T(0)));
+      e(mklit(V_MIN_U32, v(v_bud_), kJitLoopCap, T(0)));   // (<= 0: unlimited -> the cap)
     }
     for (int r = 0; r < kMaxRegs; ++r) {
       if (!(live_in_[0] >> r & 1)) continue;
@@ -1022,9 +1191,13 @@ class Codegen {
       // their EXEC frames (an ENDIF after a then-branch that always returns
       // is unreached by flow, yet the IF branches to it)
       if (!reached_[pc] && !structural(P_.code[pc].op)) continue;
+      cur_bc_ = P_.code[pc].op;
+      cur_pc_ = pc;
       spill_in(pc);
       emit_op(pc);
       spill_out(pc);
+      cur_bc_ = 255;
+      cur_pc_ = -1;
     }
     if (!frames_.empty()) throw CodegenError("unbalanced control flow");
     // epilogue: v[0:1] = exc ? -exc : out
@@ -1178,6 +1351,15 @@ class Codegen {
           set_tag_static(d, false);
           break;
         }
+        if (tb == TY_I && kval(b) >= 0 && (all_in_[pc] >> a & 1)) {
+          // node.gpus[k], k a small constant: GPU k where k < len, else IndexError
+          e(mk(V_LSHRREV_B32, Th(1), ic(16), v(4)));
+          cmp(V_CMP_GE_U32, ST(0), ic(kval(b)), Th(1));
+          soft_raise(ST(0), EXC_INDEX);
+          e(mk(V_MOV_B64, R(d), ic(kval(b))));
+          set_tag_static(d, false);
+          break;
+        }
         emit_glist_get(in, tb);
         break;
       case OP_GLIST_SLICE: emit_glist_slice(in, st); break;
@@ -1210,8 +1392,8 @@ class Codegen {
         if (ta == TY_I && tb == TY_I) {
           cmp(V_CMP_EQ_I64, ST(0), ic(0), R(b));
           soft_raise(ST(0), EXC_ZERO_DIVISION);
-          check_exact_int(R(a), EXEC);
-          check_exact_int(R(b), EXEC);
+          if (!exact(a)) check_exact_int(R(a), EXEC);
+          if (!exact(b)) check_exact_int(R(b), EXEC);
         }
         {
           const uint16_t fa = as_f64(a, ta, 0), fb = as_f64(b, tb, 1);
@@ -1466,6 +1648,22 @@ class Codegen {
   // ---- int64 add / sub / mul with overflow -> EXC_UNSUPPORTED
   void emit_int_arith(const Insn& in) {
     const int d = in.d, a = in.a, b = in.b;
+    const bool no_ovf = (i32(a) && i32(b)) ||
+                        (in.op != OP_MUL && ((acc(a) && i32(b)) || (i32(a) && acc(b))));
+    if (no_ovf) {   // |a|, |b| < 2^31, or an accumulator plus an int32: no int64 overflow
+      if (in.op == OP_MUL) {
+        e(mk3b(V_MAD_I64_I32, R(d), VCC, R(a), R(b), ic(0)));
+      } else {
+        MI lo = mk(in.op == OP_ADD ? V_ADD_CO_U32 : V_SUB_CO_U32, R(d), R(a), R(b));
+        lo.sd = ST(0);
+        e(lo);
+        MI hi = mk(in.op == OP_ADD ? V_ADDC_CO_U32 : V_SUBB_CO_U32, Rh(d), Rh(a), Rh(b), ST(0));
+        hi.sd = ST(0);
+        e(hi);
+      }
+      set_tag_static(d, false);
+      return;
+    }
     if (in.op == OP_MUL) {
       // operands in int32 range multiply exactly with v_mad_i64_i32; anything
       // wider is left to the next engine (EXC_UNSUPPORTED)
@@ -1509,8 +1707,8 @@ class Codegen {
     const int d = in.d, a = in.a, b = in.b;
     cmp(V_CMP_EQ_I64, ST(0), ic(0), R(b));
     soft_raise(ST(0), EXC_ZERO_DIVISION);
-    check_exact_int(R(a), EXEC);
-    check_exact_int(R(b), EXEC);
+    if (!exact(a)) check_exact_int(R(a), EXEC);
+    if (!exact(b)) check_exact_int(R(b), EXEC);
     const uint16_t fa = as_f64(a, TY_I, 0), fb = as_f64(b, TY_I, 1);
     e(mk(M_FDIV64, T(2), fa, fb));
     e(mk(V_FLOOR_F64, T(2), T(2)));
@@ -1625,6 +1823,12 @@ class Codegen {
   void emit_gpu(const Insn& in, uint8_t ta, bool uniform) {
     (void)ta;
     const int d = in.d, a = in.a;
+    if ((in.imm == 0 || in.imm == 1) && kval(a) >= 0 && kval(a) < 8) {   // a constant GPU index
+      e(mk(V_MOV_B32, R(d), v((in.imm == 0 ? 5 : 13) + kval(a))));
+      e(mk(V_ASHRREV_I32, Rh(d), ic(31), R(d)));
+      set_tag_static(d, false);
+      return;
+    }
     if (uniform && (in.imm == 0 || in.imm == 1)) {
       // j is the same in every active lane: one indexed move (GPR index mode)
       // instead of a 3-level v_cndmask tree; j & 7 keeps an empty-exec read in range

@@ -26,6 +26,7 @@ struct Emu {
   bool scc = false;
   int gidx = -1;   // GPR index mode (SRC0) offset, -1: off
   int64_t* hist = nullptr;   // executed instructions per opcode (profiling), or null
+  int64_t* hist_bc = nullptr;   // ... per bytecode opcode they lower (256 entries), or null
   std::vector<uint8_t> lds;
   std::vector<uint8_t> scratch[kW];
   int64_t steps = 0;
@@ -105,6 +106,7 @@ struct Emu {
       if (++steps > max_steps) throw std::runtime_error("emu: step limit");
       const MI& m = f.mi[pc];
       if (hist) ++hist[m.op];
+      if (hist_bc) ++hist_bc[m.bc];
       const uint64_t ex = exec();
       size_t next = pc + 1;
       auto lanes = [&](auto fn) {

@@ -85,6 +85,7 @@ struct MI {
   uint8_t neg = 0, abs = 0;
   int32_t ext = -1;     // M_RTCALL: CallInfo index
   int8_t reloc = -1;    // 0 / 1: literal of the s_add_u32 / s_addc_u32 of a runtime-table address
+  uint8_t bc = 255;     // bytecode opcode this instruction lowers (emulator profiles; 255: prologue / epilogue)
 };
 
 // Runtime-library call (jit_abi.h rt_binop / rt_unop): arguments, result and

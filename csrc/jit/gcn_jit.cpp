@@ -33,6 +33,8 @@ gcn::ProgIn make_in(const ProgramDesc& p) {
   in.iconst = p.iconst;
   in.fconst = p.fconst;
   in.n_const = (int)p.n_const;
+  in.elide_lo = p.elide_lo;
+  in.elide_hi = p.elide_hi;
   return in;
 }
 
@@ -61,9 +63,19 @@ Result compile(const ProgramDesc& p) {
   Result r;
   try {
     gcn::ProgIn in = make_in(p);
-    gcn::Codegen cg(in);
     gcn::GenStats st;
-    gcn::Func f = cg.run(&st);
+    gcn::Func f;
+    try {
+      gcn::Codegen cg(in);
+      f = cg.run(&st);
+      r.elided = in.elide_lo < in.elide_hi;
+    } catch (const gcn::CodegenError&) {
+      if (!(in.elide_lo < in.elide_hi)) throw;
+      in.elide_lo = in.elide_hi = 0;   // the whole program (valid for any caller)
+      st = gcn::GenStats{};
+      gcn::Codegen cg(in);
+      f = cg.run(&st);
+    }
     gcn::Code code = gcn::assemble(f);
     r.words = std::move(code.words);
     for (const gcn::Reloc& rl : code.relocs) {
@@ -181,13 +193,14 @@ struct EmuScorer {
 
 namespace {
 std::mutex g_prof_mu;
-std::vector<int64_t> g_prof;
+std::vector<int64_t> g_prof, g_prof_bc;
 bool g_prof_on = false;
 }  // namespace
 
 void emu_profile(bool on) {
   std::lock_guard<std::mutex> lk(g_prof_mu);
   g_prof.assign((size_t)gcn::NUM_OPC, 0);
+  g_prof_bc.assign(256, 0);
   g_prof_on = on;
 }
 
@@ -196,6 +209,8 @@ std::vector<std::pair<std::string, int64_t>> emu_profile_counts() {
   std::vector<std::pair<std::string, int64_t>> out;
   for (size_t i = 0; i < g_prof.size(); ++i)
     if (g_prof[i]) out.emplace_back(gcn::info((gcn::Opc)i).name, g_prof[i]);
+  for (size_t i = 0; i < g_prof_bc.size(); ++i)
+    if (g_prof_bc[i]) out.emplace_back("bc:" + std::to_string(i), g_prof_bc[i]);
   return out;
 }
 
@@ -218,10 +233,12 @@ std::vector<SimResult> emu_simulate_batch(const Workload& w, const std::vector<P
   parallel_for(P, threads, [&](int64_t i) {
     try {
       auto emu = std::make_unique<gcn::Emu>();
-      std::vector<int64_t> hist;
+      std::vector<int64_t> hist, hist_bc;
       if (g_prof_on) {
         hist.assign((size_t)gcn::NUM_OPC, 0);
+        hist_bc.assign(256, 0);
         emu->hist = hist.data();
+        emu->hist_bc = hist_bc.data();
       }
       const std::vector<int64_t>& k = kc[(size_t)i];
       emu->lds.resize(k.size() * 8 + 64, 0);
@@ -233,6 +250,7 @@ std::vector<SimResult> emu_simulate_batch(const Workload& w, const std::vector<P
       if (!hist.empty()) {
         std::lock_guard<std::mutex> lk(g_prof_mu);
         for (size_t j = 0; j < hist.size() && j < g_prof.size(); ++j) g_prof[j] += hist[j];
+        for (size_t j = 0; j < hist_bc.size() && j < g_prof_bc.size(); ++j) g_prof_bc[j] += hist_bc[j];
       }
     } catch (const std::exception& e) {
       errs[(size_t)i] = e.what();

@@ -83,6 +83,16 @@ STACK_LIMIT_BYTES = 1024   # HIP's default per-lane stack for dynamic-stack kern
 _FEAS_SKIP = os.environ.get("FKS_FEAS_SKIP", "1") != "0"
 
 
+def _shape_key(p) -> str:
+    """The code cache key: shape_key, plus a mark when the baseline tier
+    compiles the program's feasibility prologue out (gcnjit.elide_range) --
+    that code is only valid where the kernels skip infeasible nodes, i.e. for
+    programs whose function-table entry carries the prologue bit."""
+    from .gcnjit import elide_range
+    k = shape_key(p)
+    return k + ":fp" if elide_range(p)[1] else k
+
+
 class JitError(RuntimeError):
     """The toolchain failed on a module (a bug, not an unsupported program)."""
 
@@ -372,7 +382,7 @@ class NativeCompiler:
         """Compile every shape of `progs` not compiled yet (thread-safe: islands
         call this concurrently; a shape another thread is compiling is waited
         for, not compiled twice) and build the batch's launch data."""
-        keys = [shape_key(p) for p in progs]
+        keys = [_shape_key(p) for p in progs]
         mine: Dict[str, CompiledPolicy] = {}
         others = []
         with self._lock:

@@ -87,6 +87,10 @@ class CompiledPolicy:
     features: frozenset = field(default_factory=frozenset)
     #: numeric source literals: (pool index, line, col, end line, end col)
     literals: list = field(default_factory=list)
+    #: bytecode range [lo, hi) of the body's first two statements -- the
+    #: template's feasibility prologue when `feasibility_prologue` holds
+    #: (ops/gcnjit.py compiles it out for kernels that call feasible nodes only)
+    prologue: Optional[Tuple[int, int]] = None
 
     @property
     def n_insns(self) -> int:
@@ -262,12 +266,21 @@ class Compiler:
             flag = self.alloc()
             self.scope.flags[name] = flag
             self.emit(Op.CONST, flag, imm=self.const(0))
-        self.block(fn.body)
+        body = fn.body
+        n_doc = 1 if (body and isinstance(body[0], ast.Expr) and isinstance(body[0].value, ast.Constant)
+                      and isinstance(body[0].value.value, str)) else 0
+        prologue = None
+        lo = len(self.code)
+        for j, st in enumerate(body):
+            self.stmt(st)
+            if j == n_doc + 1 and len(body) > n_doc + 2:
+                prologue = (lo, len(self.code))
         self.emit(Op.END)
         self._renumber_registers()
         nregs = max((c[1] for c in self.code if c[1] != NO_REG), default=0) + 1
         return CompiledPolicy(b"".join(pack_insn(*c) for c in self.code), self.fconst, self.iconst,
-                              self.ctag, nregs, self.source, frozenset(self.features), list(self.literals))
+                              self.ctag, nregs, self.source, frozenset(self.features), list(self.literals),
+                              prologue)
 
     #: ops whose `imm` field names a register (or NO_REG)
     _IMM_REG_OPS = (Op.GLIST_SLICE, Op.GLIST_INSERT)

@@ -226,6 +226,58 @@ def test_small_integer_powers_equal_cpu_vm():
     _check_bodies(SMALL_POW_BODIES, seed=31, events=12)
 
 
+def test_elided_feasibility_prologue_equals_cpu_vm_on_feasible_nodes(corpus):
+    """Code compiled without the template's feasibility prologue (the kernels
+    call such programs for feasible nodes only) scores every feasible node as
+    the whole program does on the VM; a body that reads the prologue's GPU
+    count keeps its prologue."""
+    m = ce.native()
+    rng = random.Random(41)
+    elided = 0
+    for p in corpus:
+        lo, hi = gcnjit.elide_range(p)
+        if not hi:
+            continue
+        r = m.gcn_compile_many([(p.code, np.asarray(p.ctag, np.uint8), gcnjit.literal_mask(p),
+                                 np.asarray(p.iconst, np.int64), np.asarray(p.fconst, np.float64), lo, hi)], 1)[0]
+        assert r["ok"], r["reason"]
+        if not r["elided"]:
+            continue
+        elided += 1
+        kc = constant_block(p, 1 << 16).tolist()
+        for _ in range(4):
+            node, gl, gt, gm, pod = _random_event(rng)
+            emu = m.gcn_emu_event(p.code, list(map(int, p.ctag)), gcnjit.literal_mask(p).tolist(),
+                                  list(map(int, p.iconst)), list(map(float, p.fconst)), kc, node, gl, gt, gm, pod,
+                                  elide_lo=lo, elide_hi=hi)
+            podd = dict(cpu_milli=pod[0], memory_mib=pod[1], num_gpu=pod[2], gpu_milli=pod[3], creation_time=pod[4],
+                        duration_time=pod[5])
+            for n in range(16):
+                nd = dict(cpu_milli_left=node[6 * n], cpu_milli_total=node[6 * n + 1], memory_mib_left=node[6 * n + 2],
+                          memory_mib_total=node[6 * n + 3], gpu_left=node[6 * n + 4])
+                ng = node[6 * n + 5]
+                free = sum(1 for j in range(ng) if gl[8 * n + j] >= pod[3])
+                feasible = (pod[0] <= nd["cpu_milli_left"] and pod[1] <= nd["memory_mib_left"] and
+                            pod[2] <= nd["gpu_left"] and (pod[2] == 0 or free >= pod[2]))
+                if not feasible:
+                    continue
+                k, v = m.score_program_once(p.code, list(p.fconst), list(p.iconst), list(p.ctag), podd, nd,
+                                            gl[8 * n:8 * n + ng], gt[8 * n:8 * n + ng], gm[8 * n:8 * n + ng])
+                ref = _finish(k, v)
+                if ref in (-100, -101) or emu[n] in (-100, -101):
+                    continue
+                assert emu[n] == ref, (p.source[-300:], n, (k, v), emu[n])
+    assert elided >= 10
+    from funsearch_kubernetes_simulator_amd.policy.template import PolicyTemplate
+    reads = compile_policy(PolicyTemplate.TEMPLATE.replace(
+        "{llm_generated_logic}", "score = 100 + (available_gpus if pod.num_gpu > 0 else 0)"))
+    lo, hi = gcnjit.elide_range(reads)
+    assert hi > lo
+    r = m.gcn_compile_many([(reads.code, np.asarray(reads.ctag, np.uint8), gcnjit.literal_mask(reads),
+                             np.asarray(reads.iconst, np.int64), np.asarray(reads.fconst, np.float64), lo, hi)], 1)[0]
+    assert r["ok"] and not r["elided"]
+
+
 def test_gpu_list_loops_equal_cpu_vm():
     """The compiler's GPU-list loop skeletons (bytecode LOOP_INDEX): unchecked
     gets, 32-bit counters and, for node.gpus, fields read with the counter in

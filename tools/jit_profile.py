@@ -42,13 +42,24 @@ def main() -> None:
     tab = gcnjit.emulate_programs(w, progs, budget, ce.SimOptions(budget=budget))
     counts = ce.native().gcn_emu_profile_counts()
     ce.native().gcn_emu_profile(False)
+    from funsearch_kubernetes_simulator_amd.policy.bytecode import Op
     events = float(tab[:, 8].sum())
+    by_bc = {}
+    for k, v in list(counts.items()):
+        if k.startswith("bc:"):
+            code = int(k[3:])
+            by_bc[Op(code).name if code in Op._value2member_map_ else "prologue/epilogue"] = v
+            del counts[k]
     total = sum(v for k, v in counts.items() if k != "LABEL")
     rows = sorted(((k, v) for k, v in counts.items() if k != "LABEL"), key=lambda kv: -kv[1])
     print(json.dumps({"set": a.set, "programs": len(progs), "events": int(events),
                       "insns_per_event": round(total / events, 1)}))
     for k, v in rows[:a.top]:
         print(f"{k:28s} {v / events:9.2f} per event  {100.0 * v / total:5.1f}%")
+    print("-- by the bytecode op they lower (labels included)")
+    tb = sum(by_bc.values())
+    for k, v in sorted(by_bc.items(), key=lambda kv: -kv[1])[:a.top]:
+        print(f"{k:28s} {v / events:9.2f} per event  {100.0 * v / tb:5.1f}%")
 
 
 if __name__ == "__main__":
