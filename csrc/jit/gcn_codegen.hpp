@@ -167,10 +167,11 @@ class Codegen {
   uint64_t tagged_ = 0;
   bool use_node_ = false, use_gl_ = false, use_gmem_ = false, use_kc_ = false, has_loop_ = false;
   std::array<int, 6> pod_s_{};            // argument VGPR of each pod field the program reads (-1 unused)
-  int v_exc_ = -1, v_bud_ = -1, v_out_ = -1, v_spill_ = -1;
+  int v_exc_ = -1, v_out_ = -1, v_spill_ = -1;
   int v_tag_[2] = {-1, -1};
   int T_[3] = {-1, -1, -1};               // temp VGPR pairs
   int s_entry_ = -1, s_dead_ = -1, ST_[3] = {-1, -1, -1}, S_LIT_ = -1;
+  int s_bud_ = -1;   // loop iterations left this call (wave-level: the SGPR pair's low half)
   std::vector<int> free_spairs_;
   std::vector<int> ctl_spairs_;           // SGPR pairs held by open control frames
   std::vector<int> held_spairs_;          // SGPR pairs an instruction keeps across its own runtime call
@@ -652,7 +653,6 @@ class Codegen {
     for (int i = 0; i < 3; ++i) T_[i] = take_pair();
     v_out_ = take_pair();
     v_exc_ = take_single();
-    if (has_loop_) v_bud_ = take_single();
     n_tagged_ = __builtin_popcountll(tagged_);
     tagbit_.fill(-1);
     {
@@ -738,6 +738,7 @@ class Codegen {
                     88, 90, 92, 94};
     s_entry_ = take_spair();
     s_dead_ = take_spair();
+    if (has_loop_) s_bud_ = take_spair();
     for (int i = 0; i < 3; ++i) ST_[i] = take_spair();
     S_LIT_ = take_spair();
     bm_pair_[0] = take_spair();
@@ -1014,6 +1015,7 @@ class Codegen {
   // SGPR pairs live across a runtime call
   std::vector<int> live_sgprs() const {
     std::vector<int> out = {30, 31, s_entry_, s_entry_ + 1, s_dead_, s_dead_ + 1};
+    if (s_bud_ >= 0) out.push_back(s_bud_);
     for (int b : held_spairs_) { out.push_back(b); out.push_back(b + 1); }
     for (const Frame& fr : frames_)
       for (int b : {fr.s_save, fr.s_else, fr.s_entry, fr.s_brk, fr.s_cont})
@@ -1066,7 +1068,6 @@ class Codegen {
     out.push_back(v_exc_);
     out.push_back(v_out_);
     out.push_back(v_out_ + 1);
-    if (v_bud_ >= 0) out.push_back(v_bud_);
     for (int t : v_tag_)
       if (t >= 0) out.push_back(t);
     // the destination is included: lanes outside EXEC keep its old value
@@ -1165,12 +1166,15 @@ class Codegen {
     e(mk(V_MOV_B64, v(v_out_), ic(0)));
     for (int t : v_tag_)
       if (t >= 0) e(mk(V_MOV_B32, v(t), ic(0)));
-    if (v_bud_ >= 0) {
+    if (s_bud_ >= 0) {
+      // kc[0] = the iteration budget, capped (<= 0: unlimited -> the cap); one
+      // counter for the wave: a lane never runs more iterations than the wave
       MI ld = mk(DS_READ_B64, T(0), v(29));
       ld.imm = 0;
       e(ld);
       e(mkimm(S_WAITCNT, 0xC07F));
-      e(mklit(V_MIN_U32, v(v_bud_), kJitLoopCap, T(0)));   // (<= 0: unlimited -> the cap)
+      e(mklit(V_MIN_U32, T(0), kJitLoopCap, T(0)));
+      e(mk(V_READFIRSTLANE_B32, s(s_bud_), T(0)));
     }
     for (int r = 0; r < kMaxRegs; ++r) {
       if (!(live_in_[0] >> r & 1)) continue;
@@ -1579,10 +1583,14 @@ class Codegen {
         Frame* l = innermost_loop();
         if (!l || frames_.back().pc != l->pc) throw CodegenError("LOOP_NEXT not at loop level");
         if (in.imm != l->pc + 1) throw CodegenError("loop back edge not to the loop head");
-        e(mk(V_SUB_U32, v(v_bud_), v(v_bud_), ic(1)));
-        cmp(V_CMP_LT_I32, ST(0), v(v_bud_), ic(0));
-        soft_raise(ST(0), EXC_BUDGET);   // (lanes that raised in the body left EXEC already)
-        e(mkimm(S_CBRANCH_EXECNZ, l->l_head));
+        {   // budget: s_bud -= 1; on a borrow every lane still looping raises BUDGET
+          e(mk(S_SUB_U32, s(s_bud_), s(s_bud_), ic(1)));
+          const int ok = label();
+          e(mkimm(S_CBRANCH_SCC0, ok));
+          soft_raise(EXEC, EXC_BUDGET);
+          place(ok);
+        }
+        e(mkimm(S_CBRANCH_EXECNZ, l->l_head));   // (lanes that raised in the body left EXEC already)
         if (pc + 1 >= n_ || P_.code[pc + 1].op != OP_LOOP_EXIT) e(mkimm(S_BRANCH, label_for_pc(l_exit_of(pc))));
         break;
       }

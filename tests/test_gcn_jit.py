@@ -278,6 +278,20 @@ def test_elided_feasibility_prologue_equals_cpu_vm_on_feasible_nodes(corpus):
     assert r["ok"] and not r["elided"]
 
 
+def test_runaway_loop_raises_budget():
+    """The loop budget is one counter per wave (kc[0], capped): a program that
+    never leaves its loop raises BUDGET in every lane (the next engine decides)."""
+    m = ce.native()
+    p = compile_policy("def priority_function(pod, node):\n    x = 0\n    while x >= 0:\n"
+                       "        x = (x + 1) % 7\n    return x\n")
+    node, gl, gt, gm, pod = _random_event(random.Random(5))
+    for budget in (1 << 10, 1 << 16):
+        kc = constant_block(p, budget).tolist()
+        emu = m.gcn_emu_event(p.code, list(map(int, p.ctag)), gcnjit.literal_mask(p).tolist(),
+                              list(map(int, p.iconst)), list(map(float, p.fconst)), kc, node, gl, gt, gm, pod)
+        assert list(emu) == [-101] * 16
+
+
 def test_gpu_list_loops_equal_cpu_vm():
     """The compiler's GPU-list loop skeletons (bytecode LOOP_INDEX): unchecked
     gets, 32-bit counters and, for node.gpus, fields read with the counter in
