@@ -261,10 +261,13 @@ void k_replay_rows_prof(fksk::BuiltinArgs a, int P, uint32_t* queue, uint32_t qb
 // policy's JIT function (wave-uniform pointer -> a plain s_swappc).
 struct NativeScorerDev {
   ProgFn fn;
+  bool feas;             // the program opens with the feasibility prologue (jit_abi.h kFnFeasBit):
+                         // called for feasible nodes only -- its JIT code may lack the prologue
   const int64_t* gmem;   // [node][kGmax] GPU memory MiB
   KcPtr kc;              // the policy's [budget, constants...], staged in LDS
   template <int NPASS, bool GP>
   __device__ int64_t score(int ps, const NodeRegs<NPASS, GP>& nr, const PodView& pod, int& exc) {
+    if (feas && !feasible<NPASS, GP>(ps, nr, pod)) return 0;
     const int node = ps * kWave + lane_id();
     int32_t gl[kGmax], gt[kGmax];
 #pragma unroll
@@ -351,6 +354,7 @@ __global__ __launch_bounds__(64, GHEAP ? 2 : 1) void k_replay_native(fksk::Nativ
   const Slot s = policy_slot<GHEAP>(a.W, a.gheap, p);
   NativeScorerDev sc;
   sc.fn = prog_of(uniu64(a.fn[p]));
+  sc.feas = prog_feas(uniu64(a.fn[p]));
   sc.gmem = a.W.gmem_total;
   // the constant block moves into the slot's register area (the host reserves
   // kKcLds / 64 VM registers for it; the allocation is padded by kKcLds entries,

@@ -874,7 +874,7 @@ class Compiler:
         m = getattr(self, "e_" + type(e).__name__, None)
         if m is None:
             raise CompileError(f"unsupported expression {type(e).__name__}")
-        key = self._cse_key(e)
+        key = self._cse_key(e) if self.CSE_MAX else None
         if key is not None:
             hit = self._cse.get(key)
             if hit is not None:
