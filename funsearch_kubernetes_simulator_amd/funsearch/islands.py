@@ -108,8 +108,14 @@ class IslandFunSearch:
         # one HIP stream (slot) per island, so pipelined islands never share one,
         # plus one for the family coupler (funsearch/coupling.py)
         cpl = dict(self.config.get("coupling") or {})
+        # steady mode may ask for more slots than islands: more batches in flight
+        # than the chip holds, so one batch's slowest programs never idle the CUs
+        # the rest of it has left (each slot is a stream: run with
+        # GPU_MAX_HW_QUEUES >= slots so the launches overlap)
+        st_slots = int(((self.config.get("islands") or {}).get("steady") or {}).get("slots") or 0)
         self.evaluator = evaluator or Evaluator(device=dev, options=opts,
-                                                n_slots=max(4, self.n_islands) + (1 if cpl.get("every") else 0))
+                                                n_slots=max(4, self.n_islands, st_slots) +
+                                                (1 if cpl.get("every") else 0))
         llm_cfg = dict(self.config.get("llm") or {})
         base_seed = int(llm_cfg.get("seed", 0)) + 1000003 * self.ctx.rank
         self.islands: List[SimpleFunSearch] = []
