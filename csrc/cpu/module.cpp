@@ -511,7 +511,7 @@ PYBIND11_MODULE(_fks_cpu, m) {
   m.def("gcn_emu_batch", [](const Workload& w, std::vector<py::bytes> codes, std::vector<std::vector<uint8_t>> ctags,
                             std::vector<std::vector<uint8_t>> lits, std::vector<std::vector<int64_t>> iconsts,
                             std::vector<std::vector<double>> fconsts, std::vector<std::vector<int64_t>> kcs,
-                            py::dict opts, int threads) {
+                            py::dict opts, int threads, std::vector<std::pair<int, int>> elide) {
     const size_t P = codes.size();
     std::vector<std::string> cs(P);
     std::vector<gcnapi::ProgramDesc> ps(P);
@@ -521,6 +521,7 @@ PYBIND11_MODULE(_fks_cpu, m) {
       ps[i].code_bytes = cs[i].size();
       ps[i].ctag = ctags[i].data(); ps[i].is_lit = lits[i].data(); ps[i].iconst = iconsts[i].data();
       ps[i].fconst = fconsts[i].data(); ps[i].n_const = ctags[i].size();
+      if (i < elide.size()) { ps[i].elide_lo = elide[i].first; ps[i].elide_hi = elide[i].second; }
     }
     SimOptions o = make_options(opts);
     std::vector<SimResult> rs;
@@ -531,7 +532,8 @@ PYBIND11_MODULE(_fks_cpu, m) {
     py::array_t<double> out({(int64_t)P, (int64_t)kCols});
     for (size_t i = 0; i < P; ++i) fill_row(out.mutable_data() + i * kCols, rs[i]);
     return out;
-  });
+  }, py::arg("w"), py::arg("codes"), py::arg("ctags"), py::arg("lits"), py::arg("iconsts"), py::arg("fconsts"),
+     py::arg("kcs"), py::arg("opts"), py::arg("threads"), py::arg("elide") = std::vector<std::pair<int, int>>{});
   m.attr("RESULT_COLUMNS") = py::make_tuple("score", "avg_cpu", "avg_mem", "avg_gpu_count", "avg_gpu_milli",
                                             "frag", "n_snapshots", "n_frag_events", "n_events", "n_unplaced",
                                             "exc", "inexact", "trace_hash_hi");

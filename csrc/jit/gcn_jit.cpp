@@ -137,6 +137,7 @@ struct EmuScorer {
   gcn::Emu* emu;
   std::vector<int64_t> res;
   int32_t exc = EXC_NONE;
+  bool feas_only = false;   // called for feasible nodes only (code without its prologue), others score 0
 
   ScoreOut operator()(const ScoreCtx& c, int n) {
     if (n == 0) run_event(c);
@@ -181,11 +182,28 @@ struct EmuScorer {
     }
     E.sg[32] = 0;
     E.wr64s(30, kRetMagic);
-    E.set_exec(N == 64 ? ~0ull : ((1ull << N) - 1));
+    uint64_t lanes = N == 64 ? ~0ull : ((1ull << N) - 1);
+    if (feas_only) {   // as the kernels' feasible() (scorers.hip.h)
+      const int32_t pc = w.pcpu[(size_t)c.pod], pm = w.pmem[(size_t)c.pod];
+      const int32_t pg = w.pngpu[(size_t)c.pod], gm = w.pgmilli[(size_t)c.pod];
+      for (int l = 0; l < N; ++l) {
+        bool ok = pc <= c.s.cpu_left[(size_t)l] && pm <= c.s.mem_left[(size_t)l] && pg <= c.s.gpu_left[(size_t)l];
+        if (ok && pg > 0) {
+          const int g0 = w.gpu_start[(size_t)l], ng = std::min(8, w.gpu_start[(size_t)l + 1] - g0);
+          int avail = 0;
+          for (int j = 0; j < ng; ++j) avail += c.s.gmilli_left[(size_t)(g0 + j)] >= gm;
+          ok = avail >= pg;
+        }
+        if (!ok) lanes &= ~(1ull << l);
+      }
+    }
+    res.assign((size_t)N, 0);
+    if (lanes == 0) return;
+    E.set_exec(lanes);
     E.scc = false;
     E.run(*f, kRetMagic);
-    res.assign((size_t)N, 0);
-    for (int l = 0; l < N; ++l) res[(size_t)l] = (int64_t)((uint64_t)E.vg[0][l] | (uint64_t)E.vg[1][l] << 32);
+    for (int l = 0; l < N; ++l)
+      if (lanes >> l & 1) res[(size_t)l] = (int64_t)((uint64_t)E.vg[0][l] | (uint64_t)E.vg[1][l] << 32);
   }
 };
 
@@ -219,10 +237,19 @@ std::vector<SimResult> emu_simulate_batch(const Workload& w, const std::vector<P
                                           int threads) {
   const int64_t P = (int64_t)progs.size();
   std::vector<gcn::Func> funcs((size_t)P);
+  std::vector<char> elided((size_t)P, 0);
   for (int64_t i = 0; i < P; ++i) {
     gcn::ProgIn in = make_in(progs[(size_t)i]);
-    gcn::Codegen cg(in);
-    funcs[(size_t)i] = cg.run();
+    try {
+      gcn::Codegen cg(in);
+      funcs[(size_t)i] = cg.run();
+      elided[(size_t)i] = in.elide_lo < in.elide_hi;
+    } catch (const gcn::CodegenError&) {
+      if (!(in.elide_lo < in.elide_hi)) throw;
+      in.elide_lo = in.elide_hi = 0;   // as compile(): the whole program
+      gcn::Codegen cg(in);
+      funcs[(size_t)i] = cg.run();
+    }
   }
   std::vector<int64_t> gmem8((size_t)w.n_nodes * 8, 0);
   for (int n = 0; n < w.n_nodes; ++n)
@@ -243,7 +270,7 @@ std::vector<SimResult> emu_simulate_batch(const Workload& w, const std::vector<P
       const std::vector<int64_t>& k = kc[(size_t)i];
       emu->lds.resize(k.size() * 8 + 64, 0);
       std::memcpy(emu->lds.data(), k.data(), k.size() * 8);
-      EmuScorer sc{&funcs[(size_t)i], &k, &gmem8, emu.get(), {}, EXC_NONE};
+      EmuScorer sc{&funcs[(size_t)i], &k, &gmem8, emu.get(), {}, EXC_NONE, elided[(size_t)i] != 0};
       SimResult r = simulate(w, sc, o);
       if (r.exc == EXC_NONE && sc.exc) r.exc = sc.exc;
       out[(size_t)i] = std::move(r);

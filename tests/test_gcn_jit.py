@@ -100,6 +100,26 @@ def test_emulated_replays_equal_cpu_vm(default_workload, corpus):
     assert len(keep) >= len(corpus) // 2 - 4 and compared >= len(progs) - 4
 
 
+def test_emulated_replays_without_prologue_equal_cpu_vm(default_workload, corpus):
+    """Full replays as the device runs them: the feasibility prologue compiled
+    out and the program called for feasible nodes only -- rows bit-identical
+    to the CPU VM running the whole program on every node."""
+    budget = 1 << 16
+    progs = [p for p in corpus if gcnjit.elide_range(p)[1]][::2]
+    assert len(progs) >= 8
+    vm = ce.simulate_program_batch(default_workload, progs, ce.SimOptions(budget=budget))
+    keep = [i for i in range(len(progs)) if vm[i, 8] < 60000]
+    progs, vm = [progs[i] for i in keep], vm[keep]
+    emu = gcnjit.emulate_programs(default_workload, progs, budget, ce.SimOptions(budget=budget), elide=True)
+    compared = 0
+    for i, p in enumerate(progs):
+        if int(emu[i, 10]) in SKIP_EXC or int(vm[i, 10]) in SKIP_EXC:
+            continue
+        assert np.array_equal(emu[i], vm[i]), (i, p.source[-300:], emu[i], vm[i])
+        compared += 1
+    assert compared >= len(progs) - 2
+
+
 def _finish(kind, v):
     if kind == "exc":
         return -v

@@ -20,6 +20,7 @@ def main() -> None:
     ap.add_argument("--programs", type=int, default=24)
     ap.add_argument("--ck", default="data/populations/config3_steady_r4_islands.json")
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--no-elide", action="store_true", help="keep the feasibility prologue (call every node)")
     a = ap.parse_args()
     from funsearch_kubernetes_simulator_amd.core import load_default_workload
     from funsearch_kubernetes_simulator_amd.ops import cpu_engine as ce
@@ -39,7 +40,7 @@ def main() -> None:
     w = load_default_workload()
     budget = 1 << 16
     ce.native().gcn_emu_profile(True)
-    tab = gcnjit.emulate_programs(w, progs, budget, ce.SimOptions(budget=budget))
+    tab = gcnjit.emulate_programs(w, progs, budget, ce.SimOptions(budget=budget), elide=not a.no_elide)
     counts = ce.native().gcn_emu_profile_counts()
     ce.native().gcn_emu_profile(False)
     from funsearch_kubernetes_simulator_amd.policy.bytecode import Op
