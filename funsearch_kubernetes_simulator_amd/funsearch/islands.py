@@ -81,6 +81,9 @@ class IslandFunSearch:
         # random variants, even when it has been polished before (a (1 + lambda)
         # strategy over its constants that keeps running on the device)
         self.polish_repeat = bool(pol.get("repeat", False))
+        #: steady mode: also polish island champions on HIP slots that would
+        #: otherwise idle while the producers refill the child queue
+        self.polish_idle = bool(pol.get("idle", False))
         self._polished = set()
         # islands step independently (LLM / JIT / device stages overlap across islands)
         self.pipeline = bool(isl.get("pipeline", False))

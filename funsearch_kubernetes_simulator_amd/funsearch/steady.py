@@ -143,6 +143,7 @@ class SteadyStats:
     polish_batches: int = 0          # constant-polish batches (variants of an island champion)
     polish_evals: int = 0            # their device evaluations (not children)
     polish_improved: int = 0         # polished champions re-entered as children
+    polish_idle: int = 0             # of the polish batches: run on a slot that would have idled
     inflight_sum: float = 0.0        # programs in flight x seconds
     inflight_n: float = 0.0          # seconds observed
     history: List[dict] = field(default_factory=list)
@@ -168,6 +169,8 @@ class SteadyStateSearch:
         #: ``polish`` config: every / variants; 0 = off)
         self.polish_every = int(getattr(fs, "polish_every", 0) or 0)
         self.polish_variants = int(getattr(fs, "polish_variants", 512) or 512)
+        self.polish_idle = bool(getattr(fs, "polish_idle", False)) and self.polish_every > 0
+        self._idle_rr = -1
         self._polish_count: dict = {}
         dev = getattr(fs.evaluator, "device", None)
         if dev is not None and not tierup:
@@ -231,20 +234,26 @@ class SteadyStateSearch:
                 fs.save_checkpoint()
         return bool(results)
 
-    def _polish_job(self, merged, start_gen, polish_next) -> Optional[_Polish]:
+    def _polish_job(self, merged, start_gen, polish_next, idle: bool = False) -> Optional[_Polish]:
         """The next due constant polish (round robin over the islands): variants
         of the island champion's literals, one (1 + lambda) round per polish with
-        the step size cycling through the schedule of funsearch/polish.py."""
+        the step size cycling through the schedule of funsearch/polish.py.
+        idle: not due -- a slot would idle (the next island in turn)."""
         from ..policy.bytecode import TAG_FLOAT
         from ..policy.compiler import try_compile
         from .polish import _perturb, tunable_literals, with_values
         fs = self.fs
         gens = self._gen_of(merged)
-        for i in range(len(gens)):
+        order = list(range(len(gens)))
+        if idle:
+            self._idle_rr = (self._idle_rr + 1) % max(1, len(gens))
+            order = order[self._idle_rr:] + order[:self._idle_rr]
+        for i in order:
             g = start_gen + gens[i]
-            if g < polish_next[i]:
-                continue
-            polish_next[i] = g + self.polish_every
+            if not idle:
+                if g < polish_next[i]:
+                    continue
+                polish_next[i] = g + self.polish_every
             s = fs.islands[i]
             if not s.population:
                 continue
@@ -385,6 +394,12 @@ class SteadyStateSearch:
                 # of an island champion goes first
                 if self.polish_every and not stop and len(staged) < self.ahead:
                     job = self._polish_job(merged, start_gen, polish_next)
+                    if job is None and self.polish_idle and not staged and len(ready) < self.batch \
+                            and any(b is None for b in batches):
+                        # a slot would idle until the producers refill a batch
+                        job = self._polish_job(merged, start_gen, polish_next, idle=True)
+                        if job is not None:
+                            self.stats.polish_idle += 1
                     if job is not None:
                         items = [(job.island, job.code, pv) for pv in job.progs]
                         staged.append((items, stager.submit(ev.prepare_compiled, [job.code] * len(items),
@@ -574,7 +589,8 @@ class SteadyStateSearch:
                    new_shape_fraction=round(st.new_shapes / max(1, st.evaluations), 4),
                    native_fraction=round(st.native / max(1, st.evaluations), 4), host_fallback=st.fallback,
                    shed=st.shed, abandoned=st.abandoned, polish_batches=st.polish_batches,
-                   polish_evals=st.polish_evals, polish_improved=st.polish_improved,
+                   polish_evals=st.polish_evals, polish_improved=st.polish_improved, polish_idle=st.polish_idle,
+                   all_evals_per_s=round((st.evaluations + st.polish_evals) / wall, 2),
                    inflight=inflight, inflight_mean=round(st.inflight_sum / max(1e-9, st.inflight_n), 1),
                    resident_capacity=capacity,
                    occupancy=round(inflight / capacity, 4) if capacity else None,

@@ -172,3 +172,20 @@ def test_steady_constant_polish_batches(tmp_path):
     assert len(pol) == st.polish_batches and all(r["variants"] == 8 for r in pol)
     fin = [r for r in recs if r["kind"] == "steady_final"][-1]
     assert fin["polish_batches"] == st.polish_batches
+
+
+def test_steady_idle_slot_polish(tmp_path):
+    """polish.idle: while the producers refill the child queue, a free slot
+    runs a champion's constant polish instead of idling; children accounting
+    (evals_per_s) stays children-only, all_evals_per_s adds the variants."""
+    from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
+    cfg = _cfg(tmp_path, gens=6)
+    cfg["polish"] = {"every": 1000, "variants": 8, "repeat": True, "idle": True}
+    fs = IslandFunSearch(cfg)
+    fs.run(6)
+    st = fs.steady.stats
+    assert st.polish_idle > 0 and st.polish_batches >= st.polish_idle
+    assert st.polish_evals == 8 * st.polish_batches
+    assert st.evaluations == st.produced - st.rejected + st.polish_improved
+    fin = [json.loads(l) for l in open(tmp_path / "log.jsonl") if '"steady_final"' in l][-1]
+    assert fin["polish_idle"] == st.polish_idle and fin["all_evals_per_s"] >= fin["evals_per_s"]
