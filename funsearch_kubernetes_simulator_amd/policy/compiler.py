@@ -1657,7 +1657,9 @@ def same_shape_child(parent: CompiledPolicy, child: str) -> Optional[CompiledPol
     src = parent.source
     if len(child) > 2 * len(src) + 64:
         return None
-    tp = [(m.start(), m.end()) for m in _NUM_TOKEN.finditer(src)]
+    tp = parent.__dict__.get("_num_tokens")   # a parent serves many children
+    if tp is None:
+        tp = parent.__dict__["_num_tokens"] = [(m.start(), m.end()) for m in _NUM_TOKEN.finditer(src)]
     tc = [(m.start(), m.end()) for m in _NUM_TOKEN.finditer(child)]
     if len(tp) != len(tc):
         return None
