@@ -103,7 +103,9 @@ class Codegen {
     analyse_flow();
     list_facts();
     value_facts();
+    const_facts();
     infer_types();
+    fold_masks();
     liveness();
     // a value the elided prologue would have computed (e.g. its GPU count)
     // must not be read afterwards: the caller then compiles the whole program
@@ -143,6 +145,10 @@ class Codegen {
   // value 0-15, or -1) -- overflow / exactness checks and list indexing they make moot
   std::vector<uint64_t> i32_in_, ex_in_, acc_in_;
   std::vector<std::array<int8_t, kMaxRegs>> kin_;
+  // registers holding a constant compiled into the code (pool index, -1: unknown)
+  // and, per pc, the operands folded into the instruction as inline constants
+  std::vector<std::array<int16_t, kMaxRegs>> kpool_;
+  std::vector<uint64_t> fold_;
   int cur_pc_ = -1;
   bool i32(int r) const { return cur_pc_ >= 0 && r != kNoReg && (i32_in_[cur_pc_] >> r & 1); }
   bool exact(int r) const { return cur_pc_ >= 0 && r != kNoReg && (ex_in_[cur_pc_] >> r & 1); }
@@ -215,6 +221,7 @@ class Codegen {
                                in.a != kNoReg && !all_in_.empty() && (all_in_[pc] >> in.a & 1);
     if (in.a != kNoReg && !all_list_read) u |= 1ull << in.a;
     if (in.b != kNoReg) u |= 1ull << in.b;
+    if (!fold_.empty()) u &= ~fold_[pc];   // read as inline constants
     if ((in.op == OP_GLIST_SLICE || in.op == OP_GLIST_INSERT) && in.imm != kNoReg) u |= 1ull << in.imm;
     return u;
   }
@@ -437,6 +444,85 @@ class Codegen {
         seen[t] = 1;
         if (changed) work.push_back(t);
       }
+    }
+  }
+
+  void const_facts() {
+    kpool_.assign(n_, {});
+    for (auto& a : kpool_) a.fill(-1);
+    std::vector<char> seen(n_, 0);
+    seen[0] = 1;
+    std::vector<int> work{0};
+    while (!work.empty()) {
+      const int pc = work.back();
+      work.pop_back();
+      std::array<int16_t, kMaxRegs> out = kpool_[pc];
+      const Insn& in = P_.code[pc];
+      if (defines(in.op) && in.d != kNoReg) {
+        int16_t v = -1;
+        if (in.op == OP_CONST && in.imm >= 0 && in.imm < P_.n_const && !P_.is_lit[in.imm]) v = (int16_t)in.imm;
+        else if ((in.op == OP_MOV || in.op == OP_POS) && in.a != kNoReg) v = kpool_[pc][in.a];
+        out[in.d] = v;
+      }
+      for (int t : succ_[pc]) {
+        if (t < 0) continue;
+        bool changed = !seen[t];
+        for (int r = 0; r < kMaxRegs; ++r) {
+          const int16_t nv = !seen[t] ? out[r] : (kpool_[t][r] == out[r] ? out[r] : (int16_t)-1);
+          if (nv != kpool_[t][r]) { kpool_[t][r] = nv; changed = true; }
+        }
+        seen[t] = 1;
+        if (changed) work.push_back(t);
+      }
+    }
+  }
+  // inline operand code of register r's constant at pc (NONE: not foldable):
+  // int context -- a sign-extended integer in [-16, 64]; float context -- an
+  // integral value in [-16, 64] (converted by the hardware) or +-0.5
+  uint16_t fold_code(int pc, int r, bool as_float) const {
+    if (r == kNoReg || pc < 0 || kpool_.empty()) return NONE;
+    const int k = kpool_[pc][r];
+    if (k < 0) return NONE;
+    if (P_.ctag[k] != TAG_FLOAT) return ic(P_.iconst[k]);
+    if (!as_float) return NONE;
+    const double x = P_.fconst[k];
+    if (std::signbit(x) && x == 0.0) return NONE;   // -0.0 is not the integer 0
+    if (x == 0.5) return F_HALF;
+    if (x == -0.5) return (uint16_t)(F_HALF + 1);
+    if (x == std::floor(x) && x >= -16.0 && x <= 64.0) return ic((int64_t)x);
+    return NONE;
+  }
+  // which operands the lowering below takes as inline constants (so their
+  // CONST need not be materialised when nothing else reads it)
+  void fold_masks() {
+    fold_.assign(n_, 0);
+    for (int pc = 0; pc < n_; ++pc) {
+      const Insn& in = P_.code[pc];
+      const uint8_t ta = in.a != kNoReg ? ty_[pc][in.a] : TY_I, tb = in.b != kNoReg ? ty_[pc][in.b] : TY_I;
+      uint64_t m = 0;
+      auto f = [&](int r, bool fl) { if (fold_code(pc, r, fl) != NONE) m |= 1ull << r; };
+      switch (in.op) {
+        case OP_LT: case OP_LE: case OP_GT: case OP_GE: case OP_EQ: case OP_NE:
+          if (in.imm == kLoopIndex && ta == TY_I && tb == TY_I) break;
+          if (ta == TY_I && tb == TY_I) { f(in.a, false); f(in.b, false); }
+          else if (ta != TY_IF && tb != TY_IF) { f(in.a, true); f(in.b, true); }
+          break;
+        case OP_ADD: case OP_SUB: case OP_MUL:
+          if (ta == TY_I && tb == TY_I) {
+            cur_pc_ = pc;
+            const bool no_ovf = (i32(in.a) && i32(in.b)) ||
+                                (in.op != OP_MUL && ((acc(in.a) && i32(in.b)) || (i32(in.a) && acc(in.b))));
+            cur_pc_ = -1;
+            if (no_ovf && !(in.op == OP_ADD && in.imm == kLoopIndex)) { f(in.a, false); f(in.b, false); }
+          } else if (ta != TY_IF && tb != TY_IF) {
+            f(in.a, true);
+            f(in.b, true);
+          }
+          break;
+        default: break;
+      }
+      if (in.a != kNoReg && in.a == in.b) m &= ~(1ull << in.a);   // (both operands: keep it simple)
+      fold_[pc] = m;
     }
   }
 
@@ -989,7 +1075,22 @@ class Codegen {
     }
   }
   // f64 value of register r (type t) -> operand code of a pair
+  // operand r of the instruction being lowered as an inline constant (fold_), or NONE
+  uint16_t fold_of(int r, bool as_float) const {
+    if (cur_pc_ < 0 || fold_.empty() || r == kNoReg || !(fold_[cur_pc_] >> r & 1)) return NONE;
+    return fold_code(cur_pc_, r, as_float);
+  }
+  uint16_t opi(int r) const { const uint16_t c = fold_of(r, false); return c != NONE ? c : R(r); }
+  uint16_t opih(int r) const {   // high dword (sign of an inline integer)
+    const uint16_t c = fold_of(r, false);
+    if (c == NONE) return Rh(r);
+    return (c >= 193 && c <= 208) ? ic(-1) : ic(0);
+  }
   uint16_t as_f64(int r, uint8_t t, int tmp) {
+    if (t != TY_IF) {
+      const uint16_t c = fold_of(r, true);
+      if (c != NONE) return c;
+    }
     if (t == TY_F) return R(r);
     if (t == TY_I && i32(r)) {   // exact from the low dword
       e(mk(V_CVT_F64_I32, T(tmp), R(r)));
@@ -1660,12 +1761,12 @@ class Codegen {
                         (in.op != OP_MUL && ((acc(a) && i32(b)) || (i32(a) && acc(b))));
     if (no_ovf) {   // |a|, |b| < 2^31, or an accumulator plus an int32: no int64 overflow
       if (in.op == OP_MUL) {
-        e(mk3b(V_MAD_I64_I32, R(d), VCC, R(a), R(b), ic(0)));
+        e(mk3b(V_MAD_I64_I32, R(d), VCC, opi(a), opi(b), ic(0)));
       } else {
-        MI lo = mk(in.op == OP_ADD ? V_ADD_CO_U32 : V_SUB_CO_U32, R(d), R(a), R(b));
+        MI lo = mk(in.op == OP_ADD ? V_ADD_CO_U32 : V_SUB_CO_U32, R(d), opi(a), opi(b));
         lo.sd = ST(0);
         e(lo);
-        MI hi = mk(in.op == OP_ADD ? V_ADDC_CO_U32 : V_SUBB_CO_U32, Rh(d), Rh(a), Rh(b), ST(0));
+        MI hi = mk(in.op == OP_ADD ? V_ADDC_CO_U32 : V_SUBB_CO_U32, Rh(d), opih(a), opih(b), ST(0));
         hi.sd = ST(0);
         e(hi);
       }
@@ -2014,8 +2115,8 @@ class Codegen {
     static const Opc ci[6] = {V_CMP_LT_I64, V_CMP_LE_I64, V_CMP_GT_I64, V_CMP_GE_I64, V_CMP_EQ_I64, V_CMP_NE_I64};
     static const Opc cf[6] = {V_CMP_LT_F64, V_CMP_LE_F64, V_CMP_GT_F64, V_CMP_GE_F64, V_CMP_EQ_F64, V_CMP_NEQ_F64};
     const int k = op - OP_LT;
-    if (ta == TY_I && tb == TY_I) { cmp(ci[k], dst, R(a), R(b)); return; }
-    if (ta == TY_F && tb == TY_F) { cmp(cf[k], dst, R(a), R(b)); return; }
+    if (ta == TY_I && tb == TY_I) { cmp(ci[k], dst, opi(a), opi(b)); return; }
+    if (ta == TY_F && tb == TY_F) { cmp(cf[k], dst, as_f64(a, ta, 0), as_f64(b, tb, 1)); return; }
     // mixed: int operands within +-2^53 convert exactly; others -> EXC_UNSUPPORTED
     if (ta != TY_F) int_lanes_exact(a, ta);
     if (tb != TY_F) int_lanes_exact(b, tb);
@@ -2035,7 +2136,10 @@ class Codegen {
   // lanes where register r (type t) holds an int outside +-2^53 -> EXC_UNSUPPORTED
   // (conservative for the int / int lanes of a dynamic pair: the next engine decides them)
   void int_lanes_exact(int r, uint8_t t) {
-    if (t == TY_I) { check_exact_int(R(r), EXEC); return; }
+    if (t == TY_I) {
+      if (!exact(r) && fold_of(r, true) == NONE) check_exact_int(R(r), EXEC);
+      return;
+    }
     tag_mask(r, ST(0));
     e(mk(S_ANDN2_B64, ST(0), EXEC, ST(0)));
     check_exact_int(R(r), ST(0));
