@@ -477,19 +477,20 @@ class Codegen {
     }
   }
   // inline operand code of register r's constant at pc (NONE: not foldable):
-  // int context -- a sign-extended integer in [-16, 64]; float context -- an
-  // integral value in [-16, 64] (converted by the hardware) or +-0.5
+  // int context -- a sign-extended integer in [-16, 64]; float context -- one
+  // of the float inline constants (0, +-0.5, +-1, +-2, +-4; an integer inline
+  // constant in a float operand is a bit pattern, not a converted value)
   uint16_t fold_code(int pc, int r, bool as_float) const {
     if (r == kNoReg || pc < 0 || kpool_.empty()) return NONE;
     const int k = kpool_[pc][r];
     if (k < 0) return NONE;
-    if (P_.ctag[k] != TAG_FLOAT) return ic(P_.iconst[k]);
-    if (!as_float) return NONE;
-    const double x = P_.fconst[k];
-    if (std::signbit(x) && x == 0.0) return NONE;   // -0.0 is not the integer 0
-    if (x == 0.5) return F_HALF;
-    if (x == -0.5) return (uint16_t)(F_HALF + 1);
-    if (x == std::floor(x) && x >= -16.0 && x <= 64.0) return ic((int64_t)x);
+    if (!as_float) return P_.ctag[k] != TAG_FLOAT ? ic(P_.iconst[k]) : NONE;
+    const double x = P_.ctag[k] == TAG_FLOAT ? P_.fconst[k] : (double)P_.iconst[k];
+    if (P_.ctag[k] != TAG_FLOAT && (P_.iconst[k] < -4 || P_.iconst[k] > 4)) return NONE;
+    if (x == 0.0) return std::signbit(x) ? NONE : ic(0);
+    static const double kF[8] = {0.5, -0.5, 1.0, -1.0, 2.0, -2.0, 4.0, -4.0};
+    for (int i = 0; i < 8; ++i)
+      if (x == kF[i]) return (uint16_t)(F_HALF + i);
     return NONE;
   }
   // which operands the lowering below takes as inline constants (so their

@@ -63,10 +63,8 @@ struct Emu {
       return k[c - 240];
     }
     uint64_t b;
-    if (c >= 128 && c <= 208) {   // integer inline constant converted to double
-      const int64_t iv = (int64_t)r64(c, l, lit);
-      return (double)iv;
-    }
+    // (an integer inline constant, 128-208, is its sign-extended bit pattern
+    // in a 64-bit float operand -- not converted -- as on the hardware)
     if (c == LIT) b = (uint64_t)lit << 32;
     else b = r64(c, l, lit);
     std::memcpy(&x, &b, 8);
