@@ -80,6 +80,35 @@ def test_generated_code_round_trips_through_llvm_mc(corpus):
         assert bytes(out) == raw
 
 
+@have_mc
+def test_no_integer_inline_constants_in_f64_value_operands(corpus):
+    """In a 64-bit float operand an integer inline constant is a bit pattern
+    (1 -> 4.9e-324), not a converted value: generated f64 arithmetic / compares
+    use the float inline constants (0.5, 1.0, 2.0, 4.0, ...) or 0 only."""
+    import re
+    bodies = ["x = node.cpu_milli_left / node.cpu_milli_total\n    return (1 - x) * 2.0 + (x > 1) * 4 - (x < 0.5) * 3"]
+    progs = list(corpus[::4]) + [compile_policy("def priority_function(pod, node):\n    " + b + "\n") for b in bodies]
+    bad = []
+    for p in progs:
+        code, why = gcnjit.compile_program(p)
+        assert code is not None, why
+        words = code.words.copy()
+        for lo, hi, _ in code.relocs.reshape(-1, 3):
+            words[int(lo)], words[int(hi)] = 0x12345678, 0xFFFFF000
+        txt = " ".join(f"0x{b:02x}" for b in words.tobytes())
+        dis = subprocess.run([MC, "-disassemble", "-triple=amdgcn-amd-amdhsa", "-mcpu=gfx950"], input=txt,
+                             capture_output=True, text=True).stdout
+        for line in dis.splitlines():
+            line = line.strip()
+            op = line.split(" ")[0]
+            if not op.startswith("v_") or "_f64" not in op or op.startswith(("v_ldexp_f64", "v_cmp_class_f64")):
+                continue
+            for tok in re.split(r"[ ,]+", line)[1:]:
+                if re.fullmatch(r"-?\d+", tok) and int(tok) != 0:
+                    bad.append(line)
+    assert not bad, bad[:5]
+
+
 def test_emulated_replays_equal_cpu_vm(default_workload, corpus):
     """Full replays of the 8,152-pod trace with the generated machine code on
     the wave64 emulator: rows bit-identical to the CPU VM."""
