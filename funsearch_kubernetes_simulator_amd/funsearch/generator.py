@@ -40,7 +40,10 @@ class LLMCodeGenerator:
         return m.group(1) if m else text
 
     def generate_policy(self, parent_policies: Optional[Sequence[Tuple[str, float]]] = None,
-                        performance_feedback: str = "") -> Optional[str]:
+                        performance_feedback: str = "", prevalidated=None) -> Optional[str]:
+        """prevalidated(code) -> True: the caller vouches for the code's safety
+        (steady mode: a child that differs from an already-validated parent in
+        numeric literal digits only), so the two checks are skipped."""
         prompt = PolicyTemplate.create_prompt_for_llm(parent_policies or [], performance_feedback)
         try:
             t0 = time.time()
@@ -52,8 +55,9 @@ class LLMCodeGenerator:
             code = PolicyTemplate.fill_template(logic)
             if self.verbose:
                 print(code)
-            self.safe_executor.validate_code_content(code)
-            self.safe_executor.validate_code_structure(code)
+            if prevalidated is None or not prevalidated(code):
+                self.safe_executor.validate_code_content(code)
+                self.safe_executor.validate_code_structure(code)
             return code
         except Exception as exc:
             self.rejected += 1

@@ -79,24 +79,38 @@ def _produce(task):
     out = []
     for _ in range(n):
         parents = rng.sample(elites, min(2, len(elites)))
-        code = gen.generate_policy(parent_policies=parents, performance_feedback=FEEDBACK)
+        reuse = []
+
+        def same_shape(child, parents=parents, reuse=reuse):
+            # a constant-only mutation keeps its parent's shape: bytecode reused,
+            # and -- the parent having passed validation, only digits differing --
+            # the sandbox checks need not run again
+            for pc, _ in parents:
+                pp = pcache.get(pc)
+                if pp is None:
+                    if len(pcache) > 256:
+                        pcache.clear()
+                    try:   # the parent itself passes the sandbox checks (once per parent text)
+                        gen.safe_executor.validate(pc)
+                        pp = try_compile(pc)[0] or False
+                    except Exception:
+                        pp = False
+                    pcache[pc] = pp
+                if pp:
+                    prog = same_shape_child(pp, child)
+                    if prog is not None:
+                        reuse.append(prog)
+                        return True
+            return False
+
+        code = gen.generate_policy(parent_policies=parents, performance_feedback=FEEDBACK, prevalidated=same_shape)
         if not code:             # LLM / validation failure: the child slot is spent
             out.append((island, None, None))
             continue
-        prog = None
-        # a constant-only mutation keeps its parent's shape: bytecode reused
-        for pc, _ in parents:
-            pp = pcache.get(pc)
-            if pp is None:
-                if len(pcache) > 256:
-                    pcache.clear()
-                pp = pcache[pc] = try_compile(pc)[0] or False
-            if pp:
-                prog = same_shape_child(pp, code)
-                if prog is not None:
-                    _W["reused"] = _W.get("reused", 0) + 1
-                    break
-        if prog is None:
+        if reuse:
+            prog = reuse[0]
+            _W["reused"] = _W.get("reused", 0) + 1
+        else:
             prog, _ = try_compile(code)
         out.append((island, code, prog))
     return out, time.process_time() - t0
