@@ -1269,13 +1269,16 @@ class Codegen {
     for (int t : v_tag_)
       if (t >= 0) e(mk(V_MOV_B32, v(t), ic(0)));
     if (s_bud_ >= 0) {
-      // kc[0] = the iteration budget, capped (<= 0: unlimited -> the cap); one
-      // counter for the wave: a lane never runs more iterations than the wave
+      // kc[0] = the iteration budget, capped; one counter for the wave: a lane
+      // never runs more iterations than the wave
       MI ld = mk(DS_READ_B64, T(0), v(29));
       ld.imm = 0;
       e(ld);
       e(mkimm(S_WAITCNT, 0xC07F));
-      e(mklit(V_MIN_U32, T(0), kJitLoopCap, T(0)));
+      // min(kc[0], cap) with kc[0] <= 0 (unlimited) -> the cap: (x - 1 as unsigned) min (cap - 1), + 1
+      e(mklit(V_ADD_U32, T(0), 0xFFFFFFFFu, T(0)));
+      e(mklit(V_MIN_U32, T(0), kJitLoopCap - 1, T(0)));
+      e(mk(V_ADD_U32, T(0), ic(1), T(0)));
       e(mk(V_READFIRSTLANE_B32, s(s_bud_), T(0)));
     }
     for (int r = 0; r < kMaxRegs; ++r) {

@@ -334,7 +334,7 @@ def test_runaway_loop_raises_budget():
     p = compile_policy("def priority_function(pod, node):\n    x = 0\n    while x >= 0:\n"
                        "        x = (x + 1) % 7\n    return x\n")
     node, gl, gt, gm, pod = _random_event(random.Random(5))
-    for budget in (1 << 10, 1 << 16):
+    for budget in (1 << 10, 1 << 16, 0):   # (0: unlimited -> the per-call cap)
         kc = constant_block(p, budget).tolist()
         emu = m.gcn_emu_event(p.code, list(map(int, p.ctag)), gcnjit.literal_mask(p).tolist(),
                               list(map(int, p.iconst)), list(map(float, p.fconst)), kc, node, gl, gt, gm, pod)
