@@ -9,6 +9,10 @@ choices can be A/B'd on the same programs in one GPU session:
 
     python tools/population_bench.py --ck gpurun_out/r4g/ck/islands_rank0.json \
         --children 2048 --variant base= --variant narrow=FKS_JIT_NARROW_SAVES=1
+
+--save-sources FILE writes the children's sources (CPU only); --sources FILE
+replays exactly those programs, so code-generation changes can be compared
+across commits on identical programs.
 """
 from __future__ import annotations
 
@@ -21,6 +25,19 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+
+def _programs_from(sources: str, n: int):
+    """Programs from a JSON list of source strings (--save-sources output):
+    the same programs whatever the compiler or mutator version (A/B of code
+    generation changes across commits)."""
+    from funsearch_kubernetes_simulator_amd.policy.compiler import try_compile
+    out = []
+    for src in json.load(open(sources)):
+        p, _ = try_compile(src)
+        if p is not None and p.device_ok:
+            out.append(p)
+    return out[:n]
 
 
 def _programs(path: str, n: int, seed: int):
@@ -62,7 +79,7 @@ def child(args) -> None:
     import numpy as np
     from funsearch_kubernetes_simulator_amd.core import load_default_workload
     from funsearch_kubernetes_simulator_amd.ops.hip_engine import DeviceEvaluator
-    progs = _programs(args.ck, args.children, args.seed)
+    progs = _programs_from(args.sources, args.children) if args.sources else _programs(args.ck, args.children, args.seed)
     dev = DeviceEvaluator(load_default_workload())
     dev.set_options(native_inflight=args.batch)
     if args.rows:
@@ -110,7 +127,14 @@ def main() -> None:
     ap.add_argument("--name", default="base")
     ap.add_argument("--rows", type=int, default=0, help="native programs per wave (0: the two-wave kernel)")
     ap.add_argument("--polish", action="store_true", help="constant variants of one program instead of children")
+    ap.add_argument("--sources", default="", help="JSON list of program sources to run instead of fresh children")
+    ap.add_argument("--save-sources", default="", help="write the children's sources (JSON) and exit (no GPU)")
     args = ap.parse_args()
+    if args.save_sources:
+        progs = _programs(args.ck, args.children, args.seed)
+        json.dump([p.source for p in progs], open(args.save_sources, "w"))
+        print(json.dumps({"saved": len(progs), "file": args.save_sources}))
+        return
     if args.child:
         child(args)
         return
@@ -121,6 +145,7 @@ def main() -> None:
             k, _, v = kv.partition("=")
             env[k] = v
         cmd = [sys.executable, "-u", os.path.abspath(__file__), "--child", "--name", name, "--ck", args.ck,
+               "--sources", args.sources,
                "--children", str(args.children), "--batch", str(args.batch), "--reps", str(args.reps),
                "--seed", str(args.seed), "--rows", str(args.rows)] + (["--polish"] if args.polish else [])
         r = subprocess.run(cmd, env=env, timeout=600)
