@@ -359,7 +359,7 @@ PYBIND11_MODULE(_fks_cpu, m) {
     out["words"] = np_of(r.words);
     out["relocs"] = np_of(r.relocs);
     out["n_insns"] = r.n_insns; out["vgprs"] = r.vgprs; out["sgprs"] = r.sgprs; out["calls"] = r.calls;
-    out["vregs"] = r.vregs; out["tagged"] = r.tagged; out["mir"] = r.mir; out["spills"] = r.spills;
+    out["vregs"] = r.vregs; out["tagged"] = r.tagged; out["mir"] = r.mir; out["spills"] = r.spills; out["unrolled"] = r.unrolled;
     return out;
   }, py::arg("code"), py::arg("ctag"), py::arg("is_lit"), py::arg("iconst"), py::arg("fconst"));
   // A batch of programs on `threads` host threads (the generator is
@@ -427,7 +427,7 @@ PYBIND11_MODULE(_fks_cpu, m) {
       d["words"] = np_of(r.words);
       d["relocs"] = np_of(r.relocs);
       d["n_insns"] = r.n_insns; d["vgprs"] = r.vgprs; d["sgprs"] = r.sgprs; d["calls"] = r.calls;
-      d["vregs"] = r.vregs; d["tagged"] = r.tagged; d["mir"] = r.mir; d["spills"] = r.spills;
+      d["vregs"] = r.vregs; d["tagged"] = r.tagged; d["mir"] = r.mir; d["spills"] = r.spills; d["unrolled"] = r.unrolled;
       out.append(d);
     }
     return out;
@@ -476,16 +476,21 @@ PYBIND11_MODULE(_fks_cpu, m) {
   // test hook: at most `pairs` VGPR pairs for virtual registers (0: no cap),
   // which sends ordinary programs down the spill path
   m.def("gcn_set_pair_cap", [](int pairs) { fks::gcnapi::set_pair_cap(pairs); });
+  // unrolling of node.gpus loops: max expanded body (bytecode insns); 0 = off; returns the previous cap
+  m.def("gcn_set_unroll_cap", [](int cap) { return fks::gcnapi::set_unroll_cap(cap); });
   m.def("gcn_listing", [](py::bytes code, std::vector<uint8_t> ctag, std::vector<uint8_t> is_lit,
-                          std::vector<int64_t> iconst, std::vector<double> fconst) {
+                          std::vector<int64_t> iconst, std::vector<double> fconst, int elide_lo, int elide_hi) {
     const std::string c = code;
     gcnapi::ProgramDesc p;
     p.code = reinterpret_cast<const uint8_t*>(c.data());
     p.code_bytes = c.size();
     p.ctag = ctag.data(); p.is_lit = is_lit.data(); p.iconst = iconst.data(); p.fconst = fconst.data();
     p.n_const = ctag.size();
+    p.elide_lo = elide_lo;
+    p.elide_hi = elide_hi;
     return gcnapi::listing(p);
-  });
+  }, py::arg("code"), py::arg("ctag"), py::arg("is_lit"), py::arg("iconst"), py::arg("fconst"),
+     py::arg("elide_lo") = 0, py::arg("elide_hi") = 0);
   m.def("gcn_emu_event", [](py::bytes code, std::vector<uint8_t> ctag, std::vector<uint8_t> is_lit,
                             std::vector<int64_t> iconst, std::vector<double> fconst, std::vector<int64_t> kc,
                             std::vector<int64_t> node, std::vector<int32_t> gl, std::vector<int32_t> gt,

@@ -29,7 +29,7 @@ struct Result {
   std::string reason;
   std::vector<uint32_t> words;      // machine code (position independent except relocs)
   std::vector<uint32_t> relocs;     // triples: lo literal word, hi literal word, byte offset of the PC
-  int n_insns = 0, vgprs = 0, sgprs = 0, calls = 0, vregs = 0, tagged = 0, mir = 0, spills = 0;
+  int n_insns = 0, vgprs = 0, sgprs = 0, calls = 0, vregs = 0, tagged = 0, mir = 0, spills = 0, unrolled = 0;
   bool elided = false;              // compiled without the prologue (ProgramDesc elide range)
 };
 
@@ -38,6 +38,7 @@ Result compile(const ProgramDesc& p);
 
 // Test hook: cap the VGPR pairs for virtual registers (0: none) -> forces spills.
 void set_pair_cap(int pairs);
+int set_unroll_cap(int cap);
 
 // Human-readable listing of the generated machine-instruction stream (debugging).
 std::string listing(const ProgramDesc& p);

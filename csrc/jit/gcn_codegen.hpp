@@ -36,6 +36,9 @@
 #pragma once
 
 #include <array>
+#include <cmath>
+#include <cstdlib>
+#include <functional>
 #include <map>
 #include <set>
 #include <stdexcept>
@@ -67,10 +70,11 @@ struct ProgIn {
   // when every caller calls only for nodes its own feasible() accepts (the
   // prologue then falls through with no effect); 0, 0: none
   int elide_lo = 0, elide_hi = 0;
+  bool no_unroll = false;   // keep node.gpus loops rolled (the fallback when unrolled code does not fit)
 };
 
 struct GenStats {
-  int vregs = 0, vgprs_used = 0, sgprs_used = 0, calls = 0, tagged = 0, spills = 0;
+  int vregs = 0, vgprs_used = 0, sgprs_used = 0, calls = 0, tagged = 0, spills = 0, unrolled = 0;
 };
 
 // Test hook: at most this many VGPR pairs for virtual registers (0: no cap),
@@ -80,6 +84,18 @@ inline int& pair_cap() {
   return cap;
 }
 constexpr int kMaxSpills = 16;   // 128 B of scratch per lane
+
+// Unrolling of the compiler's node.gpus loop skeletons (Codegen::unroll_gpu_loops):
+// a loop whose expanded body would exceed this many bytecode instructions stays
+// rolled; 0 disables unrolling (A/B: FKS_JIT_UNROLL=0, or this hook in tests).
+inline int& unroll_cap() {
+  static int cap = [] {
+    const char* e = std::getenv("FKS_JIT_UNROLL");
+    return e ? std::atoi(e) : 1600;
+  }();
+  return cap;
+}
+constexpr int kUnrollTotalCap = 6000;   // bytecode instructions of the whole unrolled program
 
 class Codegen {
  public:
@@ -100,16 +116,22 @@ class Codegen {
   Func run(GenStats* st = nullptr) {
     if (n_ <= 0) throw CodegenError("empty program");
     if (P_.n_const + 1 > 256) throw CodegenError("constant block larger than the LDS staging area");
+    elide_hi_ = P_.elide_hi;
+    if (unroll_cap() > 0 && !P_.no_unroll) unroll_gpu_loops();
     analyse_flow();
-    list_facts();
-    value_facts();
-    const_facts();
+    for (int round = 0; round < 6; ++round) {
+      list_facts();
+      value_facts();
+      const_facts();
+      bool_facts();
+      if (!prune_static_ifs()) break;
+    }
     infer_types();
     fold_masks();
     liveness();
     // a value the elided prologue would have computed (e.g. its GPU count)
     // must not be read afterwards: the caller then compiles the whole program
-    if (elided_defs_ && P_.elide_hi < n_ && (live_in_[(size_t)P_.elide_hi] & elided_defs_))
+    if (elided_defs_ && elide_hi_ < n_ && (live_in_[(size_t)elide_hi_] & elided_defs_))
       throw CodegenError("elided prologue defines a value the body reads");
     simt_liveness();
     layout_registers();
@@ -122,6 +144,7 @@ class Codegen {
       st->vgprs_used = max_vgpr_ + 1;
       st->sgprs_used = max_sgpr_ + 1;
       st->spills = __builtin_popcountll(spilled_);
+      st->unrolled = n_unrolled_;
     }
     return F_;
   }
@@ -130,7 +153,15 @@ class Codegen {
   ProgIn P_;
   std::vector<Insn> own_code_;   // the bytecode with the elided prologue as NOPs
   uint64_t elided_defs_ = 0;     // registers the elided prologue defined
+  int elide_hi_ = 0;             // P_.elide_hi in the (unrolled) code
   int n_;
+  // ---- unrolled node.gpus loops (unroll_gpu_loops): the rewritten code and the
+  // constant pool extended by the GPU indices 0-7
+  std::vector<Insn> unrolled_code_;
+  std::vector<uint8_t> own_ctag_, own_lit_;
+  std::vector<int64_t> own_iconst_;
+  std::vector<double> own_fconst_;
+  int n_unrolled_ = 0;
   Func F_;
   // ---- flow
   std::vector<int> brk_t_, cont_t_;
@@ -144,6 +175,13 @@ class Codegen {
   // (i32_in_) / |x| <= 2^53 (ex_in_), and small non-negative constants (kin_:
   // value 0-15, or -1) -- overflow / exactness checks and list indexing they make moot
   std::vector<uint64_t> i32_in_, ex_in_, acc_in_;
+  // ints with |x| < 2^32 (i33_in_: a sum / difference of two int32), and values
+  // that are > 0 or NaN -- never zero, so a division by them cannot raise
+  // (pos_in_: positive compiled-in constants and max / min built from them)
+  std::vector<uint64_t> i33_in_, pos_in_;
+  using MagRow = std::array<uint8_t, kMaxRegs>;
+  std::vector<MagRow> mag_in_;   // |x| < 2^m of int registers per pc entry (64: unknown; value_facts)
+  int mag(int r) const { return cur_pc_ >= 0 && r != kNoReg && !mag_in_.empty() ? mag_in_[cur_pc_][r] : 64; }
   std::vector<std::array<int8_t, kMaxRegs>> kin_;
   // registers holding a constant compiled into the code (pool index, -1: unknown)
   // and, per pc, the operands folded into the instruction as inline constants
@@ -153,6 +191,19 @@ class Codegen {
   bool i32(int r) const { return cur_pc_ >= 0 && r != kNoReg && (i32_in_[cur_pc_] >> r & 1); }
   bool exact(int r) const { return cur_pc_ >= 0 && r != kNoReg && (ex_in_[cur_pc_] >> r & 1); }
   bool acc(int r) const { return cur_pc_ >= 0 && r != kNoReg && (acc_in_[cur_pc_] >> r & 1); }
+  bool i33(int r) const { return cur_pc_ >= 0 && r != kNoReg && (i33_in_[cur_pc_] >> r & 1); }
+  bool acc_term_i33_ = false;   // accumulators may take |term| < 2^32 (few enough ADD / SUB sites)
+  // int64 ADD / SUB / MUL of a and b that cannot overflow: both int32, or an
+  // accumulator plus / minus a bounded term
+  bool no_int_overflow(uint8_t op, int a, int b) const {
+    if (i32(a) && i32(b)) return true;
+    if (op == OP_MUL) return false;   // (the unchecked product is v_mad_i64_i32: int32 operands only)
+    const int ma = mag(a), mb = mag(b);
+    if (ma < 64 && mb < 64 && std::max(ma, mb) + 1 <= 63) return true;
+    auto term = [&](int r) { return acc_term_i33_ ? i33(r) : i32(r); };
+    return (acc(a) && term(b)) || (term(a) && acc(b));
+  }
+  bool nonzero(int r) const { return cur_pc_ >= 0 && r != kNoReg && (pos_in_[cur_pc_] >> r & 1); }
   // Loop iterations per call are capped at kJitLoopCap (more -> EXC_BUDGET, the
   // next engine decides), so a static ADD / SUB runs at most 2 * cap + 1 times
   // a call; with at most kAccSites of them, a value built from int32 terms by
@@ -194,10 +245,208 @@ class Codegen {
     int pc;
     int s_save = -1, s_else = -1;         // IF
     int s_entry = -1, s_brk = -1, s_cont = -1;   // LOOP
+    bool static_branch = false;           // IF with a known condition: one branch, no mask
     int l_exit = -1, l_head = -1;
   };
   std::vector<Frame> frames_;
   std::map<int, int> label_at_pc_;        // pc -> label placed before its code
+  int skip_to_ = 0;                       // emission resumes at this pc (a dead branch)
+
+  // ============================================================ unrolling
+  // The compiler's loop over node.gpus (policy/compiler.py _for_glist /
+  // _gen_loop; bytecode LOOP_INDEX):
+  //
+  //   GLIST_LEN n, src; CONST idx (0); CONST one (1); LOOP_BEGIN s
+  //   LT c, idx, n [LOOP_INDEX]; LOOP_TEST c; GLIST_GET g, src, idx [LOOP_INDEX]
+  //   body; LOOP_CONT; ADD idx, idx, one [LOOP_INDEX]; LOOP_NEXT; LOOP_EXIT s
+  //
+  // with src = node.gpus unchanged runs at most 8 iterations (a node has at
+  // most kGmax GPUs), so it becomes eight guarded copies of the body:
+  //
+  //   LOOP_BEGIN s
+  //   { CONST idx (k); LT c, idx, n; IF c; CONST g (k); body; ENDIF; [LOOP_CONT] } k = 0..7
+  //   LOOP_EXIT s
+  //
+  // Same lanes, same order, same values: a lane runs copy k iff k < len(its
+  // node.gpus), g is GPU k there (node.gpus[k] == k), and BREAK / CONTINUE /
+  // RET keep their loop-frame meaning (a CONTINUE leaves the copy; LOOP_CONT,
+  // kept only when the body continues, takes the lane back for the next one).
+  // What it buys: the counter, the per-iteration test / back edge / budget
+  // charge go away, and every GPU field read gets a constant index -- one move
+  // from the argument VGPR instead of a readfirstlane + GPR-index-mode move.
+  // The loop budget is charged by the back edges of the loops that remain (an
+  // unrolled loop has none: it is bounded by construction).
+  struct LoopPat {
+    int b = -1, e = -1;                  // LOOP_BEGIN / LOOP_EXIT pcs
+    int idx = -1, n = -1, g = -1, src = -1;
+    bool cont = false;                   // the body CONTINUEs this loop
+    int body_size = 0;                   // expanded size of the body (inner unrolled loops counted)
+    bool unroll = false;
+  };
+  int pool_int(int64_t v) {
+    // a non-literal int constant of the (own) pool with value v
+    for (int k = 0; k < (int)own_iconst_.size(); ++k)
+      if (!own_lit_[(size_t)k] && own_ctag_[(size_t)k] != TAG_FLOAT && own_iconst_[(size_t)k] == v) return k;
+    own_ctag_.push_back(TAG_INT);
+    own_lit_.push_back(0);
+    own_iconst_.push_back(v);
+    own_fconst_.push_back(0.0);
+    return (int)own_iconst_.size() - 1;
+  }
+  void unroll_gpu_loops() {
+    analyse_flow();
+    list_facts();
+    liveness();
+    std::map<int, LoopPat> pats;   // by LOOP_BEGIN pc: loops that match the skeleton
+    {
+      std::vector<int> stk;
+      std::map<int, int> exit_of;
+      for (int pc = 0; pc < n_; ++pc) {
+        if (P_.code[pc].op == OP_LOOP_BEGIN) stk.push_back(pc);
+        else if (P_.code[pc].op == OP_LOOP_EXIT) { exit_of[stk.back()] = pc; stk.pop_back(); }
+      }
+      for (const auto& kv : exit_of) {
+        const int b = kv.first, e = kv.second;
+        if (b < 3 || e - b < 7) continue;
+        const Insn* c = P_.code;
+        const Insn &len = c[b - 3], &k0 = c[b - 2], &k1 = c[b - 1], &lt = c[b + 1], &tst = c[b + 2], &get = c[b + 3];
+        const Insn &lc = c[e - 3], &add = c[e - 2], &nxt = c[e - 1];
+        auto int_const = [&](const Insn& in, int64_t v) {
+          return in.op == OP_CONST && in.imm >= 0 && in.imm < P_.n_const && !P_.is_lit[in.imm] &&
+                 P_.ctag[in.imm] != TAG_FLOAT && P_.iconst[in.imm] == v;
+        };
+        if (len.op != OP_GLIST_LEN || !int_const(k0, 0) || !int_const(k1, 1)) continue;
+        if (lt.op != OP_LT || lt.imm != kLoopIndex || lt.a != k0.d || lt.b != len.d) continue;
+        if (tst.op != OP_LOOP_TEST || tst.a != lt.d || tst.imm != e) continue;
+        if (get.op != OP_GLIST_GET || get.imm != kLoopIndex || get.a != len.a || get.b != k0.d) continue;
+        if (lc.op != OP_LOOP_CONT || add.op != OP_ADD || add.imm != kLoopIndex || add.d != k0.d || add.a != k0.d ||
+            add.b != k1.d || nxt.op != OP_LOOP_NEXT || nxt.imm != b + 1)
+          continue;
+        if (!(all_in_[(size_t)b + 3] >> get.a & 1)) continue;   // node.gpus itself
+        if (k0.d == k1.d || k0.d == len.d || get.d == k0.d || get.d == len.d || get.d == get.a) continue;
+        LoopPat L;
+        L.b = b; L.e = e; L.idx = k0.d; L.n = len.d; L.g = get.d; L.src = get.a;
+        // the counter, its step, the length and the list are the skeleton's own:
+        // nothing in the body writes them, and the counter / step are dead after the loop
+        bool ok = true;
+        int inner_conts = 0;
+        for (int pc = b + 4; pc < e - 3 && ok; ++pc) {
+          const Insn& in = c[pc];
+          if (defines(in.op) && in.d != kNoReg && (in.d == L.idx || in.d == k1.d || in.d == L.n || in.d == L.src))
+            ok = false;
+          if (in.op == OP_CONTINUE && cont_t_[(size_t)pc] == e - 3) L.cont = true;
+          if (in.op == OP_LOOP_CONT) ++inner_conts;
+        }
+        (void)inner_conts;
+        if (!ok) continue;
+        if (e + 1 < n_ && (live_in_[(size_t)e + 1] >> L.idx & 1 || live_in_[(size_t)e + 1] >> k1.d & 1)) continue;
+        pats[b] = L;
+      }
+    }
+    if (pats.empty()) return;
+    // sizes, innermost first: a loop is unrolled when its eight copies stay under the cap
+    std::function<int(int, int)> size_of = [&](int lo, int hi) {
+      int sz = 0;
+      for (int pc = lo; pc < hi; ++pc) {
+        auto it = pats.find(pc);
+        if (it == pats.end()) { ++sz; continue; }
+        LoopPat& L = it->second;
+        L.body_size = size_of(L.b + 4, L.e - 3);
+        const int unrolled = 2 + 8 * (L.body_size + 5 + (L.cont ? 1 : 0));
+        L.unroll = 8 * L.body_size <= unroll_cap();
+        sz += L.unroll ? unrolled : (L.e - L.b + 1 - (L.e - 3 - (L.b + 4)) + L.body_size);
+        pc = L.e;
+      }
+      return sz;
+    };
+    if (size_of(0, n_) > kUnrollTotalCap) return;
+    bool any = false;
+    for (const auto& kv : pats) any = any || kv.second.unroll;
+    if (!any) return;
+    own_ctag_.assign(P_.ctag, P_.ctag + P_.n_const);
+    own_lit_.assign(P_.is_lit, P_.is_lit + P_.n_const);
+    own_iconst_.assign(P_.iconst, P_.iconst + P_.n_const);
+    own_fconst_.assign(P_.fconst, P_.fconst + P_.n_const);
+    int kidx[8];
+    for (int k = 0; k < 8; ++k) kidx[k] = pool_int(k);
+    std::vector<Insn> out;
+    out.reserve((size_t)n_ * 2);
+    auto mk_insn = [](uint8_t op, int d, int a, int b, int32_t imm) {
+      Insn in{};
+      in.op = op; in.d = (uint8_t)d; in.a = (uint8_t)a; in.b = (uint8_t)b; in.imm = imm;
+      return in;
+    };
+    auto has_target = [](uint8_t op) {
+      return op == OP_IF || op == OP_ELSE || op == OP_LOOP_TEST || op == OP_LOOP_NEXT;
+    };
+    // copy old pcs [lo, hi) (structured: every jump target of the range lies in
+    // it, or is hi itself for the top level's end); top: record elide_hi
+    std::function<void(int, int, bool)> emit_range = [&](int lo, int hi, bool top) {
+      std::map<int, int> at;              // old pc -> new pc
+      std::vector<size_t> fix;
+      for (int pc = lo; pc < hi; ++pc) {
+        at[pc] = (int)out.size();
+        if (top && pc == P_.elide_hi) elide_hi_ = (int)out.size();
+        auto it = pats.find(pc);
+        if (it != pats.end() && it->second.unroll) {
+          const LoopPat& L = it->second;
+          out.push_back(P_.code[L.b]);    // LOOP_BEGIN
+          const Insn& lt = P_.code[L.b + 1];
+          // a body that never CONTINUEs: copy k + 1 nested in copy k (a lane
+          // that reaches it ran every copy before it -- the analyses see that
+          // path, e.g. a max()'s "seen" flag is a constant from copy 1 on --
+          // and the wave skips every remaining copy once no lane has more GPUs);
+          // otherwise flat copies, each ended by LOOP_CONT at loop level
+          std::vector<size_t> open_ifs;
+          for (int k = 0; k < 8; ++k) {
+            out.push_back(mk_insn(OP_CONST, L.idx, kNoReg, kNoReg, kidx[k]));
+            out.push_back(mk_insn(OP_LT, lt.d, L.idx, L.n, 0));
+            open_ifs.push_back(out.size());
+            out.push_back(mk_insn(OP_IF, kNoReg, lt.d, kNoReg, 0));
+            out.push_back(mk_insn(OP_CONST, L.g, kNoReg, kNoReg, kidx[k]));
+            emit_range(L.b + 4, L.e - 3, false);
+            if (L.cont) {
+              out[open_ifs.back()].imm = (int32_t)out.size();
+              open_ifs.pop_back();
+              out.push_back(mk_insn(OP_ENDIF, kNoReg, kNoReg, kNoReg, 0));
+              out.push_back(mk_insn(OP_LOOP_CONT, kNoReg, kNoReg, kNoReg, 0));
+            }
+          }
+          while (!open_ifs.empty()) {
+            out[open_ifs.back()].imm = (int32_t)out.size();
+            open_ifs.pop_back();
+            out.push_back(mk_insn(OP_ENDIF, kNoReg, kNoReg, kNoReg, 0));
+          }
+          at[L.e] = (int)out.size();
+          out.push_back(P_.code[L.e]);    // LOOP_EXIT
+          for (int q = L.b + 1; q < L.e; ++q) at.erase(q);   // (nothing outside jumps into the loop)
+          pc = L.e;
+          ++n_unrolled_;
+          continue;
+        }
+        out.push_back(P_.code[pc]);
+        if (has_target(P_.code[pc].op)) fix.push_back(out.size() - 1);
+      }
+      at[hi] = (int)out.size();
+      if (top && hi == P_.elide_hi) elide_hi_ = (int)out.size();
+      for (size_t i : fix) {
+        auto t = at.find(out[i].imm);
+        if (t == at.end()) throw CodegenError("internal: jump out of an unrolled range");
+        out[i].imm = t->second;
+      }
+    };
+    emit_range(0, n_, true);
+    unrolled_code_ = std::move(out);
+    P_.code = unrolled_code_.data();
+    n_ = (int)unrolled_code_.size();
+    P_.ctag = own_ctag_.data();
+    P_.is_lit = own_lit_.data();
+    P_.iconst = own_iconst_.data();
+    P_.fconst = own_fconst_.data();
+    P_.n_const = (int)own_iconst_.size();
+    // (the analyses run again on the new code)
+    all_in_.clear(); uni_in_.clear(); live_in_.clear(); live_out_.clear();
+  }
 
   // ============================================================ analysis
   static bool defines(uint8_t op) {
@@ -210,6 +459,12 @@ class Codegen {
         return true;
     }
   }
+  // truth value of node.gpus (register r unchanged on every path) read at pc
+  bool list_truth(int pc, int r) const {
+    if (pc < 0 || r == kNoReg || all_in_.empty() || !(all_in_[(size_t)pc] >> r & 1)) return false;
+    const uint8_t op = P_.code[pc].op;
+    return (op == OP_IF || op == OP_LOOP_TEST || op == OP_NOT || op == OP_TRUTH) && P_.code[pc].a == r;
+  }
   uint64_t uses(int pc) const {
     const Insn& in = P_.code[pc];
     uint64_t u = 0;
@@ -219,7 +474,10 @@ class Codegen {
     // node.gpus itself is not read by its length or a loop-counter get (all_in_)
     const bool all_list_read = (in.op == OP_GLIST_LEN || (in.op == OP_GLIST_GET && in.imm == kLoopIndex)) &&
                                in.a != kNoReg && !all_in_.empty() && (all_in_[pc] >> in.a & 1);
-    if (in.a != kNoReg && !all_list_read) u |= 1ull << in.a;
+    // a GPU index known to be a constant is not read either (emit_gpu: a direct move)
+    const bool const_gpu = in.op == OP_GPU && (in.imm == 0 || in.imm == 1) && in.a != kNoReg && !kin_.empty() &&
+                           kin_[(size_t)pc][in.a] >= 0 && kin_[(size_t)pc][in.a] < 8;
+    if (in.a != kNoReg && !all_list_read && !const_gpu && !list_truth(pc, in.a)) u |= 1ull << in.a;
     if (in.b != kNoReg) u |= 1ull << in.b;
     if (!fold_.empty()) u &= ~fold_[pc];   // read as inline constants
     if ((in.op == OP_GLIST_SLICE || in.op == OP_GLIST_INSERT) && in.imm != kNoReg) u |= 1ull << in.imm;
@@ -366,39 +624,93 @@ class Codegen {
         default: return is_bool_op(in.op);
       }
     };
-    must_solve(i32_in_, [&](int pc, uint64_t st) {
-      const Insn& in = P_.code[pc];
-      if (!defines(in.op) || in.d == kNoReg) return st;
-      const uint64_t bit = 1ull << in.d;
-      return i32_def(in, st) ? (st | bit) : (st & ~bit);
-    });
-    must_solve(ex_in_, [&](int pc, uint64_t st) {
-      const Insn& in = P_.code[pc];
-      if (!defines(in.op) || in.d == kNoReg) return st;
-      const uint64_t bit = 1ull << in.d;
-      const uint64_t i = i32_in_[pc];
-      bool r = i32_def(in, i);
-      switch (in.op) {
-        case OP_MOV: case OP_POS: r = r || (st >> in.a & 1); break;
-        case OP_ADD: case OP_SUB: r = r || ((i >> in.a & 1) && (i >> in.b & 1)); break;   // |x| < 2^32
-        case OP_NEG: case OP_ABS: r = r || (i >> in.a & 1); break;
-        case OP_MIN2: case OP_MAX2: r = r || ((st >> in.a & 1) && (st >> in.b & 1)); break;
-        case OP_CONST:
-          r = r || (fixed_int(in.imm) && P_.iconst[in.imm] >= -(1ll << 53) && P_.iconst[in.imm] <= (1ll << 53));
-          break;
-        default: break;
+    // magnitudes: per pc entry and register, m with |x| < 2^m for an int value
+    // (64: not known to be a bounded int -- a float, a mixed type, or grown
+    // around a loop).  Forward, join = max; at a loop head a register that
+    // grows is widened to 64 (an unrolled node.gpus loop has no back edge, so
+    // a sum over the GPUs keeps its bound).  i32 / i33 / exact are its views.
+    {
+      std::vector<MagRow>& mag = mag_in_;
+      mag.assign(n_, MagRow{});
+      std::vector<char> seen(n_, 0), head(n_, 0);
+      for (int pc = 0; pc < n_; ++pc)
+        if (P_.code[pc].op == OP_LOOP_NEXT && P_.code[pc].imm >= 0 && P_.code[pc].imm < n_) head[P_.code[pc].imm] = 1;
+      auto bits_of = [](int64_t v) {
+        const uint64_t a = v < 0 ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
+        int m = 0;
+        while (m < 64 && (a >> m) != 0) ++m;
+        return (uint8_t)(m < 1 ? 1 : m);   // |v| < 2^m (0 and 1: 1)
+      };
+      auto cap = [](int m) { return (uint8_t)(m > 64 ? 64 : m); };
+      mag[0].fill(64);
+      seen[0] = 1;
+      std::vector<int> work{0};
+      while (!work.empty()) {
+        const int pc = work.back();
+        work.pop_back();
+        MagRow out = mag[pc];
+        const Insn& in = P_.code[pc];
+        if (defines(in.op) && in.d != kNoReg) {
+          const uint8_t ma = in.a != kNoReg && in.a < kMaxRegs ? mag[pc][in.a] : 64;
+          const uint8_t mb = in.b != kNoReg && in.b < kMaxRegs ? mag[pc][in.b] : 64;
+          uint8_t m = 64;
+          switch (in.op) {
+            case OP_CONST: if (fixed_int(in.imm)) m = bits_of(P_.iconst[in.imm]); break;
+            case OP_MOV: case OP_POS: case OP_NEG: case OP_ABS: m = ma; break;
+            case OP_NODE: m = 31; break;                                 // int32 argument fields
+            case OP_GLIST_LEN: case OP_GLIST_GET: m = 4; break;          // [0, 15]
+            case OP_POD: m = in.imm >= 0 && in.imm <= 3 ? 31 : 64; break;   // creation / duration: int64
+            case OP_GPU: m = in.imm == 0 || in.imm == 1 ? 31 : 64; break;   // GPU memory: int64
+            case OP_ADD: case OP_SUB: m = (ma < 64 && mb < 64) ? cap(std::max(ma, mb) + 1) : 64; break;
+            case OP_MUL: m = (ma < 64 && mb < 64) ? cap(ma + mb) : 64; break;
+            case OP_MIN2: case OP_MAX2: m = std::max(ma, mb); break;
+            case OP_FDIV: m = (ma < 64 && mb < 64) ? ma : 64; break;     // |a // b| <= |a| (b != 0 int)
+            case OP_MOD: m = (ma < 64 && mb < 64) ? mb : 64; break;      // |a % b| < |b|
+            default: m = is_bool_op(in.op) ? 1 : 64; break;
+          }
+          out[in.d] = m;
+        }
+        for (int t : succ_[pc]) {
+          if (t < 0) continue;
+          bool changed = !seen[t];
+          for (int r = 0; r < kMaxRegs; ++r) {
+            uint8_t nv = !seen[t] ? out[r] : std::max(mag[t][r], out[r]);
+            if (seen[t] && head[t] && nv > mag[t][r]) nv = 64;   // widen around a loop
+            if (nv != mag[t][r]) { mag[t][r] = nv; changed = true; }
+          }
+          seen[t] = 1;
+          if (changed) work.push_back(t);
+        }
       }
-      return r ? (st | bit) : (st & ~bit);
-    });
+      i32_in_.assign(n_, ~0ull);
+      ex_in_.assign(n_, ~0ull);
+      i33_in_.assign(n_, ~0ull);
+      for (int pc = 0; pc < n_; ++pc) {
+        if (!seen[pc]) continue;   // unreached: every fact (as must_solve)
+        uint64_t a = 0, b = 0, c = 0;
+        for (int r = 0; r < kMaxRegs; ++r) {
+          if (mag[pc][r] <= 31) a |= 1ull << r;
+          if (mag[pc][r] <= 32) c |= 1ull << r;
+          if (mag[pc][r] <= 53) b |= 1ull << r;
+        }
+        i32_in_[pc] = a;
+        ex_in_[pc] = b;
+        i33_in_[pc] = c;
+      }
+    }
     int add_sites = 0;
     for (int pc = 0; pc < n_; ++pc)
       if (P_.code[pc].op == OP_ADD || P_.code[pc].op == OP_SUB) ++add_sites;
+    // an accumulator: built from int32 terms by ADD / SUB with an int32 operand
+    // (<= kAccSites sites: below 2^62, see kJitLoopCap) -- or with |term| < 2^32
+    // when there are at most half as many sites (the same bound)
+    acc_term_i33_ = add_sites <= kAccSites / 2;
     must_solve(acc_in_, [&](int pc, uint64_t st) {
       const Insn& in = P_.code[pc];
       if (!defines(in.op) || in.d == kNoReg) return st;
       const uint64_t bit = 1ull << in.d;
-      const uint64_t i = i32_in_[pc];
-      bool r = i32_def(in, i);
+      const uint64_t i = add_sites <= kAccSites / 2 ? i33_in_[pc] : i32_in_[pc];
+      bool r = i32_def(in, i32_in_[pc]);
       if (add_sites <= kAccSites) {
         switch (in.op) {
           case OP_MOV: case OP_POS: case OP_NEG: case OP_ABS: r = r || (st >> in.a & 1); break;
@@ -408,6 +720,22 @@ class Codegen {
           case OP_MIN2: case OP_MAX2: r = r || ((st >> in.a & 1) && (st >> in.b & 1)); break;
           default: break;
         }
+      }
+      return r ? (st | bit) : (st & ~bit);
+    });
+    must_solve(pos_in_, [&](int pc, uint64_t st) {
+      const Insn& in = P_.code[pc];
+      if (!defines(in.op) || in.d == kNoReg) return st;
+      const uint64_t bit = 1ull << in.d;
+      bool r = false;
+      switch (in.op) {
+        case OP_CONST: r = fixed_int(in.imm) && P_.iconst[in.imm] > 0; break;
+        case OP_MOV: case OP_POS: r = (st >> in.a & 1) != 0; break;
+        // max(a, b) is b only where b > a: a > 0 (or NaN) -> the result is too;
+        // b > 0 and a an int (never NaN) or > 0 -> likewise; a NaN a stays NaN
+        case OP_MAX2: r = (st >> in.a & 1) || (st >> in.b & 1); break;
+        case OP_MIN2: r = (st >> in.a & 1) && (st >> in.b & 1); break;   // one of the two
+        default: break;
       }
       return r ? (st | bit) : (st & ~bit);
     });
@@ -445,6 +773,62 @@ class Codegen {
         if (changed) work.push_back(t);
       }
     }
+  }
+
+  // ---- truth values known at compile time (kbool_: per pc entry and register,
+  // -1 unknown, 0 / 1): compiled-in constants, and NOT / TRUTH / copies of them
+  std::vector<std::array<int8_t, kMaxRegs>> kbool_;
+  std::vector<int8_t> static_if_;   // per IF pc: -1 dynamic, 0 never taken, 1 always taken
+  void bool_facts() {
+    kbool_.assign(n_, {});
+    for (auto& a : kbool_) a.fill(-2);
+    kbool_[0].fill(-1);
+    std::vector<char> seen(n_, 0);
+    seen[0] = 1;
+    std::vector<int> work{0};
+    while (!work.empty()) {
+      const int pc = work.back();
+      work.pop_back();
+      std::array<int8_t, kMaxRegs> out = kbool_[pc];
+      const Insn& in = P_.code[pc];
+      if (defines(in.op) && in.d != kNoReg) {
+        int8_t v = -1;
+        if (in.op == OP_CONST && in.imm >= 0 && in.imm < P_.n_const && !P_.is_lit[in.imm])
+          v = P_.ctag[in.imm] == TAG_FLOAT ? (int8_t)(P_.fconst[in.imm] != 0.0 || std::isnan(P_.fconst[in.imm]))
+                                           : (int8_t)(P_.iconst[in.imm] != 0);
+        else if ((in.op == OP_MOV || in.op == OP_POS || in.op == OP_TRUTH) && in.a != kNoReg)
+          v = kbool_[pc][in.a] >= 0 ? kbool_[pc][in.a] : -1;
+        else if (in.op == OP_NOT && in.a != kNoReg)
+          v = kbool_[pc][in.a] >= 0 ? (int8_t)(1 - kbool_[pc][in.a]) : -1;
+        out[in.d] = v;
+      }
+      for (int t : succ_[pc]) {
+        if (t < 0) continue;
+        bool changed = !seen[t];
+        for (int r = 0; r < kMaxRegs; ++r) {
+          const int8_t nv = !seen[t] ? out[r] : (kbool_[t][r] == out[r] ? out[r] : (int8_t)-1);
+          if (nv != kbool_[t][r]) { kbool_[t][r] = nv; changed = true; }
+        }
+        seen[t] = 1;
+        if (changed) work.push_back(t);
+      }
+    }
+  }
+  // IFs whose condition is a known truth value: the dead branch leaves the
+  // CFG (the next round of analyses is more precise); true: a change
+  bool prune_static_ifs() {
+    if (static_if_.empty()) static_if_.assign(n_, -1);
+    bool changed = false;
+    for (int pc = 0; pc < n_; ++pc) {
+      const Insn& in = P_.code[pc];
+      if (in.op != OP_IF || static_if_[pc] >= 0 || in.a == kNoReg) continue;
+      const int8_t v = kbool_[pc][in.a];
+      if (v < 0) continue;
+      static_if_[pc] = v;
+      succ_[pc] = v ? std::array<int, 2>{pc + 1, -1} : std::array<int, 2>{in.imm + 1, -1};
+      changed = true;
+    }
+    return changed;
   }
 
   void const_facts() {
@@ -511,8 +895,7 @@ class Codegen {
         case OP_ADD: case OP_SUB: case OP_MUL:
           if (ta == TY_I && tb == TY_I) {
             cur_pc_ = pc;
-            const bool no_ovf = (i32(in.a) && i32(in.b)) ||
-                                (in.op != OP_MUL && ((acc(in.a) && i32(in.b)) || (i32(in.a) && acc(in.b))));
+            const bool no_ovf = no_int_overflow(in.op, in.a, in.b);
             cur_pc_ = -1;
             if (no_ovf && !(in.op == OP_ADD && in.imm == kLoopIndex)) { f(in.a, false); f(in.b, false); }
           } else if (ta != TY_IF && tb != TY_IF) {
@@ -593,6 +976,19 @@ class Codegen {
     }
   }
 
+  // side-effect-free definitions that emit nothing when their result is dead
+  // (emit_op): they read nothing then either (strong liveness -- a chain of
+  // dead copies, e.g. node.gpus built only for an unrolled loop, is dead as a whole)
+  bool elidable_def(int pc) const {
+    const Insn& in = P_.code[pc];
+    if (in.d == kNoReg) return false;
+    switch (in.op) {
+      case OP_CONST: case OP_MOV: case OP_POS: case OP_POD: case OP_NODE: case OP_GLIST_ALL: case OP_GLIST_LEN:
+        return true;
+      case OP_GPU: return in.imm <= 1;
+      default: return false;
+    }
+  }
   void liveness() {
     live_in_.assign(n_, 0);
     live_out_.assign(n_, 0);
@@ -603,7 +999,8 @@ class Codegen {
         uint64_t out = 0;
         for (int s : succ_[pc])
           if (s >= 0) out |= live_in_[s];
-        const uint64_t in = uses(pc) | (out & ~defs(pc));
+        const bool dead = elidable_def(pc) && !(out >> P_.code[pc].d & 1);
+        const uint64_t in = (dead ? 0 : uses(pc)) | (out & ~defs(pc));
         if (out != live_out_[pc] || in != live_in_[pc]) {
           live_out_[pc] = out;
           live_in_[pc] = in;
@@ -632,7 +1029,8 @@ class Codegen {
         int t = -1;
         if (ins.op == OP_IF || ins.op == OP_ELSE || ins.op == OP_LOOP_TEST || ins.op == OP_LOOP_NEXT) t = ins.imm;
         if (t >= 0 && t < n_) out |= in[t];
-        const uint64_t li = uses(pc) | (out & ~defs(pc));
+        const bool dead = elidable_def(pc) && !(live_out_[pc] >> ins.d & 1);   // emits nothing
+        const uint64_t li = (dead ? 0 : uses(pc)) | (out & ~defs(pc));
         if (out != slive_out_[pc] || li != in[pc]) {
           slive_out_[pc] = out;
           in[pc] = li;
@@ -1148,7 +1546,8 @@ class Codegen {
     };
     for (int pc = 0; pc < n_; ++pc) {
       const Insn& in = P_.code[pc];
-      if (in.op == OP_NODE || in.op == OP_GLIST_ALL || in.op == OP_GLIST_LEN) mark(AC_NODE, pc);
+      if (in.op == OP_NODE || in.op == OP_GLIST_ALL || in.op == OP_GLIST_LEN || list_truth(pc, in.a))
+        mark(AC_NODE, pc);
       if (in.op == OP_GPU) mark(in.imm == 0 || in.imm == 1 ? AC_GL : AC_GMEM, pc);
       if (in.op == OP_GPU) mark(AC_NODE, pc);   // (GPU j exists: the count in v4)
       if (in.op == OP_POD) mark(AC_POD, pc);
@@ -1230,8 +1629,8 @@ class Codegen {
   void restore_exec(uint16_t base) {
     e(mk(S_ANDN2_B64, EXEC, base, s(s_dead_)));
     if (Frame* l = innermost_loop()) {
-      e(mk(S_ANDN2_B64, EXEC, EXEC, s(l->s_brk)));
-      e(mk(S_ANDN2_B64, EXEC, EXEC, s(l->s_cont)));
+      if (l->s_brk >= 0) e(mk(S_ANDN2_B64, EXEC, EXEC, s(l->s_brk)));
+      if (l->s_cont >= 0) e(mk(S_ANDN2_B64, EXEC, EXEC, s(l->s_cont)));
     }
   }
   // lanes of EXEC leave the function here
@@ -1242,6 +1641,11 @@ class Codegen {
   // truth(r) -> SGPR pair
   uint16_t truth(int r, uint8_t t, uint16_t dst) {
     if (bm_of_[r] >= 0) return s(bm_pair_[bm_of_[r]]);
+    if (list_truth(cur_pc_, r)) {   // node.gpus: nonempty = a GPU count above 0 (the list itself unread)
+      e(mk(V_LSHRREV_B32, Th(1), ic(16), v(4)));
+      cmp(V_CMP_NE_U32, dst, ic(0), Th(1));
+      return dst;
+    }
     if (t == TY_I) { cmp(V_CMP_NE_I64, dst, ic(0), R(r)); return dst; }
     if (t == TY_F) { cmp(V_CMP_NEQ_F64, dst, ic(0), R(r)); return dst; }
     tag_mask(r, ST(1));
@@ -1255,6 +1659,24 @@ class Codegen {
   void set_bool(int d, uint16_t mask) {   // d = int(mask), materialised lazily
     set_tag_static(d, false);
     bm_set(d, mask);
+    pend_ |= 1ull << d;
+  }
+  // the mask slot a new bool d is computed into directly (no copy from a
+  // scratch pair): its other occupants are materialised first; commit_bool
+  // then makes d pending in it
+  uint16_t bool_slot(int d) {
+    const int slot = bm_next_ & 1;
+    for (int q = 0; q < kMaxRegs; ++q)
+      if (bm_of_[q] == slot && q != d) {
+        materialize(q);
+        bm_of_[q] = -1;
+      }
+    return s(bm_pair_[slot]);
+  }
+  void commit_bool(int d) {
+    const int slot = bm_next_++ & 1;
+    set_tag_static(d, false);
+    bm_of_[d] = (int8_t)slot;
     pend_ |= 1ull << d;
   }
 
@@ -1292,6 +1714,7 @@ class Codegen {
     }
     const int l_end = label();
     for (int pc = 0; pc < n_; ++pc) {
+      if (pc < skip_to_) continue;   // the dead branch of a known condition
       auto it = label_at_pc_.find(pc);
       if (it != label_at_pc_.end() && P_.code[pc].op != OP_ENDIF && P_.code[pc].op != OP_ELSE &&
           P_.code[pc].op != OP_LOOP_EXIT)
@@ -1328,6 +1751,14 @@ class Codegen {
     const uint8_t ta = in.a != kNoReg ? st[in.a] : TY_I;
     const uint8_t tb = in.b != kNoReg ? st[in.b] : TY_I;
     const int d = in.d, a = in.a, b = in.b;
+    // a side-effect-free definition nothing reads (e.g. node.gpus built for a
+    // len() or an unrolled loop) emits nothing -- its operands are not read
+    // either (strong liveness: they need not even hold a value)
+    if (elidable_def(pc) && !(live_out_[pc] >> d & 1)) {
+      pend_ &= ~(1ull << d);
+      bm_of_[d] = -1;
+      return;
+    }
     const bool exec_change = structural(in.op) || in.op == OP_BREAK || in.op == OP_CONTINUE || in.op == OP_RET ||
                              in.op == OP_RAISE || in.op == OP_END;
     const bool via_mask = in.op == OP_IF || in.op == OP_LOOP_TEST || in.op == OP_NOT || in.op == OP_TRUTH;
@@ -1341,7 +1772,7 @@ class Codegen {
     // take their operand's mask first, then materialise)
     uint16_t mask_a = NONE;
     if (exec_change) {
-      if (in.op == OP_IF || in.op == OP_LOOP_TEST) mask_a = truth(a, ta, ST(0));
+      if ((in.op == OP_IF && static_if_[pc] < 0) || in.op == OP_LOOP_TEST) mask_a = truth(a, ta, ST(0));
       // (a bool's mask pair survives the materialisation below: used in place)
       materialize_live(slive_out_[pc] | live_out_[pc]);
       bm_clear();
@@ -1349,15 +1780,6 @@ class Codegen {
       // (NOT / TRUTH read their operand's mask first and set d's state themselves)
       if (!(in.op == OP_MOV || in.op == OP_POS)) bm_of_[d] = -1;
       if (!((in.op == OP_MOV || in.op == OP_POS) && (pend_ >> a & 1))) pend_ &= ~(1ull << d);
-    }
-    // a side-effect-free definition nothing reads (e.g. node.gpus built for a
-    // len() or a counter-indexed loop) emits nothing
-    if (d != kNoReg && !(live_out_[pc] >> d & 1) &&
-        (in.op == OP_CONST || in.op == OP_MOV || in.op == OP_POS || in.op == OP_POD || in.op == OP_NODE ||
-         in.op == OP_GLIST_ALL || in.op == OP_GLIST_LEN || (in.op == OP_GPU && in.imm <= 1))) {
-      pend_ &= ~(1ull << d);
-      bm_of_[d] = -1;
-      return;
     }
     switch (in.op) {
       case OP_NOP: break;
@@ -1499,14 +1921,16 @@ class Codegen {
       case OP_TDIV:
         if (ta == TY_IF || tb == TY_IF) { rtcall(0, in.op, pc, d, a, ta, b, tb); break; }
         if (ta == TY_I && tb == TY_I) {
-          cmp(V_CMP_EQ_I64, ST(0), ic(0), R(b));
-          soft_raise(ST(0), EXC_ZERO_DIVISION);
+          if (!nonzero(b)) {
+            cmp(V_CMP_EQ_I64, ST(0), ic(0), R(b));
+            soft_raise(ST(0), EXC_ZERO_DIVISION);
+          }
           if (!exact(a)) check_exact_int(R(a), EXEC);
           if (!exact(b)) check_exact_int(R(b), EXEC);
         }
         {
           const uint16_t fa = as_f64(a, ta, 0), fb = as_f64(b, tb, 1);
-          if (!(ta == TY_I && tb == TY_I)) {
+          if (!(ta == TY_I && tb == TY_I) && !nonzero(b)) {
             cmp(V_CMP_EQ_F64, ST(0), ic(0), fb);
             soft_raise(ST(0), EXC_ZERO_DIVISION);
           }
@@ -1594,8 +2018,10 @@ class Codegen {
         }
         const uint16_t m = truth(a, ta, ST(0));
         if (in.op == OP_NOT) {
-          e(mk(S_ANDN2_B64, ST(0), EXEC, m));
-          set_bool(d, ST(0));
+          // (the operand's own slot may be the one d takes: read before written)
+          const uint16_t slot = bool_slot(d);
+          e(mk(S_ANDN2_B64, slot, EXEC, m));
+          commit_bool(d);
         } else {
           set_bool(d, m);
         }
@@ -1611,22 +2037,41 @@ class Codegen {
           set_tag_static(d, false);
         }
         break;
-      case OP_LT: case OP_LE: case OP_GT: case OP_GE: case OP_EQ: case OP_NE:
+      case OP_LT: case OP_LE: case OP_GT: case OP_GE: case OP_EQ: case OP_NE: {
+        const uint16_t slot = bool_slot(d);   // the compare writes d's mask slot itself
         if (in.op == OP_LT && in.imm == kLoopIndex && ta == TY_I && tb == TY_I)
-          cmp(V_CMP_LT_I32, ST(0), R(a), R(b));   // counter < length, both in [0, 15]
+          cmp(V_CMP_LT_I32, slot, R(a), R(b));   // counter < length, both in [0, 15]
         else
-          emit_compare(in.op, a, ta, b, tb, ST(0));
-        set_bool(d, ST(0));
+          emit_compare(in.op, a, ta, b, tb, slot);
+        commit_bool(d);
         break;
+      }
       case OP_MIN2: case OP_MAX2: emit_minmax(in, ta, tb); break;
       // ---- control flow
       case OP_IF: {
+        const int t = in.imm;
+        if (t <= pc || t >= n_) throw CodegenError("bad IF target");
+        if (static_if_[pc] >= 0) {
+          // a known condition: no mask, no branch; the dead branch is not emitted
+          const bool has_else = P_.code[t].op == OP_ELSE;
+          if (!static_if_[pc] && !has_else) {   // never taken: nothing at all
+            skip_to_ = t + 1;
+            break;
+          }
+          Frame fr{};
+          fr.loop = false;
+          fr.pc = pc;
+          fr.s_save = take_spair();            // (the ENDIF still drops lanes that left inside)
+          fr.static_branch = true;
+          e(mk(S_MOV_B64, s(fr.s_save), EXEC));
+          frames_.push_back(fr);
+          if (!static_if_[pc]) skip_to_ = t + 1;   // straight to the else-branch
+          break;
+        }
         Frame fr{};
         fr.loop = false;
         fr.pc = pc;
         fr.s_save = take_spair();
-        const int t = in.imm;
-        if (t <= pc || t >= n_) throw CodegenError("bad IF target");
         if (P_.code[t].op == OP_ELSE) {
           fr.s_else = take_spair();
           e(mk(S_ANDN2_B64, s(fr.s_else), EXEC, mask_a));
@@ -1639,6 +2084,10 @@ class Codegen {
         break;
       }
       case OP_ELSE: {
+        if (!frames_.empty() && !frames_.back().loop && frames_.back().static_branch) {
+          skip_to_ = in.imm;   // end of an always-taken then-branch: the else-branch is dead
+          break;
+        }
         if (frames_.empty() || frames_.back().loop || frames_.back().s_else < 0) throw CodegenError("stray ELSE");
         place(label_for_pc(pc));
         e(mk(S_MOV_B64, EXEC, s(frames_.back().s_else)));
@@ -1660,11 +2109,32 @@ class Codegen {
         fr.loop = true;
         fr.pc = pc;
         fr.s_entry = take_spair();
-        fr.s_brk = take_spair();
-        fr.s_cont = take_spair();
+        // break / continue masks only for loops that break / continue (the
+        // others skip their upkeep at every ENDIF and LOOP_CONT)
+        bool brk = false, cont = false;
+        {
+          int depth = 0, q = pc + 1;
+          std::set<int> conts;
+          for (; q < n_; ++q) {
+            const uint8_t o = P_.code[q].op;
+            if (o == OP_LOOP_BEGIN) ++depth;
+            else if (o == OP_LOOP_EXIT) { if (depth == 0) break; --depth; }
+            else if (o == OP_LOOP_CONT && depth == 0) conts.insert(q);
+          }
+          for (int r = pc + 1; r < q; ++r) {
+            if (P_.code[r].op == OP_BREAK && brk_t_[(size_t)r] == q) brk = true;
+            if (P_.code[r].op == OP_CONTINUE && conts.count(cont_t_[(size_t)r])) cont = true;
+          }
+        }
         e(mk(S_MOV_B64, s(fr.s_entry), EXEC));
-        e(mk(S_MOV_B64, s(fr.s_brk), ic(0)));
-        e(mk(S_MOV_B64, s(fr.s_cont), ic(0)));
+        if (brk) {
+          fr.s_brk = take_spair();
+          e(mk(S_MOV_B64, s(fr.s_brk), ic(0)));
+        }
+        if (cont) {
+          fr.s_cont = take_spair();
+          e(mk(S_MOV_B64, s(fr.s_cont), ic(0)));
+        }
         fr.l_head = label();
         place(fr.l_head);
         frames_.push_back(fr);
@@ -1680,19 +2150,26 @@ class Codegen {
       case OP_LOOP_CONT: {
         Frame* l = innermost_loop();
         if (!l || frames_.back().pc != l->pc) throw CodegenError("LOOP_CONT not at loop level");
-        e(mk(S_OR_B64, EXEC, EXEC, s(l->s_cont)));
-        e(mk(S_MOV_B64, s(l->s_cont), ic(0)));
+        if (l->s_cont >= 0) {
+          e(mk(S_OR_B64, EXEC, EXEC, s(l->s_cont)));
+          e(mk(S_MOV_B64, s(l->s_cont), ic(0)));
+        }
         break;
       }
       case OP_LOOP_NEXT: {
         Frame* l = innermost_loop();
         if (!l || frames_.back().pc != l->pc) throw CodegenError("LOOP_NEXT not at loop level");
         if (in.imm != l->pc + 1) throw CodegenError("loop back edge not to the loop head");
-        {   // budget: s_bud -= 1; on a borrow every lane still looping raises BUDGET
+        {   // budget: s_bud -= 1; on a borrow every lane still looping raises BUDGET,
+          // and the counter stays exhausted (0: the next back edge borrows again),
+          // so lanes outside EXEC here -- done with this loop, in another branch or
+          // an outer loop -- raise at their next back edge instead of continuing
+          // with a wrapped ~2^32 budget (kJitLoopCap is what value_facts relies on)
           e(mk(S_SUB_U32, s(s_bud_), s(s_bud_), ic(1)));
           const int ok = label();
           e(mkimm(S_CBRANCH_SCC0, ok));
           soft_raise(EXEC, EXC_BUDGET);
+          e(mk(S_MOV_B32, s(s_bud_), ic(0)));
           place(ok);
         }
         e(mkimm(S_CBRANCH_EXECNZ, l->l_head));   // (lanes that raised in the body left EXEC already)
@@ -1706,20 +2183,20 @@ class Codegen {
         frames_.pop_back();
         e(mk(S_ANDN2_B64, EXEC, s(fr.s_entry), s(s_dead_)));
         give_spair(fr.s_entry);
-        give_spair(fr.s_brk);
-        give_spair(fr.s_cont);
+        if (fr.s_brk >= 0) give_spair(fr.s_brk);
+        if (fr.s_cont >= 0) give_spair(fr.s_cont);
         break;
       }
       case OP_BREAK: {
         Frame* l = innermost_loop();
-        if (!l) throw CodegenError("BREAK outside a loop");
+        if (!l || l->s_brk < 0) throw CodegenError("internal: BREAK of a loop without a break mask");
         e(mk(S_OR_B64, s(l->s_brk), s(l->s_brk), EXEC));
         e(mk(S_MOV_B64, EXEC, ic(0)));
         break;
       }
       case OP_CONTINUE: {
         Frame* l = innermost_loop();
-        if (!l) throw CodegenError("CONTINUE outside a loop");
+        if (!l || l->s_cont < 0) throw CodegenError("internal: CONTINUE of a loop without a continue mask");
         e(mk(S_OR_B64, s(l->s_cont), s(l->s_cont), EXEC));
         e(mk(S_MOV_B64, EXEC, ic(0)));
         break;
@@ -1761,8 +2238,7 @@ class Codegen {
   // ---- int64 add / sub / mul with overflow -> EXC_UNSUPPORTED
   void emit_int_arith(const Insn& in) {
     const int d = in.d, a = in.a, b = in.b;
-    const bool no_ovf = (i32(a) && i32(b)) ||
-                        (in.op != OP_MUL && ((acc(a) && i32(b)) || (i32(a) && acc(b))));
+    const bool no_ovf = no_int_overflow(in.op, a, b);
     if (no_ovf) {   // |a|, |b| < 2^31, or an accumulator plus an int32: no int64 overflow
       if (in.op == OP_MUL) {
         e(mk3b(V_MAD_I64_I32, R(d), VCC, opi(a), opi(b), ic(0)));
@@ -1818,8 +2294,10 @@ class Codegen {
   // operands -> EXC_UNSUPPORTED (the next engine decides).
   void emit_int_divmod(const Insn& in) {
     const int d = in.d, a = in.a, b = in.b;
-    cmp(V_CMP_EQ_I64, ST(0), ic(0), R(b));
-    soft_raise(ST(0), EXC_ZERO_DIVISION);
+    if (!nonzero(b)) {
+      cmp(V_CMP_EQ_I64, ST(0), ic(0), R(b));
+      soft_raise(ST(0), EXC_ZERO_DIVISION);
+    }
     if (!exact(a)) check_exact_int(R(a), EXEC);
     if (!exact(b)) check_exact_int(R(b), EXEC);
     const uint16_t fa = as_f64(a, TY_I, 0), fb = as_f64(b, TY_I, 1);

@@ -59,23 +59,40 @@ const char* reg_name(uint16_t c, char* buf) {
 
 }  // namespace
 
+// Code for one program: with its feasibility prologue compiled out (when the
+// caller asks) and its node.gpus loops unrolled, else without either, in that
+// order of preference (a program the first form does not fit -- registers,
+// SGPR frames -- usually fits the next); *elided: the prologue is out.
+gcn::Func generate(gcn::ProgIn in, gcn::GenStats* st, bool* elided) {
+  const bool can_elide = in.elide_lo < in.elide_hi;
+  std::string first_error;
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    const bool elide = attempt < 2, unroll = attempt % 2 == 0;
+    if (elide && !can_elide) continue;
+    gcn::ProgIn q = in;
+    if (!elide) q.elide_lo = q.elide_hi = 0;   // the whole program (valid for any caller)
+    q.no_unroll = !unroll;
+    try {
+      if (st) *st = gcn::GenStats{};
+      gcn::Codegen cg(q);
+      gcn::Func f = cg.run(st);
+      if (elided) *elided = elide;
+      return f;
+    } catch (const gcn::CodegenError& e) {
+      if (first_error.empty()) first_error = e.what();
+    }
+  }
+  throw gcn::CodegenError(first_error);
+}
+
 Result compile(const ProgramDesc& p) {
   Result r;
   try {
     gcn::ProgIn in = make_in(p);
     gcn::GenStats st;
-    gcn::Func f;
-    try {
-      gcn::Codegen cg(in);
-      f = cg.run(&st);
-      r.elided = in.elide_lo < in.elide_hi;
-    } catch (const gcn::CodegenError&) {
-      if (!(in.elide_lo < in.elide_hi)) throw;
-      in.elide_lo = in.elide_hi = 0;   // the whole program (valid for any caller)
-      st = gcn::GenStats{};
-      gcn::Codegen cg(in);
-      f = cg.run(&st);
-    }
+    bool elided = false;
+    gcn::Func f = generate(in, &st, &elided);
+    r.elided = elided;
     gcn::Code code = gcn::assemble(f);
     r.words = std::move(code.words);
     for (const gcn::Reloc& rl : code.relocs) {
@@ -90,6 +107,7 @@ Result compile(const ProgramDesc& p) {
     r.vregs = st.vregs;
     r.tagged = st.tagged;
     r.spills = st.spills;
+    r.unrolled = st.unrolled;
     r.mir = (int)f.mi.size();
     r.ok = true;
   } catch (const std::exception& e) {
@@ -101,14 +119,24 @@ Result compile(const ProgramDesc& p) {
 
 void set_pair_cap(int pairs) { gcn::pair_cap() = pairs < 0 ? 0 : pairs; }
 
+int set_unroll_cap(int cap) {
+  const int old = gcn::unroll_cap();
+  gcn::unroll_cap() = cap < 0 ? 0 : cap;
+  return old;
+}
+
 std::string listing(const ProgramDesc& p) {
   std::ostringstream os;
   try {
     gcn::ProgIn in = make_in(p);
-    gcn::Codegen cg(in);
-    gcn::Func f = cg.run();
+    gcn::Func f = generate(in, nullptr, nullptr);
     char b0[16], b1[16], b2[16], b3[16], b4[16];
+    int last_bc = -1;
     for (const gcn::MI& m : f.mi) {
+      if (m.bc != last_bc) {
+        last_bc = m.bc;
+        os << "    ; bc " << (int)m.bc << "\n";
+      }
       if (m.op == gcn::LABEL) { os << "L" << m.imm << ":\n"; continue; }
       os << "  " << gcn::info(m.op).name << " d=" << reg_name(m.d, b0) << " sd=" << reg_name(m.sd, b1)
          << " s0=" << reg_name(m.s0, b2) << " s1=" << reg_name(m.s1, b3) << " s2=" << reg_name(m.s2, b4);
@@ -239,17 +267,9 @@ std::vector<SimResult> emu_simulate_batch(const Workload& w, const std::vector<P
   std::vector<gcn::Func> funcs((size_t)P);
   std::vector<char> elided((size_t)P, 0);
   for (int64_t i = 0; i < P; ++i) {
-    gcn::ProgIn in = make_in(progs[(size_t)i]);
-    try {
-      gcn::Codegen cg(in);
-      funcs[(size_t)i] = cg.run();
-      elided[(size_t)i] = in.elide_lo < in.elide_hi;
-    } catch (const gcn::CodegenError&) {
-      if (!(in.elide_lo < in.elide_hi)) throw;
-      in.elide_lo = in.elide_hi = 0;   // as compile(): the whole program
-      gcn::Codegen cg(in);
-      funcs[(size_t)i] = cg.run();
-    }
+    bool el = false;
+    funcs[(size_t)i] = generate(make_in(progs[(size_t)i]), nullptr, &el);   // as compile()
+    elided[(size_t)i] = el;
   }
   std::vector<int64_t> gmem8((size_t)w.n_nodes * 8, 0);
   for (int n = 0; n < w.n_nodes; ++n)
@@ -298,9 +318,7 @@ std::vector<int64_t> emu_event(const ProgramDesc& p, const std::vector<int64_t>&
       (pod.size() != 6 && pod.size() != (size_t)N * 6))
     throw std::invalid_argument("emu_event: bad shapes");
   const bool per_lane_pod = pod.size() != 6;   // one pod per lane: several programs' rows in one call
-  gcn::ProgIn in = make_in(p);
-  gcn::Codegen cg(in);
-  gcn::Func f = cg.run();
+  gcn::Func f = generate(make_in(p), nullptr, nullptr);
   auto E = std::make_unique<gcn::Emu>();
   E->lds.resize(kc.size() * 8 + 64, 0);
   std::memcpy(E->lds.data(), kc.data(), kc.size() * 8);

@@ -150,13 +150,13 @@ def _object_worker(args):
 NATIVE_DEFER = (int(Exc.UNSUPPORTED), int(Exc.BUDGET), int(Exc.TIMEOUT), int(Exc.INVARIANT))
 
 
-def _native_deferred(row, stats) -> bool:
-    """True: this native-program row goes to the next engine (counted)."""
+def _native_deferred(row, bump) -> bool:
+    """True: this native-program row goes to the next engine (counted through `bump`)."""
     exc = int(row[COLS["exc"]])
     if exc == Exc.TIMEOUT:
-        stats["native_timeout"] += 1
+        bump("native_timeout")
     elif exc == Exc.INVARIANT:
-        stats["native_invariant"] += 1
+        bump("native_invariant")
         import warnings
         warnings.warn("native replay failed its invariant check (kernel bug?); program re-scored on the CPU VM",
                       RuntimeWarning, stacklevel=3)
@@ -191,7 +191,14 @@ class Evaluator:
         self.compile_workers = int(self.options.pop("compile_workers", 0) or 0)
         self._compile_pool = None
         self._compile_lock = threading.Lock()
-        self._fault_rng = np.random.default_rng(int(self.options.pop("fault_seed", 0)))
+        # counters are bumped from the dispatcher and from the fallback worker
+        # threads (`fallback_async`): every update goes through `_bump`
+        self._stats_lock = threading.Lock()
+        fault_seed = int(self.options.pop("fault_seed", 0))
+        self._fault_rng = np.random.default_rng(fault_seed)
+        # the fallback threads draw from their own generator (under the stats
+        # lock), so the dispatcher's fault sequence stays deterministic
+        self._fallback_fault_rng = np.random.default_rng(fault_seed + 1)
         self.device = None
         want_gpu = device not in ("cpu", None)
         if want_gpu:
@@ -211,6 +218,10 @@ class Evaluator:
         self.stats = {"device": 0, "device_native": 0, "cpu_vm": 0, "object": 0, "compile_errors": 0,
                       "jit_s": 0.0, "jit_shapes": 0, "native_timeout": 0, "native_invariant": 0}
         self._done: Dict[int, np.ndarray] = {}   # CPU stand-in for in-flight slots
+
+    def _bump(self, key: str, n=1) -> None:
+        with self._stats_lock:
+            self.stats[key] = self.stats.get(key, 0) + n
 
     @property
     def backend(self) -> str:
@@ -262,7 +273,7 @@ class Evaluator:
         out = []
         for prog, _ in results:
             if prog is None:
-                self.stats["compile_errors"] += 1
+                self._bump("compile_errors", 1)
             out.append(prog)
         return out
 
@@ -274,7 +285,7 @@ class Evaluator:
             for i in range(len(out)):
                 if self._fault_rng.random() < self.fault_rate:
                     out[i] = EvalResult(0.0, int(Exc.VALUE), "fault-injection")
-                    self.stats["faults"] = self.stats.get("faults", 0) + 1
+                    self._bump("faults")
         return out
 
     def _evaluate_compiled(self, codes: Sequence[str], compiled: List[Optional[CompiledPolicy]],
@@ -296,7 +307,7 @@ class Evaluator:
                     if int(row[COLS["exc"]]) in (Exc.UNSUPPORTED, Exc.BUDGET) or row[COLS["inexact"]]:
                         continue
                     out[i] = _row_to_result(row, "hip")
-                    self.stats["device"] += 1
+                    self._bump("device", 1)
         # 2) native CPU VM
         cpu_idx = [i for i in pending if out[i] is None]
         if cpu_idx:
@@ -307,7 +318,7 @@ class Evaluator:
                 if int(row[COLS["exc"]]) in (Exc.UNSUPPORTED, Exc.BUDGET) or row[COLS["inexact"]]:
                     continue
                 out[i] = _row_to_result(row, "cpu")
-                self.stats["cpu_vm"] += 1
+                self._bump("cpu_vm", 1)
         # 3) object engine (exact by construction)
         rest = [i for i in range(n) if out[i] is None]
         if rest and not object_ok:
@@ -315,7 +326,7 @@ class Evaluator:
             # intermediates): engine "shed", never a score
             for i in rest:
                 out[i] = EvalResult(0.0, int(Exc.UNSUPPORTED), "shed")
-                self.stats["shed"] = self.stats.get("shed", 0) + 1
+                self._bump("shed")
             rest = []
         if rest:
             if self._object_engine_ok():
@@ -334,7 +345,7 @@ class Evaluator:
                 results = [EvalResult(0.0, int(Exc.UNSUPPORTED), "none") for _ in rest]
             for i, r in zip(rest, results):
                 out[i] = r
-                self.stats["object"] += 1
+                self._bump("object", 1)
         return out  # type: ignore[return-value]
 
     def score_compiled(self, progs: Sequence[CompiledPolicy], slot: int = 0) -> np.ndarray:
@@ -346,10 +357,10 @@ class Evaluator:
         if self.device is not None and self.native and progs:
             self.device.submit_native(slot, progs)
             tab = self.device.wait(slot)
-            ok = np.array([not _native_deferred(row, self.stats) for row in tab], dtype=bool)
+            ok = np.array([not _native_deferred(row, self._bump) for row in tab], dtype=bool)
             out[ok] = tab[ok, COLS["score"]]
             rest = [i for i in range(len(progs)) if not ok[i]]
-            self.stats["device_native"] += int(ok.sum())
+            self._bump("device_native", int(ok.sum()))
         if rest:
             from .ops import cpu_engine
             tab = cpu_engine.simulate_program_batch(self.workload, [progs[i] for i in rest],
@@ -357,7 +368,7 @@ class Evaluator:
             for row, i in zip(tab, rest):
                 exc = int(row[COLS["exc"]])
                 out[i] = 0.0 if exc else row[COLS["score"]]
-            self.stats["cpu_vm"] += len(rest)
+            self._bump("cpu_vm", len(rest))
         return out
 
     # -- asynchronous program batches (pipelined islands) ------------------------------
@@ -383,8 +394,7 @@ class Evaluator:
         pend = PendingPrograms(list(codes), -1)
         pend.compiled = list(compiled)
         if count_errors:
-            with self._compile_lock:
-                self.stats["compile_errors"] += sum(p is None for p in pend.compiled)
+            self._bump("compile_errors", sum(p is None for p in pend.compiled))
         if self.device is not None and self.native:
             idx = [i for i, p in enumerate(pend.compiled) if p is not None and p.device_ok]
             if idx:
@@ -395,9 +405,8 @@ class Evaluator:
                 pend.jit_s = batch.compile_s
                 pend.new_shapes = batch.compiled
                 pend.submit_s = time.perf_counter() - t0
-                with self._compile_lock:
-                    self.stats["jit_s"] += batch.compile_s
-                    self.stats["jit_shapes"] += batch.compiled
+                self._bump("jit_s", batch.compile_s)
+                self._bump("jit_shapes", batch.compiled)
         return pend
 
     def launch_prepared(self, pend: "PendingPrograms", slot: int) -> "PendingPrograms":
@@ -435,10 +444,10 @@ class Evaluator:
             tab = self.device.wait(pend.slot)
             pend.t_done = time.perf_counter()
             for row, i in zip(tab, pend.native_idx):
-                if _native_deferred(row, self.stats):
+                if _native_deferred(row, self._bump):
                     continue
                 out[i] = _row_to_result(row, "hip-native")
-                self.stats["device_native"] += 1
+                self._bump("device_native", 1)
         rest = [i for i in range(n) if out[i] is None]
         if rest and defer_fallback:
             pend.fallback_idx = rest
@@ -446,7 +455,7 @@ class Evaluator:
                 for i in range(n):
                     if out[i] is not None and self._fault_rng.random() < self.fault_rate:
                         out[i] = EvalResult(0.0, int(Exc.VALUE), "fault-injection")
-                        self.stats["faults"] = self.stats.get("faults", 0) + 1
+                        self._bump("faults")
             return out
         if rest:
             sub = self._evaluate_compiled([pend.codes[i] for i in rest], [pend.compiled[i] for i in rest],
@@ -457,7 +466,7 @@ class Evaluator:
             for i in range(n):
                 if self._fault_rng.random() < self.fault_rate:
                     out[i] = EvalResult(0.0, int(Exc.VALUE), "fault-injection")
-                    self.stats["faults"] = self.stats.get("faults", 0) + 1
+                    self._bump("faults")
         return out  # type: ignore[return-value]
 
     def fallback_async(self, pend: "PendingPrograms", object_ok: bool = True):
@@ -488,7 +497,9 @@ class Evaluator:
             res = self._evaluate_compiled(codes, compiled, native=False, host_only=True, object_ok=object_ok)
             if self.fault_rate > 0:
                 for k in range(len(res)):
-                    if self._fault_rng.random() < self.fault_rate:
+                    with self._stats_lock:
+                        hit = self._fallback_fault_rng.random() < self.fault_rate
+                    if hit:
                         res[k] = EvalResult(0.0, int(Exc.VALUE), "fault-injection")
             return idx, res
         return self._fallback_pool.submit(job)
@@ -505,14 +516,14 @@ class Evaluator:
 
     def _absorb_native(self, idx, compiled, out, slot: int) -> None:
         batch = self.device.submit_native(slot, [compiled[i] for i in idx])
-        self.stats["jit_s"] += batch.compile_s
-        self.stats["jit_shapes"] += batch.compiled
+        self._bump("jit_s", batch.compile_s)
+        self._bump("jit_shapes", batch.compiled)
         tab = self.device.wait(slot)
         for row, i in zip(tab, idx):
-            if _native_deferred(row, self.stats):
+            if _native_deferred(row, self._bump):
                 continue
             out[i] = _row_to_result(row, "hip-native")
-            self.stats["device_native"] += 1
+            self._bump("device_native", 1)
 
     def _object_engine_ok(self) -> bool:
         # the object engine implements only the reference's semantics

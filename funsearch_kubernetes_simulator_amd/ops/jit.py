@@ -612,16 +612,21 @@ class NativeCompiler:
                 codes.append(code)
                 keys.append(k)
         t1 = time.perf_counter()
-        if codes:
-            mod = self._baseline.load(codes, t1 - t0)
+        with self._lock:
+            self.stats["compile_s"] += t1 - t0
+            self.stats["baseline_s"] += t1 - t0
+        # one module per skeleton-sized chunk (thousands of long programs can
+        # exceed the largest arena)
+        for lo, hi in (self._baseline.chunks(codes) if codes else []):
+            t1 = time.perf_counter()
+            mod = self._baseline.load(codes[lo:hi], 0.0)
             t2 = time.perf_counter()
             with self._lock:
                 mi = self._add_module(mod.handle, "baseline")
-                self.stats["compile_s"] += t2 - t0
-                self.stats["baseline_s"] += t1 - t0
+                self.stats["compile_s"] += t2 - t1
                 self.stats["load_s"] += t2 - t1
                 self.stats["probed_loads"] = self.stats.get("probed_loads", 0) + int(mod.probed)
-                for j, k in enumerate(keys):
+                for j, k in enumerate(keys[lo:hi]):
                     self._map_shape(k, mi, j, int(mod.pointers[j]))
                     self._tier_of[k] = "baseline"
                     self._uses.pop(k, None)

@@ -1701,7 +1701,11 @@ def same_shape_child(parent: CompiledPolicy, child: str) -> Optional[CompiledPol
         if is_float:
             f[idx] = float(ctxt)
         else:
+            if len(ctxt) > 1 and ctxt[0] == "0":
+                return None        # `007`: a SyntaxError in Python 3 (int() would accept it)
             i[idx] = int(ctxt)
+            if not INT64_MIN <= i[idx] <= INT64_MAX:
+                return None        # Compiler.const's range check (the compile path reports it)
             if ptxt != ctxt and (parent.iconst[idx] in (0, 1) or i[idx] in (0, 1)):
                 return None        # int 0 / 1 decide common-subexpression eligibility (Compiler._cse_key)
         while cstarts[line_c + 1] <= cs:
@@ -1710,8 +1714,11 @@ def same_shape_child(parent: CompiledPolicy, child: str) -> Optional[CompiledPol
     if seen != len(parent.literals):
         return None
     span = {lt[0]: lt for lt in lits}
+    # the parent's bytecode range of the opening statements (whether they are the
+    # template's feasibility prologue is decided on the child's own text)
     return CompiledPolicy(parent.code, f, i, list(parent.ctag), parent.nregs, child, parent.features,
-                          [span[lt[0]] for lt in parent.literals])   # the compiler's order
+                          [span[lt[0]] for lt in parent.literals],   # the compiler's order
+                          prologue=parent.prologue)
 
 
 def try_compile(source: str) -> Tuple[Optional[CompiledPolicy], Optional[str]]:

@@ -222,7 +222,7 @@ def test_same_shape_child_equals_full_compile():
             if fast is None:
                 continue
             full, _ = try_compile(child)
-            for k in ("code", "fconst", "iconst", "ctag", "literals", "nregs", "features", "source"):
+            for k in ("code", "fconst", "iconst", "ctag", "literals", "nregs", "features", "source", "prologue"):
                 assert getattr(fast, k) == getattr(full, k), k
             hits += 1
     assert hits >= 20
@@ -230,3 +230,7 @@ def test_same_shape_child_equals_full_compile():
     assert same_shape_child(p, parents[0].replace("17 * a", "17.0 * a")) is None        # int -> float literal
     assert same_shape_child(p, parents[0].replace("tuned 2 times", "tuned 3 times")) is None   # comment digit
     assert same_shape_child(p, parents[0].replace("score += 17", "score -= 17")) is None  # operator
+    # what the compile path rejects is refused too: a leading-zero int (SyntaxError), an int beyond int64
+    assert same_shape_child(p, parents[0].replace("17 * a", "017 * a")) is None
+    assert try_compile(parents[0].replace("17 * a", "017 * a"))[0] is None
+    assert same_shape_child(p, parents[0].replace("17 * a", "99999999999999999999 * a")) is None

@@ -341,24 +341,80 @@ def test_runaway_loop_raises_budget():
         assert list(emu) == [-101] * 16
 
 
-def test_gpu_list_loops_equal_cpu_vm():
+def test_exhausted_budget_stays_exhausted():
+    """Lanes that were outside EXEC when the budget ran out (here: the other
+    branch of an if) must not get a wrapped ~2^32 budget for a later loop:
+    they raise BUDGET within the cap like every other lane."""
+    m = ce.native()
+    p = compile_policy("def priority_function(pod, node):\n    x = 0\n"
+                       "    if node.cpu_milli_left % 2 == 0:\n        while x >= 0:\n"
+                       "            x = (x + 1) % 7\n    y = 0\n    for i in range(5000):\n"
+                       "        y += 1\n    return x + y\n")
+    rng = random.Random(11)
+    for _ in range(20):
+        node, gl, gt, gm, pod = _random_event(rng)
+        even = [node[6 * j] % 2 == 0 for j in range(16)]
+        if any(even) and not all(even):
+            break
+    else:
+        raise AssertionError("no mixed event")
+    kc = constant_block(p, 1 << 10).tolist()
+    emu = m.gcn_emu_event(p.code, list(map(int, p.ctag)), gcnjit.literal_mask(p).tolist(),
+                          list(map(int, p.iconst)), list(map(float, p.fconst)), kc, node, gl, gt, gm, pod)
+    assert list(emu) == [-101] * 16
+    # with a budget above both loops' needs, the odd lanes finish
+    p2 = compile_policy(p.source.replace("while x >= 0", "while x >= 0 and x < 3"))
+    kc = constant_block(p2, 1 << 20).tolist()
+    emu = m.gcn_emu_event(p2.code, list(map(int, p2.ctag)), gcnjit.literal_mask(p2).tolist(),
+                          list(map(int, p2.iconst)), list(map(float, p2.fconst)), kc, node, gl, gt, gm, pod)
+    assert list(emu) == [5003 if e else 5000 for e in even]
+
+
+@pytest.mark.parametrize("unroll", [True, False])
+def test_gpu_list_loops_equal_cpu_vm(unroll):
     """The compiler's GPU-list loop skeletons (bytecode LOOP_INDEX): unchecked
     gets, 32-bit counters and, for node.gpus, fields read with the counter in
     GPR index mode -- and the cases that must not take that path (outer
-    element in an inner loop, after the loop, reassigned, other lists)."""
-    _check_bodies(GPU_LOOP_BODIES, seed=21)
+    element in an inner loop, after the loop, reassigned, other lists); node.gpus
+    loops both unrolled (the default) and rolled."""
+    m = ce.native()
+    old = m.gcn_set_unroll_cap(0 if not unroll else 1600)
+    try:
+        _check_bodies(GPU_LOOP_BODIES, seed=21)
+    finally:
+        m.gcn_set_unroll_cap(old)
+
+
+@have_mc
+def _disassemble(code):
+    txt = " ".join(f"0x{b:02x}" for b in code.words.tobytes())
+    return subprocess.run([MC, "-disassemble", "-triple=amdgcn-amd-amdhsa", "-mcpu=gfx950"], input=txt,
+                          capture_output=True, text=True).stdout
 
 
 @have_mc
 def test_node_gpus_loop_indexes_fields_uniformly():
+    """Rolled (unrolling off): the counter-indexed field read in GPR index mode;
+    unrolled (the default): eight guarded copies, each reading its GPU's field
+    straight from the argument VGPR, no counter, no back edge."""
+    m = ce.native()
     p = compile_policy("def priority_function(pod, node):\n    " + GPU_LOOP_BODIES[0] + "\n")
-    code, why = gcnjit.compile_program(p)
+    old = m.gcn_set_unroll_cap(0)
+    try:
+        code, why = gcnjit.compile_program(p)
+    finally:
+        m.gcn_set_unroll_cap(old)
     assert code is not None, why
-    txt = " ".join(f"0x{b:02x}" for b in code.words.tobytes())
-    dis = subprocess.run([MC, "-disassemble", "-triple=amdgcn-amd-amdhsa", "-mcpu=gfx950"], input=txt,
-                         capture_output=True, text=True).stdout
+    dis = _disassemble(code)
     assert dis.count("s_set_gpr_idx_on") == 1 and dis.count("s_set_gpr_idx_off") == 1
     assert "v_cmp_lt_i32" in dis
+    code, why = gcnjit.compile_program(p)
+    assert code is not None, why
+    assert code.info["unrolled"] == 1
+    dis = _disassemble(code)
+    assert "s_set_gpr_idx_on" not in dis and "s_cbranch_scc0" not in dis   # (no budget charge: no back edge)
+    for k in range(8):
+        assert f"v_mov_b32_e32 v{{}}, v{5 + k}".split("{}")[1] in dis
 
 
 def test_evolved_population_compiles_natively():

@@ -55,6 +55,8 @@ def main():
     ap.add_argument("--programs", type=int, default=48)
     ap.add_argument("--tier", default="auto", choices=["auto", "baseline", "llvm"],
                     help="JIT tier of the programs (ops/jit.py)")
+    ap.add_argument("--probes", action="store_true", help="also: the call-cost probes of tools/call_probes.py")
+    ap.add_argument("--only-probes", action="store_true", help="only the call-cost probes (and the population set)")
     ap.add_argument("--ck", default="", help="also: children of this evolved population (tools/population_bench.py)")
     a = ap.parse_args()
     from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
@@ -69,8 +71,14 @@ def main():
             # every argument once, one with four libm calls
             "all_args": [compile_policy(_ALL_ARGS)],
             "pow4": [compile_policy(_POW4)]}
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    if a.only_probes:
+        sets = {}
+    if a.probes or a.only_probes:
+        from call_probes import probe_sources
+        for k, src in probe_sources().items():
+            sets["probe_" + k] = [compile_policy(src)]
     if a.ck:
-        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
         from population_bench import _programs
         sets["population"] = _programs(a.ck, a.programs, 7)
     for name, progs in sets.items():

@@ -111,6 +111,8 @@ def child(args) -> None:
                       "first_pass_s": round(first, 3), "cached_s": round(best, 3),
                       "cached_evals_per_s": round(len(progs) / best, 1),
                       "exc_rows": int((tab[:, 10] != 0).sum()), "mean_events": float(tab[:, 8].mean()),
+                      # every replayed program-event (first pass + reps): the PMC summary's denominator
+                      "events": float(tab[:, 8].sum()) * (1 + args.reps),
                       "jit": {k: v for k, v in dev.native_compiler.stats.items()
                               if k in ("baseline_shapes", "rejected", "compile_s", "load_s")}}), flush=True)
 
