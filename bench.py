@@ -84,6 +84,9 @@ def main() -> None:
     ap.add_argument("--novel-large", type=int, default=2048,
                     help="after the timed region: an LLM-scale batch of this many new-shape programs (JIT included, "
                          "chunks over the slots, all in flight at once); reported as `program_path.novel_large` (0: skip)")
+    ap.add_argument("--evolved", type=int, default=2048,
+                    help="children of an evolved population (data/populations, frozen sources) through the "
+                         "native backend, all in flight; reported as `program_path.evolved` (0: skip)")
     ap.add_argument("--time-budget", type=float, default=0.0,
                     help="run generations until this many seconds have passed (instead of --steps); "
                          "steps = generations completed")
@@ -253,6 +256,10 @@ def main() -> None:
     events_total = dist.all_reduce_sum(events[0])
 
     program_path = None
+    jit_init_s = None
+    if ev.device is not None and (args.programs > 0 or args.novel > 0 or args.novel_large > 0 or args.evolved > 0):
+        # first-use JIT initialisation, reported on its own (not in the first batch's jit_s)
+        jit_init_s = round(ev.device.warm_native(), 3)
     if args.programs > 0 and ev.device is not None:
         # the program-for-program comparison with the reference's eval path (outside the timed region)
         from funsearch_kubernetes_simulator_amd.bench.programs import measure_native, mutation_children
@@ -271,6 +278,12 @@ def main() -> None:
             big = measure_novel_large(ev.device, workload, args.novel_large, seed=args.seed + 31 + 1000 * ctx.rank)
             big["vs_baseline"] = round(big["evals_per_s_incl_jit"] / BASELINE_EVALS_PER_S, 2)
             program_path["novel_large"] = big
+        if args.evolved > 0 and args.trace == "default":
+            # the search's late-run workload: children of an evolved population
+            from funsearch_kubernetes_simulator_amd.bench.programs import measure_evolved
+            evo = measure_evolved(ev.device, workload, args.evolved)
+            evo["vs_baseline"] = round(evo["evals_per_s_incl_jit"] / BASELINE_EVALS_PER_S, 2)
+            program_path["evolved"] = evo
 
     per_step = args.islands * args.candidates
     total = per_step * args.steps * ctx.world_size
@@ -326,7 +339,11 @@ def main() -> None:
                                 "divided by the reference's PROGRAM evals/s (15.84, 8 CPU workers); program_path "
                                 "is the program-for-program comparison",
             "program_path": program_path,
+            "program_path_jit_init_s": jit_init_s,
         }
+        if ev.device is not None:
+            from funsearch_kubernetes_simulator_amd.ops.hip_engine import math_selfcheck_info
+            out["device_math"] = math_selfcheck_info()
         if args.time_budget > 0:
             out["time_budget_s"] = args.time_budget
         if args.save_best:

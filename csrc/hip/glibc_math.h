@@ -27,6 +27,29 @@
 // log(x) x > 0 finite, pow(x, y) x > 0 finite, x != 1, y finite non-zero.
 // Status: 0 ok, 1 overflow (glibc returns inf with ERANGE: OverflowError).
 // Underflow returns 0 / a subnormal, as glibc (CPython ignores ERANGE there).
+//
+// ---------------------------------------------------------------------------
+// Provenance and licence.  The algorithms, operation order and polynomial
+// coefficients below are those of glibc's sysdeps/ieee754/dbl-64/e_exp.c,
+// e_log.c and e_pow.c (with e_exp_data.c, e_log_data.c, e_pow_log_data.c),
+// which glibc took from Arm's Optimized Routines:
+//
+//   Copyright (C) 2018-2022 Free Software Foundation, Inc.
+//   This file is part of the GNU C Library.  The GNU C Library is free
+//   software; you can redistribute it and/or modify it under the terms of the
+//   GNU Lesser General Public License as published by the Free Software
+//   Foundation; either version 2.1 of the License, or (at your option) any
+//   later version.  It is distributed WITHOUT ANY WARRANTY; see the GNU
+//   Lesser General Public License (https://www.gnu.org/licenses/) for details.
+//
+//   Copyright (c) 2018, Arm Limited.
+//   SPDX-License-Identifier: MIT (Arm Optimized Routines, exp / log / pow)
+//
+// This is an independent re-implementation for HIP (host and gfx950), written
+// from the algorithm descriptions and checked bit for bit against the host's
+// libm; the data tables are read from the installed libm.so.6 itself
+// (tools/gen_glibc_math_tables.py), not copied from glibc sources.
+// ---------------------------------------------------------------------------
 #pragma once
 
 #include "jit_env.h"

@@ -212,3 +212,114 @@ def measure_novel_large(dev, workload, n: int = 2048, seed: int = 0, compare: in
             "resident_capacity": int(info.get("native_duo_per_cu_last", 0)) * int(info.get("num_cus", 0)),
             "repeat_identical": bool((tab == tab2).all()),
             "compared": int(cmp.sum()), "bit_identical": bool((a[cmp] == b[cmp]).all())}
+
+
+# ---------------------------------------------------------------------------- evolved programs
+#: 2,048 offline-mutation children of the best programs of an evolved steady-state
+#: population (data/populations/config3_steady_r4f_islands.json, tools/population_bench.py
+#: --save-sources): the programs the search evaluates late in a run (long bodies,
+#: ~12 GPU-list loops), frozen so every commit replays the same set
+EVOLVED_SET = "config3_steady_r4f_children2048.json.gz"
+
+
+def save_program_set(path: str, sources) -> None:
+    """Program texts as template bodies where they are template-shaped
+    (gzip JSON; `load_program_set` restores the exact text)."""
+    import gzip
+    import json
+    from ..parallel.dist import program_body
+    items = []
+    for src in sources:
+        body, templ = program_body(src)
+        items.append({"b": body} if templ else {"s": src})
+    with gzip.open(path, "wt", encoding="utf-8") as f:
+        json.dump({"format": "fks-program-set-v1", "programs": items}, f)
+
+
+def load_program_set(path: str) -> List[str]:
+    import gzip
+    import json
+    from ..policy.template import PolicyTemplate
+    with gzip.open(path, "rt", encoding="utf-8") as f:
+        d = json.load(f)
+    return [PolicyTemplate.fill_template(it["b"]) if "b" in it else it["s"] for it in d["programs"]]
+
+
+def _compile_worker(sources):
+    out = []
+    for src in sources:
+        try:
+            out.append(compile_policy(src))
+        except CompileError:
+            out.append(None)
+    return out
+
+
+def evolved_children(n: int = 2048, workers: int = 8) -> List[CompiledPolicy]:
+    """The frozen evolved-population children (EVOLVED_SET), compiled in
+    `workers` spawned processes; device-capable ones, in file order."""
+    import concurrent.futures
+    import multiprocessing
+    import os
+    from .._paths import DATA_DIR
+    srcs = load_program_set(os.path.join(DATA_DIR, "populations", EVOLVED_SET))[:n]
+    if workers > 1 and len(srcs) > 64:
+        parts = [srcs[i::workers] for i in range(workers)]
+        with concurrent.futures.ProcessPoolExecutor(workers, mp_context=multiprocessing.get_context("spawn")) as ex:
+            res = list(ex.map(_compile_worker, parts))
+        progs = [None] * len(srcs)
+        for w, part in enumerate(res):
+            for j, p in enumerate(part):
+                progs[w + j * workers] = p
+    else:
+        progs = _compile_worker(srcs)
+    return [p for p in progs if p is not None and p.device_ok]
+
+
+def measure_evolved(dev, workload, n: int = 2048, compare: int = 128, cpu_threads: int = 0) -> dict:
+    """The evolved-population children (EVOLVED_SET) at LLM-batch scale: split
+    over the device's slots, all in flight at once, JIT included (first pass)
+    and cached (second pass); mean replayed events, exception fraction, and the
+    first `compare` rows checked against the CPU VM."""
+    import numpy as np
+    from ..engine import COLS
+    from ..ops import cpu_engine as ce
+    t_c = time.perf_counter()
+    progs = evolved_children(n)
+    t_compile = time.perf_counter() - t_c
+    n = len(progs)
+    slots = max(1, dev.n_slots)
+    size = -(-n // slots)
+    chunks = [progs[i:i + size] for i in range(0, n, size)]
+    dev.set_options(native_inflight=n)
+    try:
+        t0 = time.perf_counter()
+        batches = [dev.submit_native(s, c) for s, c in enumerate(chunks)]
+        tabs = [dev.wait(s) for s in range(len(chunks))]
+        t1 = time.perf_counter()
+        for s, c in enumerate(chunks):
+            dev.submit_native(s, c)
+        tabs2 = [dev.wait(s) for s in range(len(chunks))]
+        t2 = time.perf_counter()
+    finally:
+        dev.set_options(native_inflight=0)
+    tab, tab2 = np.concatenate(tabs), np.concatenate(tabs2)
+    threads = cpu_threads or ce.default_threads()
+    sub = progs[:compare]
+    vm = ce.simulate_program_batch(workload, sub, threads=threads)
+    skip = (100, 101)
+    exc, vexc = tab[:compare, COLS["exc"]].astype(int), vm[:, COLS["exc"]].astype(int)
+    cmp = ~np.isin(exc, skip) & ~np.isin(vexc, skip)
+    a, b = tab[:compare], vm
+    if not dev.options.get("trace_hash", True):
+        a, b = a[:, :COLS["trace_hash_hi"]], b[:, :COLS["trace_hash_hi"]]
+    st = dev.native_compiler.stats
+    return {"programs": n, "source": f"data/populations/{EVOLVED_SET}", "bytecode_compile_s": round(t_compile, 3),
+            "native": int(sum(int(b.ok.sum()) for b in batches)),
+            "new_shapes": int(sum(int(b.compiled) for b in batches)),
+            "evals_per_s_incl_jit": round(n / (t1 - t0), 1), "evals_per_s_cached": round(n / (t2 - t1), 1),
+            "mean_events": round(float(tab[:, COLS["n_events"]].mean()), 1),
+            "exception_fraction": round(float((tab[:, COLS["exc"]] != 0).mean()), 4),
+            "repeat_identical": bool((tab == tab2).all()),
+            "compared_vs_cpu_vm": int(cmp.sum()), "bit_identical": bool((a[cmp] == b[cmp]).all()),
+            "baseline_shapes_total": int(st.get("baseline_shapes", 0))}

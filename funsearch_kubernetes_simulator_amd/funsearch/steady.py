@@ -158,6 +158,7 @@ class SteadyStats:
     polish_evals: int = 0            # their device evaluations (not children)
     polish_improved: int = 0         # polished champions re-entered as children
     polish_idle: int = 0             # of the polish batches: run on a slot that would have idled
+    coupled: int = 0                 # family-coupler champions offered to the islands
     inflight_sum: float = 0.0        # programs in flight x seconds
     inflight_n: float = 0.0          # seconds observed
     history: List[dict] = field(default_factory=list)
@@ -195,6 +196,8 @@ class SteadyStateSearch:
         # host fallbacks run at low priority: the producers come first
         fs.evaluator.fallback_nice = 15
         n_slots = dev.n_slots if dev is not None else 1
+        if getattr(fs, "coupler", None) is not None:
+            n_slots = max(1, n_slots - 1)   # the last slot is the family coupler's
         self.slots = max(1, min(int(slots or n_slots), n_slots))
         if dev is not None:
             # the two-wave kernel sizes its LDS heap top so that every slot's batch
@@ -347,6 +350,15 @@ class SteadyStateSearch:
         polish_next = [start_gen + self.polish_every] * k   # generation of each island's next polish
         staged: collections.deque = collections.deque()   # (batch items, future of prepare_compiled, polish job)
         stager = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="fks-stage")
+        # family coupler (funsearch/coupling.py, `coupling.every` > 0): device family
+        # search rounds on a worker thread and the evaluator's last HIP slot, next to
+        # the program batches; each round's improved champions enter the islands as
+        # program text (re-scored exactly through the normal program path)
+        coupler = fs.coupler
+        cpl_exec = (concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="fks-couple")
+                    if coupler is not None else None)
+        cpl_fut = None
+        cpl_next = start_gen
         ready: List[tuple] = []          # produced children waiting for a batch
         batches: List[Optional[_Batch]] = [None] * self.slots
         # children requested per island: production stops at the island's target
@@ -394,7 +406,7 @@ class SteadyStateSearch:
                             if prog is None:     # no program: counts toward the island's generation
                                 self.stats.rejected += 1
                                 if code is not None:
-                                    fs.evaluator.stats["compile_errors"] += 1
+                                    fs.evaluator._bump("compile_errors")
                                 merged[isl] += 1
                                 continue
                             ready.append((isl, code, prog))
@@ -510,10 +522,14 @@ class SteadyStateSearch:
                     self.stats.batches += 1
                     fs.evaluations += len(b.items)
                     inflight = sum(len(x.items) for x in batches if x is not None)
+                    ev_n = [r.n_events for r in results if r is not None and r.engine == "hip-native"]
                     log.write(kind="steady_batch", rank=ctx.rank, slot=si, programs=len(b.items),
                               new_shapes=b.new_shapes, jit_s=round(b.jit_s, 4),
                               device_s=round(t_done - b.t_launch, 4), inflight_after=inflight,
-                              queued=len(ready))
+                              queued=len(ready),
+                              # replayed events per program: the batch's mean and its longest (tail)
+                              events_mean=round(sum(ev_n) / len(ev_n), 1) if ev_n else 0,
+                              events_max=max(ev_n) if ev_n else 0)
                     progressed = True
                 gens = self._gen_of(merged)
                 g_min = start_gen + min(gens)
@@ -532,6 +548,17 @@ class SteadyStateSearch:
                         progressed = True
                     if chan.stopping:
                         stop = True
+                # 5b) family coupling: start a round when one is due, merge a finished one
+                if coupler is not None:
+                    if cpl_fut is not None and cpl_fut.done():
+                        for rec in cpl_fut.result():
+                            fs.inject_coupled(rec)
+                            self.stats.coupled += 1
+                        cpl_fut = None
+                        progressed = True
+                    if cpl_fut is None and not stop and g_min >= cpl_next:
+                        cpl_fut = cpl_exec.submit(fs.run_coupling)
+                        cpl_next = g_min + coupler.every
                 global_best = max(chan.best_global, fs.best[1])
                 want_stop = want_stop or global_best >= threshold or bool(wall_s and time.time() - t_start > wall_s)
                 if want_stop and not chan.active:
@@ -557,7 +584,7 @@ class SteadyStateSearch:
                 # 7) done?  (every child merged, or stopping; then every agreed gather finished)
                 all_launched = all(requested[i] >= target_children[i] for i in range(k))
                 idle = (not inflight_tasks and all(b is None for b in batches) and not fallbacks
-                        and not staged)
+                        and not staged and cpl_fut is None)
                 if idle and (stop or (all_launched and not ready)):
                     ready.clear()
                     due = chan.every and chan.next is not None and (
@@ -572,6 +599,8 @@ class SteadyStateSearch:
         finally:
             pool.shutdown(wait=False, cancel_futures=True)
             stager.shutdown(wait=True, cancel_futures=True)
+            if cpl_exec is not None:
+                cpl_exec.shutdown(wait=True, cancel_futures=True)
             for _, fut, _pj in staged:   # compiled but never launched: give the modules back
                 if fut.done() and not fut.cancelled() and fut.exception() is None:
                     ev.discard_prepared(fut.result())
@@ -604,6 +633,8 @@ class SteadyStateSearch:
                    native_fraction=round(st.native / max(1, st.evaluations), 4), host_fallback=st.fallback,
                    shed=st.shed, abandoned=st.abandoned, polish_batches=st.polish_batches,
                    polish_evals=st.polish_evals, polish_improved=st.polish_improved, polish_idle=st.polish_idle,
+                   coupled=st.coupled,
+                   coupler_evals=(fs.coupler.evaluated if fs.coupler is not None else 0),
                    all_evals_per_s=round((st.evaluations + st.polish_evals) / wall, 2),
                    inflight=inflight, inflight_mean=round(st.inflight_sum / max(1e-9, st.inflight_n), 1),
                    resident_capacity=capacity,

@@ -55,6 +55,16 @@ def native():
 _MATH_OK: Optional[bool] = None
 
 
+_MATH_INFO: Dict[str, object] = {}
+
+
+def math_selfcheck_info() -> dict:
+    """Outcome of `glibc_math_ok` (which math path this process uses), for logs
+    and the bench record."""
+    glibc_math_ok()
+    return dict(_MATH_INFO, ok=bool(_MATH_OK))
+
+
 def glibc_math_ok(n: int = 200_000) -> bool:
     """The device's exp / log / pow (csrc/hip/glibc_math.h, glibc's own FMA
     algorithms and tables) equal this host's libm -- the one CPython calls --
@@ -81,6 +91,9 @@ def glibc_math_ok(n: int = 200_000) -> bool:
             warnings.warn(f"device exp/log/pow differ from this host's libm ({r}); programs using them run on "
                           "the CPU VM", RuntimeWarning)
         _MATH_OK = bool(ok)
+        _MATH_INFO.update(checked_per_function=n, mismatches={k: int(r[k]) for k in ("exp", "log", "pow")},
+                          device_math=("glibc-exact (device exp/log/pow == host libm)" if ok else
+                                       "host fallback (programs using exp/log/pow replay on the CPU VM)"))
     return _MATH_OK
 
 
@@ -259,6 +272,22 @@ class DeviceEvaluator:
 
     def info(self) -> dict:
         return dict(self._eng.info())
+
+    def warm_native(self) -> float:
+        """First-use initialisation of the native program path -- the JIT's
+        code-object skeleton load and layout probe, the first module load and
+        launch -- done once, outside any measured batch; returns its seconds
+        (0 when already done)."""
+        if getattr(self, "_warm_s", None) is not None:
+            return 0.0
+        from ..models.library import reference_policies
+        from ..policy.compiler import compile_policy
+        t0 = time.perf_counter()
+        prog = compile_policy(reference_policies()["first_fit"])
+        self.submit_native(0, [prog])
+        self.wait(0)
+        self._warm_s = time.perf_counter() - t0
+        return self._warm_s
 
     # -- natively compiled programs (policy/native_codegen.py, ops/jit.py) ------------------
     @property

@@ -349,8 +349,13 @@ class NativeCompiler:
         self._seq = 0
         # bounded module lifetime: beyond this many live modules the least recently
         # used ones that no batch in flight calls into are unloaded (their shapes are
-        # recompiled if they come back -- the baseline tier takes ~0.2 ms a shape)
-        self.max_modules = int(os.environ.get("FKS_JIT_MAX_MODULES", "256"))
+        # recompiled if they come back -- the baseline tier takes ~0.2 ms a shape).
+        # A module is one batch's new shapes (~512 programs, a few MB of code), so
+        # 2048 hold a long steady-state run in HBM: a 200 s config-3 run loads ~1,100
+        # (round 5), and most of a retired module's shapes were one-off children --
+        # `recompiled_shapes` counts the evicted shapes that did come back
+        self.max_modules = int(os.environ.get("FKS_JIT_MAX_MODULES", "2048"))
+        self._evicted: set = set()     # hashes of evicted shape keys (recompile accounting)
         self._lock = threading.Lock()
         self._inflight: Dict[str, threading.Event] = {}
         self._procs = threading.BoundedSemaphore(self.workers)
@@ -367,7 +372,7 @@ class NativeCompiler:
                       "baseline_shapes": 0, "llvm_shapes": 0, "baseline_s": 0.0, "llvm_s": 0.0, "load_s": 0.0,
                       "disk_hits": 0, "tierup_queued": 0, "tierup_done": 0, "tierup_s": 0.0,
                       "live_modules": 0, "max_live_modules": 0, "retired_modules": 0, "evicted_shapes": 0,
-                      "unload_s": 0.0}
+                      "recompiled_shapes": 0, "unload_s": 0.0}
         # tier-up (auto tier): a baseline shape used in this many batches is
         # recompiled by the LLVM tier in the background (its code runs ~1.3x
         # faster on the device) and swapped in when ready; never on the
@@ -517,6 +522,7 @@ class NativeCompiler:
                         self._tier_of.pop(k, None)
                         self._uses.pop(k, None)
                         self.stats["evicted_shapes"] += 1
+                        self._evicted.add(hash(k))
                 victims.append(rec)
             self.stats["retired_modules"] += len(victims)
             self.stats["live_modules"] = len(self._modules)
@@ -627,6 +633,8 @@ class NativeCompiler:
                 self.stats["load_s"] += t2 - t1
                 self.stats["probed_loads"] = self.stats.get("probed_loads", 0) + int(mod.probed)
                 for j, k in enumerate(keys[lo:hi]):
+                    if self._evicted and hash(k) in self._evicted:
+                        self.stats["recompiled_shapes"] += 1
                     self._map_shape(k, mi, j, int(mod.pointers[j]))
                     self._tier_of[k] = "baseline"
                     self._uses.pop(k, None)

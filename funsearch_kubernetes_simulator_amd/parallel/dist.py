@@ -31,22 +31,34 @@ class DistContext:
 
     @property
     def distributed(self) -> bool:
+        """Several ranks (the island search's multi-rank semantics)."""
         return self.world_size > 1
+
+    @property
+    def group(self) -> bool:
+        """A process group exists: the collective helpers go through it (RCCL /
+        gloo) -- also for a one-rank group (FKS_DIST_GROUP=1), which exercises
+        the collective path on a single GPU with results equal to the local one."""
+        return self.backend != "none"
 
 
 _ctx: Optional[DistContext] = None
 
 
-def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = None) -> DistContext:
+def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = None,
+                     force_group: Optional[bool] = None) -> DistContext:
     """Initialise from torchrun-style env vars (RANK/WORLD_SIZE/LOCAL_RANK,
-    MASTER_ADDR defaults to 127.0.0.1).  Single-process runs need nothing."""
+    MASTER_ADDR defaults to 127.0.0.1).  Single-process runs need nothing,
+    unless `force_group` (or FKS_DIST_GROUP=1) asks for a one-rank group."""
     global _ctx
     if _ctx is not None:
         return _ctx
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    if world <= 1:
+    if force_group is None:
+        force_group = os.environ.get("FKS_DIST_GROUP", "0") == "1"
+    if world <= 1 and not force_group:
         _ctx = DistContext(rank=0, world_size=1, local_rank=local, backend="none")
         return _ctx
     import torch
@@ -91,7 +103,7 @@ def context() -> DistContext:
 
 def barrier() -> None:
     ctx = context()
-    if ctx.distributed:
+    if ctx.group:
         import torch.distributed as dist
         if ctx.backend == "nccl":
             import torch
@@ -104,7 +116,7 @@ def barrier() -> None:
 def all_gather_array(x: np.ndarray) -> np.ndarray:
     """[world, *x.shape]: every rank's array (same shape/dtype on all ranks)."""
     ctx = context()
-    if not ctx.distributed:
+    if not ctx.group:
         return x[None].copy()
     import torch
     import torch.distributed as dist
@@ -134,7 +146,7 @@ def all_gather_array_async(x: np.ndarray) -> PendingGather:
     """Start an all-gather and return at once (RCCL runs it on its own stream
     while the caller keeps the GPU busy); the result is read with `.wait()`."""
     ctx = context()
-    if not ctx.distributed:
+    if not ctx.group:
         return PendingGather(ready=x[None].copy())
     import torch
     import torch.distributed as dist
@@ -146,7 +158,7 @@ def all_gather_array_async(x: np.ndarray) -> PendingGather:
 
 def all_reduce_max(v: float) -> float:
     ctx = context()
-    if not ctx.distributed:
+    if not ctx.group:
         return float(v)
     import torch
     import torch.distributed as dist
@@ -157,7 +169,7 @@ def all_reduce_max(v: float) -> float:
 
 def all_reduce_sum(v: float) -> float:
     ctx = context()
-    if not ctx.distributed:
+    if not ctx.group:
         return float(v)
     import torch
     import torch.distributed as dist
@@ -175,7 +187,7 @@ def degrade_to_local(reason: str = "") -> DistContext:
     `IslandFunSearch.load_elastic`)."""
     global _ctx
     ctx = context()
-    if ctx.distributed:
+    if ctx.group:
         import torch.distributed as dist
         try:
             if dist.is_initialized():
@@ -189,7 +201,7 @@ def degrade_to_local(reason: str = "") -> DistContext:
 
 def shutdown() -> None:
     global _ctx
-    if _ctx is not None and _ctx.distributed:
+    if _ctx is not None and _ctx.group:
         import torch.distributed as dist
         if dist.is_initialized():
             dist.destroy_process_group()
@@ -202,7 +214,7 @@ def all_gather_bytes(payload: bytes):
     collectives; used where a record must never be truncated, e.g. the
     final cross-rank champion)."""
     ctx = context()
-    if not ctx.distributed:
+    if not ctx.group:
         return [bytes(payload)]
     n = all_gather_array(np.array([len(payload)], dtype=np.int64)).reshape(-1)
     buf = np.zeros(max(1, int(n.max())), dtype=np.uint8)

@@ -22,8 +22,9 @@ def _compiler(max_modules):
     nc._modules, nc._shapes, nc._ptr, nc._tier_of, nc._uses = {}, {}, {}, {}, {}
     nc._next_mod = nc._seq = 0
     nc.max_modules = max_modules
+    nc._evicted = set()
     nc.stats = {"modules": 0, "live_modules": 0, "max_live_modules": 0, "retired_modules": 0,
-                "evicted_shapes": 0, "unload_s": 0.0}
+                "evicted_shapes": 0, "recompiled_shapes": 0, "unload_s": 0.0}
     return nc
 
 
@@ -57,6 +58,7 @@ def test_lru_retirement_skips_modules_in_flight():
     assert mods[1][1].unloaded and mods[2][1].unloaded and not mods[0][1].unloaded
     assert "s1a" not in nc._shapes and "s2b" not in nc._shapes and "s0a" in nc._shapes
     assert nc.stats["evicted_shapes"] == 4
+    assert hash("s1a") in nc._evicted and hash("s0a") not in nc._evicted   # recompile accounting
     nc.release([mods[0][0]])
     assert not mods[0][1].unloaded          # at the cap: nothing more to retire
 

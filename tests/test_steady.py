@@ -189,3 +189,24 @@ def test_steady_idle_slot_polish(tmp_path):
     assert st.evaluations == st.produced - st.rejected + st.polish_improved
     fin = [json.loads(l) for l in open(tmp_path / "log.jsonl") if '"steady_final"' in l][-1]
     assert fin["polish_idle"] == st.polish_idle and fin["all_evals_per_s"] >= fin["evals_per_s"]
+
+
+def test_steady_with_family_coupler(tmp_path):
+    """`coupling.every` in steady mode: family-search rounds run on a worker
+    thread and the evaluator's last slot (the program batches use the others);
+    their champions enter the islands as exactly re-scored program text."""
+    from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
+    cfg = _cfg(tmp_path, gens=4)
+    cfg["coupling"] = {"every": 1, "generations": 1, "candidates": 64, "elite": 8,
+                       "families": ["random_linear"], "seed": 1}
+    fs = IslandFunSearch(cfg)
+    code, score = fs.run(4)
+    assert fs.coupler is not None and fs.coupler.rounds >= 1
+    recs = [json.loads(l) for l in open(tmp_path / "log.jsonl")]
+    coupled = [r for r in recs if r["kind"] == "coupling"]
+    assert coupled and all(r["family"] == "random_linear" for r in coupled)
+    final = [r for r in recs if r["kind"] == "steady_final"][-1]
+    assert final["coupled"] == len(coupled) and final["coupler_evals"] >= 64
+    # the exported program re-scores to the family score it was exported with
+    best = max(coupled, key=lambda r: r["score"])
+    assert best["score"] == best["family_score"]

@@ -359,3 +359,33 @@ def test_device_workload_requires_one_gpu_model_per_node(default_workload):
     w.cluster.gpu_milli_total[a + 1] = 500
     with pytest.raises(UnsupportedWorkload, match="milli totals"):
         prepare_device_workload(w)
+
+
+def test_one_rank_group_collectives_equal_local(tmp_path):
+    """FKS_DIST_GROUP=1 creates a one-rank process group (gloo here, RCCL on the
+    GPU box: tests/test_gpu_rccl.py); the collective helpers then go through it
+    and return what the local path returns."""
+    import subprocess
+    import sys
+    script = tmp_path / "one.py"
+    script.write_text(
+        "import json, numpy as np\n"
+        "from funsearch_kubernetes_simulator_amd.parallel import dist\n"
+        "ctx = dist.init_distributed(backend='gloo', use_gpu=False, force_group=True)\n"
+        "x = np.arange(12.0).reshape(3, 4)\n"
+        "h = dist.all_gather_array_async(x)\n"
+        "g = h.wait()\n"
+        "out = {'group': ctx.group, 'distributed': ctx.distributed, 'backend': ctx.backend,\n"
+        "       'gather': bool(np.array_equal(g, x[None])), 'bytes': dist.all_gather_bytes(b'abc') == [b'abc'],\n"
+        "       'max': dist.all_reduce_max(2.5), 'sum': dist.all_reduce_sum(1.5)}\n"
+        "dist.barrier()\n"
+        "dist.shutdown()\n"
+        "print(json.dumps(out))\n")
+    env = dict(os.environ, PYTHONPATH=os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+               WORLD_SIZE="1", RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29400 + os.getpid() % 300),
+               GLOO_SOCKET_IFNAME="lo")
+    r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out == {"group": True, "distributed": False, "backend": "gloo", "gather": True, "bytes": True,
+                   "max": 2.5, "sum": 1.5}

@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--programs", type=int, default=48)
     ap.add_argument("--tier", default="auto", choices=["auto", "baseline", "llvm"],
                     help="JIT tier of the programs (ops/jit.py)")
+    ap.add_argument("--no-evolved", action="store_true", help="skip the evolved-population set")
     ap.add_argument("--probes", action="store_true", help="also: the call-cost probes of tools/call_probes.py")
     ap.add_argument("--only-probes", action="store_true", help="only the call-cost probes (and the population set)")
     ap.add_argument("--ck", default="", help="also: children of this evolved population (tools/population_bench.py)")
@@ -78,6 +79,10 @@ def main():
         from call_probes import probe_sources
         for k, src in probe_sources().items():
             sets["probe_" + k] = [compile_policy(src)]
+    if not a.no_evolved:
+        # the frozen evolved-population children (bench.py program_path.evolved)
+        from funsearch_kubernetes_simulator_amd.bench.programs import evolved_children
+        sets["evolved"] = evolved_children(a.programs, workers=1)
     if a.ck:
         from population_bench import _programs
         sets["population"] = _programs(a.ck, a.programs, 7)

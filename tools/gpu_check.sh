@@ -11,7 +11,8 @@
 #   smoke               __graft_entry__.smoke()
 #   bench[=ARGS]        python bench.py ARGS            -> bench.json
 #   prof[=ARGS]         rocprofv3 --kernel-trace --stats of bench.py ARGS -> prof/
-#   steady=SECS[:CFG]   steady-state program islands for SECS seconds (CFG: configs/config3_steady.json)
+#   steady=SECS[:CFG[:GENS]]  steady-state program islands for SECS seconds (CFG: configs/config3_steady.json;
+#                       GENS: generation target, so a long run keeps producing children)
 #   native=ARGS         tools/native_bench.py ARGS      -> native.jsonl
 #   c5[=ARGS]           config-5 bench (synthetic 65,536 pods / 256 nodes) -> c5.json
 #   pmc=COUNTERS[:ARGS] one rocprofv3 --pmc pass over bench.py ARGS (counters comma-separated)
@@ -51,8 +52,14 @@ for step in "$@"; do
     steady)
       secs=${val%%:*}
       cfg=configs/config3_steady.json
-      [ "$secs" != "$val" ] && cfg=${val#*:}
-      timeout -k 10 $((secs + 240)) python -u -m funsearch_kubernetes_simulator_amd.funsearch --config "$cfg" \
+      gens=""
+      if [ "$secs" != "$val" ]; then
+        rest=${val#*:}
+        cfg=${rest%%:*}
+        [ "$cfg" != "$rest" ] && gens="--generations ${rest#*:}"
+        [ -z "$cfg" ] && cfg=configs/config3_steady.json
+      fi
+      timeout -k 10 $((secs + 240)) python -u -m funsearch_kubernetes_simulator_amd.funsearch --config "$cfg" $gens \
         --verbose --wall-s "$secs" --save "$O/top5.json" --checkpoint-dir "$O/ck" --metrics-log "$O/metrics.jsonl" \
         > "$O/steady.log" 2>&1 || die steady "$O/steady.log"
       grep steady_final "$O/steady.log" | cut -c1-600 ;;

@@ -33,7 +33,12 @@ def _programs_from(sources: str, n: int):
     generation changes across commits)."""
     from funsearch_kubernetes_simulator_amd.policy.compiler import try_compile
     out = []
-    for src in json.load(open(sources)):
+    if sources.endswith(".gz"):
+        from funsearch_kubernetes_simulator_amd.bench.programs import load_program_set
+        srcs = load_program_set(sources)
+    else:
+        srcs = json.load(open(sources))
+    for src in srcs:
         p, _ = try_compile(src)
         if p is not None and p.device_ok:
             out.append(p)
@@ -119,7 +124,7 @@ def child(args) -> None:
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--ck", required=True)
+    ap.add_argument("--ck", default="data/populations/config3_steady_r4f_islands.json")
     ap.add_argument("--children", type=int, default=2048)
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--reps", type=int, default=2)

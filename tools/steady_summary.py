@@ -43,6 +43,29 @@ def main() -> None:
               f"phases {ph} load_s {r.get('jit', {}).get('load_s')} busy {r.get('device_busy')}")
     if last is not None:
         print(json.dumps(last))
+    # steady_batch records by quintile of the run: device seconds per batch
+    # (child batches only), the ready queue, and the replayed events per program
+    bs = []
+    for line in open(path):
+        if '"steady_batch"' not in line:
+            continue
+        try:
+            r = json.loads(line.strip())
+        except ValueError:
+            continue
+        bs.append(r)
+    if bs:
+        q = max(1, len(bs) // 5)
+        print("# steady_batch quintiles: batches, device_s mean, queued mean, events mean / max per program")
+        for i in range(5):
+            part = bs[i * q:(i + 1) * q] if i < 4 else bs[4 * q:]
+            if not part:
+                continue
+            dm = sum(r["device_s"] for r in part) / len(part)
+            qm = sum(r.get("queued", 0) for r in part) / len(part)
+            em = sum(r.get("events_mean", 0) for r in part) / len(part)
+            ex = max(r.get("events_max", 0) for r in part)
+            print(f"Q{i + 1}: {len(part):4d} batches  device_s {dm:7.3f}  queued {qm:6.1f}  events mean {em:9.0f} max {ex}")
 
 
 if __name__ == "__main__":
