@@ -66,6 +66,11 @@ class IslandFunSearch:
         # one lineage through migration
         self.reset_every = int(isl.get("reset_every", 0))
         self.reset_fraction = float(isl.get("reset_fraction", 0.5))
+        # reset_diverse: a reset island restarts from the best program of the
+        # surviving islands' populations that is NOT similar (the dedup ratio) to
+        # any program another island already leads with -- so resets keep
+        # lineages apart instead of cloning one island's champion
+        self.reset_diverse = bool(isl.get("reset_diverse", False))
         # migrants enter only if no equal-or-better member is too similar
         # (the island's own dedup rule) and they beat its worst member
         self.migrant_dedup = bool(isl.get("migrant_dedup", False))
@@ -308,9 +313,26 @@ class IslandFunSearch:
             return []
         order = sorted(range(k), key=lambda i: (self.islands[i].best_score, -i))
         weak, keep = order[:n], order[n:]
+        if self.reset_diverse:
+            from .search import _similar_at_least
+            thr = self.islands[0].similarity_threshold
+            leads = [self.islands[j].best_policy.strip() for j in keep if self.islands[j].best_policy]
+            pool = sorted({(c, sc) for j in keep for c, sc in self.islands[j].population}, key=lambda x: -x[1])
         for i in weak:
-            src = self.islands[self._reset_rng.choice(keep)]
             s = self.islands[i]
+            pick = None
+            if self.reset_diverse:
+                for c, sc in pool:
+                    cs = c.strip()
+                    if not any(_similar_at_least(cs, t, thr) for t in leads):
+                        pick = (c, sc)
+                        leads.append(cs)
+                        break
+            if pick is not None:
+                s.population = [pick]
+                s.best_policy, s.best_score = pick
+                continue
+            src = self.islands[self._reset_rng.choice(keep)]
             s.population = [(src.best_policy, src.best_score)] if src.best_policy else list(src.population[:1])
             s.best_policy, s.best_score = src.best_policy, src.best_score
         self.resets += 1

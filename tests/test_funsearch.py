@@ -551,6 +551,30 @@ def test_island_reset_and_migrant_dedup(tmp_path):
     assert 0.44 in [sc for _, sc in s.population]
 
 
+def test_diverse_island_reset_keeps_lineages_apart(tmp_path):
+    """islands.reset_diverse: a reset island restarts from the best surviving
+    program that is not similar to any program another island leads with."""
+    from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
+    cfg = _cfg(tmp_path)
+    cfg["islands"] = {"per_rank": 4, "migrate_every": 0, "migrants": 1, "reset_every": 1, "reset_diverse": True}
+    fs = IslandFunSearch(cfg)
+    fs.initialize()
+    lead = "def priority_function(pod, node):\n    return 3 * node.cpu_milli_left + 3\n"
+    near = lead.replace("3 *", "4 *")                                   # similar to the lead
+    other = "def priority_function(pod, node):\n    return node.memory_mib_left // 7 - pod.cpu_milli\n"
+    weakp = [f"def priority_function(pod, node):\n    return {k}\n" for k in range(2)]
+    for i, s in enumerate(fs.islands):
+        s.population = [(weakp[i], 0.30)] if i < 2 else [(lead, 0.50), (near, 0.49), (other, 0.45)]
+        s.best_policy, s.best_score = s.population[0]
+    weak = fs.reset_weak_islands()
+    assert sorted(weak) == [0, 1]
+    # the lead (0.50) and its near copy (0.49) are taken by / similar to island 2-3's lead:
+    # the first reset island gets `other`; nothing dissimilar is left for the second one,
+    # which falls back to a survivor's best
+    assert fs.islands[weak[0]].best_policy == other
+    assert fs.islands[weak[1]].best_policy == lead
+
+
 def test_mutator_library_terms_compile_for_the_device():
     """Every term and feature the offline mutator can insert passes the
     sandbox and compiles to device bytecode (a term that does not would only

@@ -13,6 +13,8 @@
 #   prof[=ARGS]         rocprofv3 --kernel-trace --stats of bench.py ARGS -> prof/
 #   steady=SECS[:CFG[:GENS]]  steady-state program islands for SECS seconds (CFG: configs/config3_steady.json;
 #                       GENS: generation target, so a long run keeps producing children)
+#   rccl[=ARGS]         tools/rccl_check.py (default --steady-s 0: no producer processes under the profiler)
+#                       under rocprofv3 --kernel-trace --stats -> rccl.log, rccl_prof/
 #   native=ARGS         tools/native_bench.py ARGS      -> native.jsonl
 #   c5[=ARGS]           config-5 bench (synthetic 65,536 pods / 256 nodes) -> c5.json
 #   pmc=COUNTERS[:ARGS] one rocprofv3 --pmc pass over bench.py ARGS (counters comma-separated)
@@ -46,7 +48,7 @@ for step in "$@"; do
       timeout -k 10 600 python -u bench.py $val > "$O/bench.json" 2> "$O/bench.err" || die bench "$O/bench.err"
       cut -c1-400 "$O/bench.json" ;;
     prof)
-      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py ${val:---steps 3 --warmup 1 --programs 0 --novel 0 --novel-large 0} \
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py ${val:---steps 3 --warmup 1 --programs 0 --novel 0 --novel-large 0 --evolved 0} \
         > "$O/prof.log" 2>&1 || die prof "$O/prof.log"
       echo "profile written" ;;
     steady)
@@ -63,16 +65,22 @@ for step in "$@"; do
         --verbose --wall-s "$secs" --save "$O/top5.json" --checkpoint-dir "$O/ck" --metrics-log "$O/metrics.jsonl" \
         > "$O/steady.log" 2>&1 || die steady "$O/steady.log"
       grep steady_final "$O/steady.log" | cut -c1-600 ;;
+    rccl)
+      # one-rank RCCL group beside the replay slots, under a kernel trace (RCCL kernels next to the replay kernel)
+      FKS_DIST_GROUP=1 WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29731 \
+        timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/rccl_prof" -o run -- python3 tools/rccl_check.py \
+        ${val:---steady-s 0} > "$O/rccl.log" 2>&1 || die rccl "$O/rccl.log"
+      grep '^{' "$O/rccl.log" | tail -1 | cut -c1-400 ;;
     native)
       timeout -k 10 400 python -u tools/native_bench.py $val > "$O/native.jsonl" 2>&1 || die native "$O/native.jsonl"
       tail -3 "$O/native.jsonl" | cut -c1-300 ;;
     c5)
-      timeout -k 10 600 python -u bench.py --trace synthetic --programs 0 --novel 0 --novel-large 0 ${val:---steps 3 --warmup 1 --candidates 4096} \
+      timeout -k 10 600 python -u bench.py --trace synthetic --programs 0 --novel 0 --novel-large 0 --evolved 0 ${val:---steps 3 --warmup 1 --candidates 4096} \
         > "$O/c5.json" 2> "$O/c5.err" || die c5 "$O/c5.err"
       cut -c1-300 "$O/c5.json" ;;
     pmc)
       ctrs=${val%%:*}
-      args="--steps 2 --warmup 1 --programs 0 --novel 0 --novel-large 0"
+      args="--steps 2 --warmup 1 --programs 0 --novel 0 --novel-large 0 --evolved 0"
       [ "$ctrs" != "$val" ] && args=${val#*:}
       timeout -s KILL 120 rocprofv3 --pmc ${ctrs//,/ } -d "$O/pmc_${ctrs//,/_}" -o run -- python3 bench.py $args \
         > "$O/pmc_${ctrs//,/_}.log" 2>&1 || die pmc "$O/pmc_${ctrs//,/_}.log"

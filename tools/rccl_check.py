@@ -80,6 +80,10 @@ def main() -> None:
     tabs = [dev.wait(s) for s in range(4)]
     ref = ev.device.evaluate_native(progs[:64])
     out["replays_equal_after_collectives"] = bool(np.array_equal(tabs[0][:, :13], ref[:, :13]))
+    if a.steady_s <= 0:
+        dist.shutdown()
+        print(json.dumps(out), flush=True)
+        return
     # a steady config-3 run with RCCL migrations
     from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
     from funsearch_kubernetes_simulator_amd.funsearch.search import load_config
