@@ -116,12 +116,13 @@ struct HostBuf {
   void* p = nullptr;   // host address
   void* d = nullptr;   // device address of the same pages
   size_t cap = 0;
-  void reserve(size_t bytes) {
+  void reserve(size_t bytes, bool coherent = false) {
     if (bytes <= cap) return;
     // geometric growth, as DevBuf: batch sizes vary (native constant blocks)
     bytes = std::max(bytes, cap + cap / 2);
     if (p) HIP_OK(hipHostFree(p));
-    HIP_OK(hipHostMalloc(&p, bytes, hipHostMallocMapped));
+    // coherent (fine-grained): read and written while a kernel runs (the program service)
+    HIP_OK(hipHostMalloc(&p, bytes, hipHostMallocMapped | (coherent ? hipHostMallocCoherent : 0)));
     HIP_OK(hipHostGetDevicePointer(&d, p, 0));
     cap = bytes;
   }
@@ -241,8 +242,10 @@ class DeviceEngine {
     // (csrc/jit) sit on that per-lane stack, next to the runtime library's frames
     {
       size_t st = 0;
-      if (hipDeviceGetLimit(&st, hipLimitStackSize) == hipSuccess && st < kJitStackBytes)
-        (void)hipDeviceSetLimit(hipLimitStackSize, kJitStackBytes);
+      size_t want = kJitStackBytes;
+      if (const char* e = std::getenv("FKS_JIT_STACK_BYTES")) want = (size_t)std::atoll(e);
+      if (hipDeviceGetLimit(&st, hipLimitStackSize) == hipSuccess && st < want)
+        (void)hipDeviceSetLimit(hipLimitStackSize, want);
       if (hipDeviceGetLimit(&st, hipLimitStackSize) == hipSuccess) stack_bytes_ = st;
       (void)hipGetLastError();
     }
@@ -261,6 +264,12 @@ class DeviceEngine {
 
   ~DeviceEngine() {
     (void)hipSetDevice(device_);
+    if (svc_.running) {   // the resident grid drains before anything it reads is freed
+      __atomic_store_n(svc_.ctl.as<uint32_t>() + 1, 1u, __ATOMIC_RELEASE);
+      (void)hipStreamSynchronize(svc_.stream);
+      svc_.running = false;
+    }
+    svc_.release();
     for (auto& s : slots_) {
       if (s->stream) (void)hipStreamSynchronize(s->stream);
       s->release();
@@ -460,6 +469,186 @@ class DeviceEngine {
     HIP_OK(hipStreamSynchronize(s.stream));
     (void)hipFree(d);
     return out;
+  }
+
+  // ---- resident program service (replay_duo.hip.h native_service) ---------------------
+  // A grid of resident two-wave workgroups replays programs from a host ring:
+  // a workgroup whose replay ends takes the next program at once, so no
+  // program's slot waits for a batch's longest replay.  Host memory
+  // (coherent, mapped): published / stop, per-slot fn / koff / constant block,
+  // result rows and done flags; `claimed` lives in HBM.
+  struct Service {
+    hipStream_t stream = nullptr;
+    DevBuf claimed, res, gheap;
+    HostBuf ctl, done, fn, koff, kc, tab;
+    std::vector<uint8_t> busy;   // slot holds an unconsumed program
+    std::vector<uint32_t> held;  // the index published last into each slot
+    uint32_t ring = 0, published = 0;
+    int blocks = 0, T = 0;
+    size_t lds = 0;
+    bool running = false;
+    int64_t launches = 0;
+    void release() {
+      for (DevBuf* b : {&claimed, &res, &gheap}) b->release();
+      for (HostBuf* b : {&ctl, &done, &fn, &koff, &kc, &tab}) b->release();
+      if (stream) (void)hipStreamDestroy(stream);
+      stream = nullptr;
+    }
+  };
+  Service svc_;
+
+  void service_launch(uint32_t first_claim) {
+    Service& v = svc_;
+    __atomic_store_n(v.ctl.as<uint32_t>() + 1, 0u, __ATOMIC_RELEASE);   // stop = 0
+    // claim counter, HBM mirror of `published` (a lower bound: every index below
+    // it is published) and of `stop` (replay_kernels.hip service_claim)
+    uint32_t init[96] = {};
+    init[0] = first_claim;
+    init[32] = first_claim;
+    HIP_OK(hipMemcpyAsync(v.claimed.p, init, sizeof(init), hipMemcpyHostToDevice, v.stream));
+    HIP_OK(hipStreamSynchronize(v.stream));
+    DevWorkload Wl = W_;
+    Wl.heap_top = v.T;
+    const fksk::BuiltinArgs a{Wl, nullptr, nullptr, nullptr, nullptr, v.res.as<DevResult>(), v.gheap.as<uint64_t>(),
+                              nullptr, v.tab.dev<double>()};
+    const RowNativeArgs nat{v.fn.dev<const uint64_t>(), v.kc.dev<const int64_t>(), v.koff.dev<const int32_t>()};
+    // ~57 s of s_sleep(127) polls with nothing published: the grid drains (a lost host)
+    const ServiceCtl c{v.claimed.as<uint32_t>(), v.ctl.dev<const uint32_t>(), v.ctl.dev<const uint32_t>() + 1,
+                       v.done.dev<uint32_t>(), v.ring, 1u << 24};
+    HIP_OK(fksk::launch_native_service(v.blocks, v.lds, v.stream, fksk::ServiceArgs{a, nat, c}));
+    v.running = true;
+    ++v.launches;
+  }
+
+  // start the resident grid: `share` of the two-wave kernel's resident capacity
+  // (the rest of the chip stays free for other slots' launches), `ring` slots
+  py::dict service_start(int ring, double share) {
+    HIP_OK(hipSetDevice(device_));
+    Service& v = svc_;
+    if (v.running) throw std::runtime_error("the program service is already running");
+    if (!rows_ok_) throw std::invalid_argument("the program service needs the row-kernel layout (<= 16 nodes)");
+    if (ring < 64 || ring > (1 << 22)) throw std::invalid_argument("ring must be in [64, 2^22]");
+    if (!v.stream) HIP_OK(hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking));
+    v.T = duo_top(1 << 30);   // the heap top that keeps the register-limited count of workgroups per CU
+    v.lds = duo_lds_bytes(W_.n_pods, v.T);
+    if (v.lds + 64 > kMaxLds) throw std::invalid_argument("service layout exceeds the 160 KiB LDS");
+    const int per_cu = std::max(1, fksk::native_service_blocks_per_cu(v.lds));
+    v.blocks = std::max(1, (int)(share * per_cu * num_cus_));
+    v.ring = (uint32_t)ring;
+    v.claimed.reserve(4 * 96);
+    v.res.reserve(sizeof(DevResult) * (size_t)ring);
+    v.gheap.reserve((size_t)row_heap_entries(W_.n_pods) * 8 * (size_t)v.blocks);
+    v.ctl.reserve(64, true);
+    v.done.reserve(4 * (size_t)ring, true);
+    v.fn.reserve(8 * (size_t)ring, true);
+    v.koff.reserve(4 * (size_t)ring, true);
+    v.kc.reserve(8 * (size_t)kKcLds * ((size_t)ring + 1), true);
+    v.tab.reserve(8 * 13 * (size_t)ring, true);
+    std::memset(v.ctl.p, 0, 64);
+    std::memset(v.done.p, 0, 4 * (size_t)ring);
+    std::memset(v.kc.p, 0, 8 * (size_t)kKcLds * ((size_t)ring + 1));
+    for (uint32_t i = 0; i < v.ring; ++i) v.koff.as<int32_t>()[i] = (int32_t)(i * (uint32_t)kKcLds);
+    v.busy.assign((size_t)ring, 0);
+    v.held.assign((size_t)ring, 0);
+    v.published = 0;
+    service_launch(0);
+    py::dict d;
+    d["blocks"] = v.blocks; d["per_cu"] = per_cu; d["heap_top"] = v.T; d["lds"] = (int64_t)v.lds; d["ring"] = ring;
+    return d;
+  }
+
+  // enqueue programs (fn / kc / koff as for submit_native): returns the index of
+  // the first one (they get consecutive indexes), or -1 when the ring has no
+  // room for all of them (collect earlier submissions first)
+  int64_t service_submit(py::array_t<uint64_t, py::array::c_style | py::array::forcecast> fn,
+                         py::array_t<int64_t, py::array::c_style | py::array::forcecast> kc,
+                         py::array_t<int32_t, py::array::c_style | py::array::forcecast> koff) {
+    Service& v = svc_;
+    if (!v.running) throw std::runtime_error("the program service is not running");
+    const int P = (int)fn.size();
+    if (P < 1 || (int)koff.size() != P) throw std::invalid_argument("fn / koff sizes");
+    if ((uint32_t)P > v.ring) throw std::invalid_argument("more programs than ring slots");
+    const int64_t nk = (int64_t)kc.size();
+    for (int i = 0; i < P; ++i) {
+      if (fn.at(i) == 0) throw std::invalid_argument("null program pointer");
+      if (koff.at(i) < 0 || koff.at(i) >= nk) throw std::invalid_argument("koff out of range");
+      if (v.busy[(v.published + (uint32_t)i) % v.ring]) return -1;
+    }
+    const uint32_t first = v.published;
+    for (int i = 0; i < P; ++i) {
+      const uint32_t slot = (first + (uint32_t)i) % v.ring;
+      const int64_t a = koff.at(i);
+      const int64_t b = (i + 1 < P && koff.at(i + 1) > a) ? koff.at(i + 1) : nk;
+      const int64_t len = std::min<int64_t>(b - a, kKcLds);
+      int64_t* dst = v.kc.as<int64_t>() + (size_t)slot * kKcLds;
+      std::memcpy(dst, kc.data() + a, (size_t)len * 8);
+      if (len < kKcLds) std::memset(dst + len, 0, (size_t)(kKcLds - len) * 8);
+      v.fn.as<uint64_t>()[slot] = fn.at(i);
+      __atomic_store_n(v.done.as<uint32_t>() + slot, 0u, __ATOMIC_RELAXED);
+      v.busy[slot] = 1;
+      v.held[slot] = first + (uint32_t)i;
+    }
+    v.published = first + (uint32_t)P;
+    __atomic_store_n(v.ctl.as<uint32_t>(), v.published, __ATOMIC_RELEASE);   // after every slot's data
+    return (int64_t)first;
+  }
+
+  // all of [first, first + count) replayed?  (relaunches the grid if it drained
+  // while work was pending: an idle-timeout exit)
+  bool service_ready(int64_t first, int count) {
+    Service& v = svc_;
+    bool all = true;
+    for (int i = 0; i < count && all; ++i) {
+      const uint32_t idx = (uint32_t)first + (uint32_t)i;
+      all = __atomic_load_n(v.done.as<uint32_t>() + idx % v.ring, __ATOMIC_ACQUIRE) == idx + 1u;
+    }
+    if (!all && v.running && hipStreamQuery(v.stream) == hipSuccess) {
+      // the grid left (no work for ~1 min): claims it burned must be re-issued
+      uint32_t lo = v.published;
+      for (uint32_t k = 0; k < v.ring; ++k) {
+        if (!v.busy[k]) continue;
+        const uint32_t j = v.held[k];
+        if (__atomic_load_n(v.done.as<uint32_t>() + k, __ATOMIC_ACQUIRE) != j + 1u && (int32_t)(j - lo) < 0) lo = j;
+      }
+      service_launch(lo);
+    }
+    return all;
+  }
+
+  // result rows of [first, first + count) (must be ready); frees their slots
+  py::array_t<double> service_collect(int64_t first, int count) {
+    Service& v = svc_;
+    if (!service_ready(first, count)) throw std::runtime_error("service_collect: not every program is done");
+    py::array_t<double> out({(py::ssize_t)count, (py::ssize_t)13});
+    double* o = out.mutable_data();
+    for (int i = 0; i < count; ++i) {
+      const uint32_t slot = ((uint32_t)first + (uint32_t)i) % v.ring;
+      std::memcpy(o + (size_t)i * 13, v.tab.as<double>() + (size_t)slot * 13, 13 * sizeof(double));
+      v.busy[slot] = 0;
+    }
+    return out;
+  }
+
+  // tell the grid to leave once nothing published is left, and wait for it
+  void service_stop() {
+    Service& v = svc_;
+    if (!v.running) return;
+    __atomic_store_n(v.ctl.as<uint32_t>() + 1, 1u, __ATOMIC_RELEASE);
+    {
+      py::gil_scoped_release rel;
+      HIP_OK(hipStreamSynchronize(v.stream));
+    }
+    v.running = false;
+  }
+
+  py::dict service_info() {
+    py::dict d;
+    d["running"] = svc_.running; d["blocks"] = svc_.blocks; d["ring"] = (int64_t)svc_.ring;
+    d["published"] = (int64_t)svc_.published; d["launches"] = svc_.launches; d["heap_top"] = svc_.T;
+    int64_t busy = 0;
+    for (uint8_t b : svc_.busy) busy += b;
+    d["unconsumed"] = busy;
+    return d;
   }
 
   bool ready(int slot) {
@@ -700,6 +889,7 @@ class DeviceEngine {
     HIP_OK(fksk::set_native_attrs_np4(mx));
     HIP_OK(fksk::set_native_rows_attrs(mx));
     HIP_OK(fksk::set_native_duo_attrs(mx));
+    HIP_OK(fksk::set_native_service_attrs(mx));
   }
 
   // 4-policies-per-wave row kernel: clusters of <= 16 nodes, exact repush

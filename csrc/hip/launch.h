@@ -100,6 +100,17 @@ hipError_t launch_native_duo(int P, size_t lds, hipStream_t stream, const Builti
 hipError_t set_native_duo_attrs(int max_lds);
 int native_rows_waves_per_cu(size_t lds);
 int native_duo_blocks_per_cu(size_t lds);   // resident two-wave workgroups per CU
+// the resident program service (replay_kernels.hip k_native_service): its one
+// kernel argument, read back through the kernarg segment pointer
+struct ServiceArgs {
+  BuiltinArgs a;
+  fksd::RowNativeArgs nat;
+  fksd::ServiceCtl c;
+};
+static_assert(offsetof(ServiceArgs, a) == 0, "BuiltinArgs (and its DevWorkload) must open the service arguments");
+hipError_t launch_native_service(int blocks, size_t lds, hipStream_t stream, const ServiceArgs& s);
+hipError_t set_native_service_attrs(int max_lds);
+int native_service_blocks_per_cu(size_t lds);
 
 // addresses of the native programs' runtime library (fks_rt_binop, fks_rt_unop, register floor)
 hipError_t native_rt_table(uint64_t* dev_out, hipStream_t s);

@@ -123,9 +123,13 @@ __device__ void pop_reinsert64(const RowHeap& hp, int n, uint64_t last, int j, u
 // S: wait, pod, score, verdict, delete, eval, args, call; `score` is the
 // argmax after the call, `args` the node-state load, `call` the feasibility
 // test, argument set-up and the program call)
+// slot: the program's index into nat / out / table (the block index of a batch
+// launch; a ring slot under k_native_service); hslot: the HBM heap slice used
+// (per program in a batch, per resident workgroup in the service)
 template <bool PROF = false>
 __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64_t* gheap, DevResult* out,
-                           RowNativeArgs nat, double* table, uint64_t* prof_out = nullptr) {
+                           RowNativeArgs nat, double* table, uint64_t* prof_out = nullptr, int slot = -1,
+                           int hslot = -1) {
   uint64_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t plast = 0;
   auto mark = [&](int ph) {
@@ -153,7 +157,8 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
   extern __shared__ uint64_t lds_raw[];
   const int lane = lane_id();
   const int wave = (int)(threadIdx.x >> 6);   // 0: H (heap), 1: S (scoring)
-  const int p = blockIdx.x;
+  const int p = slot >= 0 ? slot : (int)blockIdx.x;
+  const int hs = hslot >= 0 ? hslot : p;
   const int N = W.n_pods;
   const int T = W.heap_top;
   const int lb = W.low_bits, nb = W.node_bits, rb = W.rank_bits;
@@ -195,7 +200,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
     RowHeap heap;
     heap.delmap = reinterpret_cast<FKS_LDS uint32_t*>(rowbase);
     heap.top = reinterpret_cast<FKS_LDS uint64_t*>(rowbase + (size_t)lds_delmap_words(N) * 4);
-    heap.h = global_ptr(gheap + (size_t)p * row_heap_entries(N));
+    heap.h = global_ptr(gheap + (size_t)hs * row_heap_entries(N));
     heap.bind();
     heap.T = T;
     heap.lb = lb;
@@ -612,3 +617,6 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
 }
 
 }  // namespace fksd
+
+// k_native_service (the resident program service built on replay_duo):
+// replay_kernels.hip, where its kernel arguments are defined.

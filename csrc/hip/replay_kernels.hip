@@ -332,6 +332,112 @@ __global__ __launch_bounds__(128, 1) void k_replay_native_duo(fksk::BuiltinArgs 
 __global__ __launch_bounds__(128, 1) void k_replay_native_duo_prof(fksk::BuiltinArgs a, RowNativeArgs nat) {
   replay_duo<true>(a.W, kernarg_workload(), a.gheap, a.out, nat, a.table, a.prof);
 }
+// The resident program service (replay_duo.hip.h native_service): one workgroup
+// per resident two-wave slot, programs from the host's ring until told to stop.
+// ----------------------------------------------------------------------------
+// k_native_service: a resident pool of two-wave workgroups that replays
+// native programs from a ring the host keeps filling, one program after the
+// other per workgroup -- a program's replay ends, its workgroup takes the next
+// one.  A batch launch instead holds every one of its CU slots until its
+// longest replay is done (the tail of a launch: ~40% mean occupancy on evolved
+// programs, and one slow program pinned a 512-program slot in the steady loop).
+//
+// Host <-> device protocol (host memory: fine-grained, mapped; `claimed` in HBM):
+//   the host writes ring slot i % ring (fn, kc block, koff), then publishes
+//   `published` = i + 1 (release); a workgroup claims the next index from
+//   `claimed` (atomic), waits until it is published, replays it, writes its
+//   result row and then done[i % ring] = i + 1 (system-scope release).  The
+//   host reuses a slot only after it consumed that row.
+//   Exit: `stop` set and nothing left to claim, or `max_idle_polls` polls with
+//   nothing published (a lost host: the grid drains instead of spinning on).
+//
+// The replay is a call (service_replay, not inlined): inlined into the service
+// loop, values of its prologue and epilogue were hoisted out of the loop and
+// kept live across every event -- 144-156 VGPRs (6 workgroups per CU) against
+// the 128 of k_replay_native_duo.  Called, it reads every argument from the
+// kernarg segment afresh and the kernel holds the two-wave kernel's 8 per CU
+// (a 224 B stack frame: the callee-saved registers, saved once per program).
+constexpr uint32_t kServiceExit = 0xFFFFFFFFu;
+
+// The kernarg segment pointer exists in the kernel only (a callee reading
+// __builtin_amdgcn_kernarg_segment_ptr gets null): the kernel passes it down,
+// the callees make it wave-uniform again (scalar loads of the arguments).
+__device__ __forceinline__ const FKS_CONST fksk::ServiceArgs* service_args(uint64_t kp) {
+  return (const FKS_CONST fksk::ServiceArgs*)uniu64(kp);
+}
+
+__device__ __forceinline__ void service_replay_body(uint64_t kp, int slot) {
+  const FKS_CONST fksk::ServiceArgs* A = service_args(kp);
+  const fksd::DevWorkload& W = *(const fksd::DevWorkload*)&A->a.W;
+  const RowNativeArgs nat{A->nat.fn, A->nat.kc, A->nat.koff};
+  replay_duo<false>(W, (const fksd::DevWorkload*)uniu64(kp), A->a.gheap, A->a.out, nat, A->a.table, nullptr, slot,
+                    (int)blockIdx.x);
+}
+
+// Claim the next index and wait until it is published.  Only the workgroups
+// at the front (within kServiceFront of the HBM mirror of `published`) read
+// the host's counter -- thousands of waiting workgroups polling host memory
+// (one PCIe read each) starved the link and the replays' own host traffic --
+// and advance the mirror; the rest poll the mirror (HBM, device scope),
+// sleeping longer the further their index lies ahead.  Every index below the
+// mirror is published, and the lowest unprocessed index is always claimed by
+// a front workgroup (claims are handed out in order), so the mirror advances
+// whenever the host publishes.  `stop` propagates the same way.
+constexpr uint32_t kServiceFront = 2;
+
+__device__ __noinline__ void service_replay(uint64_t kp, int slot) { service_replay_body(kp, slot); }
+
+__device__ __noinline__ uint32_t service_claim(uint64_t kp) {
+  const FKS_CONST ServiceCtl& c = service_args(kp)->c;
+  uint32_t* mirror = c.claimed + 32;   // HBM: published (lower bound), then stop
+  uint32_t* stopd = c.claimed + 64;
+  const uint32_t idx = __hip_atomic_fetch_add(c.claimed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t polls = 0;
+  for (;;) {
+    uint32_t pub = __hip_atomic_load(mirror, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if ((int32_t)(idx - pub) < 0) return idx;   // published (wrap-safe)
+    if (__hip_atomic_load(stopd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return kServiceExit;
+    if (idx - pub < kServiceFront) {
+      const uint32_t hp = __hip_atomic_load(c.published, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if ((int32_t)(hp - pub) > 0) {
+        __hip_atomic_fetch_max(mirror, hp, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        pub = hp;
+        if ((int32_t)(idx - pub) < 0) return idx;
+      }
+      if (__hip_atomic_load(c.stop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+        __hip_atomic_store(stopd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return kServiceExit;
+      }
+    }
+    const uint32_t d = idx - pub + 1u < 32u ? idx - pub + 1u : 32u;
+    for (uint32_t z = d; z > 0; --z) __builtin_amdgcn_s_sleep(127);
+    polls += d;
+    if (polls > c.max_idle_polls) return kServiceExit;
+  }
+}
+
+__global__ __launch_bounds__(128, 1) void k_native_service(fksk::ServiceArgs) {
+  __shared__ uint32_t claim;
+  for (;;) {
+    uint64_t kp = (uint64_t)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));   // re-derived per program, not held across the replay
+    if (threadIdx.x == 0) claim = service_claim(kp);
+    __syncthreads();
+    const uint32_t idx = claim;
+    if (idx == kServiceExit) return;   // (uniform across the workgroup)
+    service_replay(kp, (int)(idx % service_args(kp)->c.ring));
+    if (threadIdx.x >= kWave) {
+      // the scoring wave wrote the result row: make it visible to the host, then flag it
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      if (threadIdx.x == kWave) {
+        const uint32_t i2 = claim;
+        const FKS_CONST ServiceCtl& c = service_args((uint64_t)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr())->c;
+        __hip_atomic_store(&c.done[i2 % c.ring], i2 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    __syncthreads();   // both waves are done with the LDS (and with `claim`) before the next program
+  }
+}
 // glibc-exact exp / log / pow (glibc_math.h) on device, one argument per lane:
 // the device side of tests/test_gpu_glibc_math.py
 __global__ __launch_bounds__(256) void k_gm_batch(int fn, const double* x, const double* y, double* out, int32_t* st,
@@ -513,6 +619,16 @@ hipError_t launch_native_duo(int P, size_t lds, hipStream_t st, const BuiltinArg
 hipError_t set_native_duo_attrs(int mx) {
   const hipError_t e = raise_lds(&k_replay_native_duo, mx);
   return e != hipSuccess ? e : raise_lds(&k_replay_native_duo_prof, mx);
+}
+hipError_t launch_native_service(int blocks, size_t lds, hipStream_t st, const ServiceArgs& s) {
+  hipLaunchKernelGGL(k_native_service, dim3(blocks), dim3(128), lds, st, s);
+  return hipGetLastError();
+}
+// (the kernel's static LDS -- the claim word -- counts against the 160 KiB too)
+hipError_t set_native_service_attrs(int mx) { return raise_lds(&k_native_service, mx - 64); }
+int native_service_blocks_per_cu(size_t lds) {
+  int n = 0;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_native_service, 128, lds) == hipSuccess ? n : -1;
 }
 int native_duo_blocks_per_cu(size_t lds) {
   int n = 0;

@@ -46,6 +46,15 @@ struct RowNativeArgs {
   const int64_t* kc;      // concatenated constant blocks
   const int32_t* koff;    // [P] offset of policy p's block in kc
 };
+// Control block of the resident program service (replay_kernels.hip k_native_service)
+struct ServiceCtl {
+  uint32_t* claimed;            // HBM: [0] next index to claim, [32] mirror of published, [64] of stop
+  const uint32_t* published;    // host: indexes < published are written
+  const uint32_t* stop;         // host: 1 = leave once nothing is left to claim
+  uint32_t* done;               // host: [ring] index + 1 once the slot's row is written
+  uint32_t ring;
+  uint32_t max_idle_polls;
+};
 
 constexpr int kRow = 16;            // lanes per DPP row = max nodes per policy
 constexpr int kRowsPerWave = 4;

@@ -10,6 +10,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -30,6 +32,7 @@ struct Emu {
   std::vector<uint8_t> lds;
   std::vector<uint8_t> scratch[kW];
   int64_t steps = 0;
+  int trace_lane = std::getenv("FKS_EMU_TRACE_LANE") ? std::atoi(std::getenv("FKS_EMU_TRACE_LANE")) : -1;
 
   uint64_t rd64s(uint16_t c) const { return (uint64_t)sg[c] | (uint64_t)sg[c + 1] << 32; }
   void wr64s(uint16_t c, uint64_t x) { sg[c] = (uint32_t)x; sg[c + 1] = (uint32_t)(x >> 32); }
@@ -351,7 +354,19 @@ struct Emu {
             }
             w64v(c.res, l, (uint64_t)o.x);
             w32(c.resy, l, (uint32_t)o.y);
+            if (std::getenv("FKS_EMU_TRACE_RT") && (o.y >> 8) != 0)
+              std::fprintf(stderr, "rt kind=%d op=%d a=%016llx afl=%d b=%016llx bfl=%d -> x=%016llx y=%llx\n", c.kind,
+                           c.op, (unsigned long long)ab, afl,
+                           c.kind == 0 ? (unsigned long long)r64(c.b, l, 0) : 0ull,
+                           c.kind == 0 ? (int)r32(c.bfl, l, 0) : 0, (unsigned long long)o.x, (unsigned long long)o.y);
           });
+          if (trace_lane >= 0) {
+            std::fprintf(stderr, "RTCALL sgprs:");
+            for (int x : c.sgprs) std::fprintf(stderr, " %d", x);
+            std::fprintf(stderr, " vgprs:");
+            for (int x : c.vgprs) std::fprintf(stderr, " %d", x);
+            std::fprintf(stderr, " res=%d resy=%d spill=%d\n", c.res - 256, c.resy - 256, c.spill_vgpr - 256);
+          }
           // the callee may clobber every caller-saved register: model the ones
           // the spill set does not cover as garbage, so a missing spill shows
           for (int g = 0; g < 128; ++g) {
@@ -359,7 +374,9 @@ struct Emu {
             if (!cs) continue;
             if (std::find(c.vgprs.begin(), c.vgprs.end(), g) != c.vgprs.end()) continue;
             if (g == c.res - 256 || g == c.res - 255 || g == c.resy - 256 || g == c.spill_vgpr - 256) continue;
-            for (int l = 0; l < kW; ++l) vg[g][l] = 0xDEADBEEFu;
+            // (active lanes only: a callee preserves the inactive lanes of every
+            // VGPR -- its whole-wave code saves them, see fks_rt_binop's v34)
+            for (uint64_t b = ex; b; b &= b - 1) vg[g][__builtin_ctzll(b)] = 0xDEADBEEFu;
           }
           for (int sgi = 0; sgi < 96; ++sgi) {
             const bool cs = sgi < 30 || (sgi >= 40 && ((sgi - 40) % 16) < 8);   // s0-29, s40-47, s56-63, ...
@@ -372,6 +389,13 @@ struct Emu {
         }
         default:
           throw std::logic_error(std::string("emu: unhandled ") + info(m.op).name);
+      }
+      if (trace_lane >= 0) {
+        std::fprintf(stderr, "%4zu %-22s exec=%d", pc, info(m.op).name, (int)(ex >> trace_lane & 1));
+        if (m.d != NONE && m.d >= 256) std::fprintf(stderr, " v%d=%08x", m.d - 256, vg[m.d - 256][trace_lane]);
+        else if (m.d != NONE && m.d < 128) std::fprintf(stderr, " s%d=%08x", m.d, sg[m.d]);
+        if (m.sd != NONE && m.sd < 128) std::fprintf(stderr, " s%d=%08x:%08x", m.sd, sg[m.sd], sg[m.sd + 1]);
+        std::fprintf(stderr, "\n");
       }
       pc = next;
     }

@@ -4,6 +4,7 @@
 // runtime-library host build it emulates (pyops_dev.h under FKS_HOST_JIT)
 // defines HIP-style attribute macros.
 #include <chrono>
+#include <cstdlib>
 #include <mutex>
 #include <cstring>
 #include <sstream>
@@ -166,6 +167,8 @@ struct EmuScorer {
   std::vector<int64_t> res;
   int32_t exc = EXC_NONE;
   bool feas_only = false;   // called for feasible nodes only (code without its prologue), others score 0
+  uint64_t poison_seq = 0;
+  bool traced = false;
 
   ScoreOut operator()(const ScoreCtx& c, int n) {
     if (n == 0) run_event(c);
@@ -183,9 +186,22 @@ struct EmuScorer {
     gcn::Emu& E = *emu;
     // registers the caller does not pass hold garbage (the first 120 VGPRs:
     // everything the generator may allocate)
-    for (int g = 0; g < 120; ++g)
-      for (int l = 0; l < N; ++l) E.vg[g][l] = 0xBADC0DE5u;
-    for (auto& x : E.sg) x = 0x5CA1AB1Eu;
+    // (FKS_EMU_POISON=1: a different value per register, lane and call -- a
+    // read of a register the caller did not pass then shows as a result that
+    // changes with the seed)
+    static const bool vary = std::getenv("FKS_EMU_POISON") != nullptr;
+    uint64_t z = vary ? 0x9E3779B97F4A7C15ull * (uint64_t)(++poison_seq) : 0;
+    auto next = [&](uint32_t dflt) {
+      if (!vary) return dflt;
+      z += 0x9E3779B97F4A7C15ull;
+      uint64_t x = z;
+      x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+      x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+      return (uint32_t)(x ^ (x >> 31));
+    };
+    for (int g = 0; g < 256; ++g)
+      for (int l = 0; l < 64; ++l) E.vg[g][l] = (g < 120 && l < N) || vary ? next(0xBADC0DE5u) : E.vg[g][l];
+    for (auto& x : E.sg) x = next(0x5CA1AB1Eu);
     for (int l = 0; l < N; ++l) {
       const int g0 = w.gpu_start[(size_t)l], ng = w.gpu_start[(size_t)l + 1] - g0;
       E.vg[0][l] = (uint32_t)(int32_t)c.s.cpu_left[(size_t)l];
@@ -232,6 +248,29 @@ struct EmuScorer {
     E.run(*f, kRetMagic);
     for (int l = 0; l < N; ++l)
       if (lanes >> l & 1) res[(size_t)l] = (int64_t)((uint64_t)E.vg[0][l] | (uint64_t)E.vg[1][l] << 32);
+    if (std::getenv("FKS_EMU_TRACE_EXC") && !traced)
+      for (int l = 0; l < N; ++l)
+        if ((lanes >> l & 1) && res[(size_t)l] < 0) {
+          traced = true;
+          std::fprintf(stderr, "exc %lld lane %d pod %d ctime %lld: node cpu %d/%d mem %d/%d gpu_left %d ngpu %d gl", (long long)-res[(size_t)l], l, c.pod,
+                       (long long)c.pod_ctime, (int)c.s.cpu_left[(size_t)l], (int)w.cpu_total[(size_t)l],
+                       (int)c.s.mem_left[(size_t)l], (int)w.mem_total[(size_t)l], (int)c.s.gpu_left[(size_t)l],
+                       (int)w.ngpus[(size_t)l]);
+          for (int j = 0; j < 8; ++j) std::fprintf(stderr, " %u/%u", E.vg[5 + j][l], E.vg[13 + j][l]);
+          std::fprintf(stderr, " pod cpu %d mem %d gm %d ng %d dur %d\n", (int)w.pcpu[(size_t)c.pod], (int)w.pmem[(size_t)c.pod],
+                       (int)w.pgmilli[(size_t)c.pod], (int)w.pngpu[(size_t)c.pod], (int)w.pdur[(size_t)c.pod]);
+          std::fprintf(stderr, "LANES %llx", (unsigned long long)lanes);
+          for (int q = 0; q < N; ++q) {
+            std::fprintf(stderr, " |%d,%d,%d,%d,%d,%d", (int)c.s.cpu_left[(size_t)q], (int)w.cpu_total[(size_t)q],
+                         (int)c.s.mem_left[(size_t)q], (int)w.mem_total[(size_t)q], (int)c.s.gpu_left[(size_t)q],
+                         (int)w.ngpus[(size_t)q]);
+            const int g0 = w.gpu_start[(size_t)q], ng = w.gpu_start[(size_t)q + 1] - g0;
+            for (int j = 0; j < 8; ++j) std::fprintf(stderr, ",%d", j < ng ? (int)c.s.gmilli_left[(size_t)(g0 + j)] : 0);
+            for (int j = 0; j < 8; ++j) std::fprintf(stderr, ",%d", j < ng ? (int)w.gmilli_total[(size_t)(g0 + j)] : 0);
+          }
+          std::fprintf(stderr, "\n");
+          break;
+        }
   }
 };
 

@@ -683,7 +683,8 @@ class IslandFunSearch:
                                             status_every_s=float(sc.get("status_every_s", 5.0)),
                                             tierup=bool(sc.get("tierup", False)),
                                             ahead=int(sc.get("ahead", 2)),
-                                            host_object=bool(sc.get("host_object", False)))
+                                            host_object=bool(sc.get("host_object", False)),
+                                            service=sc.get("service"))
             self.steady.run(generations, threshold, wall_s=float(sc.get("wall_s", 0.0)))
             return self.global_best()
         if self.pipeline:

@@ -170,7 +170,7 @@ class SteadyStateSearch:
 
     def __init__(self, fs, batch: int = 256, slots: Optional[int] = None, producers: int = 0,
                  task_size: int = 8, status_every_s: float = 5.0, tierup: bool = False, ahead: int = 2,
-                 host_object: bool = False):
+                 host_object: bool = False, service=None):
         self.fs = fs
         #: children only CPython can score (bigint / complex intermediates, ~1% of
         #: mutated programs, ~3 s each on one core) go to the object engine only
@@ -199,6 +199,16 @@ class SteadyStateSearch:
         if getattr(fs, "coupler", None) is not None:
             n_slots = max(1, n_slots - 1)   # the last slot is the family coupler's
         self.slots = max(1, min(int(slots or n_slots), n_slots))
+        #: resident program service (ops/hip_engine.py start_service): batches are
+        #: queued to one persistent grid instead of launched per slot, so the
+        #: number of batches in flight is no longer the engine's stream count
+        svc = service if isinstance(service, dict) else ({} if service else None)
+        self.service_cfg = None
+        self.slot_base = 0
+        if svc is not None and dev is not None and hasattr(dev, "start_service"):
+            self.service_cfg = dict(svc)
+            self.slots = max(1, int(svc.get("slots", slots or 12)))
+            self.slot_base = dev.SERVICE_SLOT_BASE
         if dev is not None:
             # the two-wave kernel sizes its LDS heap top so that every slot's batch
             # stays resident at once (csrc/hip/engine_host.hip.h duo_top)
@@ -331,6 +341,19 @@ class SteadyStateSearch:
         merged = [0] * k
         target_children = [generations * max(1, s.policies_per_generation) for s in islands]
         from .migration import MigrationChannel
+        dev = getattr(ev, "device", None)
+        if dev is not None and hasattr(dev, "warm_native"):
+            # first-use JIT set-up (every code-object skeleton's layout probe) before
+            # the replays fill the chip: a probe queued behind them waits seconds
+            fs.log.write(kind="steady_warm", rank=ctx.rank, warm_s=round(dev.warm_native(), 3))
+        svc_started = False
+        if self.service_cfg is not None:
+            sc = self.service_cfg
+            share = float(sc.get("share", 0.75 if fs.coupler is not None else 1.0))
+            ring = max(int(sc.get("ring", 16384)), 4 * self.batch * (self.slots + 2))
+            info = dev.start_service(ring=ring, share=share)
+            svc_started = True
+            fs.log.write(kind="steady_service", rank=ctx.rank, slots=self.slots, share=share, **info)
         chan = MigrationChannel(fs, fs.migrate_every, start_gen)
         self.channel = chan
         stop = False             # no more children: drain and finish
@@ -449,7 +472,7 @@ class SteadyStateSearch:
                     pend = fut.result()
                     with roctx_range(f"steady.launch slot {si} ({len(take)} programs)"):
                         t_ph = time.perf_counter()
-                        ev.launch_prepared(pend, si)
+                        ev.launch_prepared(pend, self.slot_base + si)
                         self.phase["submit"] += time.perf_counter() - t_ph
                     b = _Batch(si, take, pend, time.time(), pend.new_shapes, pend.jit_s, pjob)
                     batches[si] = b
@@ -604,6 +627,8 @@ class SteadyStateSearch:
             for _, fut, _pj in staged:   # compiled but never launched: give the modules back
                 if fut.done() and not fut.cancelled() and fut.exception() is None:
                     ev.discard_prepared(fut.result())
+            if svc_started:
+                dev.stop_service()
         now = time.time()
         rec = self._status(now, t_start, busy_since, batches, ready, inflight_tasks, merged, global_best, final=True)
         if fs.ck_dir:
@@ -626,6 +651,8 @@ class SteadyStateSearch:
         if dev is not None:
             info = dev.info()
             capacity = int(info.get("native_duo_per_cu_last", 0)) * int(info.get("num_cus", 0))
+            if "service" in info:
+                capacity = int(info["service"]["blocks"])
         rec = dict(kind="steady_final" if final else "steady_status", rank=fs.ctx.rank, wall_s=round(wall, 3),
                    evaluations=st.evaluations, evals_per_s=round(st.evaluations / wall, 2),
                    device_busy=round(busy / wall, 4),

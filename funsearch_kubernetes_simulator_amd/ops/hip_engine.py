@@ -269,9 +269,55 @@ class DeviceEvaluator:
         #: device exp / log / pow == host libm (else programs using them stay on the host)
         self.math_exact = glibc_math_ok()
         self._native_mods: Dict[int, tuple] = {}   # slot -> JIT modules its batch in flight calls into
+        #: the resident program service (start_service): slot -> (P, native rows, first ring index)
+        self._svc: Optional[dict] = None
+        self._svc_post: Dict[int, Tuple[int, np.ndarray, int]] = {}
 
     def info(self) -> dict:
-        return dict(self._eng.info())
+        d = dict(self._eng.info())
+        if self._svc is not None:
+            d["service"] = dict(self._eng.service_info())
+        return d
+
+    # -- resident program service (csrc/hip/replay_duo.hip.h native_service) ---------------
+    #: slot ids of the service's callers start here (the engine's own stream
+    #: slots, e.g. the family coupler's, stay below)
+    SERVICE_SLOT_BASE = 64
+
+    def start_service(self, ring: int = 16384, share: float = 1.0) -> dict:
+        """Launch the resident two-wave grid: from now on every native program
+        batch (`submit_native`, any slot) is queued to it instead of launched
+        as a kernel of its own, and a batch's `ready` / `wait` follow its own
+        programs only -- a slow program no longer holds a launch's CU slots
+        while the rest of them idle.  share: fraction of the two-wave kernel's
+        resident capacity the grid takes (the rest stays free for other
+        streams' kernels, e.g. the family coupler's row-kernel batches)."""
+        if self._svc is not None:
+            return dict(self._svc)
+        self.warm_native()
+        self._svc = dict(self._eng.service_start(int(ring), float(share)))
+        if not getattr(self, "_svc_atexit", False):
+            # a grid left running at interpreter exit would hold every later
+            # device-wide synchronisation (JIT module teardown) until its idle timeout
+            import atexit
+            import weakref
+            ref = weakref.ref(self)
+            atexit.register(lambda: ref() is not None and ref()._eng.service_stop())
+            self._svc_atexit = True
+        return dict(self._svc)
+
+    def stop_service(self) -> None:
+        """Drain and end the resident grid (batches still queued are waited for)."""
+        if self._svc is None:
+            return
+        for slot in list(self._svc_post):
+            self.wait(slot)
+        self._eng.service_stop()
+        self._svc = None
+
+    @property
+    def service(self) -> Optional[dict]:
+        return self._svc
 
     def warm_native(self) -> float:
         """First-use initialisation of the native program path -- the JIT's
@@ -286,6 +332,12 @@ class DeviceEvaluator:
         prog = compile_policy(reference_policies()["first_fit"])
         self.submit_native(0, [prog])
         self.wait(0)
+        bj = getattr(self.native_compiler, "_baseline", None)
+        if bj is not None:
+            from .gcnjit import compile_program
+            code, _ = compile_program(prog)
+            if code is not None:
+                bj.verify_all(code)   # every code-object skeleton size, before replays fill the chip
         self._warm_s = time.perf_counter() - t0
         return self._warm_s
 
@@ -340,10 +392,20 @@ class DeviceEvaluator:
             with open(dump, "a") as f:
                 f.write(json.dumps({"slot": slot, "t": time.time(), "P": int(idx.size),
                                     "codes": [progs[i].source for i in idx]}) + "\n")
-        self._native_post[slot] = (len(progs), idx)
         try:
-            if idx.size:
-                self._eng.submit_native(slot, batch.fn[idx], batch.kc, batch.koff[idx])
+            if self._svc is not None:
+                if slot in self._svc_post:
+                    raise RuntimeError(f"service slot {slot} still holds a batch")
+                first = -1
+                if idx.size:
+                    first = self._eng.service_submit(batch.fn[idx], batch.kc, batch.koff[idx])
+                    if first < 0:
+                        raise RuntimeError("program service ring full: collect finished batches first")
+                self._svc_post[slot] = (len(progs), idx, first)
+            else:
+                self._native_post[slot] = (len(progs), idx)
+                if idx.size:
+                    self._eng.submit_native(slot, batch.fn[idx], batch.kc, batch.koff[idx])
         except BaseException:
             self.native_compiler.release(batch.modules)
             raise
@@ -404,6 +466,21 @@ class DeviceEvaluator:
 
     def wait(self, slot: int) -> np.ndarray:
         """[P, 13] result table of the batch in flight on `slot`."""
+        svc = self._svc_post.pop(slot, None)
+        if svc is not None:
+            P, idx, first = svc
+            out = np.zeros((P, len(RESULT_COLUMNS)))
+            out[:, 10] = 100.0
+            try:
+                if idx.size:
+                    while not self._eng.service_ready(first, int(idx.size)):
+                        time.sleep(0.0002)
+                    out[idx] = self._eng.service_collect(first, int(idx.size))
+            finally:
+                mods = self._native_mods.pop(slot, None)
+                if mods:
+                    self.native_compiler.release(mods)
+            return out
         post = self._native_post.pop(slot, None)
         if post is None:
             return self._eng.wait(slot)
@@ -420,6 +497,9 @@ class DeviceEvaluator:
         return out
 
     def ready(self, slot: int) -> bool:
+        svc = self._svc_post.get(slot)
+        if svc is not None:
+            return svc[1].size == 0 or self._eng.service_ready(svc[2], int(svc[1].size))
         post = self._native_post.get(slot)
         if post is not None and post[1].size == 0:
             return True

@@ -1,0 +1,100 @@
+"""The resident program service (k_native_service, csrc/hip/replay_duo.hip.h):
+a persistent grid of two-wave workgroups replaying programs from a host ring
+must give rows bit-identical to the per-batch two-wave launch -- across ring
+wrap-around, interleaved batches, a program that runs out of loop budget, and
+a stop / restart of the grid."""
+import numpy as np
+import pytest
+
+from funsearch_kubernetes_simulator_amd.policy.bytecode import Exc
+from funsearch_kubernetes_simulator_amd.policy.compiler import compile_policy
+
+from program_corpus import programs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev(default_workload):
+    from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
+    if not he.device_available():
+        pytest.fail("GPU test collected but no HIP device is visible")
+    d = he.DeviceEvaluator(default_workload)
+    yield d
+    d.stop_service()
+
+
+def _batched(dev, progs, size):
+    return np.concatenate([dev.evaluate_native(progs[i:i + size]) for i in range(0, len(progs), size)])
+
+
+def test_service_rows_equal_batch_rows(dev):
+    progs = programs()[:96]
+    want = _batched(dev, progs, 32)
+    info = dev.start_service(ring=64, share=0.25)   # a 64-slot ring: every index wraps
+    try:
+        assert info["blocks"] >= 1 and info["ring"] == 64
+        base = dev.SERVICE_SLOT_BASE
+        got = np.zeros_like(want)
+        # four batches of 16 in flight at once (the whole ring), collected out of order
+        order = [(k, progs[k * 16:(k + 1) * 16]) for k in range(6)]
+        inflight = {}
+        for k, chunk in order:
+            if len(inflight) == 4:
+                old = max(inflight)          # the newest first: done flags are per program
+                got[old * 16:(old + 1) * 16] = dev.wait(base + inflight.pop(old))
+            dev.submit_native(base + k % 8, chunk)
+            inflight[k] = k % 8
+        for k, s in inflight.items():
+            got[k * 16:(k + 1) * 16] = dev.wait(base + s)
+        for i in range(len(progs)):
+            assert np.array_equal(got[i], want[i]), (i, got[i], want[i])
+        sv = dev.info()["service"]
+        # (the corpus holds programs only the host engines take: not published)
+        assert sv["running"] and sv["unconsumed"] == 0 and 48 <= sv["published"] <= 96
+    finally:
+        dev.stop_service()
+    assert dev.service is None
+
+
+def test_service_budget_exhaustion_and_restart(dev):
+    runaway = compile_policy("def priority_function(pod, node):\n    x = 0\n    while True:\n        x += 1\n    return x\n")
+    good = [compile_policy("def priority_function(pod, node):\n    return node.cpu_milli_left\n")] * 3
+    want = dev.evaluate_native(good)
+    dev.native_compiler.budget = 2000
+    try:
+        b = dev.native_compiler.prepare([runaway])
+        assert b.ok.all()
+        dev.release_native(b)
+    finally:
+        dev.native_compiler.budget = 1 << 22
+    for _ in range(2):                      # start, stop, start again
+        dev.start_service(ring=256, share=0.5)
+        try:
+            tab = dev.evaluate_native([runaway] + good)
+        finally:
+            dev.stop_service()
+        assert int(tab[0, 10]) == Exc.BUDGET, tab[0]
+        for i in range(3):
+            assert np.array_equal(tab[1 + i], want[i])
+    # batch launches work again after the grid left
+    assert np.array_equal(dev.evaluate_native(good), want)
+
+
+def test_service_many_small_batches(dev):
+    """More batches than ring slots over the run (indexes far past the ring),
+    one and two programs at a time: the claim / publish / done handshake."""
+    progs = programs()[:40]
+    want = _batched(dev, progs, 40)
+    dev.start_service(ring=64, share=1.0)
+    try:
+        got = []
+        for rep in range(3):
+            for i in range(0, len(progs), 2):
+                got.append(dev.evaluate_native(progs[i:i + 2]))
+        got = np.concatenate(got)
+    finally:
+        dev.stop_service()
+    for rep in range(3):
+        for i in range(len(progs)):
+            assert np.array_equal(got[rep * len(progs) + i], want[i]), (rep, i)
