@@ -84,6 +84,9 @@ def main() -> None:
     ap.add_argument("--novel-large", type=int, default=2048,
                     help="after the timed region: an LLM-scale batch of this many new-shape programs (JIT included, "
                          "chunks over the slots, all in flight at once); reported as `program_path.novel_large` (0: skip)")
+    ap.add_argument("--evolved-service-s", type=float, default=8.0,
+                    help="seconds of sustained evolved-program replay through the resident program service "
+                         "(`program_path.evolved.service`; 0: skip)")
     ap.add_argument("--evolved", type=int, default=2048,
                     help="children of an evolved population (data/populations, frozen sources) through the "
                          "native backend, all in flight; reported as `program_path.evolved` (0: skip)")
@@ -281,7 +284,7 @@ def main() -> None:
         if args.evolved > 0 and args.trace == "default":
             # the search's late-run workload: children of an evolved population
             from funsearch_kubernetes_simulator_amd.bench.programs import measure_evolved
-            evo = measure_evolved(ev.device, workload, args.evolved)
+            evo = measure_evolved(ev.device, workload, args.evolved, service_s=args.evolved_service_s)
             evo["vs_baseline"] = round(evo["evals_per_s_incl_jit"] / BASELINE_EVALS_PER_S, 2)
             program_path["evolved"] = evo
 

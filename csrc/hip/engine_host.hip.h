@@ -471,29 +471,36 @@ class DeviceEngine {
     return out;
   }
 
-  // ---- resident program service (replay_duo.hip.h native_service) ---------------------
-  // A grid of resident two-wave workgroups replays programs from a host ring:
-  // a workgroup whose replay ends takes the next program at once, so no
-  // program's slot waits for a batch's longest replay.  Host memory
-  // (coherent, mapped): published / stop, per-slot fn / koff / constant block,
-  // result rows and done flags; `claimed` lives in HBM.
+  // ---- resident program service (replay_kernels.hip k_native_service) ----------------
+  // A grid of resident two-wave workgroups replays programs the host queues:
+  // a workgroup whose replay ends claims the next program at once, so no
+  // program waits for another's replay.  Programs are numbered in submission
+  // order (the claim order); each gets a data slot (fn, koff, constant block,
+  // result row, done flag) from a free list, so a straggler -- a replay of
+  // millions of events -- holds its slot and nothing else.  The index queue
+  // (`qslot`, `nq` entries) maps index -> slot; the device marks an index
+  // `started` once it has read its entry, and the host reuses an entry only
+  // after that.  Host memory (coherent, mapped): published / stop, qslot,
+  // started, the per-slot arrays; `claimed` and the mirrors live in HBM.
   struct Service {
     hipStream_t stream = nullptr;
     DevBuf claimed, res, gheap;
-    HostBuf ctl, done, fn, koff, kc, tab;
-    std::vector<uint8_t> busy;   // slot holds an unconsumed program
-    std::vector<uint32_t> held;  // the index published last into each slot
-    uint32_t ring = 0, published = 0;
+    HostBuf ctl, qslot, started, done, fn, koff, kc, tab;
+    std::vector<uint8_t> busy;        // slot holds a program not collected yet
+    std::vector<uint32_t> held;       // index of the program in each slot
+    std::vector<uint32_t> free_slots;
+    uint32_t nslots = 0, nq = 0, published = 0;
     int blocks = 0, T = 0;
     size_t lds = 0;
     bool running = false;
     int64_t launches = 0;
     void release() {
       for (DevBuf* b : {&claimed, &res, &gheap}) b->release();
-      for (HostBuf* b : {&ctl, &done, &fn, &koff, &kc, &tab}) b->release();
+      for (HostBuf* b : {&ctl, &qslot, &started, &done, &fn, &koff, &kc, &tab}) b->release();
       if (stream) (void)hipStreamDestroy(stream);
       stream = nullptr;
     }
+    uint32_t ld(const HostBuf& b, uint32_t i) const { return __atomic_load_n(b.as<uint32_t>() + i, __ATOMIC_ACQUIRE); }
   };
   Service svc_;
 
@@ -514,69 +521,88 @@ class DeviceEngine {
     const RowNativeArgs nat{v.fn.dev<const uint64_t>(), v.kc.dev<const int64_t>(), v.koff.dev<const int32_t>()};
     // ~57 s of s_sleep(127) polls with nothing published: the grid drains (a lost host)
     const ServiceCtl c{v.claimed.as<uint32_t>(), v.ctl.dev<const uint32_t>(), v.ctl.dev<const uint32_t>() + 1,
-                       v.done.dev<uint32_t>(), v.ring, 1u << 24};
+                       v.done.dev<uint32_t>(), v.qslot.dev<const uint32_t>(), v.started.dev<uint32_t>(), v.nq,
+                       1u << 24};
     HIP_OK(fksk::launch_native_service(v.blocks, v.lds, v.stream, fksk::ServiceArgs{a, nat, c}));
     v.running = true;
     ++v.launches;
   }
 
   // start the resident grid: `share` of the two-wave kernel's resident capacity
-  // (the rest of the chip stays free for other slots' launches), `ring` slots
-  py::dict service_start(int ring, double share) {
+  // (the rest of the chip stays free for other kernels: JIT module loads, other
+  // slots' launches), `slots` programs queued or running at most
+  py::dict service_start(int slots, double share) {
     HIP_OK(hipSetDevice(device_));
     Service& v = svc_;
     if (v.running) throw std::runtime_error("the program service is already running");
     if (!rows_ok_) throw std::invalid_argument("the program service needs the row-kernel layout (<= 16 nodes)");
-    if (ring < 64 || ring > (1 << 22)) throw std::invalid_argument("ring must be in [64, 2^22]");
+    if (slots < 64 || slots > (1 << 22)) throw std::invalid_argument("slots must be in [64, 2^22]");
     if (!v.stream) HIP_OK(hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking));
     v.T = duo_top(1 << 30);   // the heap top that keeps the register-limited count of workgroups per CU
     v.lds = duo_lds_bytes(W_.n_pods, v.T);
     if (v.lds + 64 > kMaxLds) throw std::invalid_argument("service layout exceeds the 160 KiB LDS");
     const int per_cu = std::max(1, fksk::native_service_blocks_per_cu(v.lds));
     v.blocks = std::max(1, (int)(share * per_cu * num_cus_));
-    v.ring = (uint32_t)ring;
+    v.nslots = (uint32_t)slots;
+    v.nq = 2 * (uint32_t)slots;
+    const size_t S = v.nslots, Q = v.nq;
     v.claimed.reserve(4 * 96);
-    v.res.reserve(sizeof(DevResult) * (size_t)ring);
+    v.res.reserve(sizeof(DevResult) * S);
     v.gheap.reserve((size_t)row_heap_entries(W_.n_pods) * 8 * (size_t)v.blocks);
     v.ctl.reserve(64, true);
-    v.done.reserve(4 * (size_t)ring, true);
-    v.fn.reserve(8 * (size_t)ring, true);
-    v.koff.reserve(4 * (size_t)ring, true);
-    v.kc.reserve(8 * (size_t)kKcLds * ((size_t)ring + 1), true);
-    v.tab.reserve(8 * 13 * (size_t)ring, true);
+    v.qslot.reserve(4 * Q, true);
+    v.started.reserve(4 * Q, true);
+    v.done.reserve(4 * S, true);
+    v.fn.reserve(8 * S, true);
+    v.koff.reserve(4 * S, true);
+    v.kc.reserve(8 * (size_t)kKcLds * (S + 1), true);
+    v.tab.reserve(8 * 13 * S, true);
     std::memset(v.ctl.p, 0, 64);
-    std::memset(v.done.p, 0, 4 * (size_t)ring);
-    std::memset(v.kc.p, 0, 8 * (size_t)kKcLds * ((size_t)ring + 1));
-    for (uint32_t i = 0; i < v.ring; ++i) v.koff.as<int32_t>()[i] = (int32_t)(i * (uint32_t)kKcLds);
-    v.busy.assign((size_t)ring, 0);
-    v.held.assign((size_t)ring, 0);
+    std::memset(v.qslot.p, 0, 4 * Q);
+    std::memset(v.started.p, 0, 4 * Q);
+    std::memset(v.done.p, 0, 4 * S);
+    std::memset(v.kc.p, 0, 8 * (size_t)kKcLds * (S + 1));
+    for (uint32_t i = 0; i < v.nslots; ++i) v.koff.as<int32_t>()[i] = (int32_t)(i * (uint32_t)kKcLds);
+    v.busy.assign(S, 0);
+    v.held.assign(S, 0);
+    v.free_slots.resize(S);
+    for (uint32_t i = 0; i < v.nslots; ++i) v.free_slots[i] = v.nslots - 1 - i;
     v.published = 0;
     service_launch(0);
     py::dict d;
-    d["blocks"] = v.blocks; d["per_cu"] = per_cu; d["heap_top"] = v.T; d["lds"] = (int64_t)v.lds; d["ring"] = ring;
+    d["blocks"] = v.blocks; d["per_cu"] = per_cu; d["heap_top"] = v.T; d["lds"] = (int64_t)v.lds;
+    d["slots"] = slots; d["queue"] = (int64_t)v.nq;
     return d;
   }
 
-  // enqueue programs (fn / kc / koff as for submit_native): returns the index of
-  // the first one (they get consecutive indexes), or -1 when the ring has no
-  // room for all of them (collect earlier submissions first)
-  int64_t service_submit(py::array_t<uint64_t, py::array::c_style | py::array::forcecast> fn,
-                         py::array_t<int64_t, py::array::c_style | py::array::forcecast> kc,
-                         py::array_t<int32_t, py::array::c_style | py::array::forcecast> koff) {
+  // queue programs (fn / kc / koff as for submit_native): (index of the first
+  // -- they get consecutive ones --, their data slots), or (-1, []) when there
+  // is no room (too many programs not collected, or the oldest index-queue
+  // entry not yet started)
+  py::tuple service_submit(py::array_t<uint64_t, py::array::c_style | py::array::forcecast> fn,
+                           py::array_t<int64_t, py::array::c_style | py::array::forcecast> kc,
+                           py::array_t<int32_t, py::array::c_style | py::array::forcecast> koff) {
     Service& v = svc_;
     if (!v.running) throw std::runtime_error("the program service is not running");
     const int P = (int)fn.size();
     if (P < 1 || (int)koff.size() != P) throw std::invalid_argument("fn / koff sizes");
-    if ((uint32_t)P > v.ring) throw std::invalid_argument("more programs than ring slots");
     const int64_t nk = (int64_t)kc.size();
     for (int i = 0; i < P; ++i) {
       if (fn.at(i) == 0) throw std::invalid_argument("null program pointer");
       if (koff.at(i) < 0 || koff.at(i) >= nk) throw std::invalid_argument("koff out of range");
-      if (v.busy[(v.published + (uint32_t)i) % v.ring]) return -1;
+    }
+    auto refuse = [] { return py::make_tuple((int64_t)-1, py::array_t<int32_t>(0)); };
+    if (v.free_slots.size() < (size_t)P || (uint32_t)P > v.nq) return refuse();
+    for (int i = 0; i < P; ++i) {   // the entries this submission reuses: their last index must have started
+      const uint32_t idx = v.published + (uint32_t)i;
+      if (idx >= v.nq && v.ld(v.started, idx % v.nq) != idx - v.nq + 1u) return refuse();
     }
     const uint32_t first = v.published;
+    py::array_t<int32_t> slots(P);
     for (int i = 0; i < P; ++i) {
-      const uint32_t slot = (first + (uint32_t)i) % v.ring;
+      const uint32_t idx = first + (uint32_t)i;
+      const uint32_t slot = v.free_slots.back();
+      v.free_slots.pop_back();
       const int64_t a = koff.at(i);
       const int64_t b = (i + 1 < P && koff.at(i + 1) > a) ? koff.at(i + 1) : nk;
       const int64_t len = std::min<int64_t>(b - a, kKcLds);
@@ -585,48 +611,84 @@ class DeviceEngine {
       if (len < kKcLds) std::memset(dst + len, 0, (size_t)(kKcLds - len) * 8);
       v.fn.as<uint64_t>()[slot] = fn.at(i);
       __atomic_store_n(v.done.as<uint32_t>() + slot, 0u, __ATOMIC_RELAXED);
+      __atomic_store_n(v.qslot.as<uint32_t>() + idx % v.nq, slot, __ATOMIC_RELAXED);
       v.busy[slot] = 1;
-      v.held[slot] = first + (uint32_t)i;
+      v.held[slot] = idx;
+      slots.mutable_data()[i] = (int32_t)slot;
     }
     v.published = first + (uint32_t)P;
     __atomic_store_n(v.ctl.as<uint32_t>(), v.published, __ATOMIC_RELEASE);   // after every slot's data
-    return (int64_t)first;
+    return py::make_tuple((int64_t)first, slots);
   }
 
-  // all of [first, first + count) replayed?  (relaunches the grid if it drained
-  // while work was pending: an idle-timeout exit)
-  bool service_ready(int64_t first, int count) {
+  bool svc_done(uint32_t idx, int32_t slot) const {
+    return slot >= 0 && (uint32_t)slot < svc_.nslots && svc_.ld(svc_.done, (uint32_t)slot) == idx + 1u;
+  }
+
+  // if the grid drained (nothing published for ~1 min) while programs wait,
+  // launch it again from the first index no workgroup started
+  void service_revive() {
     Service& v = svc_;
-    bool all = true;
-    for (int i = 0; i < count && all; ++i) {
-      const uint32_t idx = (uint32_t)first + (uint32_t)i;
-      all = __atomic_load_n(v.done.as<uint32_t>() + idx % v.ring, __ATOMIC_ACQUIRE) == idx + 1u;
-    }
-    if (!all && v.running && hipStreamQuery(v.stream) == hipSuccess) {
-      // the grid left (no work for ~1 min): claims it burned must be re-issued
-      uint32_t lo = v.published;
-      for (uint32_t k = 0; k < v.ring; ++k) {
-        if (!v.busy[k]) continue;
-        const uint32_t j = v.held[k];
-        if (__atomic_load_n(v.done.as<uint32_t>() + k, __ATOMIC_ACQUIRE) != j + 1u && (int32_t)(j - lo) < 0) lo = j;
+    if (!v.running || hipStreamQuery(v.stream) != hipSuccess) return;
+    uint32_t lo = v.published > v.nq ? v.published - v.nq : 0;
+    while (lo != v.published && v.ld(v.started, lo % v.nq) == lo + 1u) ++lo;
+    if (lo != v.published) service_launch(lo);
+  }
+
+  // all of the submission (first, slots) replayed?
+  bool service_ready(int64_t first, py::array_t<int32_t, py::array::c_style | py::array::forcecast> slots) {
+    const int n = (int)slots.size();
+    for (int i = 0; i < n; ++i)
+      if (!svc_done((uint32_t)first + (uint32_t)i, slots.at(i))) {
+        service_revive();
+        return false;
       }
-      service_launch(lo);
-    }
-    return all;
+    return true;
   }
 
-  // result rows of [first, first + count) (must be ready); frees their slots
-  py::array_t<double> service_collect(int64_t first, int count) {
+  // result rows of the submission (must be ready); frees its slots
+  py::array_t<double> service_collect(int64_t first, py::array_t<int32_t, py::array::c_style | py::array::forcecast> slots) {
     Service& v = svc_;
-    if (!service_ready(first, count)) throw std::runtime_error("service_collect: not every program is done");
-    py::array_t<double> out({(py::ssize_t)count, (py::ssize_t)13});
+    if (!service_ready(first, slots)) throw std::runtime_error("service_collect: not every program is done");
+    const int n = (int)slots.size();
+    py::array_t<double> out({(py::ssize_t)n, (py::ssize_t)13});
     double* o = out.mutable_data();
-    for (int i = 0; i < count; ++i) {
-      const uint32_t slot = ((uint32_t)first + (uint32_t)i) % v.ring;
+    for (int i = 0; i < n; ++i) {
+      const uint32_t slot = (uint32_t)slots.at(i);
       std::memcpy(o + (size_t)i * 13, v.tab.as<double>() + (size_t)slot * 13, 13 * sizeof(double));
-      v.busy[slot] = 0;
+      if (v.busy[slot] && v.held[slot] == (uint32_t)first + (uint32_t)i) {
+        v.busy[slot] = 0;
+        v.free_slots.push_back(slot);
+      }
     }
     return out;
+  }
+
+  // streaming collection: the rows of the submission finished since the last
+  // call -- (offsets into it, rows) -- their slots freed.  A caller that takes
+  // rows as they finish never waits for the submission's slowest program.
+  py::tuple service_take(int64_t first, py::array_t<int32_t, py::array::c_style | py::array::forcecast> slots) {
+    Service& v = svc_;
+    const int n = (int)slots.size();
+    std::vector<int32_t> offs;
+    for (int i = 0; i < n; ++i) {
+      const uint32_t idx = (uint32_t)first + (uint32_t)i;
+      const int32_t slot = slots.at(i);
+      if (slot < 0 || (uint32_t)slot >= v.nslots || !v.busy[slot] || v.held[slot] != idx) continue;   // taken
+      if (svc_done(idx, slot)) offs.push_back(i);
+    }
+    py::array_t<int32_t> o((py::ssize_t)offs.size());
+    py::array_t<double> rows({(py::ssize_t)offs.size(), (py::ssize_t)13});
+    double* r = rows.mutable_data();
+    for (size_t k = 0; k < offs.size(); ++k) {
+      const uint32_t slot = (uint32_t)slots.at(offs[k]);
+      o.mutable_data()[k] = offs[k];
+      std::memcpy(r + k * 13, v.tab.as<double>() + (size_t)slot * 13, 13 * sizeof(double));
+      v.busy[slot] = 0;
+      v.free_slots.push_back(slot);
+    }
+    if (offs.empty() && n > 0) service_revive();
+    return py::make_tuple(o, rows);
   }
 
   // tell the grid to leave once nothing published is left, and wait for it
@@ -643,11 +705,10 @@ class DeviceEngine {
 
   py::dict service_info() {
     py::dict d;
-    d["running"] = svc_.running; d["blocks"] = svc_.blocks; d["ring"] = (int64_t)svc_.ring;
-    d["published"] = (int64_t)svc_.published; d["launches"] = svc_.launches; d["heap_top"] = svc_.T;
-    int64_t busy = 0;
-    for (uint8_t b : svc_.busy) busy += b;
-    d["unconsumed"] = busy;
+    d["running"] = svc_.running; d["blocks"] = svc_.blocks; d["slots"] = (int64_t)svc_.nslots;
+    d["queue"] = (int64_t)svc_.nq; d["published"] = (int64_t)svc_.published; d["launches"] = svc_.launches;
+    d["heap_top"] = svc_.T;
+    d["unconsumed"] = (int64_t)(svc_.nslots - svc_.free_slots.size());
     return d;
   }
 

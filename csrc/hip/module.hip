@@ -457,10 +457,11 @@ PYBIND11_MODULE(_fks_hip, m) {
       .def("evaluate_programs", &DeviceEngine::evaluate_programs)
       .def("submit_builtin", &DeviceEngine::submit_builtin)
       .def("submit_programs", &DeviceEngine::submit_programs)
-      .def("service_start", &DeviceEngine::service_start, py::arg("ring") = 16384, py::arg("share") = 1.0)
+      .def("service_start", &DeviceEngine::service_start, py::arg("slots") = 16384, py::arg("share") = 1.0)
       .def("service_submit", &DeviceEngine::service_submit)
       .def("service_ready", &DeviceEngine::service_ready)
       .def("service_collect", &DeviceEngine::service_collect)
+      .def("service_take", &DeviceEngine::service_take)
       .def("service_stop", &DeviceEngine::service_stop)
       .def("service_info", &DeviceEngine::service_info)
       .def("ready", &DeviceEngine::ready)

@@ -343,11 +343,13 @@ __global__ __launch_bounds__(128, 1) void k_replay_native_duo_prof(fksk::Builtin
 // programs, and one slow program pinned a 512-program slot in the steady loop).
 //
 // Host <-> device protocol (host memory: fine-grained, mapped; `claimed` in HBM):
-//   the host writes ring slot i % ring (fn, kc block, koff), then publishes
-//   `published` = i + 1 (release); a workgroup claims the next index from
-//   `claimed` (atomic), waits until it is published, replays it, writes its
-//   result row and then done[i % ring] = i + 1 (system-scope release).  The
-//   host reuses a slot only after it consumed that row.
+//   the host writes program i into a free data slot s (fn, kc block, koff),
+//   qslot[i % nq] = s, then publishes `published` = i + 1 (release); a
+//   workgroup claims the next index from `claimed` (atomic), waits until it is
+//   published, reads s, marks started[i % nq] = i + 1, replays slot s, writes
+//   its result row and then done[s] = i + 1 (system-scope release).  The host
+//   frees a slot when it consumed the row, and reuses a queue entry only once
+//   it is marked started -- a straggler holds its slot, nothing else.
 //   Exit: `stop` set and nothing left to claim, or `max_idle_polls` polls with
 //   nothing published (a lost host: the grid drains instead of spinning on).
 //
@@ -387,22 +389,39 @@ constexpr uint32_t kServiceFront = 2;
 
 __device__ __noinline__ void service_replay(uint64_t kp, int slot) { service_replay_body(kp, slot); }
 
-__device__ __noinline__ uint32_t service_claim(uint64_t kp) {
+// The queued program's data slot (its index-queue entry, then marked started
+// so the host may reuse the entry), or kServiceExit; an index a previous
+// launch already started (a relaunch after an idle drain) is skipped.
+__device__ __forceinline__ uint32_t service_entry(const FKS_CONST ServiceCtl& c, uint32_t idx, uint32_t* slot) {
+  const uint32_t e = idx % c.nq;
+  if (__hip_atomic_load(&c.started[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == idx + 1u) return 0u;
+  *slot = __hip_atomic_load(&c.qslot[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&c.started[e], idx + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return 1u;
+}
+
+__device__ __noinline__ uint32_t service_claim(uint64_t kp, uint32_t* slot) {
   const FKS_CONST ServiceCtl& c = service_args(kp)->c;
   uint32_t* mirror = c.claimed + 32;   // HBM: published (lower bound), then stop
   uint32_t* stopd = c.claimed + 64;
-  const uint32_t idx = __hip_atomic_fetch_add(c.claimed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t idx = __hip_atomic_fetch_add(c.claimed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   uint32_t polls = 0;
   for (;;) {
     uint32_t pub = __hip_atomic_load(mirror, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    if ((int32_t)(idx - pub) < 0) return idx;   // published (wrap-safe)
+    if ((int32_t)(idx - pub) < 0) {   // published (wrap-safe)
+      // (the mirror's acquire orders this after the host's queue writes: the
+      // front workgroup that advanced it acquired them at system scope)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      if (service_entry(c, idx, slot)) return idx;
+      idx = __hip_atomic_fetch_add(c.claimed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      continue;
+    }
     if (__hip_atomic_load(stopd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return kServiceExit;
     if (idx - pub < kServiceFront) {
       const uint32_t hp = __hip_atomic_load(c.published, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
       if ((int32_t)(hp - pub) > 0) {
         __hip_atomic_fetch_max(mirror, hp, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        pub = hp;
-        if ((int32_t)(idx - pub) < 0) return idx;
+        continue;   // published now: take it through the path above
       }
       if (__hip_atomic_load(c.stop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
         __hip_atomic_store(stopd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -417,22 +436,25 @@ __device__ __noinline__ uint32_t service_claim(uint64_t kp) {
 }
 
 __global__ __launch_bounds__(128, 1) void k_native_service(fksk::ServiceArgs) {
-  __shared__ uint32_t claim;
+  __shared__ uint32_t claim[2];   // index, data slot
   for (;;) {
     uint64_t kp = (uint64_t)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(kp));   // re-derived per program, not held across the replay
-    if (threadIdx.x == 0) claim = service_claim(kp);
+    if (threadIdx.x == 0) {
+      uint32_t slot = 0;
+      claim[0] = service_claim(kp, &slot);
+      claim[1] = slot;
+    }
     __syncthreads();
-    const uint32_t idx = claim;
+    const uint32_t idx = claim[0];
     if (idx == kServiceExit) return;   // (uniform across the workgroup)
-    service_replay(kp, (int)(idx % service_args(kp)->c.ring));
+    service_replay(kp, (int)claim[1]);
     if (threadIdx.x >= kWave) {
       // the scoring wave wrote the result row: make it visible to the host, then flag it
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       if (threadIdx.x == kWave) {
-        const uint32_t i2 = claim;
         const FKS_CONST ServiceCtl& c = service_args((uint64_t)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr())->c;
-        __hip_atomic_store(&c.done[i2 % c.ring], i2 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&c.done[claim[1]], claim[0] + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
     __syncthreads();   // both waves are done with the LDS (and with `claim`) before the next program

@@ -49,10 +49,12 @@ struct RowNativeArgs {
 // Control block of the resident program service (replay_kernels.hip k_native_service)
 struct ServiceCtl {
   uint32_t* claimed;            // HBM: [0] next index to claim, [32] mirror of published, [64] of stop
-  const uint32_t* published;    // host: indexes < published are written
+  const uint32_t* published;    // host: indexes < published are queued
   const uint32_t* stop;         // host: 1 = leave once nothing is left to claim
-  uint32_t* done;               // host: [ring] index + 1 once the slot's row is written
-  uint32_t ring;
+  uint32_t* done;               // host: [slots] index + 1 once the slot's row is written
+  const uint32_t* qslot;        // host: [nq] data slot of index i (entry i % nq)
+  uint32_t* started;            // host: [nq] index + 1 once a workgroup read entry i % nq
+  uint32_t nq;
   uint32_t max_idle_polls;
 };
 

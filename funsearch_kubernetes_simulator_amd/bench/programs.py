@@ -276,11 +276,61 @@ def evolved_children(n: int = 2048, workers: int = 8) -> List[CompiledPolicy]:
     return [p for p in progs if p is not None and p.device_ok]
 
 
-def measure_evolved(dev, workload, n: int = 2048, compare: int = 128, cpu_threads: int = 0) -> dict:
+def service_rolling(dev, progs, seconds: float, chunk: int = 256, slots: int = 16, ref=None) -> dict:
+    """Sustained programs/s through the resident program service
+    (`DeviceEvaluator.start_service`), driven like the steady loop: `slots`
+    batches of `chunk` programs in flight, each replaced when it completes;
+    the first pass over `progs` is checked against `ref` rows."""
+    import numpy as np
+    n = len(progs)
+    info = dev.start_service(slots=max(16384, 4 * chunk * slots), share=1.0)
+    base = dev.SERVICE_SLOT_BASE
+    nxt, done, inflight, lat = 0, 0, {}, []
+    first = [None] * (-(-n // chunk))
+    try:
+        t0 = time.perf_counter()
+        while True:
+            for s in range(slots):
+                if s not in inflight and time.perf_counter() - t0 < seconds:
+                    lo = nxt % n
+                    part = progs[lo:lo + chunk] if lo + chunk <= n else progs[lo:] + progs[:lo + chunk - n]
+                    dev.submit_native(base + s, part)
+                    inflight[s] = (time.perf_counter(), nxt)
+                    nxt += chunk
+            if not inflight:
+                break
+            busy = True
+            for s in list(inflight):
+                if dev.ready(base + s):
+                    tab = dev.wait(base + s)
+                    t_sub, at = inflight.pop(s)
+                    lat.append(time.perf_counter() - t_sub)
+                    if at + chunk <= n and at % chunk == 0:
+                        first[at // chunk] = tab
+                    done += chunk
+                    busy = False
+            if busy:
+                time.sleep(0.0005)
+        wall = time.perf_counter() - t0
+    finally:
+        dev.stop_service()
+    rec = {"seconds": round(wall, 3), "programs": done, "evals_per_s": round(done / wall, 1), "chunk": chunk,
+           "batches_in_flight": slots, "resident_workgroups": int(info["blocks"]),
+           "batch_latency_mean_s": round(float(np.mean(lat)), 4) if lat else None}
+    if ref is not None:
+        parts = [(k, t) for k, t in enumerate(first) if t is not None]
+        rec["checked"] = sum(len(t) for _, t in parts)
+        rec["bit_identical"] = all(bool((t == ref[k * chunk:k * chunk + len(t)]).all()) for k, t in parts)
+    return rec
+
+
+def measure_evolved(dev, workload, n: int = 2048, compare: int = 128, cpu_threads: int = 0,
+                    service_s: float = 0.0) -> dict:
     """The evolved-population children (EVOLVED_SET) at LLM-batch scale: split
     over the device's slots, all in flight at once, JIT included (first pass)
     and cached (second pass); mean replayed events, exception fraction, and the
-    first `compare` rows checked against the CPU VM."""
+    first `compare` rows checked against the CPU VM.  service_s > 0: also the
+    sustained rate through the resident program service (`service_rolling`)."""
     import numpy as np
     from ..engine import COLS
     from ..ops import cpu_engine as ce
@@ -314,6 +364,7 @@ def measure_evolved(dev, workload, n: int = 2048, compare: int = 128, cpu_thread
     if not dev.options.get("trace_hash", True):
         a, b = a[:, :COLS["trace_hash_hi"]], b[:, :COLS["trace_hash_hi"]]
     st = dev.native_compiler.stats
+    svc = service_rolling(dev, progs, service_s, ref=tab2) if service_s > 0 else None
     return {"programs": n, "source": f"data/populations/{EVOLVED_SET}", "bytecode_compile_s": round(t_compile, 3),
             "native": int(sum(int(b.ok.sum()) for b in batches)),
             "new_shapes": int(sum(int(b.compiled) for b in batches)),
@@ -322,4 +373,5 @@ def measure_evolved(dev, workload, n: int = 2048, compare: int = 128, cpu_thread
             "exception_fraction": round(float((tab[:, COLS["exc"]] != 0).mean()), 4),
             "repeat_identical": bool((tab == tab2).all()),
             "compared_vs_cpu_vm": int(cmp.sum()), "bit_identical": bool((a[cmp] == b[cmp]).all()),
-            "baseline_shapes_total": int(st.get("baseline_shapes", 0))}
+            "baseline_shapes_total": int(st.get("baseline_shapes", 0)),
+            **({"service": svc} if svc is not None else {})}

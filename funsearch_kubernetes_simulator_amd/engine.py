@@ -34,7 +34,7 @@ import threading
 import time
 from concurrent.futures import ProcessPoolExecutor
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -469,6 +469,33 @@ class Evaluator:
                     self._bump("faults")
         return out  # type: ignore[return-value]
 
+    def collect_partial(self, pend: "PendingPrograms") -> Tuple[List[Tuple[int, EvalResult]], bool]:
+        """Streaming `collect` (device program service, `DeviceEvaluator.
+        service_take`): the (index, result) pairs of the batch's programs that
+        finished since the last call, and whether the batch is complete; on
+        completion the programs the device did not score are listed in
+        ``pend.fallback_idx`` (for `fallback_async`)."""
+        got: List[Tuple[int, EvalResult]] = []
+        complete = True
+        if pend.native_idx:
+            pos, rows, complete = self.device.service_take(pend.slot)
+            for j, row in zip(pos, rows):
+                i = pend.native_idx[int(j)]
+                if _native_deferred(row, self._bump):
+                    pend.deferred_idx.append(i)
+                    continue
+                r = _row_to_result(row, "hip-native")
+                self._bump("device_native", 1)
+                if self.fault_rate > 0 and self._fault_rng.random() < self.fault_rate:
+                    r = EvalResult(0.0, int(Exc.VALUE), "fault-injection")
+                    self._bump("faults")
+                got.append((i, r))
+        if complete:
+            pend.t_done = time.perf_counter()
+            native = set(pend.native_idx or ())
+            pend.fallback_idx = sorted([i for i in range(len(pend.codes)) if i not in native] + pend.deferred_idx)
+        return got, complete
+
     def fallback_async(self, pend: "PendingPrograms", object_ok: bool = True):
         """Score ``pend.fallback_idx`` on the host engines (CPU VM, then
         CPython unless `object_ok` is False) in a worker thread; the future
@@ -549,6 +576,7 @@ class PendingPrograms:
     t_launch: float = 0.0
     t_done: float = 0.0
     fallback_idx: List[int] = field(default_factory=list)
+    deferred_idx: List[int] = field(default_factory=list)   # device rows deferred to the host (collect_partial)
 
 
 _default: Dict[str, Evaluator] = {}

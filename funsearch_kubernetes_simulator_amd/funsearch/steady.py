@@ -137,6 +137,8 @@ class _Batch:
     new_shapes: int = 0
     jit_s: float = 0.0
     polish: Optional[_Polish] = None
+    results: Optional[list] = None   # streaming (program service): results so far
+    left: int = 0                    # programs not merged yet
 
 
 @dataclass
@@ -207,8 +209,13 @@ class SteadyStateSearch:
         self.slot_base = 0
         if svc is not None and dev is not None and hasattr(dev, "start_service"):
             self.service_cfg = dict(svc)
-            self.slots = max(1, int(svc.get("slots", slots or 12)))
+            # batches in flight at once (a batch holds its entry until its
+            # slowest program is done; results stream out before that) and the
+            # programs kept queued on the grid (`inflight`, default 1.5 x its
+            # resident workgroups, set when the service starts)
+            self.slots = max(1, int(svc.get("slots", slots or 64)))
             self.slot_base = dev.SERVICE_SLOT_BASE
+        self.service_inflight = 0
         if dev is not None:
             # the two-wave kernel sizes its LDS heap top so that every slot's batch
             # stays resident at once (csrc/hip/engine_host.hip.h duo_top)
@@ -326,6 +333,43 @@ class SteadyStateSearch:
                 rec["improved"] = True
         self.fs.log.write(**rec)
 
+    def _stream(self, b: _Batch, merged: List[int], islands, ready: list) -> bool:
+        """Program service: merge the batch's programs that finished since the
+        last look (a straggler -- a replay of millions of events -- holds its
+        own workgroup only, never the other results); on completion the
+        programs left to the host engines are in ``b.pend.fallback_idx``."""
+        t_ph = time.perf_counter()
+        got, complete = self.fs.evaluator.collect_partial(b.pend)
+        for i, r in got:
+            b.results[i] = r
+            b.left -= 1
+            if b.polish is None:
+                isl, code, _ = b.items[i]
+                self._merge_one(islands[isl], code, r.score)
+                merged[isl] += 1
+                self.stats.native += int(r.engine == "hip-native")
+        if b.polish is None:
+            self.stats.evaluations += len(got)
+            self.fs.evaluations += len(got)
+        if complete:
+            b.left = 0
+            if b.polish is None:
+                nfb = len(b.pend.fallback_idx)
+                self.stats.evaluations += nfb     # (merged when their fallback completes)
+                self.fs.evaluations += nfb
+            else:
+                # declined variants are not replayed on the host: the best device-scored setting
+                self._polish_done(b.polish, b.results, ready)
+        self.phase["merge"] += time.perf_counter() - t_ph
+        return bool(got) or complete
+
+    def _log_batch(self, log, ctx, si: int, b: _Batch, batches, ready) -> None:
+        ev_n = [r.n_events for r in b.results if r is not None and r.engine == "hip-native"]
+        log.write(kind="steady_batch", rank=ctx.rank, slot=si, programs=len(b.items), new_shapes=b.new_shapes,
+                  jit_s=round(b.jit_s, 4), device_s=round(time.time() - b.t_launch, 4),
+                  inflight_after=sum(x.left for x in batches if x is not None), queued=len(ready),
+                  events_mean=round(sum(ev_n) / len(ev_n), 1) if ev_n else 0, events_max=max(ev_n) if ev_n else 0)
+
     def _gen_of(self, merged: List[int]) -> List[int]:
         return [m // max(1, s.policies_per_generation) for m, s in zip(merged, self.fs.islands)]
 
@@ -349,11 +393,16 @@ class SteadyStateSearch:
         svc_started = False
         if self.service_cfg is not None:
             sc = self.service_cfg
-            share = float(sc.get("share", 0.75 if fs.coupler is not None else 1.0))
-            ring = max(int(sc.get("ring", 16384)), 4 * self.batch * (self.slots + 2))
-            info = dev.start_service(ring=ring, share=share)
+            # (not the whole chip: JIT module loads and copies run as kernels of
+            # their own, and at full share they waited for workgroups to leave --
+            # tens of seconds of a stalled dispatcher)
+            share = float(sc.get("share", 0.75 if fs.coupler is not None else 0.875))
+            # data slots: the programs queued or running, stragglers included
+            info = dev.start_service(slots=int(sc.get("data_slots", 16384)), share=share)
             svc_started = True
-            fs.log.write(kind="steady_service", rank=ctx.rank, slots=self.slots, share=share, **info)
+            self.service_inflight = int(sc.get("inflight", 0)) or int(1.5 * info["blocks"])
+            fs.log.write(kind="steady_service", rank=ctx.rank, batch_slots=self.slots, share=share,
+                         inflight=self.service_inflight, **info)
         chan = MigrationChannel(fs, fs.migrate_every, start_gen)
         self.channel = chan
         stop = False             # no more children: drain and finish
@@ -393,12 +442,15 @@ class SteadyStateSearch:
         t_prev = t_start
         busy_since = None
         want_buffer = self.batch * (self.slots + self.ahead + 1)
+        if self.service_inflight:
+            # streaming: the grid's queue, plus the batches being staged
+            want_buffer = self.service_inflight + self.batch * (self.ahead + 1)
         next_reset = ((start_gen // fs.reset_every) + 1) * fs.reset_every if fs.reset_every else 0
         try:
             while True:
                 progressed = False
                 # 1) keep producers busy (children from the islands' CURRENT elites)
-                queued = len(ready) + sum(len(b.items) for b in batches if b is not None) + \
+                queued = len(ready) + sum(b.left for b in batches if b is not None) + \
                     sum(len(t) for t, _, pj in staged if pj is None) + self.task_size * len(inflight_tasks)
                 while (not stop and queued < want_buffer + self.task_size * self.producers
                        and len(inflight_tasks) < 2 * self.producers):
@@ -444,7 +496,9 @@ class SteadyStateSearch:
                 if self.polish_every and not stop and len(staged) < self.ahead:
                     job = self._polish_job(merged, start_gen, polish_next)
                     if job is None and self.polish_idle and not staged and len(ready) < self.batch \
-                            and any(b is None for b in batches):
+                            and any(b is None for b in batches) and (
+                                not self.service_inflight
+                                or sum(b.left for b in batches if b is not None) < self.service_inflight // 2):
                         # a slot would idle until the producers refill a batch
                         job = self._polish_job(merged, start_gen, polish_next, idle=True)
                         if job is not None:
@@ -468,13 +522,17 @@ class SteadyStateSearch:
                 for si in range(self.slots):
                     if batches[si] is not None or not staged or not staged[0][1].done():
                         continue
+                    if self.service_inflight and sum(b.left for b in batches if b is not None) \
+                            >= self.service_inflight:
+                        break   # the grid has enough queued: results stream back first
                     take, fut, pjob = staged.popleft()
                     pend = fut.result()
                     with roctx_range(f"steady.launch slot {si} ({len(take)} programs)"):
                         t_ph = time.perf_counter()
                         ev.launch_prepared(pend, self.slot_base + si)
                         self.phase["submit"] += time.perf_counter() - t_ph
-                    b = _Batch(si, take, pend, time.time(), pend.new_shapes, pend.jit_s, pjob)
+                    b = _Batch(si, take, pend, time.time(), pend.new_shapes, pend.jit_s, pjob,
+                               [None] * len(take), len(take))
                     batches[si] = b
                     self.stats.jit_s += pend.jit_s
                     self.stats.new_shapes += pend.new_shapes
@@ -507,7 +565,27 @@ class SteadyStateSearch:
                 # CPU-VM or CPython replay itself)
                 for si in range(self.slots):
                     b = batches[si]
-                    if b is None or not ev.ready(b.pend):
+                    if b is None:
+                        continue
+                    if self.service_cfg is not None:
+                        if self._stream(b, merged, islands, ready):
+                            progressed = True
+                        if b.left > 0:
+                            continue
+                        # complete: its host fallbacks and the batch record
+                        batches[si] = None
+                        if busy_since is not None and all(x is None for x in batches):
+                            self.stats.busy_s += time.time() - busy_since
+                            busy_since = None
+                        if b.polish is None and b.pend.fallback_idx:
+                            fallbacks.append((b.items, ev.fallback_async(b.pend, object_ok=self.host_object),
+                                              len(b.pend.fallback_idx)))
+                        if b.polish is None:
+                            self.stats.batches += 1
+                            self._log_batch(log, ctx, si, b, batches, ready)
+                        progressed = True
+                        continue
+                    if not ev.ready(b.pend):
                         continue
                     t_ph = time.perf_counter()
                     # (no device: a polish batch is scored here, on the host engines)
@@ -588,7 +666,7 @@ class SteadyStateSearch:
                     stop = True        # alone (or no migrations): nobody to agree with
                 # 6) status (time-weighted programs in flight, for the occupancy figure)
                 now = time.time()
-                self.stats.inflight_sum += sum(len(b.items) for b in batches if b is not None) * (now - t_prev)
+                self.stats.inflight_sum += sum(b.left for b in batches if b is not None) * (now - t_prev)
                 self.stats.inflight_n += now - t_prev
                 t_prev = now
                 if now - t_status >= self.status_every_s:
@@ -643,7 +721,7 @@ class SteadyStateSearch:
         wall = max(1e-9, now - t_start)
         busy = st.busy_s + (now - busy_since if busy_since is not None else 0.0)
         fs = self.fs
-        inflight = sum(len(b.items) for b in batches if b is not None)
+        inflight = sum(b.left for b in batches if b is not None)
         # occupancy: programs in flight / programs the device holds resident at the
         # current heap top (device_busy only says that *some* batch was in flight)
         capacity = 0

@@ -271,7 +271,8 @@ class DeviceEvaluator:
         self._native_mods: Dict[int, tuple] = {}   # slot -> JIT modules its batch in flight calls into
         #: the resident program service (start_service): slot -> (P, native rows, first ring index)
         self._svc: Optional[dict] = None
-        self._svc_post: Dict[int, Tuple[int, np.ndarray, int]] = {}
+        self._svc_post: Dict[int, Tuple[int, np.ndarray, int, np.ndarray]] = {}   # slot -> (P, rows, first, data slots)
+        self._svc_taken: Dict[int, list] = {}   # slot -> [rows taken, declined rows reported] (service_take)
 
     def info(self) -> dict:
         d = dict(self._eng.info())
@@ -284,18 +285,19 @@ class DeviceEvaluator:
     #: slots, e.g. the family coupler's, stay below)
     SERVICE_SLOT_BASE = 64
 
-    def start_service(self, ring: int = 16384, share: float = 1.0) -> dict:
+    def start_service(self, slots: int = 16384, share: float = 1.0) -> dict:
         """Launch the resident two-wave grid: from now on every native program
         batch (`submit_native`, any slot) is queued to it instead of launched
         as a kernel of its own, and a batch's `ready` / `wait` follow its own
         programs only -- a slow program no longer holds a launch's CU slots
         while the rest of them idle.  share: fraction of the two-wave kernel's
         resident capacity the grid takes (the rest stays free for other
-        streams' kernels, e.g. the family coupler's row-kernel batches)."""
+        streams' kernels, e.g. the family coupler's row-kernel batches);
+        slots: programs queued or running at most."""
         if self._svc is not None:
             return dict(self._svc)
         self.warm_native()
-        self._svc = dict(self._eng.service_start(int(ring), float(share)))
+        self._svc = dict(self._eng.service_start(int(slots), float(share)))
         if not getattr(self, "_svc_atexit", False):
             # a grid left running at interpreter exit would hold every later
             # device-wide synchronisation (JIT module teardown) until its idle timeout
@@ -396,12 +398,14 @@ class DeviceEvaluator:
             if self._svc is not None:
                 if slot in self._svc_post:
                     raise RuntimeError(f"service slot {slot} still holds a batch")
-                first = -1
+                first, dslots = -1, np.zeros(0, np.int32)
                 if idx.size:
-                    first = self._eng.service_submit(batch.fn[idx], batch.kc, batch.koff[idx])
+                    first, dslots = self._eng.service_submit(batch.fn[idx], batch.kc, batch.koff[idx])
                     if first < 0:
-                        raise RuntimeError("program service ring full: collect finished batches first")
-                self._svc_post[slot] = (len(progs), idx, first)
+                        held = sorted((v[2], v[1].size, k) for k, v in self._svc_post.items() if v[1].size)
+                        raise RuntimeError(f"program service full ({int(idx.size)} programs): batches held "
+                                           f"(first, n, slot) {held[:8]}, service {dict(self._eng.service_info())}")
+                self._svc_post[slot] = (len(progs), idx, first, np.asarray(dslots, np.int32))
             else:
                 self._native_post[slot] = (len(progs), idx)
                 if idx.size:
@@ -468,14 +472,14 @@ class DeviceEvaluator:
         """[P, 13] result table of the batch in flight on `slot`."""
         svc = self._svc_post.pop(slot, None)
         if svc is not None:
-            P, idx, first = svc
+            P, idx, first, dslots = svc
             out = np.zeros((P, len(RESULT_COLUMNS)))
             out[:, 10] = 100.0
             try:
                 if idx.size:
-                    while not self._eng.service_ready(first, int(idx.size)):
+                    while not self._eng.service_ready(first, dslots):
                         time.sleep(0.0002)
-                    out[idx] = self._eng.service_collect(first, int(idx.size))
+                    out[idx] = self._eng.service_collect(first, dslots)
             finally:
                 mods = self._native_mods.pop(slot, None)
                 if mods:
@@ -496,10 +500,44 @@ class DeviceEvaluator:
                 self.native_compiler.release(mods)
         return out
 
+    def service_take(self, slot: int):
+        """Streaming collection from the program service: (positions, rows) of
+        the programs of `slot`'s batch that finished since the last call
+        (positions index the batch as submitted; programs the JIT declined come
+        on the first call with EXC_UNSUPPORTED rows), and whether the batch is
+        now complete (its modules released, the slot free)."""
+        P, idx, first, dslots = self._svc_post[slot]
+        taken = self._svc_taken.setdefault(slot, [0, False])
+        pos_parts, row_parts = [], []
+        if not taken[1]:
+            taken[1] = True
+            rest = np.setdiff1d(np.arange(P), idx)
+            if rest.size:
+                r = np.zeros((rest.size, len(RESULT_COLUMNS)))
+                r[:, 10] = 100.0
+                pos_parts.append(rest)
+                row_parts.append(r)
+        if idx.size:
+            offs, rows = self._eng.service_take(first, dslots)
+            if len(offs):
+                pos_parts.append(idx[np.asarray(offs)])
+                row_parts.append(np.asarray(rows))
+                taken[0] += len(offs)
+        complete = taken[0] >= idx.size
+        if complete:
+            del self._svc_post[slot]
+            del self._svc_taken[slot]
+            mods = self._native_mods.pop(slot, None)
+            if mods:
+                self.native_compiler.release(mods)
+        if not pos_parts:
+            return np.zeros(0, np.int64), np.zeros((0, len(RESULT_COLUMNS))), complete
+        return np.concatenate(pos_parts), np.concatenate(row_parts), complete
+
     def ready(self, slot: int) -> bool:
         svc = self._svc_post.get(slot)
         if svc is not None:
-            return svc[1].size == 0 or self._eng.service_ready(svc[2], int(svc[1].size))
+            return svc[1].size == 0 or self._eng.service_ready(svc[2], svc[3])
         post = self._native_post.get(slot)
         if post is not None and post[1].size == 0:
             return True

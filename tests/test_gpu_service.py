@@ -31,9 +31,9 @@ def _batched(dev, progs, size):
 def test_service_rows_equal_batch_rows(dev):
     progs = programs()[:96]
     want = _batched(dev, progs, 32)
-    info = dev.start_service(ring=64, share=0.25)   # a 64-slot ring: every index wraps
+    info = dev.start_service(slots=64, share=0.25)   # 64 data slots, a 128-entry queue: both wrap
     try:
-        assert info["blocks"] >= 1 and info["ring"] == 64
+        assert info["blocks"] >= 1 and info["slots"] == 64 and info["queue"] == 128
         base = dev.SERVICE_SLOT_BASE
         got = np.zeros_like(want)
         # four batches of 16 in flight at once (the whole ring), collected out of order
@@ -69,7 +69,7 @@ def test_service_budget_exhaustion_and_restart(dev):
     finally:
         dev.native_compiler.budget = 1 << 22
     for _ in range(2):                      # start, stop, start again
-        dev.start_service(ring=256, share=0.5)
+        dev.start_service(slots=256, share=0.5)
         try:
             tab = dev.evaluate_native([runaway] + good)
         finally:
@@ -86,7 +86,7 @@ def test_service_many_small_batches(dev):
     one and two programs at a time: the claim / publish / done handshake."""
     progs = programs()[:40]
     want = _batched(dev, progs, 40)
-    dev.start_service(ring=64, share=1.0)
+    dev.start_service(slots=64, share=1.0)
     try:
         got = []
         for rep in range(3):

@@ -1,9 +1,11 @@
 """DeviceEvaluator's routing of native batches to the resident program service
-(ops/hip_engine.py start_service / submit_native / ready / wait), against a
-stand-in engine on the CPU: slots map to ring index ranges, rows the device
-did not take come back EXC_UNSUPPORTED, the ring-full refusal surfaces, and
-modules are held until the batch is collected.  The device side is covered by
-tests/test_gpu_service.py."""
+(ops/hip_engine.py start_service / submit_native / ready / wait /
+service_take), against a stand-in engine on the CPU that models the data
+slots and done flags of csrc/hip/engine_host.hip.h: batches map to index
+ranges and slots, rows the device did not take come back EXC_UNSUPPORTED, a
+full service refuses, streaming collection returns finished rows early (a
+straggler holds its own slot only), and modules are held until a batch is
+complete.  The device side is covered by tests/test_gpu_service.py."""
 import types
 
 import numpy as np
@@ -13,37 +15,59 @@ from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
 
 
 class _FakeEngine:
-    def __init__(self, ring):
-        self.ring, self.published, self.rows, self.done = ring, 0, {}, set()
-        self.started = self.stopped = 0
+    def __init__(self, nslots):
+        self.nslots, self.published = nslots, 0
+        self.free = list(range(nslots))[::-1]
+        self.row = {}           # slot -> fn value (the "result")
+        self.held = {}          # slot -> index
+        self.done = set()       # indexes finished on the "device"
+        self.stopped = 0
 
-    def service_start(self, ring, share):
-        self.started += 1
-        return {"blocks": 8, "ring": ring, "per_cu": 8, "heap_top": 63, "lds": 1}
+    def service_start(self, slots, share):
+        return {"blocks": 8, "slots": slots, "queue": 2 * slots, "per_cu": 8, "heap_top": 63, "lds": 1}
 
     def service_submit(self, fn, kc, koff):
-        if self.published + len(fn) - min(self.rows or [self.published]) > self.ring:
-            return -1
+        if len(self.free) < len(fn):
+            return -1, np.zeros(0, np.int32)
         first = self.published
+        slots = []
         for i, f in enumerate(fn):
-            self.rows[first + i] = float(f)
+            s = self.free.pop()
+            self.row[s], self.held[s] = float(f), first + i
+            slots.append(s)
         self.published += len(fn)
-        return first
+        return first, np.array(slots, np.int32)
 
-    def service_ready(self, first, n):
-        return all(first + i in self.done for i in range(n))
+    def _done(self, first, i, s):
+        return self.held.get(int(s)) == first + i and first + i in self.done
 
-    def service_collect(self, first, n):
-        out = np.zeros((n, 13))
-        for i in range(n):
-            out[i, 0] = self.rows.pop(first + i)
+    def service_ready(self, first, slots):
+        return all(self._done(first, i, s) for i, s in enumerate(slots))
+
+    def service_collect(self, first, slots):
+        out = np.zeros((len(slots), 13))
+        for i, s in enumerate(slots):
+            out[i, 0] = self.row[int(s)]
+            self._free(int(s))
         return out
+
+    def service_take(self, first, slots):
+        offs = [i for i, s in enumerate(slots) if self._done(first, i, s)]
+        rows = np.zeros((len(offs), 13))
+        for k, i in enumerate(offs):
+            rows[k, 0] = self.row[int(slots[i])]
+            self._free(int(slots[i]))
+        return np.array(offs, np.int32), rows
+
+    def _free(self, s):
+        del self.held[s]
+        self.free.append(s)
 
     def service_stop(self):
         self.stopped += 1
 
     def service_info(self):
-        return {"blocks": 8}
+        return {"blocks": 8, "unconsumed": self.nslots - len(self.free)}
 
 
 class _FakeCompiler:
@@ -61,22 +85,23 @@ class _FakeCompiler:
         self.released.append(mods)
 
 
-def _dev(ring=8):
+def _dev(nslots=8):
     d = object.__new__(he.DeviceEvaluator)
-    d._eng = _FakeEngine(ring)
+    d._eng = _FakeEngine(nslots)
     d._jit = _FakeCompiler()
     d.math_exact = True
-    d._native_post, d._native_mods, d._svc, d._svc_post = {}, {}, None, {}
+    d._native_post, d._native_mods, d._svc, d._svc_post, d._svc_taken = {}, {}, None, {}, {}
     d._warm_s = 0.0
+    d._svc_atexit = True
     return d
 
 
 def test_service_routes_batches_by_slot():
     d = _dev()
-    d.start_service(ring=8, share=1.0)
+    d.start_service(slots=8, share=1.0)
     base = d.SERVICE_SLOT_BASE
-    d.submit_native(base, ["a", "host", "b"])        # native rows 0 and 2 -> ring indexes 0, 1
-    d.submit_native(base + 1, ["c"])                 # ring index 2
+    d.submit_native(base, ["a", "host", "b"])        # native rows 0 and 2 -> indexes 0, 1
+    d.submit_native(base + 1, ["c"])                 # index 2
     assert not d.ready(base) and not d.ready(base + 1)
     d._eng.done.update({2})
     assert d.ready(base + 1) and not d.ready(base)
@@ -88,7 +113,7 @@ def test_service_routes_batches_by_slot():
     assert out0[1, 10] == 100.0                      # not taken by the device: EXC_UNSUPPORTED
     assert ("m", 1) in d._jit.released and ("m", 3) in d._jit.released
     with pytest.raises(RuntimeError):
-        d.submit_native(base, ["x"] * 9)             # more than the ring holds
+        d.submit_native(base, ["x"] * 9)             # more programs than data slots
     d.stop_service()
     assert d._eng.stopped == 1 and d.service is None
 
@@ -107,3 +132,26 @@ def test_all_host_batch_is_ready_at_once():
     d.submit_native(3, ["host", "host"])
     assert d.ready(3)
     assert (d.wait(3)[:, 10] == 100.0).all()
+
+
+def test_streaming_take_returns_finished_rows_early():
+    """A straggler keeps its own data slot; the rest of its batch's rows and
+    slots come back (and are reused by later batches) before it finishes."""
+    d = _dev(nslots=4)
+    d.start_service(slots=4)
+    d.submit_native(0, ["a", "host", "b", "c"])      # indexes 0, 1, 2 in three data slots
+    pos, rows, complete = d.service_take(0)          # nothing done yet: the declined row only
+    assert list(pos) == [1] and rows[0, 10] == 100.0 and not complete
+    d._eng.done.update({0, 2})                       # index 1 ("b") is the straggler
+    pos, rows, complete = d.service_take(0)
+    assert sorted(pos.tolist()) == [0, 3] and not complete
+    assert sorted(rows[:, 0].tolist()) == [10.0, 40.0]
+    d.submit_native(1, ["d", "e", "f"])              # reuses the two freed slots + the spare one
+    d._eng.done.update({3, 4, 5})
+    assert d.service_take(1)[2]
+    pos, rows, complete = d.service_take(0)
+    assert len(pos) == 0 and not complete
+    d._eng.done.add(1)
+    pos, rows, complete = d.service_take(0)
+    assert pos.tolist() == [2] and rows[0, 0] == 30.0 and complete
+    assert ("m", 4) in d._jit.released and 0 not in d._svc_post

@@ -101,7 +101,7 @@ def main():
     out["batch_rolling"]["chunk"] = args.batch_chunk
     print(json.dumps({"batch_rolling": out["batch_rolling"]}), flush=True)
 
-    info = dev.start_service(ring=max(16384, 4 * args.chunk * args.service_slots), share=args.share)
+    info = dev.start_service(slots=max(16384, 4 * args.chunk * args.service_slots), share=args.share)
     out["service_info"] = info
     try:
         base = dev.SERVICE_SLOT_BASE
