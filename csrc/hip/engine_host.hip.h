@@ -621,10 +621,6 @@ class DeviceEngine {
     return py::make_tuple((int64_t)first, slots);
   }
 
-  bool svc_done(uint32_t idx, int32_t slot) const {
-    return slot >= 0 && (uint32_t)slot < svc_.nslots && svc_.ld(svc_.done, (uint32_t)slot) == idx + 1u;
-  }
-
   // if the grid drained (nothing published for ~1 min) while programs wait,
   // launch it again from the first index no workgroup started
   void service_revive() {
@@ -635,60 +631,26 @@ class DeviceEngine {
     if (lo != v.published) service_launch(lo);
   }
 
-  // all of the submission (first, slots) replayed?
-  bool service_ready(int64_t first, py::array_t<int32_t, py::array::c_style | py::array::forcecast> slots) {
-    const int n = (int)slots.size();
-    for (int i = 0; i < n; ++i)
-      if (!svc_done((uint32_t)first + (uint32_t)i, slots.at(i))) {
-        service_revive();
-        return false;
-      }
-    return true;
-  }
-
-  // result rows of the submission (must be ready); frees its slots
-  py::array_t<double> service_collect(int64_t first, py::array_t<int32_t, py::array::c_style | py::array::forcecast> slots) {
+  // every program finished since the last call, over all submissions:
+  // (indexes, rows), their slots freed -- one scan of the data slots instead of
+  // one call per submission (the steady loop keeps dozens in flight)
+  py::tuple service_poll() {
     Service& v = svc_;
-    if (!service_ready(first, slots)) throw std::runtime_error("service_collect: not every program is done");
-    const int n = (int)slots.size();
-    py::array_t<double> out({(py::ssize_t)n, (py::ssize_t)13});
-    double* o = out.mutable_data();
-    for (int i = 0; i < n; ++i) {
-      const uint32_t slot = (uint32_t)slots.at(i);
-      std::memcpy(o + (size_t)i * 13, v.tab.as<double>() + (size_t)slot * 13, 13 * sizeof(double));
-      if (v.busy[slot] && v.held[slot] == (uint32_t)first + (uint32_t)i) {
-        v.busy[slot] = 0;
-        v.free_slots.push_back(slot);
-      }
-    }
-    return out;
-  }
-
-  // streaming collection: the rows of the submission finished since the last
-  // call -- (offsets into it, rows) -- their slots freed.  A caller that takes
-  // rows as they finish never waits for the submission's slowest program.
-  py::tuple service_take(int64_t first, py::array_t<int32_t, py::array::c_style | py::array::forcecast> slots) {
-    Service& v = svc_;
-    const int n = (int)slots.size();
-    std::vector<int32_t> offs;
-    for (int i = 0; i < n; ++i) {
-      const uint32_t idx = (uint32_t)first + (uint32_t)i;
-      const int32_t slot = slots.at(i);
-      if (slot < 0 || (uint32_t)slot >= v.nslots || !v.busy[slot] || v.held[slot] != idx) continue;   // taken
-      if (svc_done(idx, slot)) offs.push_back(i);
-    }
-    py::array_t<int32_t> o((py::ssize_t)offs.size());
-    py::array_t<double> rows({(py::ssize_t)offs.size(), (py::ssize_t)13});
+    std::vector<uint32_t> hit;
+    for (uint32_t slot = 0; slot < v.nslots; ++slot)
+      if (v.busy[slot] && v.ld(v.done, slot) == v.held[slot] + 1u) hit.push_back(slot);
+    py::array_t<int64_t> idx((py::ssize_t)hit.size());
+    py::array_t<double> rows({(py::ssize_t)hit.size(), (py::ssize_t)13});
     double* r = rows.mutable_data();
-    for (size_t k = 0; k < offs.size(); ++k) {
-      const uint32_t slot = (uint32_t)slots.at(offs[k]);
-      o.mutable_data()[k] = offs[k];
+    for (size_t k = 0; k < hit.size(); ++k) {
+      const uint32_t slot = hit[k];
+      idx.mutable_data()[k] = (int64_t)v.held[slot];
       std::memcpy(r + k * 13, v.tab.as<double>() + (size_t)slot * 13, 13 * sizeof(double));
       v.busy[slot] = 0;
       v.free_slots.push_back(slot);
     }
-    if (offs.empty() && n > 0) service_revive();
-    return py::make_tuple(o, rows);
+    if (hit.empty() && v.free_slots.size() < v.nslots) service_revive();
+    return py::make_tuple(idx, rows);
   }
 
   // tell the grid to leave once nothing published is left, and wait for it

@@ -459,9 +459,7 @@ PYBIND11_MODULE(_fks_hip, m) {
       .def("submit_programs", &DeviceEngine::submit_programs)
       .def("service_start", &DeviceEngine::service_start, py::arg("slots") = 16384, py::arg("share") = 1.0)
       .def("service_submit", &DeviceEngine::service_submit)
-      .def("service_ready", &DeviceEngine::service_ready)
-      .def("service_collect", &DeviceEngine::service_collect)
-      .def("service_take", &DeviceEngine::service_take)
+      .def("service_poll", &DeviceEngine::service_poll)
       .def("service_stop", &DeviceEngine::service_stop)
       .def("service_info", &DeviceEngine::service_info)
       .def("ready", &DeviceEngine::ready)

@@ -13,6 +13,7 @@ On a GPU box the extension must load: there is no silent CPU fallback here
 
 from __future__ import annotations
 
+import bisect
 import heapq
 import math
 import os
@@ -273,6 +274,11 @@ class DeviceEvaluator:
         self._svc: Optional[dict] = None
         self._svc_post: Dict[int, Tuple[int, np.ndarray, int, np.ndarray]] = {}   # slot -> (P, rows, first, data slots)
         self._svc_taken: Dict[int, list] = {}   # slot -> [rows taken, declined rows reported] (service_take)
+        self._svc_firsts: List[int] = []         # first index of every batch in flight (sorted) ...
+        self._svc_keys: List[int] = []           # ... and its slot key
+        self._svc_buf: Dict[int, list] = {}      # slot key -> [(offset, row)] polled, not taken yet
+        self._svc_pumped = 0.0
+        self._svc_lock = threading.Lock()
 
     def info(self) -> dict:
         d = dict(self._eng.info())
@@ -396,16 +402,23 @@ class DeviceEvaluator:
                                     "codes": [progs[i].source for i in idx]}) + "\n")
         try:
             if self._svc is not None:
-                if slot in self._svc_post:
-                    raise RuntimeError(f"service slot {slot} still holds a batch")
-                first, dslots = -1, np.zeros(0, np.int32)
-                if idx.size:
-                    first, dslots = self._eng.service_submit(batch.fn[idx], batch.kc, batch.koff[idx])
-                    if first < 0:
-                        held = sorted((v[2], v[1].size, k) for k, v in self._svc_post.items() if v[1].size)
-                        raise RuntimeError(f"program service full ({int(idx.size)} programs): batches held "
-                                           f"(first, n, slot) {held[:8]}, service {dict(self._eng.service_info())}")
-                self._svc_post[slot] = (len(progs), idx, first, np.asarray(dslots, np.int32))
+                with self._svc_lock:   # (indexes and their registration in one step: the list stays sorted)
+                    if slot in self._svc_post:
+                        raise RuntimeError(f"service slot {slot} still holds a batch")
+                    first, dslots = -1, np.zeros(0, np.int32)
+                    if idx.size:
+                        first, dslots = self._eng.service_submit(batch.fn[idx], batch.kc, batch.koff[idx])
+                        if first < 0:
+                            held = sorted((v[2], v[1].size, k) for k, v in self._svc_post.items() if v[1].size)
+                            raise RuntimeError(
+                                f"program service full ({int(idx.size)} programs): batches held (first, n, slot) "
+                                f"{held[:8]}, service {dict(self._eng.service_info())}")
+                    self._svc_post[slot] = (len(progs), idx, first, np.asarray(dslots, np.int32))
+                    if idx.size:
+                        self._svc_firsts.append(int(first))
+                        self._svc_keys.append(slot)
+                    self._native_mods[slot] = batch.modules
+                return batch
             else:
                 self._native_post[slot] = (len(progs), idx)
                 if idx.size:
@@ -470,21 +483,8 @@ class DeviceEvaluator:
 
     def wait(self, slot: int) -> np.ndarray:
         """[P, 13] result table of the batch in flight on `slot`."""
-        svc = self._svc_post.pop(slot, None)
-        if svc is not None:
-            P, idx, first, dslots = svc
-            out = np.zeros((P, len(RESULT_COLUMNS)))
-            out[:, 10] = 100.0
-            try:
-                if idx.size:
-                    while not self._eng.service_ready(first, dslots):
-                        time.sleep(0.0002)
-                    out[idx] = self._eng.service_collect(first, dslots)
-            finally:
-                mods = self._native_mods.pop(slot, None)
-                if mods:
-                    self.native_compiler.release(mods)
-            return out
+        if slot in self._svc_post:
+            return self._service_wait(slot)
         post = self._native_post.pop(slot, None)
         if post is None:
             return self._eng.wait(slot)
@@ -500,44 +500,95 @@ class DeviceEvaluator:
                 self.native_compiler.release(mods)
         return out
 
+    #: seconds between two scans of the service's done flags (`_service_pump`)
+    SERVICE_POLL_S = 0.001
+
+    def _service_pump(self, min_interval_s: Optional[float] = None) -> None:
+        """One `service_poll` (every finished program, all batches) at most
+        every `min_interval_s`; rows are filed under their batches.  (Caller
+        holds `_svc_lock`: island / coupler threads collect concurrently.)"""
+        now = time.perf_counter()
+        if now - self._svc_pumped < (self.SERVICE_POLL_S if min_interval_s is None else min_interval_s):
+            return
+        self._svc_pumped = now
+        ids, rows = self._eng.service_poll()
+        if not len(ids):
+            return
+        firsts = self._svc_firsts
+        for k, ix in enumerate(ids.tolist()):
+            j = bisect.bisect_right(firsts, ix) - 1
+            self._svc_buf.setdefault(self._svc_keys[j], []).append((ix - firsts[j], rows[k]))
+
     def service_take(self, slot: int):
         """Streaming collection from the program service: (positions, rows) of
         the programs of `slot`'s batch that finished since the last call
         (positions index the batch as submitted; programs the JIT declined come
         on the first call with EXC_UNSUPPORTED rows), and whether the batch is
         now complete (its modules released, the slot free)."""
-        P, idx, first, dslots = self._svc_post[slot]
-        taken = self._svc_taken.setdefault(slot, [0, False])
-        pos_parts, row_parts = [], []
-        if not taken[1]:
-            taken[1] = True
-            rest = np.setdiff1d(np.arange(P), idx)
-            if rest.size:
-                r = np.zeros((rest.size, len(RESULT_COLUMNS)))
-                r[:, 10] = 100.0
-                pos_parts.append(rest)
-                row_parts.append(r)
-        if idx.size:
-            offs, rows = self._eng.service_take(first, dslots)
-            if len(offs):
-                pos_parts.append(idx[np.asarray(offs)])
-                row_parts.append(np.asarray(rows))
-                taken[0] += len(offs)
-        complete = taken[0] >= idx.size
-        if complete:
-            del self._svc_post[slot]
-            del self._svc_taken[slot]
-            mods = self._native_mods.pop(slot, None)
-            if mods:
-                self.native_compiler.release(mods)
+        with self._svc_lock:
+            P, idx, first, _ = self._svc_post[slot]
+            taken = self._svc_taken.setdefault(slot, [0, False])
+            pos_parts, row_parts = [], []
+            if not taken[1]:
+                taken[1] = True
+                rest = np.setdiff1d(np.arange(P), idx)
+                if rest.size:
+                    r = np.zeros((rest.size, len(RESULT_COLUMNS)))
+                    r[:, 10] = 100.0
+                    pos_parts.append(rest)
+                    row_parts.append(r)
+            if idx.size:
+                self._service_pump()
+                got = self._svc_buf.pop(slot, None)
+                if got:
+                    pos_parts.append(idx[np.array([o for o, _ in got])])
+                    row_parts.append(np.array([r for _, r in got]))
+                    taken[0] += len(got)
+            complete = taken[0] >= idx.size
+            if complete:
+                self._service_forget(slot)
         if not pos_parts:
             return np.zeros(0, np.int64), np.zeros((0, len(RESULT_COLUMNS))), complete
         return np.concatenate(pos_parts), np.concatenate(row_parts), complete
 
+    def _service_forget(self, slot: int) -> None:
+        P, idx, first, _ = self._svc_post.pop(slot)
+        self._svc_taken.pop(slot, None)
+        self._svc_buf.pop(slot, None)
+        if idx.size:
+            j = bisect.bisect_left(self._svc_firsts, first)
+            del self._svc_firsts[j], self._svc_keys[j]
+        mods = self._native_mods.pop(slot, None)
+        if mods:
+            self.native_compiler.release(mods)
+
+    def _service_wait(self, slot: int) -> np.ndarray:
+        """Whole-batch collection (`wait` on a service slot)."""
+        P, idx, _, _ = self._svc_post[slot]
+        out = np.zeros((P, len(RESULT_COLUMNS)))
+        out[:, 10] = 100.0
+        try:
+            while idx.size:
+                with self._svc_lock:
+                    self._service_pump(0.0)
+                    got = self._svc_buf.get(slot, [])
+                    if len(got) >= idx.size:
+                        for o, r in got:
+                            out[idx[o]] = r
+                        break
+                time.sleep(0.0002)
+        finally:
+            with self._svc_lock:
+                self._service_forget(slot)
+        return out
+
     def ready(self, slot: int) -> bool:
         svc = self._svc_post.get(slot)
         if svc is not None:
-            return svc[1].size == 0 or self._eng.service_ready(svc[2], svc[3])
+            # (whole batches: callers of ready() / wait() do not use service_take)
+            with self._svc_lock:
+                self._service_pump()
+                return len(self._svc_buf.get(slot, ())) >= svc[1].size
         post = self._native_post.get(slot)
         if post is not None and post[1].size == 0:
             return True

@@ -1,11 +1,12 @@
 """DeviceEvaluator's routing of native batches to the resident program service
 (ops/hip_engine.py start_service / submit_native / ready / wait /
 service_take), against a stand-in engine on the CPU that models the data
-slots and done flags of csrc/hip/engine_host.hip.h: batches map to index
-ranges and slots, rows the device did not take come back EXC_UNSUPPORTED, a
+slots and done flags of csrc/hip/engine_host.hip.h (`service_poll`: every
+finished program, filed under its batch): batches map to index ranges, rows the device did not take come back EXC_UNSUPPORTED, a
 full service refuses, streaming collection returns finished rows early (a
 straggler holds its own slot only), and modules are held until a batch is
 complete.  The device side is covered by tests/test_gpu_service.py."""
+import threading
 import types
 
 import numpy as np
@@ -38,26 +39,14 @@ class _FakeEngine:
         self.published += len(fn)
         return first, np.array(slots, np.int32)
 
-    def _done(self, first, i, s):
-        return self.held.get(int(s)) == first + i and first + i in self.done
-
-    def service_ready(self, first, slots):
-        return all(self._done(first, i, s) for i, s in enumerate(slots))
-
-    def service_collect(self, first, slots):
-        out = np.zeros((len(slots), 13))
-        for i, s in enumerate(slots):
-            out[i, 0] = self.row[int(s)]
-            self._free(int(s))
-        return out
-
-    def service_take(self, first, slots):
-        offs = [i for i, s in enumerate(slots) if self._done(first, i, s)]
-        rows = np.zeros((len(offs), 13))
-        for k, i in enumerate(offs):
-            rows[k, 0] = self.row[int(slots[i])]
-            self._free(int(slots[i]))
-        return np.array(offs, np.int32), rows
+    def service_poll(self):
+        hit = sorted(s for s, ix in self.held.items() if ix in self.done)
+        ids = np.array([self.held[s] for s in hit], np.int64)
+        rows = np.zeros((len(hit), 13))
+        for k, s in enumerate(hit):
+            rows[k, 0] = self.row[s]
+            self._free(s)
+        return ids, rows
 
     def _free(self, s):
         del self.held[s]
@@ -91,6 +80,9 @@ def _dev(nslots=8):
     d._jit = _FakeCompiler()
     d.math_exact = True
     d._native_post, d._native_mods, d._svc, d._svc_post, d._svc_taken = {}, {}, None, {}, {}
+    d._svc_firsts, d._svc_keys, d._svc_buf, d._svc_pumped = [], [], {}, 0.0
+    d._svc_lock = threading.Lock()
+    d.SERVICE_POLL_S = 0.0
     d._warm_s = 0.0
     d._svc_atexit = True
     return d
@@ -155,3 +147,30 @@ def test_streaming_take_returns_finished_rows_early():
     pos, rows, complete = d.service_take(0)
     assert pos.tolist() == [2] and rows[0, 0] == 30.0 and complete
     assert ("m", 4) in d._jit.released and 0 not in d._svc_post
+
+
+def test_evaluator_collect_partial_streams_and_lists_fallbacks(default_workload):
+    """`Evaluator.collect_partial`: finished native rows become results as they
+    arrive; on completion the programs the device did not score (not native,
+    or rows deferred to the host) are in ``fallback_idx``."""
+    from funsearch_kubernetes_simulator_amd.engine import COLS, Evaluator, PendingPrograms
+
+    class _Dev:
+        def __init__(self):
+            self.calls = 0
+
+        def service_take(self, slot):
+            self.calls += 1
+            if self.calls == 1:   # native position 0 finished, scored
+                r = np.zeros((1, 13)); r[0, COLS["score"]] = 0.5; r[0, COLS["n_events"]] = 7
+                return np.array([0]), r, False
+            r = np.zeros((1, 13)); r[0, COLS["exc"]] = 100.0   # position 1: declined -> host
+            return np.array([1]), r, True
+
+    ev = Evaluator(default_workload, device="cpu")
+    ev.device = _Dev()
+    pend = PendingPrograms(codes=["a", "b", "c"], slot=64, native_idx=[0, 2])
+    got, complete = ev.collect_partial(pend)
+    assert not complete and len(got) == 1 and got[0][0] == 0 and got[0][1].score == 0.5
+    got, complete = ev.collect_partial(pend)
+    assert complete and got == [] and pend.fallback_idx == [1, 2]
