@@ -303,6 +303,13 @@ class DeviceEvaluator:
         if self._svc is not None:
             return dict(self._svc)
         self.warm_native()
+        nc = self.native_compiler
+        nc.defer_unloads = True
+        # modules are small next to 288 GB of HBM: keep ~8x more live while
+        # retirements cannot unload (a 200 s steady run loads ~2,000)
+        self._svc_saved_max = nc.max_modules
+        if 0 < nc.max_modules < 16384:
+            nc.max_modules = 16384
         self._svc = dict(self._eng.service_start(int(slots), float(share)))
         if not getattr(self, "_svc_atexit", False):
             # a grid left running at interpreter exit would hold every later
@@ -322,6 +329,10 @@ class DeviceEvaluator:
             self.wait(slot)
         self._eng.service_stop()
         self._svc = None
+        nc = self.native_compiler
+        nc.defer_unloads = False
+        nc.max_modules = getattr(self, "_svc_saved_max", nc.max_modules)
+        nc.flush_unloads()
 
     @property
     def service(self) -> Optional[dict]:

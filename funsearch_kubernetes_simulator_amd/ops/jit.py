@@ -362,6 +362,10 @@ class NativeCompiler:
         # (round 5), and most of a retired module's shapes were one-off children --
         # `recompiled_shapes` counts the evicted shapes that did come back
         self.max_modules = int(os.environ.get("FKS_JIT_MAX_MODULES", "2048"))
+        #: retired modules stay loaded until `flush_unloads` (set while the
+        #: device's program service runs: an unload waits on the device)
+        self.defer_unloads = False
+        self._deferred: List[object] = []
         self._evicted: set = set()     # hashes of evicted shape keys (recompile accounting)
         self._lock = threading.Lock()
         self._inflight: Dict[str, threading.Event] = {}
@@ -540,11 +544,30 @@ class NativeCompiler:
                 victims.append(rec)
             self.stats["retired_modules"] += len(victims)
             self.stats["live_modules"] = len(self._modules)
+        if getattr(self, "defer_unloads", False):
+            # a persistent grid is running (the program service): hipModuleUnload
+            # waits on the device (~0.2 s per module measured, 107 s for one
+            # retirement burst), so the modules stay loaded until `flush_unloads`
+            with self._lock:
+                self._deferred.extend(victims)
+            return
         t0 = time.perf_counter()
         for rec in victims:
             rec.handle.unload()
         with self._lock:
             self.stats["unload_s"] += time.perf_counter() - t0
+
+    def flush_unloads(self) -> int:
+        """Unload the modules retired while `defer_unloads` was set (call with
+        no persistent kernel running); returns their number."""
+        with self._lock:
+            victims, self._deferred = getattr(self, "_deferred", []), []
+        t0 = time.perf_counter()
+        for rec in victims:
+            rec.handle.unload()
+        with self._lock:
+            self.stats["unload_s"] += time.perf_counter() - t0
+        return len(victims)
 
     # -- background tier-up --------------------------------------------------------------
     def _tierup_candidates(self, keys, progs):

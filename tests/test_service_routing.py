@@ -60,8 +60,14 @@ class _FakeEngine:
 
 
 class _FakeCompiler:
+    max_modules = 2048
+    defer_unloads = False
+
     def __init__(self):
         self.released = []
+
+    def flush_unloads(self):
+        return 0
 
     def prepare(self, progs):
         n = len(progs)
