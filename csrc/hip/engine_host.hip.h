@@ -28,6 +28,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -87,6 +88,41 @@ inline double fks_recip_verified(int64_t d, int64_t hi, std::vector<std::pair<st
   return z;
 }
 
+// hipFree / hipHostFree wait for the whole device.  While a persistent kernel
+// runs (the program service) such a wait lasts until the kernel leaves, so
+// frees are parked here instead and done when it has stopped.
+struct FreeQueue {
+  std::mutex mu;
+  bool defer = false;
+  std::vector<std::pair<void*, bool>> parked;   // (pointer, pinned host memory)
+  void free(void* p, bool host) {
+    if (!p) return;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      if (defer) { parked.push_back({p, host}); return; }
+    }
+    if (host) (void)hipHostFree(p);
+    else (void)hipFree(p);
+  }
+  size_t resume() {   // stop deferring and free what was parked
+    std::vector<std::pair<void*, bool>> items;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      defer = false;
+      items.swap(parked);
+    }
+    for (auto& it : items) {
+      if (it.second) (void)hipHostFree(it.first);
+      else (void)hipFree(it.first);
+    }
+    return items.size();
+  }
+};
+inline FreeQueue& free_queue() {
+  static FreeQueue q;
+  return q;
+}
+
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -95,12 +131,12 @@ struct DevBuf {
     // geometric growth: hipFree waits for the whole device (every slot), so
     // regrowing per batch would serialise the slots' streams
     bytes = std::max(bytes, cap + cap / 2);
-    if (p) HIP_OK(hipFree(p));
+    free_queue().free(p, false);
     HIP_OK(hipMalloc(&p, bytes));
     cap = bytes;
   }
   void release() {
-    if (p) (void)hipFree(p);
+    free_queue().free(p, false);
     p = nullptr;
     cap = 0;
   }
@@ -120,14 +156,14 @@ struct HostBuf {
     if (bytes <= cap) return;
     // geometric growth, as DevBuf: batch sizes vary (native constant blocks)
     bytes = std::max(bytes, cap + cap / 2);
-    if (p) HIP_OK(hipHostFree(p));
+    free_queue().free(p, true);
     // coherent (fine-grained): read and written while a kernel runs (the program service)
     HIP_OK(hipHostMalloc(&p, bytes, hipHostMallocMapped | (coherent ? hipHostMallocCoherent : 0)));
     HIP_OK(hipHostGetDevicePointer(&d, p, 0));
     cap = bytes;
   }
   void release() {
-    if (p) (void)hipHostFree(p);
+    free_queue().free(p, true);
     p = d = nullptr;
     cap = 0;
   }
@@ -268,6 +304,7 @@ class DeviceEngine {
       __atomic_store_n(svc_.ctl.as<uint32_t>() + 1, 1u, __ATOMIC_RELEASE);
       (void)hipStreamSynchronize(svc_.stream);
       svc_.running = false;
+      free_queue().resume();
     }
     svc_.release();
     for (auto& s : slots_) {
@@ -568,6 +605,7 @@ class DeviceEngine {
     v.free_slots.resize(S);
     for (uint32_t i = 0; i < v.nslots; ++i) v.free_slots[i] = v.nslots - 1 - i;
     v.published = 0;
+    free_queue().defer = true;   // (set before the launch; the grid's own buffers are sized above)
     service_launch(0);
     py::dict d;
     d["blocks"] = v.blocks; d["per_cu"] = per_cu; d["heap_top"] = v.T; d["lds"] = (int64_t)v.lds;
@@ -663,6 +701,7 @@ class DeviceEngine {
       HIP_OK(hipStreamSynchronize(v.stream));
     }
     v.running = false;
+    free_queue().resume();
   }
 
   py::dict service_info() {

@@ -398,6 +398,10 @@ class SteadyStateSearch:
             # tens of seconds of a stalled dispatcher)
             share = float(sc.get("share", 0.75 if fs.coupler is not None else 0.875))
             # data slots: the programs queued or running, stragglers included
+            if fs.coupler is not None:
+                # the coupler's row-kernel batches take part of what the grid
+                # leaves, not all of it: JIT module loads need free slots too
+                dev.set_options(row_wave_share=float(sc.get("coupler_share", 0.25)))
             info = dev.start_service(slots=int(sc.get("data_slots", 16384)), share=share)
             svc_started = True
             self.service_inflight = int(sc.get("inflight", 0)) or int(1.5 * info["blocks"])
