@@ -544,6 +544,7 @@ class DeviceEngine {
   void service_launch(uint32_t first_claim) {
     Service& v = svc_;
     __atomic_store_n(v.ctl.as<uint32_t>() + 1, 0u, __ATOMIC_RELEASE);   // stop = 0
+    __atomic_store_n(v.ctl.as<uint32_t>() + 2, 0u, __ATOMIC_RELEASE);   // abort = 0
     // claim counter, HBM mirror of `published` (a lower bound: every index below
     // it is published) and of `stop` (replay_kernels.hip service_claim)
     uint32_t init[96] = {};
@@ -555,7 +556,8 @@ class DeviceEngine {
     Wl.heap_top = v.T;
     const fksk::BuiltinArgs a{Wl, nullptr, nullptr, nullptr, nullptr, v.res.as<DevResult>(), v.gheap.as<uint64_t>(),
                               nullptr, v.tab.dev<double>()};
-    const RowNativeArgs nat{v.fn.dev<const uint64_t>(), v.kc.dev<const int64_t>(), v.koff.dev<const int32_t>()};
+    const RowNativeArgs nat{v.fn.dev<const uint64_t>(), v.kc.dev<const int64_t>(), v.koff.dev<const int32_t>(),
+                            v.ctl.dev<const uint32_t>() + 2};
     // ~57 s of s_sleep(127) polls with nothing published: the grid drains (a lost host)
     const ServiceCtl c{v.claimed.as<uint32_t>(), v.ctl.dev<const uint32_t>(), v.ctl.dev<const uint32_t>() + 1,
                        v.done.dev<uint32_t>(), v.qslot.dev<const uint32_t>(), v.started.dev<uint32_t>(), v.nq,
@@ -689,6 +691,12 @@ class DeviceEngine {
     }
     if (hit.empty() && v.free_slots.size() < v.nslots) service_revive();
     return py::make_tuple(idx, rows);
+  }
+
+  // end every replay in flight within ~1k events (rows come back EXC_TIMEOUT):
+  // a run that stops does not wait for a straggler's millions of events
+  void service_abort() {
+    if (svc_.running) __atomic_store_n(svc_.ctl.as<uint32_t>() + 2, 1u, __ATOMIC_RELEASE);
   }
 
   // tell the grid to leave once nothing published is left, and wait for it

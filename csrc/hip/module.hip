@@ -461,6 +461,7 @@ PYBIND11_MODULE(_fks_hip, m) {
       .def("service_submit", &DeviceEngine::service_submit)
       .def("service_poll", &DeviceEngine::service_poll)
       .def("service_stop", &DeviceEngine::service_stop)
+      .def("service_abort", &DeviceEngine::service_abort)
       .def("service_info", &DeviceEngine::service_info)
       .def("ready", &DeviceEngine::ready)
       .def("wait", &DeviceEngine::wait)

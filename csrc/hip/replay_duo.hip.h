@@ -42,6 +42,7 @@ struct DuoBox {
   uint32_t rseq;           // creations answered by S (the event index + 1)
   int32_t code;            // DuoReply of the last answer
   uint32_t term;           // H: no more events
+  uint32_t sabort;         // S: the replay was aborted (RowNativeArgs::abort) -- H stops too
   int32_t h_exc, n_repush, n_dropped;
 };
 // Scoring-wave state kept in LDS between events (16 lanes): the mutable node
@@ -183,6 +184,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
     fill_node_tables(W, ntab, lane);
     if (lane == 0) {
       box->item = 0; box->head = 0; box->tail = 0; box->rseq = 0; box->code = DUO_NONE; box->term = 0;
+      box->sabort = 0;
       box->h_exc = EXC_NONE; box->n_repush = 0; box->n_dropped = 0;
     }
   } else {
@@ -232,6 +234,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
       while (k - tail_seen >= (uint32_t)kDuoRing) {
         tail_seen = duo_ld(&box->tail);
         if (k - tail_seen < (uint32_t)kDuoRing) break;
+        if (duo_ld(&box->sabort)) return false;
         __builtin_amdgcn_s_sleep(FKS_DUO_SLEEP);
         if (++spins > kDuoSpinCap) { hexc = EXC_TIMEOUT; return false; }
       }
@@ -259,6 +262,7 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
       if ((int)(top & 3) != kDelete) {
         uint32_t spins = 0;
         while (duo_ld(&box->rseq) != k + 1) {
+          if (duo_ld(&box->sabort)) { hexc = EXC_TIMEOUT; break; }
           __builtin_amdgcn_s_sleep(FKS_DUO_SLEEP);
           if (++spins > kDuoSpinCap) { hexc = EXC_TIMEOUT; break; }
         }
@@ -383,6 +387,12 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
   if constexpr (PROF) plast = __builtin_amdgcn_s_memtime();
   for (;;) {
     asm volatile("" : "+v"(jv));
+    if ((k & 1023u) == 1023u && nat.abort != nullptr &&
+        __hip_atomic_load(nat.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+      exc = EXC_TIMEOUT;   // the host gave up on the replays in flight (a stopping run)
+      if (jv == 0) duo_st(&box->sabort, 1u);
+      break;
+    }
     // next event, or the end of the replay
     uint32_t spins = 0;
     bool have = false;

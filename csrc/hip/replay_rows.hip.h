@@ -45,6 +45,7 @@ struct RowNativeArgs {
   const uint64_t* fn;     // [P] device addresses of the programs' scorers
   const int64_t* kc;      // concatenated constant blocks
   const int32_t* koff;    // [P] offset of policy p's block in kc
+  const uint32_t* abort = nullptr;   // host flag (two-wave kernel): nonzero ends replays early, EXC_TIMEOUT
 };
 // Control block of the resident program service (replay_kernels.hip k_native_service)
 struct ServiceCtl {

@@ -353,11 +353,7 @@ class SteadyStateSearch:
             self.fs.evaluations += len(got)
         if complete:
             b.left = 0
-            if b.polish is None:
-                nfb = len(b.pend.fallback_idx)
-                self.stats.evaluations += nfb     # (merged when their fallback completes)
-                self.fs.evaluations += nfb
-            else:
+            if b.polish is not None:
                 # declined variants are not replayed on the host: the best device-scored setting
                 self._polish_done(b.polish, b.results, ready)
         self.phase["merge"] += time.perf_counter() - t_ph
@@ -391,6 +387,7 @@ class SteadyStateSearch:
             # the replays fill the chip: a probe queued behind them waits seconds
             fs.log.write(kind="steady_warm", rank=ctx.rank, warm_s=round(dev.warm_native(), 3))
         svc_started = False
+        svc_aborted = False
         if self.service_cfg is not None:
             sc = self.service_cfg
             # (not the whole chip: JIT module loads and copies run as kernels of
@@ -582,8 +579,14 @@ class SteadyStateSearch:
                             self.stats.busy_s += time.time() - busy_since
                             busy_since = None
                         if b.polish is None and b.pend.fallback_idx:
-                            fallbacks.append((b.items, ev.fallback_async(b.pend, object_ok=self.host_object),
-                                              len(b.pend.fallback_idx)))
+                            nfb = len(b.pend.fallback_idx)
+                            if svc_aborted:   # (aborted replays and the rest: the run is over)
+                                self.stats.abandoned += nfb
+                            else:             # (merged when their fallback completes)
+                                self.stats.evaluations += nfb
+                                fs.evaluations += nfb
+                                fallbacks.append((b.items, ev.fallback_async(b.pend, object_ok=self.host_object),
+                                                  nfb))
                         if b.polish is None:
                             self.stats.batches += 1
                             self._log_batch(log, ctx, si, b, batches, ready)
@@ -668,6 +671,11 @@ class SteadyStateSearch:
                 want_stop = want_stop or global_best >= threshold or bool(wall_s and time.time() - t_start > wall_s)
                 if want_stop and not chan.active:
                     stop = True        # alone (or no migrations): nobody to agree with
+                if stop and svc_started and not svc_aborted:
+                    # the replays still in flight are not needed: a straggler of
+                    # millions of events would hold the end of the run
+                    dev.abort_service()
+                    svc_aborted = True
                 # 6) status (time-weighted programs in flight, for the occupancy figure)
                 now = time.time()
                 self.stats.inflight_sum += sum(b.left for b in batches if b is not None) * (now - t_prev)

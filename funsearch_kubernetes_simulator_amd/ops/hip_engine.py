@@ -321,6 +321,13 @@ class DeviceEvaluator:
             self._svc_atexit = True
         return dict(self._svc)
 
+    def abort_service(self) -> None:
+        """Replays in flight on the service end within ~1k events (their rows
+        come back EXC_TIMEOUT, deferred like any timeout): for a run that is
+        stopping and does not need them."""
+        if self._svc is not None:
+            self._eng.service_abort()
+
     def stop_service(self) -> None:
         """Drain and end the resident grid (batches still queued are waited for)."""
         if self._svc is None:

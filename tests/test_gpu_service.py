@@ -98,3 +98,28 @@ def test_service_many_small_batches(dev):
     for rep in range(3):
         for i in range(len(progs)):
             assert np.array_equal(got[rep * len(progs) + i], want[i]), (rep, i)
+
+
+def test_service_abort_ends_replays_in_flight(dev):
+    """abort_service: the replays in flight end early with EXC_TIMEOUT rows
+    (programs already done keep their rows); a restarted grid replays normally."""
+    progs = programs()[:32]
+    want = dev.evaluate_native(progs)
+    dev.start_service(slots=256, share=0.5)
+    try:
+        dev.submit_native(dev.SERVICE_SLOT_BASE, progs)
+        dev.abort_service()
+        got = dev.wait(dev.SERVICE_SLOT_BASE)
+    finally:
+        dev.stop_service()
+    for i in range(len(progs)):
+        if int(got[i, 10]) == Exc.TIMEOUT and int(want[i, 10]) != Exc.TIMEOUT:
+            continue   # aborted
+        assert np.array_equal(got[i], want[i]), i
+    assert (got[:, 10] == Exc.TIMEOUT).sum() >= 1
+    dev.start_service(slots=256, share=0.5)
+    try:
+        again = dev.evaluate_native(progs)
+    finally:
+        dev.stop_service()
+    assert np.array_equal(again, want)
