@@ -67,6 +67,8 @@ def main() -> None:
                     help="composite row kernel with exec-masked LDS/HBM heap accesses instead of flat ones")
     ap.add_argument("--row-wave-share", type=float, default=1.0,
                     help="fraction of the chip's resident waves one island launch takes (row kernel)")
+    ap.add_argument("--wave-duo", type=int, default=-1, choices=[-1, 0, 1],
+                    help="256-node clusters: two-wave (heap wave + scoring wave) kernel on/off (-1: engine default)")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--trace", default="default", choices=["default", "synthetic"],
                     help="default: 8,152-pod OpenB trace on 16 nodes; synthetic: BASELINE config 5 shape")
@@ -122,6 +124,8 @@ def main() -> None:
             "row_min_lds": args.row_min_lds}
     if args.heap_top >= 0:
         opts["heap_top"] = args.heap_top
+    if args.wave_duo >= 0:
+        opts["wave_duo"] = bool(args.wave_duo)
     ev = Evaluator(workload, device=device, options=opts,
                    n_slots=max(1, args.islands))
     if args.device == "gpu" and ev.device is None:

@@ -334,6 +334,8 @@ class DeviceEngine {
       row_mode_ = m;
     }
     if (o.contains("native_duo")) native_duo_ = o["native_duo"].cast<bool>();
+    // 256-node clusters: heap wave + scoring wave per builtin policy (replay_wave_duo.hip.h)
+    if (o.contains("wave_duo")) wave_duo_ = o["wave_duo"].cast<bool>();
     // programs the caller keeps in flight on the device at once (all slots): the
     // two-wave kernel sizes its LDS heap top so that many stay resident
     if (o.contains("native_inflight")) native_inflight_ = std::max(0, o["native_inflight"].cast<int>());
@@ -853,6 +855,8 @@ class DeviceEngine {
     d["native_duo_per_cu_last"] = last_duo_per_cu_;   // resident programs per CU at that heap top
     d["native_duo_reg_cap"] = fksk::native_duo_blocks_per_cu(0);   // register-limited programs per CU
     d["native_inflight"] = native_inflight_;
+    d["wave_duo"] = wave_duo_;
+    d["wave_duo_heap_top"] = npass_ >= 4 ? heap_top_for(0, false, true) : 0;
     return d;
   }
 
@@ -1043,21 +1047,23 @@ class DeviceEngine {
 
   // HBM-heap launches keep the top 2^L - 1 heap slots in LDS, as many levels as
   // fit a 16-policies-per-CU share of the 160 KiB (or the `heap_top` option).
-  int heap_top_for(int nregs, bool vm) const {
+  int heap_top_for(int nregs, bool vm, bool duo = false) const {
     const int entries = (int)(heap_bytes_ / 8);
     if (heap_top_opt_ >= 0) return std::min(heap_top_opt_, entries);
-    // (NPASS 4: 3 waves/SIMD, FKS_NP4_WAVES; NPASS 2: 3)
-    const size_t per_cu = vm ? kVmPoliciesPerCu : (npass_ >= 4 ? 4 * FKS_NP4_WAVES : npass_ == 2 ? 12 : kPoliciesPerCu);
+    // (NPASS 4: FKS_NP4_WAVES waves/SIMD, or FKS_NP4_DUO_WAVES two-wave policies; NPASS 2: 3)
+    const size_t per_cu = duo ? 2 * FKS_NP4_DUO_WAVES
+                              : vm ? kVmPoliciesPerCu : (npass_ >= 4 ? 4 * FKS_NP4_WAVES : npass_ == 2 ? 12 : kPoliciesPerCu);
     const size_t budget = kMaxLds / per_cu;
-    const size_t fixed = (size_t)delmap_slots(true) / 8 + (size_t)nregs * 64 * 8 + (size_t)(W_.inv_words + kWeightWords) * 8;
+    const size_t fixed = (size_t)delmap_slots(true) / 8 + (size_t)nregs * 64 * 8 + (size_t)(W_.inv_words + kWeightWords) * 8 +
+                         (duo ? fksd::wave_duo_box_bytes() : 0);
     int T = 0;
     while (T < entries && fixed + (size_t)(2 * T + 1) * 8 <= budget) T = 2 * T + 1;
     return std::min(T, entries);
   }
 
-  DevWorkload launch_workload(bool g, int nregs, bool vm) const {
+  DevWorkload launch_workload(bool g, int nregs, bool vm, bool duo = false) const {
     DevWorkload Wl = W_;
-    Wl.heap_top = g ? heap_top_for(nregs, vm) : 0;
+    Wl.heap_top = g ? heap_top_for(nregs, vm, duo) : 0;
     Wl.delmap_slots = delmap_slots(g);
     return Wl;
   }
@@ -1140,14 +1146,18 @@ class DeviceEngine {
       return;
     }
     const bool g = use_gheap(P);
-    const DevWorkload Wl = launch_workload(g, 0, false);
-    const size_t lds = lds_bytes(g, Wl.heap_top, 0);
+    // the two-wave kernel: 256-node clusters, HBM heap, no invariant check (it
+    // reads heap and node state together, which live on different waves there)
+    const bool duo = g && npass_ == 4 && wave_duo_ && W_.check_every == 0;
+    const DevWorkload Wl = launch_workload(g, 0, false, duo);
+    const size_t lds = lds_bytes(g, Wl.heap_top, 0) + (duo ? fksd::wave_duo_box_bytes() : 0);
     if (lds > kMaxLds) throw std::invalid_argument("replay layout exceeds the 160 KiB LDS");
     uint64_t* gh = g ? gheap_for(s, P) : nullptr;
     const size_t wb = (size_t)P * kWeights * 8;
     const fksk::BuiltinArgs a{Wl, upload_workload(s, Wl), reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + wb),
                               s.h_in.dev<double>(), s.w.as<double>(), s.res.as<DevResult>(), gh, nullptr};
-    if (npass_ == 1) HIP_OK(fksk::launch_builtin_np1(g, s.fam_spec, P, lds, s.stream, a));
+    if (duo) HIP_OK(fksk::launch_builtin_duo_np4(s.fam_spec, P, lds, s.stream, a));
+    else if (npass_ == 1) HIP_OK(fksk::launch_builtin_np1(g, s.fam_spec, P, lds, s.stream, a));
     else if (npass_ == 2) HIP_OK(fksk::launch_builtin_np2(g, s.fam_spec, P, lds, s.stream, a));
     else HIP_OK(fksk::launch_builtin_np4(g, s.fam_spec, P, lds, s.stream, a));
   }
@@ -1341,6 +1351,7 @@ class DeviceEngine {
   int64_t budget_ = 0;
   int heap_top_opt_ = -1;
   bool partial_delmap_off_ = false;
+  bool wave_duo_ = false;   // NPASS-4 builtin launches on the two-wave kernel (`wave_duo`)
   std::vector<void*> owned_;
 };
 

@@ -10,11 +10,17 @@
 #include "replay.hip.h"
 #include "vm_dev.hip.h"
 #include "replay_rows.hip.h"
+#include "replay_wave_duo.hip.h"
 
 // waves per SIMD of the 256-node (NPASS 4) wave kernels; the host sizes their
 // LDS share to match (build knob for A/B runs)
 #ifndef FKS_NP4_WAVES
 #define FKS_NP4_WAVES 4     // packed GPU milli + node constants on demand: <= 128 VGPRs
+#endif
+// waves per SIMD of the two-wave (heap wave + scoring wave) NPASS-4 kernel: 5 (96 VGPRs, a few
+// spills) measured above 4 (124 VGPRs), profiles/r5_config5_wave_duo_ab.txt
+#ifndef FKS_NP4_DUO_WAVES
+#define FKS_NP4_DUO_WAVES 5
 #endif
 
 namespace fksk {
@@ -73,6 +79,9 @@ FKS_DECLARE_NPASS(1)
 FKS_DECLARE_NPASS(2)
 FKS_DECLARE_NPASS(4)
 #undef FKS_DECLARE_NPASS
+// NPASS 4, HBM heap: one policy per 128-thread workgroup of a heap wave and a
+// scoring wave (replay_wave_duo.hip.h); lds includes fksd::wave_duo_box_bytes()
+hipError_t launch_builtin_duo_np4(int fam_spec, int P, size_t lds, hipStream_t s, const BuiltinArgs& a);
 
 // row kernels: 4 policies per wave (clusters of <= 16 nodes, replay_rows.hip.h)
 // `waves` persistent waves drain the P-policy queue: claims are

@@ -16,6 +16,7 @@
 #include "vm_dev.hip.h"
 #include "replay_rows.hip.h"
 #include "replay_duo.hip.h"
+#include "replay_wave_duo.hip.h"
 
 namespace {
 // The launch's workload struct as the kernel received it: every kernel's
@@ -168,6 +169,48 @@ hipError_t attrs_g(int mx) {
                        raise_lds(&k_replay_builtin<NPASS, GHEAP, FAM_RANDOM_LINEAR>, mx),
                        raise_lds(&k_replay_builtin<NPASS, GHEAP, FAM_FEATURE_LINEAR>, mx),
                        raise_lds(&k_replay_builtin<NPASS, GHEAP, FAM_COMPOSITE_LINEAR>, mx)})
+    if (r != hipSuccess) e = r;
+  return e;
+}
+#endif
+
+#if FKS_KIND == 0 && FKS_NPASS == 4
+// 256-node clusters, HBM heap: heap wave + scoring wave per policy
+// (replay_wave_duo.hip.h); both waves share the register allocation of the
+// scoring wave, FKS_NP4_DUO_WAVES waves per SIMD (launch.h)
+template <int FAM>
+__global__ __launch_bounds__(128, FKS_NP4_DUO_WAVES) void k_replay_builtin_duo(fksk::BuiltinArgs a) {
+  const int p = blockIdx.x;
+  const Slot s = policy_slot<true>(a.W, a.gheap, p);
+  BuiltinScorerDev<FAM> sc;
+  if (threadIdx.x >= kWave) load_policy<FAM>(sc, s, a, p);   // the scoring wave's weights
+  FKS_LDS DuoBox* box = reinterpret_cast<FKS_LDS DuoBox*>(lds_ptr(s.vregs));
+  replay_wave_duo<4, BuiltinScorerDev<FAM>, FKS_WAVE_FLAT>(a.W, kernarg_workload(), sc, s.h, s.top, s.T, s.delmap,
+                                                            box, a.out + p);
+}
+
+hipError_t launch_duo4(int fam, int P, size_t lds, hipStream_t st, const fksk::BuiltinArgs& a) {
+#define FKS_CASE(F) \
+  case F: hipLaunchKernelGGL((k_replay_builtin_duo<F>), dim3(P), dim3(128), lds, st, a); break;
+  switch (fam) {
+    FKS_CASE(FAM_FIRST_FIT)
+    FKS_CASE(FAM_BEST_FIT)
+    FKS_CASE(FAM_RANDOM_LINEAR)
+    FKS_CASE(FAM_FEATURE_LINEAR)
+    FKS_CASE(FAM_COMPOSITE_LINEAR)
+    default: hipLaunchKernelGGL((k_replay_builtin_duo<-1>), dim3(P), dim3(128), lds, st, a);
+  }
+#undef FKS_CASE
+  return hipGetLastError();
+}
+
+hipError_t attrs_duo4(int mx) {
+  hipError_t e = hipSuccess;
+  for (hipError_t r : {raise_lds(&k_replay_builtin_duo<-1>, mx), raise_lds(&k_replay_builtin_duo<FAM_FIRST_FIT>, mx),
+                       raise_lds(&k_replay_builtin_duo<FAM_BEST_FIT>, mx),
+                       raise_lds(&k_replay_builtin_duo<FAM_RANDOM_LINEAR>, mx),
+                       raise_lds(&k_replay_builtin_duo<FAM_FEATURE_LINEAR>, mx),
+                       raise_lds(&k_replay_builtin_duo<FAM_COMPOSITE_LINEAR>, mx)})
     if (r != hipSuccess) e = r;
   return e;
 }
@@ -507,9 +550,17 @@ hipError_t FKS_CAT(launch_builtin_np, FKS_NPASS)(bool gheap, int fam, int P, siz
   return gheap ? launch_g<FKS_NPASS, true>(fam, P, lds, s, a) : launch_g<FKS_NPASS, false>(fam, P, lds, s, a);
 }
 hipError_t FKS_CAT(set_builtin_attrs_np, FKS_NPASS)(int mx) {
-  const hipError_t e = attrs_g<FKS_NPASS, true>(mx);
+  hipError_t e = attrs_g<FKS_NPASS, true>(mx);
+#if FKS_NPASS == 4
+  if (e == hipSuccess) e = attrs_duo4(mx);
+#endif
   return e != hipSuccess ? e : attrs_g<FKS_NPASS, false>(mx);
 }
+#if FKS_NPASS == 4
+hipError_t launch_builtin_duo_np4(int fam, int P, size_t lds, hipStream_t s, const BuiltinArgs& a) {
+  return launch_duo4(fam, P, lds, s, a);
+}
+#endif
 #endif
 
 #if FKS_KIND == 1

@@ -135,6 +135,33 @@ def test_config5_full_shape_matches_cpu():
     assert np.array_equal(dev.evaluate_native(progs), ce.simulate_program_batch(w, progs))
 
 
+@pytest.mark.parametrize("repush", ["first", "earliest"])
+def test_wave_duo_256_nodes_matches_one_wave(repush):
+    """256-node clusters on the two-wave kernel (heap wave + scoring wave,
+    replay_wave_duo.hip.h) give the one-wave kernel's rows bit for bit, trace
+    hash included (the same events in the same order), for every family and
+    a mixed batch, under either repush rule."""
+    from funsearch_kubernetes_simulator_amd.core import synthetic_workload
+    from funsearch_kubernetes_simulator_amd.ops import hip_engine as he
+    w = synthetic_workload(n_nodes=256, n_pods=24000, seed=7)
+    opts = {"trace_hash": True, "repush": repush}
+    one = he.DeviceEvaluator(w, options={**opts, "wave_duo": False})
+    duo = he.DeviceEvaluator(w, options={**opts, "wave_duo": True})
+    assert duo.info()["wave_duo"] and not one.info()["wave_duo"]
+    for family in ("first_fit", "best_fit", "random_linear", "feature_linear", "composite_linear"):
+        W = fam.SAMPLERS[family](40, np.random.default_rng(3)) if family in fam.SAMPLERS else None
+        a = one.evaluate_builtin(family, W, n=40)
+        b = duo.evaluate_builtin(family, W, n=40)
+        assert np.array_equal(a, b), family
+        assert np.all(b[:, 10] == 0) and np.all(b[:, 8] > 24000), family
+    names = ["first_fit", "best_fit"] * 10
+    assert np.array_equal(one.evaluate_builtin(names), duo.evaluate_builtin(names))
+    if repush == "first":
+        W = fam.SAMPLERS["composite_linear"](16, np.random.default_rng(9))
+        assert np.array_equal(duo.evaluate_builtin("composite_linear", W, n=16),
+                              ce.simulate_builtin_batch(w, "composite_linear", fam.pad_weights(W)))
+
+
 # ---- row kernel: 4 policies per wave (clusters of <= 16 nodes) --------------------------
 
 def test_row_kernel_is_default_for_16_nodes(dev):
