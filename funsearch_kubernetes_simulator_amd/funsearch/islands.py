@@ -683,6 +683,7 @@ class IslandFunSearch:
                                             status_every_s=float(sc.get("status_every_s", 5.0)),
                                             tierup=bool(sc.get("tierup", False)),
                                             ahead=int(sc.get("ahead", 2)),
+                                            stagers=int(sc.get("stagers", 1)),
                                             host_object=bool(sc.get("host_object", False)),
                                             service=sc.get("service"))
             self.steady.run(generations, threshold, wall_s=float(sc.get("wall_s", 0.0)))

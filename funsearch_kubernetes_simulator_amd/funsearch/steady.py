@@ -172,7 +172,7 @@ class SteadyStateSearch:
 
     def __init__(self, fs, batch: int = 256, slots: Optional[int] = None, producers: int = 0,
                  task_size: int = 8, status_every_s: float = 5.0, tierup: bool = False, ahead: int = 2,
-                 host_object: bool = False, service=None):
+                 host_object: bool = False, service=None, stagers: int = 1):
         self.fs = fs
         #: children only CPython can score (bigint / complex intermediates, ~1% of
         #: mutated programs, ~3 s each on one core) go to the object engine only
@@ -182,6 +182,10 @@ class SteadyStateSearch:
         self.batch = int(batch)
         #: batches compiled and loaded ahead of a free slot (the stager thread)
         self.ahead = max(1, int(ahead))
+        #: stager threads: a batch's module load overlaps the next batch's code
+        #: generation (NativeCompiler.prepare is thread-safe); batches still
+        #: launch in staging order
+        self.stagers = max(1, int(stagers))
         #: constant polish of island champions as device batches (the islands'
         #: ``polish`` config: every / variants; 0 = off)
         self.polish_every = int(getattr(fs, "polish_every", 0) or 0)
@@ -422,7 +426,7 @@ class SteadyStateSearch:
         fallbacks: list = []             # (batch items, future of the host-engine fallback, programs)
         polish_next = [start_gen + self.polish_every] * k   # generation of each island's next polish
         staged: collections.deque = collections.deque()   # (batch items, future of prepare_compiled, polish job)
-        stager = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="fks-stage")
+        stager = concurrent.futures.ThreadPoolExecutor(max_workers=self.stagers, thread_name_prefix="fks-stage")
         # family coupler (funsearch/coupling.py, `coupling.every` > 0): device family
         # search rounds on a worker thread and the evaluator's last HIP slot, next to
         # the program batches; each round's improved champions enter the islands as
