@@ -163,19 +163,28 @@ struct PodView {
   double cm;      // cpu / max(mem, 1) (DevWorkload::pod_cm; set where a scorer reads it)
 };
 
+// the scorers' feasibility test (scorers.hip.h), used by the diagnostics build
+template <int NPASS, bool GP>
+__device__ __forceinline__ bool feasible(int ps, const NodeRegs<NPASS, GP>& nr, const PodView& pod);
+
 // Scorer contract:  score<NPASS>(pass, node_regs, pod, exc) -> int64 priority
 // after int(max(0, s)) truncation (>= 0), exceptions reported through `exc`.
 
 // ----------------------------------------------------------------------------
 // Phase profiler (s_memtime deltas; compiled out with NoProf).
 struct NoProf {
+  static constexpr bool kOn = false;
   __device__ void start() {}
   __device__ void mark(int) {}
+  __device__ void count(int, uint64_t) {}
   __device__ void flush(uint64_t*) {}
 };
 struct PhaseProf {
+  static constexpr bool kOn = true;
   uint64_t acc[8];
   uint64_t last;
+  // acc[6] / acc[7]: counters, not cycles (feasible node slots / creation events)
+  __device__ void count(int k, uint64_t v) { acc[k] += v; }
   __device__ void start() {
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] = 0;
@@ -418,6 +427,15 @@ __device__ void replay_one(const DevWorkload& W, const DevWorkload* Wcold, Score
       // the winning score, and the lowest node index holding it is the lowest
       // slot whose ballot hits -- the same node as a pass-by-pass argmax, with
       // NPASS - 1 fewer DPP reductions.  A score of 0 never places.
+      if constexpr (Prof::kOn) {   // how many node slots the scorer finds feasible (diagnostics build)
+        uint64_t nf = 0;
+#pragma unroll
+        for (int ps = 0; ps < NPASS; ++ps)
+          nf += __popcll(ballot((ps * kWave + lane) < W.n_nodes && feasible<NPASS>(ps, nr, pod)));
+        prof.count(6, nf);
+        prof.count(7, 1);
+        prof.mark(PH_POP);   // (the count's own cycles go to the pop phase)
+      }
       uint64_t lbest = 0;
       // packed per-lane state (one VGPR): bits 0-1 slot of lbest, bits 2-3
       // slot of the first exception, bits 8+ its code (EXC_NONE = 0)

@@ -28,5 +28,6 @@ assert np.array_equal(np.asarray(tab), np.asarray(ref)), "profiled kernel differ
 ev = float(np.asarray(tab)[:, 8].sum())
 cyc = np.asarray(prof, dtype=np.float64).sum(0)
 out = {"P": P, "events": ev, "cycles_per_event": {k: round(cyc[i] / ev, 1) for i, k in enumerate(DeviceEvaluator.PHASES)},
-       "total_per_event": round(cyc[:6].sum() / ev, 1)}
+       "total_per_event": round(cyc[:6].sum() / ev, 1),
+       "creations": float(cyc[7]), "feasible_node_slots_per_creation": round(cyc[6] / max(cyc[7], 1.0), 2)}
 print(json.dumps(out))
