@@ -66,17 +66,17 @@ def test_steady_single_rank(tmp_path):
 
 
 def test_steady_stager_depths(tmp_path):
-    """Batches compiled ahead on the stager thread (``ahead`` 1 and 3, small
-    batches so several are staged at once): every child is still evaluated
-    exactly once and merged."""
+    """Batches compiled ahead on the stager threads (``ahead`` 1 and 3, one or
+    two ``stagers``, small batches so several are staged at once): every child
+    is still evaluated exactly once and merged."""
     from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
-    for ahead in (1, 3):
-        cfg = _cfg(tmp_path / f"a{ahead}", gens=2)
-        cfg["islands"]["steady"].update(batch=3, ahead=ahead)
+    for ahead, stagers in ((1, 1), (3, 1), (3, 2)):
+        cfg = _cfg(tmp_path / f"a{ahead}s{stagers}", gens=2)
+        cfg["islands"]["steady"].update(batch=3, ahead=ahead, stagers=stagers)
         fs = IslandFunSearch(cfg)
         fs.run(2)
         st = fs.steady.stats
-        assert fs.steady.ahead == ahead
+        assert fs.steady.ahead == ahead and fs.steady.stagers == stagers
         assert st.produced == 2 * 2 * 4 and st.evaluations == st.produced - st.rejected
         assert st.batches >= st.evaluations // 3
         assert fs.generation == 2
