@@ -329,6 +329,15 @@ PYBIND11_MODULE(_fks_cpu, m) {
     // difflib.SequenceMatcher(None, a, b).ratio() >= threshold
     return SeqMatcher(a, b).at_least(threshold);
   });
+  m.def("similar_to_any", [](const std::u32string& a, const std::vector<std::u32string>& bs, double threshold) {
+    // index of the first b with difflib ratio(a, b) >= threshold, or -1: the
+    // similarity gate of one child against a population, off the GIL (the
+    // steady search's stager and collection threads keep running)
+    py::gil_scoped_release rel;
+    for (size_t i = 0; i < bs.size(); ++i)
+      if (SeqMatcher(a, bs[i]).at_least(threshold)) return (int64_t)i;
+    return (int64_t)-1;
+  });
   m.def("exact_mean", [](std::vector<double> xs) {
     FixedAcc a; for (double x : xs) a.add(x);
     return py::make_tuple(fixed_mean(a), a.inexact);

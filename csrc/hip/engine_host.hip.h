@@ -90,26 +90,33 @@ inline double fks_recip_verified(int64_t d, int64_t hi, std::vector<std::pair<st
 
 // hipFree / hipHostFree wait for the whole device.  While a persistent kernel
 // runs (the program service) such a wait lasts until the kernel leaves, so
-// frees are parked here instead and done when it has stopped.
+// frees are parked here instead and done when no persistent grid is left.
+// The queue is process-wide (a hipFree waits for every engine's grid), so
+// deferral is a count of running grids, changed under the lock: one engine's
+// stop does not free while another engine's grid still runs.
 struct FreeQueue {
   std::mutex mu;
-  bool defer = false;
+  int defer = 0;   // persistent grids running in this process
   std::vector<std::pair<void*, bool>> parked;   // (pointer, pinned host memory)
   void free(void* p, bool host) {
     if (!p) return;
     {
       std::lock_guard<std::mutex> g(mu);
-      if (defer) { parked.push_back({p, host}); return; }
+      if (defer > 0) { parked.push_back({p, host}); return; }
     }
     if (host) (void)hipHostFree(p);
     else (void)hipFree(p);
   }
-  size_t resume() {   // stop deferring and free what was parked
+  void begin_defer() {
+    std::lock_guard<std::mutex> g(mu);
+    ++defer;
+  }
+  size_t end_defer() {   // one grid left; free what was parked once none runs
     std::vector<std::pair<void*, bool>> items;
     {
       std::lock_guard<std::mutex> g(mu);
-      defer = false;
-      items.swap(parked);
+      if (defer > 0) --defer;
+      if (defer == 0) items.swap(parked);
     }
     for (auto& it : items) {
       if (it.second) (void)hipHostFree(it.first);
@@ -304,7 +311,7 @@ class DeviceEngine {
       __atomic_store_n(svc_.ctl.as<uint32_t>() + 1, 1u, __ATOMIC_RELEASE);
       (void)hipStreamSynchronize(svc_.stream);
       svc_.running = false;
-      free_queue().resume();
+      free_queue().end_defer();
     }
     svc_.release();
     for (auto& s : slots_) {
@@ -524,7 +531,7 @@ class DeviceEngine {
   struct Service {
     hipStream_t stream = nullptr;
     DevBuf claimed, res, gheap;
-    HostBuf ctl, qslot, started, done, fn, koff, kc, tab;
+    HostBuf ctl, qslot, started, done, fn, koff, kc, tab, cost;
     std::vector<uint8_t> busy;        // slot holds a program not collected yet
     std::vector<uint32_t> held;       // index of the program in each slot
     std::vector<uint32_t> free_slots;
@@ -533,9 +540,10 @@ class DeviceEngine {
     size_t lds = 0;
     bool running = false;
     int64_t launches = 0;
+    uint32_t idle_polls = 1u << 24;   // ~57 s of s_sleep(127) polls with nothing published
     void release() {
       for (DevBuf* b : {&claimed, &res, &gheap}) b->release();
-      for (HostBuf* b : {&ctl, &qslot, &started, &done, &fn, &koff, &kc, &tab}) b->release();
+      for (HostBuf* b : {&ctl, &qslot, &started, &done, &fn, &koff, &kc, &tab, &cost}) b->release();
       if (stream) (void)hipStreamDestroy(stream);
       stream = nullptr;
     }
@@ -560,10 +568,10 @@ class DeviceEngine {
                               nullptr, v.tab.dev<double>()};
     const RowNativeArgs nat{v.fn.dev<const uint64_t>(), v.kc.dev<const int64_t>(), v.koff.dev<const int32_t>(),
                             v.ctl.dev<const uint32_t>() + 2};
-    // ~57 s of s_sleep(127) polls with nothing published: the grid drains (a lost host)
+    // `idle_polls` polls with nothing published: the grid drains (a lost host)
     const ServiceCtl c{v.claimed.as<uint32_t>(), v.ctl.dev<const uint32_t>(), v.ctl.dev<const uint32_t>() + 1,
                        v.done.dev<uint32_t>(), v.qslot.dev<const uint32_t>(), v.started.dev<uint32_t>(), v.nq,
-                       1u << 24};
+                       v.idle_polls, v.cost.dev<uint64_t>()};
     HIP_OK(fksk::launch_native_service(v.blocks, v.lds, v.stream, fksk::ServiceArgs{a, nat, c}));
     v.running = true;
     ++v.launches;
@@ -572,12 +580,14 @@ class DeviceEngine {
   // start the resident grid: `share` of the two-wave kernel's resident capacity
   // (the rest of the chip stays free for other kernels: JIT module loads, other
   // slots' launches), `slots` programs queued or running at most
-  py::dict service_start(int slots, double share) {
+  py::dict service_start(int slots, double share, int64_t idle_polls) {
     HIP_OK(hipSetDevice(device_));
     Service& v = svc_;
     if (v.running) throw std::runtime_error("the program service is already running");
     if (!rows_ok_) throw std::invalid_argument("the program service needs the row-kernel layout (<= 16 nodes)");
     if (slots < 64 || slots > (1 << 22)) throw std::invalid_argument("slots must be in [64, 2^22]");
+    if (idle_polls < 64 || idle_polls > (1ll << 30)) throw std::invalid_argument("idle_polls must be in [64, 2^30]");
+    v.idle_polls = (uint32_t)idle_polls;
     if (!v.stream) HIP_OK(hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking));
     v.T = duo_top(1 << 30);   // the heap top that keeps the register-limited count of workgroups per CU
     v.lds = duo_lds_bytes(W_.n_pods, v.T);
@@ -598,10 +608,12 @@ class DeviceEngine {
     v.koff.reserve(4 * S, true);
     v.kc.reserve(8 * (size_t)kKcLds * (S + 1), true);
     v.tab.reserve(8 * 13 * S, true);
+    v.cost.reserve(8 * S, true);
     std::memset(v.ctl.p, 0, 64);
     std::memset(v.qslot.p, 0, 4 * Q);
     std::memset(v.started.p, 0, 4 * Q);
     std::memset(v.done.p, 0, 4 * S);
+    std::memset(v.cost.p, 0, 8 * S);
     std::memset(v.kc.p, 0, 8 * (size_t)kKcLds * (S + 1));
     for (uint32_t i = 0; i < v.nslots; ++i) v.koff.as<int32_t>()[i] = (int32_t)(i * (uint32_t)kKcLds);
     v.busy.assign(S, 0);
@@ -609,7 +621,7 @@ class DeviceEngine {
     v.free_slots.resize(S);
     for (uint32_t i = 0; i < v.nslots; ++i) v.free_slots[i] = v.nslots - 1 - i;
     v.published = 0;
-    free_queue().defer = true;   // (set before the launch; the grid's own buffers are sized above)
+    free_queue().begin_defer();   // (before the launch; the grid's own buffers are sized above)
     service_launch(0);
     py::dict d;
     d["blocks"] = v.blocks; d["per_cu"] = per_cu; d["heap_top"] = v.T; d["lds"] = (int64_t)v.lds;
@@ -667,15 +679,19 @@ class DeviceEngine {
   // launch it again from the first index no workgroup started
   void service_revive() {
     Service& v = svc_;
-    if (!v.running || hipStreamQuery(v.stream) != hipSuccess) return;
+    if (!v.running) return;
+    const hipError_t e = hipStreamQuery(v.stream);
+    if (e == hipErrorNotReady) return;   // still resident
+    HIP_OK(e);                           // a faulted grid is an error, not "still running"
     uint32_t lo = v.published > v.nq ? v.published - v.nq : 0;
     while (lo != v.published && v.ld(v.started, lo % v.nq) == lo + 1u) ++lo;
     if (lo != v.published) service_launch(lo);
   }
 
   // every program finished since the last call, over all submissions:
-  // (indexes, rows), their slots freed -- one scan of the data slots instead of
-  // one call per submission (the steady loop keeps dozens in flight)
+  // (indexes, rows, device cycles of each replay), their slots freed -- one
+  // scan of the data slots instead of one call per submission (the steady
+  // loop keeps dozens in flight)
   py::tuple service_poll() {
     Service& v = svc_;
     std::vector<uint32_t> hit;
@@ -683,16 +699,18 @@ class DeviceEngine {
       if (v.busy[slot] && v.ld(v.done, slot) == v.held[slot] + 1u) hit.push_back(slot);
     py::array_t<int64_t> idx((py::ssize_t)hit.size());
     py::array_t<double> rows({(py::ssize_t)hit.size(), (py::ssize_t)13});
+    py::array_t<int64_t> cyc((py::ssize_t)hit.size());
     double* r = rows.mutable_data();
     for (size_t k = 0; k < hit.size(); ++k) {
       const uint32_t slot = hit[k];
       idx.mutable_data()[k] = (int64_t)v.held[slot];
       std::memcpy(r + k * 13, v.tab.as<double>() + (size_t)slot * 13, 13 * sizeof(double));
+      cyc.mutable_data()[k] = (int64_t)__atomic_load_n(v.cost.as<uint64_t>() + slot, __ATOMIC_RELAXED);
       v.busy[slot] = 0;
       v.free_slots.push_back(slot);
     }
     if (hit.empty() && v.free_slots.size() < v.nslots) service_revive();
-    return py::make_tuple(idx, rows);
+    return py::make_tuple(idx, rows, cyc);
   }
 
   // end every replay in flight within ~1k events (rows come back EXC_TIMEOUT):
@@ -711,13 +729,14 @@ class DeviceEngine {
       HIP_OK(hipStreamSynchronize(v.stream));
     }
     v.running = false;
-    free_queue().resume();
+    free_queue().end_defer();
   }
 
   py::dict service_info() {
     py::dict d;
     d["running"] = svc_.running; d["blocks"] = svc_.blocks; d["slots"] = (int64_t)svc_.nslots;
     d["queue"] = (int64_t)svc_.nq; d["published"] = (int64_t)svc_.published; d["launches"] = svc_.launches;
+    d["idle_polls"] = (int64_t)svc_.idle_polls;
     d["heap_top"] = svc_.T;
     d["unconsumed"] = (int64_t)(svc_.nslots - svc_.free_slots.size());
     return d;
@@ -857,6 +876,11 @@ class DeviceEngine {
     d["native_inflight"] = native_inflight_;
     d["wave_duo"] = wave_duo_;
     d["wave_duo_heap_top"] = npass_ >= 4 ? heap_top_for(0, false, true) : 0;
+    size_t mfree = 0, mtotal = 0;   // (a host-side query: no device synchronisation)
+    if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess) {
+      d["mem_used_mb"] = (int64_t)((mtotal - mfree) >> 20);
+      d["mem_total_mb"] = (int64_t)(mtotal >> 20);
+    }
     return d;
   }
 

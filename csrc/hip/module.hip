@@ -457,7 +457,8 @@ PYBIND11_MODULE(_fks_hip, m) {
       .def("evaluate_programs", &DeviceEngine::evaluate_programs)
       .def("submit_builtin", &DeviceEngine::submit_builtin)
       .def("submit_programs", &DeviceEngine::submit_programs)
-      .def("service_start", &DeviceEngine::service_start, py::arg("slots") = 16384, py::arg("share") = 1.0)
+      .def("service_start", &DeviceEngine::service_start, py::arg("slots") = 16384, py::arg("share") = 1.0,
+           py::arg("idle_polls") = (int64_t)(1 << 24))
       .def("service_submit", &DeviceEngine::service_submit)
       .def("service_poll", &DeviceEngine::service_poll)
       .def("service_stop", &DeviceEngine::service_stop)

@@ -394,7 +394,8 @@ __global__ __launch_bounds__(128, 1) void k_replay_native_duo_prof(fksk::Builtin
 //   frees a slot when it consumed the row, and reuses a queue entry only once
 //   it is marked started -- a straggler holds its slot, nothing else.
 //   Exit: `stop` set and nothing left to claim, or `max_idle_polls` polls with
-//   nothing published (a lost host: the grid drains instead of spinning on).
+//   nothing published (a lost host: the whole grid drains instead of spinning
+//   on; the host relaunches it from the lowest unstarted index).
 //
 // The replay is a call (service_replay, not inlined): inlined into the service
 // loop, values of its prologue and epilogue were hoisted out of the loop and
@@ -474,12 +475,20 @@ __device__ __noinline__ uint32_t service_claim(uint64_t kp, uint32_t* slot) {
     const uint32_t d = idx - pub + 1u < 32u ? idx - pub + 1u : 32u;
     for (uint32_t z = d; z > 0; --z) __builtin_amdgcn_s_sleep(127);
     polls += d;
-    if (polls > c.max_idle_polls) return kServiceExit;
+    if (polls > c.max_idle_polls) {
+      // idle drain, all or nothing: every workgroup leaves (the stop mirror),
+      // so the grid ends as a whole and the host's revive relaunches from the
+      // lowest index no workgroup started -- an index claimed by a workgroup
+      // that left while others stayed resident would never start
+      __hip_atomic_store(stopd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return kServiceExit;
+    }
   }
 }
 
 __global__ __launch_bounds__(128, 1) void k_native_service(fksk::ServiceArgs) {
   __shared__ uint32_t claim[2];   // index, data slot
+  __shared__ uint64_t t_start;    // s_memtime when the program was claimed
   for (;;) {
     uint64_t kp = (uint64_t)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(kp));   // re-derived per program, not held across the replay
@@ -487,18 +496,24 @@ __global__ __launch_bounds__(128, 1) void k_native_service(fksk::ServiceArgs) {
       uint32_t slot = 0;
       claim[0] = service_claim(kp, &slot);
       claim[1] = slot;
+      t_start = __builtin_amdgcn_s_memtime();
     }
     __syncthreads();
     const uint32_t idx = claim[0];
     if (idx == kServiceExit) return;   // (uniform across the workgroup)
     service_replay(kp, (int)claim[1]);
     if (threadIdx.x >= kWave) {
+      const FKS_CONST ServiceCtl& c = service_args((uint64_t)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr())->c;
+      if (threadIdx.x == kWave) {
+        // the replay's device cost (the search's parent sampling and bloat
+        // control read it; never the score), covered by the release below
+        const uint64_t dt = __builtin_amdgcn_s_memtime() - t_start;
+        __hip_atomic_store(&c.cost[claim[1]], dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       // the scoring wave wrote the result row: make it visible to the host, then flag it
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      if (threadIdx.x == kWave) {
-        const FKS_CONST ServiceCtl& c = service_args((uint64_t)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr())->c;
+      if (threadIdx.x == kWave)
         __hip_atomic_store(&c.done[claim[1]], claim[0] + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
     }
     __syncthreads();   // both waves are done with the LDS (and with `claim`) before the next program
   }

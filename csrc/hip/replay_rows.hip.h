@@ -57,6 +57,7 @@ struct ServiceCtl {
   uint32_t* started;            // host: [nq] index + 1 once a workgroup read entry i % nq
   uint32_t nq;
   uint32_t max_idle_polls;
+  uint64_t* cost;               // host: [slots] s_memtime cycles of the slot's replay (written before done)
 };
 
 constexpr int kRow = 16;            // lanes per DPP row = max nodes per policy

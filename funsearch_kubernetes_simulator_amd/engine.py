@@ -57,6 +57,9 @@ class EvalResult:
     results: Optional[EvaluationResults] = None
     n_events: int = 0
     detail: Dict[str, float] = field(default_factory=dict)
+    #: device cycles of the replay (program service only; 0 elsewhere): what a
+    #: program costs the search -- parent sampling and bloat control, never the score
+    device_cycles: float = 0.0
 
     @property
     def ok(self) -> bool:
@@ -485,6 +488,8 @@ class Evaluator:
                     pend.deferred_idx.append(i)
                     continue
                 r = _row_to_result(row, "hip-native")
+                if len(row) > len(COLS):
+                    r.device_cycles = float(row[len(COLS)])
                 self._bump("device_native", 1)
                 if self.fault_rate > 0 and self._fault_rng.random() < self.fault_rate:
                     r = EvalResult(0.0, int(Exc.VALUE), "fault-injection")

@@ -19,6 +19,10 @@ unchanged with any of them:
   between the two parents, statement deletion, line crossover.  Used for
   tests, benchmarks and air-gapped runs.
 * `ScriptedClient` -- replays a fixed list of responses (tests).
+* `LatencyClient` -- wraps any client and answers after a delay drawn from
+  ``latency_s`` = [lo, hi] seconds: a remote LLM's response time, to size and
+  measure the search's request fan-out (``llm.concurrency``, steady mode)
+  without a network.
 """
 
 from __future__ import annotations
@@ -628,9 +632,33 @@ class FaultInjectingClient(BaseClient):
         return self.inner._create(**kw)
 
 
+class LatencyClient(BaseClient):
+    """The inner client's reply after a delay drawn uniformly from [lo, hi]
+    seconds (thread-safe; the wait releases the GIL, as an HTTP request does)."""
+
+    def __init__(self, inner: BaseClient, lo: float, hi: float, seed: int = 0):
+        super().__init__()
+        if not 0 <= lo <= hi:
+            raise ValueError(f"latency range [{lo}, {hi}]")
+        self.inner, self.lo, self.hi = inner, float(lo), float(hi)
+        self._rng = random.Random(seed)
+        self.waited_s = 0.0
+
+    def _create(self, **kw) -> ChatResponse:
+        with self._lock:
+            d = self._rng.uniform(self.lo, self.hi)
+            self.waited_s += d
+            self.calls += 1
+        time.sleep(d)
+        r = self.inner._create(**kw)
+        r.latency_s += d
+        return r
+
+
 def make_client(cfg: dict) -> BaseClient:
     """Client from the ``llm`` / ``openrouter`` section of a config
-    (``fault_rate`` > 0 wraps it in a `FaultInjectingClient`)."""
+    (``fault_rate`` > 0 wraps it in a `FaultInjectingClient`; ``latency_s``
+    = [lo, hi] in a `LatencyClient`)."""
     backend = cfg.get("backend", "openai")
     if backend in ("mutation", "offline"):
         client: BaseClient = MutationClient(int(cfg.get("seed", 0)))
@@ -641,4 +669,14 @@ def make_client(cfg: dict) -> BaseClient:
                                         float(cfg.get("timeout_s", 60)), int(cfg.get("max_retries", 4)))
     if float(cfg.get("fault_rate", 0) or 0) > 0:
         client = FaultInjectingClient(client, float(cfg["fault_rate"]), int(cfg.get("seed", 0)) + 17)
+    lat = cfg.get("latency_s")
+    if lat:
+        lo, hi = (float(lat), float(lat)) if isinstance(lat, (int, float)) else (float(lat[0]), float(lat[1]))
+        client = LatencyClient(client, lo, hi, int(cfg.get("seed", 0)) + 29)
     return client
+
+
+def remote_like(cfg: dict) -> bool:
+    """Requests to this backend spend their time waiting (HTTP, or a modelled
+    latency), not computing: worth many in flight per process."""
+    return cfg.get("backend", "openai") not in ("mutation", "offline", "scripted") or bool(cfg.get("latency_s"))

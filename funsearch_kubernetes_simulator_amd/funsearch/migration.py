@@ -32,7 +32,8 @@ with the slowest one (its slowest replay plus its JIT), so a migration is
   while its peers run on, and time out as a "lost" peer).
 
 `wait_s` accumulates the wall time a rank spent blocked in collectives (the
-"collective wait" of the multi-rank logs).
+"collective wait" of the multi-rank logs); `max_stall_s` is the longest single
+block and `max_gather_s` the longest post-to-completion time of a gather.
 """
 
 from __future__ import annotations
@@ -71,6 +72,9 @@ class MigrationChannel:
         self.stop_at: Optional[int] = None
         self.best_global = float(fs.best[1])
         self.wait_s = 0.0
+        self.max_stall_s = 0.0          # longest single time blocked in a post or a wait
+        self.max_gather_s = 0.0         # longest post -> completion of a gather
+        self.last_gather_s = 0.0
         self.completed = 0
 
     # ---------------------------------------------------------------------------------------
@@ -91,11 +95,13 @@ class MigrationChannel:
     def post(self, generation: int, vote: bool) -> None:
         t = time.perf_counter()
         try:
-            self.pending.append((generation, dist.all_gather_array_async(self.payload(vote))))
+            self.pending.append((generation, dist.all_gather_array_async(self.payload(vote)), t))
         except Exception as exc:      # a dead peer: carry on alone (islands.elastic)
             self.fs.rank_lost("migrate", exc)
             self.pending.clear()
-        self.wait_s += time.perf_counter() - t
+        dt = time.perf_counter() - t
+        self.wait_s += dt
+        self.max_stall_s = max(self.max_stall_s, dt)
 
     def post_due(self, g_min: int, vote: bool) -> int:
         """Post every migration whose generation the slowest local island has
@@ -117,7 +123,7 @@ class MigrationChannel:
     def poll(self, threshold: float, block: bool = False) -> List[MigrationResult]:
         out = []
         while self.pending:
-            g, h = self.pending[0]
+            g, h, t_post = self.pending[0]
             must = block or self.stop_at is not None or len(self.pending) > self.lookahead
             if not must and not h.done():
                 break
@@ -129,7 +135,11 @@ class MigrationChannel:
                 self.pending.clear()
                 self.fs.rank_lost("migrate", exc)
                 break
-            self.wait_s += time.perf_counter() - t
+            t_done = time.perf_counter()
+            self.wait_s += t_done - t
+            self.max_stall_s = max(self.max_stall_s, t_done - t)
+            self.last_gather_s = t_done - t_post
+            self.max_gather_s = max(self.max_gather_s, self.last_gather_s)
             self.pending.popleft()
             hdr = [np.frombuffer(glob[r, :HEADER_BYTES].tobytes(), np.float64) for r in range(glob.shape[0])]
             bests = [float(x[0]) for x in hdr]

@@ -59,7 +59,11 @@ def with_values(prog: CompiledPolicy, values: dict) -> CompiledPolicy:
             f[idx] = float(v)
         else:
             i[idx] = int(v)
-    return replace(prog, fconst=f, iconst=i)
+    out = replace(prog, fconst=f, iconst=i)
+    for k in ("_shape_key", "_jit_key"):   # literals are data: the variant keeps its shape
+        if k in prog.__dict__:
+            out.__dict__[k] = prog.__dict__[k]
+    return out
 
 
 def _literal_text(prog: CompiledPolicy, idx: int, v) -> str:

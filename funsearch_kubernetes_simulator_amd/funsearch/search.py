@@ -47,8 +47,15 @@ def _difflib_at_least(a: str, b: str, threshold: float) -> bool:
 
 try:
     from ..ops._fks_cpu import similar_at_least as _similar_at_least
+    from ..ops._fks_cpu import similar_to_any as _similar_to_any
 except ImportError:  # native CPU module not built: the reference's own difflib path
     _similar_at_least = _difflib_at_least
+
+    def _similar_to_any(a: str, bs, threshold: float) -> int:
+        for i, b in enumerate(bs):
+            if _difflib_at_least(a, b, threshold):
+                return i
+        return -1
 
 FEEDBACK = ("Elite policies achieve good performance by balancing resource utilization "
             "and considering GPU/CPU workload separation. "
@@ -153,10 +160,8 @@ class SimpleFunSearch:
         scores at least as well).  The ratio comes from the native exact
         SequenceMatcher (`csrc/cpu/seqmatch.hpp`, ~40x faster) when built."""
         a = new_code.strip()
-        for code, score in self.population:
-            if score >= new_score and _similar_at_least(a, code.strip(), self.similarity_threshold):
-                return True
-        return False
+        others = [code.strip() for code, score in self.population if score >= new_score]
+        return bool(others) and _similar_to_any(a, others, self.similarity_threshold) >= 0
 
     def _generate_single_policy(self, idx: int, elites, feedback: str) -> Tuple[int, Optional[str]]:
         with self.print_lock:

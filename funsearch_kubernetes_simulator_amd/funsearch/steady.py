@@ -57,7 +57,7 @@ from .search import FEEDBACK
 _W: dict = {}
 
 
-def _producer_init(llm_cfg: dict, timeout_s: int, seed: int) -> None:
+def _producer_init(llm_cfg: dict, timeout_s: int, seed: int, fanout: int = 0) -> None:
     from ..policy.sandbox import SafeExecutor
     from .generator import LLMCodeGenerator
     from .llm import make_client
@@ -67,53 +67,84 @@ def _producer_init(llm_cfg: dict, timeout_s: int, seed: int) -> None:
     _W["gen"] = LLMCodeGenerator(client, SafeExecutor(timeout_seconds=timeout_s), cfg.get("model"),
                                  cfg.get("max_tokens", 400), cfg.get("temperature", 0.7))
     _W["rng"] = random.Random(cfg["seed"])
+    if fanout > 1:
+        # a remote LLM: a task's requests wait concurrently (threads; the wait
+        # releases the GIL), so `producers x task_size` requests are in flight
+        _W["fanout"] = concurrent.futures.ThreadPoolExecutor(max_workers=fanout, thread_name_prefix="fks-llm")
 
 
 def _produce(task):
-    """(island, elites [(code, score)], n) -> [(island, code, CompiledPolicy | None)]."""
+    """(island, elites [(code, score)], n[, weights]) -> [(island, code, CompiledPolicy | None)].
+    weights: per-elite parent weights (the steady search's device-cost
+    weighting, `_parent_weights`), or None for uniform sampling."""
+    island, elites, n = task[:3]
+    weights = task[3] if len(task) > 3 else None
+    t0 = time.process_time()
+    pool = _W.get("fanout")
+    if pool is not None and n > 1:
+        out = list(pool.map(lambda _: _produce_one(island, elites, weights), range(n)))
+    else:
+        out = [_produce_one(island, elites, weights) for _ in range(n)]
+    return out, time.process_time() - t0
+
+
+def _produce_one(island, elites, weights):
+    from ..ops.jit import launch_key
     from ..policy.compiler import same_shape_child, try_compile
-    island, elites, n = task
     gen, rng = _W["gen"], _W["rng"]
     pcache = _W.setdefault("parents", {})   # parent text -> CompiledPolicy (elites repeat)
-    t0 = time.process_time()
+    parents = _sample_parents(rng, elites, weights)
+    reuse = []
+
+    def same_shape(child, parents=parents, reuse=reuse):
+        # a constant-only mutation keeps its parent's shape: bytecode reused,
+        # and -- the parent having passed validation, only digits differing --
+        # the sandbox checks need not run again
+        for pc, _ in parents:
+            pp = pcache.get(pc)
+            if pp is None:
+                if len(pcache) > 256:
+                    pcache.clear()
+                try:   # the parent itself passes the sandbox checks (once per parent text)
+                    gen.safe_executor.validate(pc)
+                    pp = try_compile(pc)[0] or False
+                except Exception:
+                    pp = False
+                pcache[pc] = pp
+            if pp:
+                prog = same_shape_child(pp, child)
+                if prog is not None:
+                    reuse.append(prog)
+                    return True
+        return False
+
+    code = gen.generate_policy(parent_policies=parents, performance_feedback=FEEDBACK, prevalidated=same_shape)
+    if not code:             # LLM / validation failure: the child slot is spent
+        return island, None, None
+    if reuse:
+        prog = reuse[0]
+        _W["reused"] = _W.get("reused", 0) + 1
+    else:
+        prog, _ = try_compile(code)
+    if prog is not None:
+        # the JIT cache key and constant payload travel with the child: the
+        # dispatcher process's stagers only look them up
+        launch_key(prog)
+    return island, code, prog
+
+
+def _sample_parents(rng, elites, weights, k: int = 2):
+    """k distinct parents: uniform (the reference's `random.sample`) or by weight."""
+    if not weights or len(elites) <= k:
+        return rng.sample(elites, min(k, len(elites)))
+    idx = list(range(len(elites)))
+    w = list(weights)
     out = []
-    for _ in range(n):
-        parents = rng.sample(elites, min(2, len(elites)))
-        reuse = []
-
-        def same_shape(child, parents=parents, reuse=reuse):
-            # a constant-only mutation keeps its parent's shape: bytecode reused,
-            # and -- the parent having passed validation, only digits differing --
-            # the sandbox checks need not run again
-            for pc, _ in parents:
-                pp = pcache.get(pc)
-                if pp is None:
-                    if len(pcache) > 256:
-                        pcache.clear()
-                    try:   # the parent itself passes the sandbox checks (once per parent text)
-                        gen.safe_executor.validate(pc)
-                        pp = try_compile(pc)[0] or False
-                    except Exception:
-                        pp = False
-                    pcache[pc] = pp
-                if pp:
-                    prog = same_shape_child(pp, child)
-                    if prog is not None:
-                        reuse.append(prog)
-                        return True
-            return False
-
-        code = gen.generate_policy(parent_policies=parents, performance_feedback=FEEDBACK, prevalidated=same_shape)
-        if not code:             # LLM / validation failure: the child slot is spent
-            out.append((island, None, None))
-            continue
-        if reuse:
-            prog = reuse[0]
-            _W["reused"] = _W.get("reused", 0) + 1
-        else:
-            prog, _ = try_compile(code)
-        out.append((island, code, prog))
-    return out, time.process_time() - t0
+    for _ in range(k):
+        j = rng.choices(range(len(idx)), weights=w)[0]
+        out.append(elites[idx.pop(j)])
+        w.pop(j)
+    return out
 
 
 @dataclass
@@ -139,6 +170,7 @@ class _Batch:
     polish: Optional[_Polish] = None
     results: Optional[list] = None   # streaming (program service): results so far
     left: int = 0                    # programs not merged yet
+    aborted: bool = False            # in flight at a grid rollover's abort: no host fallbacks
 
 
 @dataclass
@@ -163,6 +195,11 @@ class SteadyStats:
     coupled: int = 0                 # family-coupler champions offered to the islands
     inflight_sum: float = 0.0        # programs in flight x seconds
     inflight_n: float = 0.0          # seconds observed
+    cost_rejected: int = 0           # children not merged by the bloat control (device cost)
+    cost_sum: float = 0.0            # device cycles of the children replayed on the service ...
+    cost_n: int = 0                  # ... and their number
+    rollovers: int = 0               # grid rollovers (module unloads while the service runs)
+    rollover_s: float = 0.0          # wall seconds the rollovers took (drain + restart)
     history: List[dict] = field(default_factory=list)
 
 
@@ -220,6 +257,21 @@ class SteadyStateSearch:
             self.slots = max(1, int(svc.get("slots", slots or 64)))
             self.slot_base = dev.SERVICE_SLOT_BASE
         self.service_inflight = 0
+        #: device-cost selection (service runs: every child's replay cycles are
+        #: measured on the grid): parents are sampled with weight median / cost
+        #: (clipped to [1/4, 4]) among an island's elites, and a child costing more
+        #: than `bloat` x the island's median member is not merged unless it
+        #: beats the island's best.  Scores are never touched.
+        cc = dict((svc or {}).get("cost") or {}) if isinstance(svc, dict) else {}
+        self.cost_parents = bool(cc.get("parents", True))
+        self.cost_bloat = float(cc.get("bloat", 3.0))
+        #: grid rollover: retired JIT modules stay loaded while the grid runs
+        #: (an unload waits for the device); past this many the loop drains the
+        #: grid (launches paused, stragglers aborted after `rollover_grace_s`),
+        #: unloads them and starts it again
+        self.rollover_deferred = int((svc or {}).get("rollover_modules", 2048)) if isinstance(svc, dict) else 2048
+        self.rollover_grace_s = float((svc or {}).get("rollover_grace_s", 3.0)) if isinstance(svc, dict) else 3.0
+        self._cost: dict = {}            # island -> {code: device cycles}
         if dev is not None:
             # the two-wave kernel sizes its LDS heap top so that every slot's batch
             # stays resident at once (csrc/hip/engine_host.hip.h duo_top)
@@ -235,6 +287,7 @@ class SteadyStateSearch:
         self.task_size = int(task_size)
         self.status_every_s = float(status_every_s)
         self.stats = SteadyStats()
+        self.llm_concurrency = 0
         # main-thread wall time by phase (the dispatcher is one thread: its busy
         # fraction bounds the steady-state rate)
         self.phase = {"receive": 0.0, "submit": 0.0, "collect": 0.0, "merge": 0.0}
@@ -244,13 +297,40 @@ class SteadyStateSearch:
         s.population.sort(key=lambda x: x[1], reverse=True)
         return list(s.population[:s.elite_size])
 
-    def _merge_one(self, s, code: str, score: float) -> bool:
+    def _parent_weights(self, i: int, elites) -> Optional[list]:
+        """Parent weights of island i's elites: median cost / cost, in [1/4, 4]
+        (unknown cost: 1) -- cheaper parents breed more, so the population does
+        not drift toward ever costlier programs (a costlier parent still breeds)."""
+        if not self.cost_parents or self.service_cfg is None:
+            return None
+        cmap = self._cost.get(i) or {}
+        costs = [cmap.get(c) for c, _ in elites]
+        known = sorted(x for x in costs if x)
+        if len(known) < 2:
+            return None
+        med = known[len(known) // 2]
+        return [1.0 if not x else min(4.0, max(0.25, med / x)) for x in costs]
+
+    def _merge_one(self, s, code: str, score: float, cost: float = 0.0, island: Optional[int] = None) -> bool:
         if len(s.population) >= s.population_size and score <= min(sc for _, sc in s.population):
             # truncation would drop it anyway (a tie sorts after the members it
             # ties with): skip the similarity scan, same resulting population
             return False
+        cmap = self._cost.setdefault(island, {}) if island is not None else None
+        if cost > 0 and cmap is not None and self.cost_bloat > 0 and score <= s.best_score:
+            known = sorted(cmap[c] for c, _ in s.population if c in cmap)
+            if len(known) >= 3 and cost > self.cost_bloat * known[len(known) // 2]:
+                self.stats.cost_rejected += 1
+                return False
         if s._is_too_similar(code, score):
             return False
+        if cost > 0 and cmap is not None:
+            cmap[code] = cost
+            if len(cmap) > 4 * s.population_size:   # forget programs that left the population
+                live = {c for c, _ in s.population}
+                live.add(code)
+                for c in [c for c in cmap if c not in live]:
+                    del cmap[c]
         s.population.append((code, score))
         if score > s.best_score:
             s.best_score, s.best_policy = score, code
@@ -267,7 +347,8 @@ class SteadyStateSearch:
             self.stats.migrations += 1
             fs.log.write(kind="steady_migration", rank=fs.ctx.rank, generation=res.generation,
                          best_global=self.channel.best_global, bests=[round(x, 6) for x in res.bests],
-                         stop_votes=res.votes, collective_wait_s=round(self.channel.wait_s, 4))
+                         stop_votes=res.votes, collective_wait_s=round(self.channel.wait_s, 4),
+                         gather_s=round(self.channel.last_gather_s, 4), max_stall_s=round(self.channel.max_stall_s, 4))
             if fs.ck_dir:
                 fs.save_checkpoint()
         return bool(results)
@@ -349,7 +430,10 @@ class SteadyStateSearch:
             b.left -= 1
             if b.polish is None:
                 isl, code, _ = b.items[i]
-                self._merge_one(islands[isl], code, r.score)
+                if r.device_cycles > 0:
+                    self.stats.cost_sum += r.device_cycles
+                    self.stats.cost_n += 1
+                self._merge_one(islands[isl], code, r.score, r.device_cycles, isl)
                 merged[isl] += 1
                 self.stats.native += int(r.engine == "hip-native")
         if b.polish is None:
@@ -365,10 +449,14 @@ class SteadyStateSearch:
 
     def _log_batch(self, log, ctx, si: int, b: _Batch, batches, ready) -> None:
         ev_n = [r.n_events for r in b.results if r is not None and r.engine == "hip-native"]
+        cyc = [r.device_cycles for r in b.results if r is not None and r.device_cycles > 0]
         log.write(kind="steady_batch", rank=ctx.rank, slot=si, programs=len(b.items), new_shapes=b.new_shapes,
                   jit_s=round(b.jit_s, 4), device_s=round(time.time() - b.t_launch, 4),
-                  inflight_after=sum(x.left for x in batches if x is not None), queued=len(ready),
-                  events_mean=round(sum(ev_n) / len(ev_n), 1) if ev_n else 0, events_max=max(ev_n) if ev_n else 0)
+                  inflight_after=self._left, queued=len(ready),
+                  events_mean=round(sum(ev_n) / len(ev_n), 1) if ev_n else 0, events_max=max(ev_n) if ev_n else 0,
+                  # device cycles per replay (program service): mean and the longest
+                  mcycles_mean=round(sum(cyc) / len(cyc) / 1e6, 3) if cyc else 0,
+                  mcycles_max=round(max(cyc) / 1e6, 3) if cyc else 0)
 
     def _gen_of(self, merged: List[int]) -> List[int]:
         return [m // max(1, s.policies_per_generation) for m, s in zip(merged, self.fs.islands)]
@@ -418,10 +506,23 @@ class SteadyStateSearch:
             llm_cfg = dict(fs.config.get("openrouter", {}))
             llm_cfg.setdefault("backend", "openai")
         timeout_s = int((fs.config.get("safe_execution") or {}).get("timeout_seconds", 3))
+        # LLM request fan-out (``llm.concurrency``): a remote model answers in
+        # seconds, so its requests are spread over producers x task_size threads
+        # instead of one request per producer process at a time
+        from .llm import remote_like
+        conc = int(llm_cfg.get("concurrency", 0) or 0)
+        fanout = 0
+        if conc > 0 and remote_like(llm_cfg):
+            self.task_size = max(1, -(-conc // self.producers))
+            fanout = self.task_size
+        self.llm_concurrency = fanout * self.producers
+        if fanout:
+            fs.log.write(kind="steady_llm", rank=ctx.rank, concurrency=self.llm_concurrency, producers=self.producers,
+                         task_size=self.task_size, latency_s=llm_cfg.get("latency_s"))
         ctx_mp = multiprocessing.get_context("spawn")
         pool = concurrent.futures.ProcessPoolExecutor(
             max_workers=self.producers, mp_context=ctx_mp, initializer=_producer_init,
-            initargs=(llm_cfg, timeout_s, 1000 * ctx.rank + 1))
+            initargs=(llm_cfg, timeout_s, 1000 * ctx.rank + 1, fanout))
         inflight_tasks: List[concurrent.futures.Future] = []
         fallbacks: list = []             # (batch items, future of the host-engine fallback, programs)
         polish_next = [start_gen + self.polish_every] * k   # generation of each island's next polish
@@ -443,6 +544,12 @@ class SteadyStateSearch:
         rr = 0
         t_start = time.time()
         self._cpu0 = time.process_time()
+        # per-thread breakdown of the host side (FKS_THREAD_PROFILE=path: CPU
+        # seconds per thread group + sampled Python stacks, written at the end)
+        sampler = None
+        if os.environ.get("FKS_THREAD_PROFILE"):
+            from ..utils.trace import ThreadSampler
+            sampler = ThreadSampler().start()
         t_status = t_start
         t_prev = t_start
         busy_since = None
@@ -451,11 +558,14 @@ class SteadyStateSearch:
             # streaming: the grid's queue, plus the batches being staged
             want_buffer = self.service_inflight + self.batch * (self.ahead + 1)
         next_reset = ((start_gen // fs.reset_every) + 1) * fs.reset_every if fs.reset_every else 0
+        rolling = 0.0            # a grid rollover in progress: its start time (launches paused)
+        svc_share = share if svc_started else 0.0
         try:
             while True:
                 progressed = False
+                self._left = sum(b.left for b in batches if b is not None)   # programs not merged yet
                 # 1) keep producers busy (children from the islands' CURRENT elites)
-                queued = len(ready) + sum(b.left for b in batches if b is not None) + \
+                queued = len(ready) + self._left + \
                     sum(len(t) for t, _, pj in staged if pj is None) + self.task_size * len(inflight_tasks)
                 while (not stop and queued < want_buffer + self.task_size * self.producers
                        and len(inflight_tasks) < 2 * self.producers):
@@ -470,7 +580,7 @@ class SteadyStateSearch:
                         continue
                     n = min(self.task_size, target_children[i] - requested[i])
                     requested[i] += n
-                    inflight_tasks.append(pool.submit(_produce, (i, elites, n)))
+                    inflight_tasks.append(pool.submit(_produce, (i, elites, n, self._parent_weights(i, elites))))
                     queued += n
                     progressed = True
                 # 2) collect produced children
@@ -503,7 +613,7 @@ class SteadyStateSearch:
                     if job is None and self.polish_idle and not staged and len(ready) < self.batch \
                             and any(b is None for b in batches) and (
                                 not self.service_inflight
-                                or sum(b.left for b in batches if b is not None) < self.service_inflight // 2):
+                                or self._left < self.service_inflight // 2):
                         # a slot would idle until the producers refill a batch
                         job = self._polish_job(merged, start_gen, polish_next, idle=True)
                         if job is not None:
@@ -523,14 +633,27 @@ class SteadyStateSearch:
                     staged.append((take, stager.submit(ev.prepare_compiled, [c for _, c, _ in take],
                                                        [p for _, _, p in take]), None))
                     progressed = True
-                # 3b) launch staged batches (in order) on free slots
-                for si in range(self.slots):
-                    if batches[si] is not None or not staged or not staged[0][1].done():
-                        continue
-                    if self.service_inflight and sum(b.left for b in batches if b is not None) \
-                            >= self.service_inflight:
-                        break   # the grid has enough queued: results stream back first
-                    take, fut, pjob = staged.popleft()
+                # 3b) launch staged batches on free slots: in staging order on the
+                # stream slots; on the program service any batch whose staging is
+                # done (a batch of cached shapes does not wait behind one still
+                # generating code), and none while a grid rollover drains it
+                free_si = [si for si in range(self.slots) if batches[si] is None] if staged and not rolling else []
+                for si in free_si:
+                    if not staged:
+                        break
+                    if self.service_inflight:
+                        if self._left >= self.service_inflight:
+                            break   # the grid has enough queued: results stream back first
+                        j = next((j for j, st in enumerate(staged) if st[1].done()), -1)
+                        if j < 0:
+                            break
+                        staged.rotate(-j)
+                        take, fut, pjob = staged.popleft()
+                        staged.rotate(j)
+                    else:
+                        if not staged[0][1].done():
+                            break
+                        take, fut, pjob = staged.popleft()
                     pend = fut.result()
                     with roctx_range(f"steady.launch slot {si} ({len(take)} programs)"):
                         t_ph = time.perf_counter()
@@ -539,6 +662,7 @@ class SteadyStateSearch:
                     b = _Batch(si, take, pend, time.time(), pend.new_shapes, pend.jit_s, pjob,
                                [None] * len(take), len(take))
                     batches[si] = b
+                    self._left += len(take)
                     self.stats.jit_s += pend.jit_s
                     self.stats.new_shapes += pend.new_shapes
                     if busy_since is None:
@@ -567,12 +691,16 @@ class SteadyStateSearch:
                 fallbacks = still_fb
                 # 4b) finished batches -> merge (programs the device did not score go
                 # to the host engines in a worker thread: the dispatcher never runs a
-                # CPU-VM or CPython replay itself)
+                # CPU-VM or CPython replay itself).  On the program service one scan
+                # of the done flags names the batches with rows to take
+                news = dev.service_news() if svc_started and dev.service is not None else None
                 for si in range(self.slots):
                     b = batches[si]
                     if b is None:
                         continue
                     if self.service_cfg is not None:
+                        if news is not None and b.pend.native_idx and b.pend.slot not in news:
+                            continue
                         if self._stream(b, merged, islands, ready):
                             progressed = True
                         if b.left > 0:
@@ -584,7 +712,7 @@ class SteadyStateSearch:
                             busy_since = None
                         if b.polish is None and b.pend.fallback_idx:
                             nfb = len(b.pend.fallback_idx)
-                            if svc_aborted:   # (aborted replays and the rest: the run is over)
+                            if svc_aborted or b.aborted:   # (aborted replays and the rest: not needed)
                                 self.stats.abandoned += nfb
                             else:             # (merged when their fallback completes)
                                 self.stats.evaluations += nfb
@@ -680,6 +808,35 @@ class SteadyStateSearch:
                     # millions of events would hold the end of the run
                     dev.abort_service()
                     svc_aborted = True
+                # 5c) grid rollover: JIT modules retired while the grid runs stay
+                # loaded (an unload waits for the device); past `rollover_modules`
+                # pause launches, let the grid drain (stragglers aborted after the
+                # grace period), unload, and start the grid again
+                if svc_started and not svc_aborted and not stop and self.rollover_deferred > 0:
+                    nc = dev.native_compiler
+                    if not rolling and nc.deferred >= self.rollover_deferred:
+                        rolling = time.time()
+                        fs.log.write(kind="steady_rollover_begin", rank=ctx.rank, deferred=nc.deferred,
+                                     inflight=self._left)
+                    if rolling:
+                        busy = [b for b in batches if b is not None]
+                        if busy and time.time() - rolling > self.rollover_grace_s and not any(b.aborted for b in busy):
+                            dev.abort_service()
+                            for b in busy:
+                                b.aborted = True
+                        if not busy:
+                            t_r = time.time()
+                            flushed = nc.deferred
+                            dev.stop_service()
+                            dev.start_service(slots=int(self.service_cfg.get("data_slots", 16384)), share=svc_share)
+                            self.stats.rollovers += 1
+                            self.stats.rollover_s += time.time() - rolling
+                            fs.log.write(kind="steady_rollover", rank=ctx.rank, unloaded=flushed,
+                                         drain_s=round(t_r - rolling, 3), restart_s=round(time.time() - t_r, 3),
+                                         live_modules=nc.stats.get("live_modules"),
+                                         loaded_mb=nc.stats.get("loaded_mb"))
+                            rolling = 0.0
+                            progressed = True
                 # 6) status (time-weighted programs in flight, for the occupancy figure)
                 now = time.time()
                 self.stats.inflight_sum += sum(b.left for b in batches if b is not None) * (now - t_prev)
@@ -714,6 +871,17 @@ class SteadyStateSearch:
                 if not progressed:
                     time.sleep(0.0005)
         finally:
+            if sampler is not None:
+                sampler.stop()
+                rep = sampler.report()
+                rep["main_phase_s"] = {k: round(v, 3) for k, v in self.phase.items()}
+                log.write(kind="steady_threads", rank=ctx.rank, **rep)
+                import json
+                path = os.environ["FKS_THREAD_PROFILE"]
+                if ctx.world_size > 1:
+                    path = f"{path}.rank{ctx.rank}"
+                with open(path, "w") as fh:
+                    json.dump(rep, fh, indent=1)
             pool.shutdown(wait=False, cancel_futures=True)
             stager.shutdown(wait=True, cancel_futures=True)
             if cpl_exec is not None:
@@ -738,9 +906,11 @@ class SteadyStateSearch:
         busy = st.busy_s + (now - busy_since if busy_since is not None else 0.0)
         fs = self.fs
         inflight = sum(b.left for b in batches if b is not None)
+        self._left = inflight
         # occupancy: programs in flight / programs the device holds resident at the
         # current heap top (device_busy only says that *some* batch was in flight)
         capacity = 0
+        info = {}
         dev = getattr(fs.evaluator, "device", None)
         if dev is not None:
             info = dev.info()
@@ -762,7 +932,13 @@ class SteadyStateSearch:
                    occupancy=round(inflight / capacity, 4) if capacity else None,
                    occupancy_mean=round(st.inflight_sum / max(1e-9, st.inflight_n) / capacity, 4) if capacity else None,
                    queued=len(ready),
+                   # device cost of the children (program service: s_memtime cycles
+                   # per replay) and what the selection did with it
+                   mcycles_per_child=round(st.cost_sum / max(1, st.cost_n) / 1e6, 3), cost_rejected=st.cost_rejected,
+                   rollovers=st.rollovers, rollover_s=round(st.rollover_s, 2), mem_used_mb=info.get("mem_used_mb"),
                    producer_tasks=len(tasks), produced=st.produced,
+                   children_per_s=round(st.produced / wall, 2),
+                   llm_inflight=min(len(tasks), self.producers) * self.task_size if self.llm_concurrency else None,
                    producer_ms_per_child=round(1e3 * st.producer_cpu_s / max(1, st.produced), 3),
                    main_cpu_frac=round((time.process_time() - self._cpu0) / wall, 3), rejected=st.rejected, jit_s=round(st.jit_s, 3),
                    generation=fs.generation, best=round(fs.best[1], 6), best_global=round(best_global, 6),

@@ -278,6 +278,7 @@ class DeviceEvaluator:
         self._svc_keys: List[int] = []           # ... and its slot key
         self._svc_buf: Dict[int, list] = {}      # slot key -> [(offset, row)] polled, not taken yet
         self._svc_pumped = 0.0
+        self._svc_orphans = 0                   # rows of forgotten batches (dropped)
         self._svc_lock = threading.Lock()
 
     def info(self) -> dict:
@@ -291,7 +292,7 @@ class DeviceEvaluator:
     #: slots, e.g. the family coupler's, stay below)
     SERVICE_SLOT_BASE = 64
 
-    def start_service(self, slots: int = 16384, share: float = 1.0) -> dict:
+    def start_service(self, slots: int = 16384, share: float = 1.0, idle_polls: int = 1 << 24) -> dict:
         """Launch the resident two-wave grid: from now on every native program
         batch (`submit_native`, any slot) is queued to it instead of launched
         as a kernel of its own, and a batch's `ready` / `wait` follow its own
@@ -299,18 +300,17 @@ class DeviceEvaluator:
         while the rest of them idle.  share: fraction of the two-wave kernel's
         resident capacity the grid takes (the rest stays free for other
         streams' kernels, e.g. the family coupler's row-kernel batches);
-        slots: programs queued or running at most."""
+        slots: programs queued or running at most; idle_polls: polls with
+        nothing published after which the whole grid drains (it is relaunched
+        from the first unstarted program when more arrive)."""
         if self._svc is not None:
             return dict(self._svc)
         self.warm_native()
         nc = self.native_compiler
+        # retired modules are parked (an unload would wait for the grid) until
+        # stop_service; the steady search bounds them by rolling the grid over
         nc.defer_unloads = True
-        # modules are small next to 288 GB of HBM: keep ~8x more live while
-        # retirements cannot unload (a 200 s steady run loads ~2,000)
-        self._svc_saved_max = nc.max_modules
-        if 0 < nc.max_modules < 16384:
-            nc.max_modules = 16384
-        self._svc = dict(self._eng.service_start(int(slots), float(share)))
+        self._svc = dict(self._eng.service_start(int(slots), float(share), int(idle_polls)))
         if not getattr(self, "_svc_atexit", False):
             # a grid left running at interpreter exit would hold every later
             # device-wide synchronisation (JIT module teardown) until its idle timeout
@@ -338,7 +338,6 @@ class DeviceEvaluator:
         self._svc = None
         nc = self.native_compiler
         nc.defer_unloads = False
-        nc.max_modules = getattr(self, "_svc_saved_max", nc.max_modules)
         nc.flush_unloads()
 
     @property
@@ -520,6 +519,9 @@ class DeviceEvaluator:
 
     #: seconds between two scans of the service's done flags (`_service_pump`)
     SERVICE_POLL_S = 0.001
+    #: a whole-batch wait on the service gives up (with the service's state)
+    #: after this long: the replay instruction budget ends any program long before
+    SERVICE_WAIT_S = float(os.environ.get("FKS_SERVICE_WAIT_S", "900"))
 
     def _service_pump(self, min_interval_s: Optional[float] = None) -> None:
         """One `service_poll` (every finished program, all batches) at most
@@ -529,29 +531,44 @@ class DeviceEvaluator:
         if now - self._svc_pumped < (self.SERVICE_POLL_S if min_interval_s is None else min_interval_s):
             return
         self._svc_pumped = now
-        ids, rows = self._eng.service_poll()
+        ids, rows, cyc = self._eng.service_poll()
         if not len(ids):
             return
+        # rows carry the replay's device cycles as a 14th column (SERVICE_COST_COL)
+        rows = np.concatenate([rows, np.asarray(cyc, np.float64).reshape(-1, 1)], axis=1)
         firsts = self._svc_firsts
         for k, ix in enumerate(ids.tolist()):
             j = bisect.bisect_right(firsts, ix) - 1
-            self._svc_buf.setdefault(self._svc_keys[j], []).append((ix - firsts[j], rows[k]))
+            key = self._svc_keys[j] if j >= 0 else None
+            post = self._svc_post.get(key) if key is not None else None
+            # a row of a batch that was forgotten before all its rows arrived
+            # (an interrupted wait) bisects into the batch before it: it lies
+            # past that batch's programs and is dropped, never filed under it
+            if post is None or ix - firsts[j] >= post[1].size:
+                self._svc_orphans += 1
+                continue
+            self._svc_buf.setdefault(key, []).append((ix - firsts[j], rows[k]))
+
+    #: column of service_take rows holding the replay's device cycles (s_memtime
+    #: from claim to result; 0 for rows the device did not replay)
+    SERVICE_COST_COL = len(RESULT_COLUMNS)
 
     def service_take(self, slot: int):
         """Streaming collection from the program service: (positions, rows) of
         the programs of `slot`'s batch that finished since the last call
         (positions index the batch as submitted; programs the JIT declined come
         on the first call with EXC_UNSUPPORTED rows), and whether the batch is
-        now complete (its modules released, the slot free)."""
+        now complete (its modules released, the slot free).  Rows have the
+        result columns plus the replay's device cycles (`SERVICE_COST_COL`)."""
         with self._svc_lock:
             P, idx, first, _ = self._svc_post[slot]
             taken = self._svc_taken.setdefault(slot, [0, False])
             pos_parts, row_parts = [], []
             if not taken[1]:
                 taken[1] = True
-                rest = np.setdiff1d(np.arange(P), idx)
-                if rest.size:
-                    r = np.zeros((rest.size, len(RESULT_COLUMNS)))
+                if idx.size < P:
+                    rest = np.setdiff1d(np.arange(P), idx)
+                    r = np.zeros((rest.size, len(RESULT_COLUMNS) + 1))
                     r[:, 10] = 100.0
                     pos_parts.append(rest)
                     row_parts.append(r)
@@ -566,8 +583,19 @@ class DeviceEvaluator:
             if complete:
                 self._service_forget(slot)
         if not pos_parts:
-            return np.zeros(0, np.int64), np.zeros((0, len(RESULT_COLUMNS))), complete
+            return np.zeros(0, np.int64), np.zeros((0, len(RESULT_COLUMNS) + 1)), complete
         return np.concatenate(pos_parts), np.concatenate(row_parts), complete
+
+    def service_news(self) -> set:
+        """After one scan of the done flags: the slots whose batches have
+        something to take -- finished rows, or a first take still due (the
+        rows of programs the device does not replay) -- so a caller with dozens
+        of batches in flight visits only those."""
+        with self._svc_lock:
+            self._service_pump()
+            news = set(self._svc_buf)
+            news.update(s for s in self._svc_post if s not in self._svc_taken)
+        return news
 
     def _service_forget(self, slot: int) -> None:
         P, idx, first, _ = self._svc_post.pop(slot)
@@ -585,6 +613,7 @@ class DeviceEvaluator:
         P, idx, _, _ = self._svc_post[slot]
         out = np.zeros((P, len(RESULT_COLUMNS)))
         out[:, 10] = 100.0
+        t0 = time.perf_counter()
         try:
             while idx.size:
                 with self._svc_lock:
@@ -592,8 +621,12 @@ class DeviceEvaluator:
                     got = self._svc_buf.get(slot, [])
                     if len(got) >= idx.size:
                         for o, r in got:
-                            out[idx[o]] = r
+                            out[idx[o]] = r[:len(RESULT_COLUMNS)]
                         break
+                if time.perf_counter() - t0 > self.SERVICE_WAIT_S:
+                    raise TimeoutError(f"program service: batch on slot {slot} incomplete after "
+                                       f"{self.SERVICE_WAIT_S:.0f} s ({len(got)} of {idx.size} rows), "
+                                       f"service {dict(self._eng.service_info())}")
                 time.sleep(0.0002)
         finally:
             with self._svc_lock:

@@ -64,7 +64,7 @@ import numpy as np
 
 from .._paths import CSRC_DIR
 from ..policy.compiler import CompiledPolicy
-from ..policy.native_codegen import CodegenError, constant_block, module_source, shape_key
+from ..policy.native_codegen import CodegenError, constant_blocks, module_source, shape_key
 
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 CLANG = os.path.join(ROCM, "lib", "llvm", "bin", "clang")
@@ -95,9 +95,21 @@ def _shape_key(p) -> str:
     compiles the program's feasibility prologue out (gcnjit.elide_range) --
     that code is only valid where the kernels skip infeasible nodes, i.e. for
     programs whose function-table entry carries the prologue bit."""
-    from .gcnjit import elide_range
-    k = shape_key(p)
-    return k + ":fp" if elide_range(p)[1] else k
+    v = p.__dict__.get("_jit_key")
+    if v is None:
+        from .gcnjit import elide_range
+        k = shape_key(p)
+        v = p.__dict__["_jit_key"] = k + ":fp" if elide_range(p)[1] else k
+    return v
+
+
+def launch_key(p) -> str:
+    """`_shape_key`, cached on the program: the producer processes of the steady
+    search compute it (and the constant payload) before a child is pickled to
+    the dispatcher, so the stager's per-program work is a dictionary lookup."""
+    from ..policy.native_codegen import constant_payload
+    constant_payload(p)
+    return _shape_key(p)
 
 
 class JitError(RuntimeError):
@@ -329,6 +341,7 @@ class _ModRec:
     refs: int = 0                    # batches in flight calling into it
     last_use: int = 0                # prepare() sequence number of the last batch using it
     tier: str = "baseline"
+    nbytes: int = 0                  # code-object bytes
 
 
 class NativeCompiler:
@@ -435,13 +448,8 @@ class NativeCompiler:
         P = len(progs)
         fn = np.zeros(P, dtype=np.uint64)
         ok = np.zeros(P, dtype=bool)
-        koff = np.zeros(P, dtype=np.int32)
-        blocks, pos, reasons = [], 0, {}
-        for i, p in enumerate(progs):
-            kb = constant_block(p, self.budget)
-            koff[i] = pos
-            blocks.append(kb)
-            pos += len(kb)
+        kc, koff = constant_blocks(progs, self.budget)
+        reasons = {}
         used = set()
         retry = {}
         with self._lock:
@@ -485,8 +493,7 @@ class NativeCompiler:
         for k, p in up:
             self._tierup_futs.append(self._tierup_executor().submit(self._tierup, k, p))
         self._retire()
-        return NativeBatch(fn, np.concatenate(blocks) if blocks else np.zeros(1, np.int64), koff, ok, reasons, dt,
-                           len(mine), tuple(sorted(used)) + tuple(extra), load_dt)
+        return NativeBatch(fn, kc, koff, ok, reasons, dt, len(mine), tuple(sorted(used)) + tuple(extra), load_dt)
 
     # -- module lifetime ---------------------------------------------------------------------
     def release(self, modules: Sequence[int]) -> None:
@@ -498,11 +505,12 @@ class NativeCompiler:
                     rec.refs -= 1
         self._retire()
 
-    def _add_module(self, handle, tier: str) -> int:
+    def _add_module(self, handle, tier: str, nbytes: int = 0) -> int:
         """Register a loaded module (lock held); returns its id."""
         mid = self._next_mod
         self._next_mod += 1
-        self._modules[mid] = _ModRec(handle, tier=tier, last_use=self._seq)
+        self._modules[mid] = _ModRec(handle, tier=tier, last_use=self._seq, nbytes=int(nbytes))
+        self.stats["loaded_mb"] = round(self.stats.get("loaded_mb", 0.0) + nbytes / 2.0 ** 20, 3)
         self.stats["modules"] += 1
         self.stats["live_modules"] = len(self._modules)
         self.stats["max_live_modules"] = max(self.stats["max_live_modules"], len(self._modules))
@@ -548,26 +556,37 @@ class NativeCompiler:
             # a persistent grid is running (the program service): hipModuleUnload
             # waits on the device (~0.2 s per module measured, 107 s for one
             # retirement burst), so the modules stay loaded until `flush_unloads`
+            # (the steady search rolls the grid over when too many are parked)
             with self._lock:
                 self._deferred.extend(victims)
+                self.stats["deferred_modules"] = len(self._deferred)
             return
         t0 = time.perf_counter()
         for rec in victims:
             rec.handle.unload()
         with self._lock:
             self.stats["unload_s"] += time.perf_counter() - t0
+            self.stats["loaded_mb"] = round(self.stats.get("loaded_mb", 0.0) - sum(r.nbytes for r in victims) / 2.0 ** 20, 3)
 
     def flush_unloads(self) -> int:
         """Unload the modules retired while `defer_unloads` was set (call with
         no persistent kernel running); returns their number."""
         with self._lock:
             victims, self._deferred = getattr(self, "_deferred", []), []
+            self.stats["deferred_modules"] = 0
         t0 = time.perf_counter()
         for rec in victims:
             rec.handle.unload()
         with self._lock:
             self.stats["unload_s"] += time.perf_counter() - t0
+            self.stats["loaded_mb"] = round(self.stats.get("loaded_mb", 0.0) - sum(r.nbytes for r in victims) / 2.0 ** 20, 3)
+            self.stats["flushed_modules"] = self.stats.get("flushed_modules", 0) + len(victims)
         return len(victims)
+
+    @property
+    def deferred(self) -> int:
+        """Retired modules still loaded, waiting for `flush_unloads`."""
+        return len(self._deferred)
 
     # -- background tier-up --------------------------------------------------------------
     def _tierup_candidates(self, keys, progs):
@@ -665,7 +684,7 @@ class NativeCompiler:
             mod = self._baseline.load(codes[lo:hi], 0.0)
             t2 = time.perf_counter()
             with self._lock:
-                mi = self._add_module(mod.handle, "baseline")
+                mi = self._add_module(mod.handle, "baseline", mod.nbytes)
                 self.stats["compile_s"] += t2 - t1
                 self.stats["load_s"] += t2 - t1
                 self.stats["probed_loads"] = self.stats.get("probed_loads", 0) + int(mod.probed)

@@ -166,7 +166,14 @@ def shape_key(prog: CompiledPolicy) -> str:
     """Programs with equal keys share one compiled function: source literals are
     data (read from the constant block), so programs that differ only in them
     share a shape; compiler-generated constants are immediates in the code and
-    part of the key."""
+    part of the key.  Cached on the program."""
+    v = prog.__dict__.get("_shape_key")
+    if v is None:
+        v = prog.__dict__["_shape_key"] = _shape_key_uncached(prog)
+    return v
+
+
+def _shape_key_uncached(prog: CompiledPolicy) -> str:
     h = hashlib.sha1(b"imm-literals-1")
     h.update(prog.code)
     h.update(bytes(prog.ctag))
@@ -174,14 +181,47 @@ def shape_key(prog: CompiledPolicy) -> str:
     return h.hexdigest()
 
 
+def constant_payload(prog: CompiledPolicy) -> np.ndarray:
+    """The constant payloads of one program as int64 (float constants as their
+    bits), in pool order -- cached on the program (a producer process fills
+    the cache before the program is pickled to the dispatcher)."""
+    v = prog.__dict__.get("_kc")   # (bytes: pickles in a fraction of an array's time)
+    if v is None:
+        n = len(prog.ctag)
+        tags = np.asarray(prog.ctag, dtype=np.uint8).reshape(n)
+        f = np.asarray(prog.fconst, dtype=np.float64).reshape(n).view(np.int64)
+        i = np.asarray(prog.iconst, dtype=np.int64).reshape(n)
+        v = prog.__dict__["_kc"] = np.where(tags == TAG_FLOAT, f, i).astype(np.int64).tobytes()
+    return np.frombuffer(v, dtype=np.int64)
+
+
 def constant_block(prog: CompiledPolicy, budget: int) -> np.ndarray:
     """``kc`` of one program: [budget, constant payloads...] as int64 (float bits)."""
-    out = np.zeros(1 + len(prog.ctag), dtype=np.int64)
+    kc = constant_payload(prog)
+    out = np.empty(1 + kc.size, dtype=np.int64)
     out[0] = budget
-    for k, t in enumerate(prog.ctag):
-        out[1 + k] = (np.array(prog.fconst[k], dtype=np.float64).view(np.int64) if t == TAG_FLOAT
-                      else np.int64(prog.iconst[k]))
+    out[1:] = kc
     return out
+
+
+def constant_blocks(progs: Sequence[CompiledPolicy], budget: int) -> Tuple[np.ndarray, np.ndarray]:
+    """(kc, koff) of a batch: every program's `constant_block`, concatenated,
+    and the offset of each -- one numpy concatenation instead of a loop over
+    the constants of every program."""
+    P = len(progs)
+    if not P:
+        return np.zeros(1, np.int64), np.zeros(0, np.int32)
+    head = np.array([budget], dtype=np.int64)
+    parts = []
+    lens = np.empty(P, dtype=np.int64)
+    for j, p in enumerate(progs):
+        kc = constant_payload(p)
+        parts.append(head)
+        parts.append(kc)
+        lens[j] = 1 + kc.size
+    koff = np.zeros(P, dtype=np.int64)
+    np.cumsum(lens[:-1], out=koff[1:])
+    return np.concatenate(parts), koff.astype(np.int32)
 
 
 # ---------------------------------------------------------------------------- analysis
@@ -591,5 +631,5 @@ def module_source(progs: Sequence[CompiledPolicy], with_probes: bool = True, hos
     return "\n\n".join(parts) + "\n"
 
 
-__all__ = ["CodegenError", "PROG_PARAMS", "constant_block", "infer_types", "module_source", "program_source",
+__all__ = ["CodegenError", "PROG_PARAMS", "constant_block", "constant_blocks", "constant_payload", "infer_types", "module_source", "program_source",
            "shape_key"]

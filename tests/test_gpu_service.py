@@ -123,3 +123,27 @@ def test_service_abort_ends_replays_in_flight(dev):
     finally:
         dev.stop_service()
     assert np.array_equal(again, want)
+
+
+def test_service_idle_drain_and_revive(dev):
+    """A grid with a tiny idle limit drains between submissions -- all of it:
+    the first workgroup to time out sets the device-wide stop mirror -- and a
+    submission published while it drains (or after) is replayed by the
+    relaunch from the first unstarted index.  (A workgroup that left alone
+    after claiming an index, while the rest stayed resident, lost that index.)"""
+    import time
+    progs = programs()[:24]
+    want = dev.evaluate_native(progs)
+    dev.start_service(slots=128, share=0.5, idle_polls=256)
+    try:
+        got = []
+        for k, pause in enumerate((0.0, 0.0005, 0.002, 0.0, 0.01, 0.05, 0.001, 0.2)):
+            time.sleep(pause)
+            got.append(dev.evaluate_native(progs[3 * k:3 * k + 3]))
+        sv = dev.info()["service"]
+    finally:
+        dev.stop_service()
+    got = np.concatenate(got)
+    for i in range(len(progs)):
+        assert np.array_equal(got[i], want[i]), i
+    assert sv["launches"] >= 2 and sv["idle_polls"] == 256, sv

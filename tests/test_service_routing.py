@@ -24,7 +24,7 @@ class _FakeEngine:
         self.done = set()       # indexes finished on the "device"
         self.stopped = 0
 
-    def service_start(self, slots, share):
+    def service_start(self, slots, share, idle_polls=1 << 24):
         return {"blocks": 8, "slots": slots, "queue": 2 * slots, "per_cu": 8, "heap_top": 63, "lds": 1}
 
     def service_submit(self, fn, kc, koff):
@@ -46,7 +46,7 @@ class _FakeEngine:
         for k, s in enumerate(hit):
             rows[k, 0] = self.row[s]
             self._free(s)
-        return ids, rows
+        return ids, rows, 1000 * (ids + 1)   # (device cycles)
 
     def _free(self, s):
         del self.held[s]
@@ -86,7 +86,7 @@ def _dev(nslots=8):
     d._jit = _FakeCompiler()
     d.math_exact = True
     d._native_post, d._native_mods, d._svc, d._svc_post, d._svc_taken = {}, {}, None, {}, {}
-    d._svc_firsts, d._svc_keys, d._svc_buf, d._svc_pumped = [], [], {}, 0.0
+    d._svc_firsts, d._svc_keys, d._svc_buf, d._svc_pumped, d._svc_orphans = [], [], {}, 0.0, 0
     d._svc_lock = threading.Lock()
     d.SERVICE_POLL_S = 0.0
     d._warm_s = 0.0
@@ -180,3 +180,39 @@ def test_evaluator_collect_partial_streams_and_lists_fallbacks(default_workload)
     assert not complete and len(got) == 1 and got[0][0] == 0 and got[0][1].score == 0.5
     got, complete = ev.collect_partial(pend)
     assert complete and got == [] and pend.fallback_idx == [1, 2]
+
+
+def test_service_news_and_cost_column():
+    """service_news names the batches with rows to take (and first takes still
+    due); taken rows carry the replay's device cycles in SERVICE_COST_COL."""
+    d = _dev()
+    d.start_service(slots=8)
+    d.submit_native(0, ["a", "b"])          # indexes 0, 1
+    d.submit_native(1, ["host"])            # nothing published: complete at its first take
+    assert d.service_news() == {0, 1}
+    pos, rows, complete = d.service_take(1)
+    assert complete and list(pos) == [0] and rows.shape[1] == d.SERVICE_COST_COL + 1
+    d.service_take(0)
+    assert d.service_news() == set()
+    d._eng.done.add(1)
+    assert d.service_news() == {0}
+    pos, rows, complete = d.service_take(0)
+    assert list(pos) == [1] and rows[0, d.SERVICE_COST_COL] == 2000 and not complete
+
+
+def test_rows_of_a_forgotten_batch_are_dropped():
+    """A batch forgotten before all its rows arrived (an interrupted wait):
+    its late rows are counted and dropped, never filed under the batch before
+    it (they bisect into it)."""
+    d = _dev()
+    d.start_service(slots=8)
+    d.submit_native(0, ["a", "b"])          # indexes 0, 1
+    d.submit_native(1, ["c", "d"])          # indexes 2, 3
+    with d._svc_lock:
+        d._service_forget(1)
+    d._eng.done.update({0, 2, 3})
+    pos, rows, complete = d.service_take(0)
+    assert list(pos) == [0] and not complete and d._svc_orphans == 2
+    d._eng.done.add(1)
+    pos, rows, complete = d.service_take(0)
+    assert list(pos) == [1] and complete

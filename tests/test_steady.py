@@ -210,3 +210,64 @@ def test_steady_with_family_coupler(tmp_path):
     # the exported program re-scores to the family score it was exported with
     best = max(coupled, key=lambda r: r["score"])
     assert best["score"] == best["family_score"]
+
+
+def test_llm_fanout_overlaps_request_latency():
+    """llm.concurrency: a producer task's requests wait concurrently (threads),
+    so a task of 8 requests to a 0.4 s model takes ~0.4 s, not 3.2 s; the
+    children are the scripted replies, validated and compiled as usual."""
+    import time
+    from funsearch_kubernetes_simulator_amd.funsearch import steady
+    from funsearch_kubernetes_simulator_amd.funsearch.llm import LatencyClient, make_client, remote_like
+    from funsearch_kubernetes_simulator_amd.models.library import seed_policies
+    cfg = {"backend": "scripted", "responses": ["return node.cpu_milli_left - pod.cpu_milli * 0.5",
+                                                "return -node.memory_mib_left"], "latency_s": [0.4, 0.4]}
+    assert remote_like(cfg) and not remote_like({"backend": "mutation"})
+    assert isinstance(make_client(cfg), LatencyClient)
+    saved = dict(steady._W)
+    try:
+        steady._producer_init(cfg, 3, 0, fanout=8)
+        elites = [(seed_policies()["first_fit"], 0.43), (seed_policies()["best_fit"], 0.45)]
+        t0 = time.time()
+        out, _ = steady._produce((1, elites, 8, [1.0, 3.0]))
+        dt = time.time() - t0
+        assert len(out) == 8 and all(isl == 1 and prog is not None for isl, code, prog in out)
+        assert dt < 1.6, dt        # sequential: 8 x 0.4 s
+        assert steady._W["gen"].llm_client.calls == 8
+    finally:
+        pool = steady._W.get("fanout")
+        if pool is not None:
+            pool.shutdown(wait=True)
+        steady._W.clear()
+        steady._W.update(saved)
+
+
+def test_weighted_parent_sampling_prefers_cheap_parents():
+    import random
+    from funsearch_kubernetes_simulator_amd.funsearch.steady import _sample_parents
+    rng = random.Random(3)
+    elites = [("a", 1.0), ("b", 0.9), ("c", 0.8)]
+    counts = {"a": 0, "b": 0, "c": 0}
+    for _ in range(3000):
+        ps = _sample_parents(rng, elites, [0.25, 0.25, 4.0])
+        assert len(ps) == 2 and ps[0] != ps[1]
+        for c, _ in ps:
+            counts[c] += 1
+    assert counts["c"] > 2900 and counts["a"] > 1000 and counts["b"] > 1000
+    assert sorted(_sample_parents(rng, elites[:2], [1.0, 9.0])) == sorted(elites[:2])
+
+
+def test_steady_with_llm_concurrency(tmp_path):
+    """A steady run with a latency-modelled client and `llm.concurrency`:
+    requests spread over producers x task_size threads (the steady_llm record)."""
+    from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
+    cfg = _cfg(tmp_path, gens=2)
+    cfg["llm"] = {"backend": "mutation", "seed": 5, "latency_s": [0.05, 0.15], "concurrency": 8}
+    fs = IslandFunSearch(cfg)
+    fs.run(2)
+    recs = [json.loads(l) for l in open(tmp_path / "log.jsonl")]
+    llm = [r for r in recs if r["kind"] == "steady_llm"]
+    assert llm and llm[0]["concurrency"] == 8 and llm[0]["task_size"] == 4
+    assert fs.steady.stats.produced == 2 * 2 * 4
+    fin = [r for r in recs if r["kind"] == "steady_final"][-1]
+    assert fin["children_per_s"] > 0

@@ -11,8 +11,11 @@ exercises, on the one-GPU box, everything a rank does with RCCL:
   program batches replay on the extension's HIP streams, with results equal
   to the local (``backend="none"``) ones;
 * `MigrationChannel.post / poll` round trips with the search's own payloads;
-* a short steady-state config-3 run with ``migrate_every`` 5 (every
-  migration an RCCL all-gather next to the replay slots).
+* a short steady-state run of the shipped config 4 (``--config``: steady loop,
+  resident program service, family coupler; ``migrate_every`` 5 here, so every
+  few seconds an RCCL all-gather runs beside the persistent grid), ending with
+  the service's abort + stop: every gather must complete, none may block the
+  dispatcher for more than ``--max-stall-s``, and the run must end promptly.
 
 Prints one JSON line.  Run it under ``rocprofv3 --kernel-trace --stats`` to
 see the RCCL all-gather kernels beside ``k_replay_native_duo``.
@@ -35,6 +38,8 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--steady-s", type=float, default=20.0)
     ap.add_argument("--migrate-every", type=int, default=5)
+    ap.add_argument("--config", default="configs/config4.json")
+    ap.add_argument("--max-stall-s", type=float, default=1.0)
     a = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", str(29600 + os.getpid() % 300))
@@ -87,11 +92,12 @@ def main() -> None:
     # a steady config-3 run with RCCL migrations
     from funsearch_kubernetes_simulator_amd.funsearch.islands import IslandFunSearch
     from funsearch_kubernetes_simulator_amd.funsearch.search import load_config
-    cfg = load_config(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "configs",
-                                   "config3_steady.json"))
+    cfg = load_config(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), a.config))
     tmp = tempfile.mkdtemp(prefix="fks_rccl_")
     cfg["islands"]["migrate_every"] = a.migrate_every
-    cfg["islands"]["steady"].update(wall_s=a.steady_s, producers=8, status_every_s=5)
+    cfg["islands"].setdefault("steady", {}).update(wall_s=a.steady_s, producers=8, status_every_s=5)
+    out["config"] = a.config
+    out["service"] = bool(cfg["islands"]["steady"].get("service"))
     cfg["checkpoint"] = {"dir": os.path.join(tmp, "ck"), "every": 1000}
     cfg["log_path"] = os.path.join(tmp, "metrics.jsonl")
     run = IslandFunSearch(cfg, evaluator=ev)
@@ -104,9 +110,22 @@ def main() -> None:
     out["steady_best"] = round(float(score), 6)
     out["steady_evaluations"] = int(run.evaluations)
     out["collective_wait_s"] = mig[-1]["collective_wait_s"] if mig else None
+    out["max_stall_s"] = round(run.steady.channel.max_stall_s, 4)
+    out["max_gather_s"] = round(run.steady.channel.max_gather_s, 4)
+    out["posted"] = (run.steady.channel.next - run.steady.channel.every) // max(1, run.steady.channel.every) \
+        if run.steady.channel.next is not None else 0
+    svc = [json.loads(l) for l in open(cfg["log_path"]) if '"steady_service"' in l]
+    fin = [json.loads(l) for l in open(cfg["log_path"]) if '"steady_final"' in l]
+    out["service_blocks"] = svc[0]["blocks"] if svc else 0
+    if fin:
+        out["final"] = {k: fin[-1].get(k) for k in ("wall_s", "evals_per_s", "occupancy_mean", "coupled",
+                                                      "abandoned", "rollovers")}
     if st is not None:
         out["steady_stats"] = {k: getattr(st, k) for k in ("migrations", "evaluations") if hasattr(st, k)}
     assert len(mig) >= 1, "no migration completed"
+    assert not run.steady.channel.pending, "a gather never completed"
+    assert out["max_stall_s"] <= a.max_stall_s, f"a collective blocked the dispatcher {out['max_stall_s']} s"
+    assert out["steady_s"] <= a.steady_s + 60, "the run did not end promptly after its wall time"
     dist.shutdown()
     print(json.dumps(out), flush=True)
 
