@@ -329,15 +329,32 @@ PYBIND11_MODULE(_fks_cpu, m) {
     // difflib.SequenceMatcher(None, a, b).ratio() >= threshold
     return SeqMatcher(a, b).at_least(threshold);
   });
-  m.def("similar_to_any", [](const std::u32string& a, const std::vector<std::u32string>& bs, double threshold) {
-    // index of the first b with difflib ratio(a, b) >= threshold, or -1: the
+  m.def("similar_to_any", [](const std::u32string& a, const std::vector<std::u32string>& bs, double threshold,
+                             int threads) {
+    // the index of some b with difflib ratio(a, b) >= threshold, or -1: the
     // similarity gate of one child against a population, off the GIL (the
-    // steady search's stager and collection threads keep running)
+    // steady search's stager and collection threads keep running) and over
+    // `threads` host threads (a 4 kB pair is ~0.1-1 ms; an island holds ~20)
     py::gil_scoped_release rel;
-    for (size_t i = 0; i < bs.size(); ++i)
-      if (SeqMatcher(a, bs[i]).at_least(threshold)) return (int64_t)i;
-    return (int64_t)-1;
-  });
+    const size_t n = bs.size();
+    const size_t T = std::min<size_t>(n, (size_t)std::max(1, threads));
+    if (T <= 1) {
+      for (size_t i = 0; i < n; ++i)
+        if (SeqMatcher(a, bs[i]).at_least(threshold)) return (int64_t)i;
+      return (int64_t)-1;
+    }
+    std::atomic<size_t> next{0};
+    std::atomic<int64_t> found{-1};
+    auto work = [&] {
+      for (size_t i; found.load(std::memory_order_relaxed) < 0 && (i = next.fetch_add(1)) < n;)
+        if (SeqMatcher(a, bs[i]).at_least(threshold)) found.store((int64_t)i);
+    };
+    std::vector<std::thread> pool;
+    for (size_t t = 1; t < T; ++t) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
+    return found.load();
+  }, py::arg("a"), py::arg("bs"), py::arg("threshold"), py::arg("threads") = 1);
   m.def("exact_mean", [](std::vector<double> xs) {
     FixedAcc a; for (double x : xs) a.add(x);
     return py::make_tuple(fixed_mean(a), a.inexact);

@@ -430,7 +430,7 @@ class DeviceEngine {
     submit_native_impl(slot, fn, kc, koff, false);
   }
 
-  // native programs on the s_memtime-profiled row kernel: (result table, [waves, 8] phase cycles)
+  // native programs on the s_memtime-profiled row kernel: (result table, [waves, 16]: phase cycles, kind mix)
   py::tuple profile_native(py::array_t<uint64_t, py::array::c_style | py::array::forcecast> fn,
                            py::array_t<int64_t, py::array::c_style | py::array::forcecast> kc,
                            py::array_t<int32_t, py::array::c_style | py::array::forcecast> koff) {
@@ -438,8 +438,9 @@ class DeviceEngine {
     submit_native_impl(0, fn, kc, koff, true);
     Slot& s = *slots_[0];
     const int waves = last_native_waves_;
-    py::array_t<uint64_t> prof({(py::ssize_t)waves, (py::ssize_t)8});
-    HIP_OK(hipMemcpyAsync(prof.mutable_data(), s.prof.p, (size_t)waves * 64, hipMemcpyDeviceToHost, s.stream));
+    py::array_t<uint64_t> prof({(py::ssize_t)waves, (py::ssize_t)kRowProfWords});
+    HIP_OK(hipMemcpyAsync(prof.mutable_data(), s.prof.p, (size_t)waves * 8 * kRowProfWords, hipMemcpyDeviceToHost,
+                          s.stream));
     py::array_t<double> tab = wait(0);
     HIP_OK(hipStreamSynchronize(s.stream));
     return py::make_tuple(tab, prof);
@@ -832,7 +833,7 @@ class DeviceEngine {
     return py::make_tuple(tab, prof);
   }
 
-  // row kernel, s_memtime build: (result table, per-wave phase cycles [waves, 8])
+  // row kernel, s_memtime build: (result table, per wave [waves, 16]: phase cycles [0, 8), wave-steps by kind set [9, 16))
   py::tuple profile_rows(py::array_t<int32_t, py::array::c_style | py::array::forcecast> fam,
                          py::array_t<double, py::array::c_style | py::array::forcecast> weights) {
     if (!rows_ok_) throw std::invalid_argument("row kernel needs <= 16 nodes");
@@ -841,8 +842,9 @@ class DeviceEngine {
     stage_builtin(s, fam.data(), weights.data(), (int)fam.size());
     const int waves = launch_rows(s, true);
     finish(s);
-    py::array_t<uint64_t> prof({(py::ssize_t)waves, (py::ssize_t)8});
-    HIP_OK(hipMemcpyAsync(prof.mutable_data(), s.prof.p, (size_t)waves * 64, hipMemcpyDeviceToHost, s.stream));
+    py::array_t<uint64_t> prof({(py::ssize_t)waves, (py::ssize_t)kRowProfWords});
+    HIP_OK(hipMemcpyAsync(prof.mutable_data(), s.prof.p, (size_t)waves * 8 * kRowProfWords, hipMemcpyDeviceToHost,
+                          s.stream));
     py::array_t<double> tab = wait(0);
     HIP_OK(hipStreamSynchronize(s.stream));
     return py::make_tuple(tab, prof);
@@ -1206,7 +1208,7 @@ class DeviceEngine {
     const int cap = std::max(1, (int)(row_share_ * lay.second * num_cus_));
     const int waves = std::max(1, std::min((P + kRowsPerWave - 1) / kRowsPerWave, cap));
     s.gheap.reserve((size_t)row_heap_entries(W_.n_pods) * 8 * (size_t)waves * kRowsPerWave);
-    if (profiled) s.prof.reserve((size_t)waves * 64);
+    if (profiled) s.prof.reserve((size_t)waves * 8 * kRowProfWords);
     const size_t wb = (size_t)P * kWeights * 8;
     const fksk::BuiltinArgs a{Wl, upload_workload(s, Wl), reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + wb),
                               s.h_in.dev<double>(), s.w.as<double>(), s.res.as<DevResult>(), s.gheap.as<uint64_t>(),
@@ -1286,7 +1288,7 @@ class DeviceEngine {
     const int cap = std::max(1, (int)(row_share_ * per_cu * num_cus_));
     const int waves = std::max(1, std::min((P + ra - 1) / ra, cap));
     s.gheap.reserve((size_t)entries * 8 * (size_t)waves * kRowsPerWave);
-    if (profiled) s.prof.reserve((size_t)waves * 64);
+    if (profiled) s.prof.reserve((size_t)waves * 8 * kRowProfWords);
     const fksk::BuiltinArgs a{Wl, upload_workload(s, Wl), nullptr, nullptr, nullptr, s.res.as<DevResult>(),
                               s.gheap.as<uint64_t>(), profiled ? s.prof.as<uint64_t>() : nullptr, s.h_tab.dev<double>()};
     s.fused_table = true;

@@ -391,13 +391,17 @@ __host__ __device__ inline size_t rows_lds_bytes(int n_pods, int T, int rows = k
 struct RowNoProf {
   __device__ void start(FKS_LDS uint64_t*) {}
   __device__ void mark(int) {}
+  __device__ void kinds(int) {}
   __device__ void flush(uint64_t*) {}
 };
+// s_memtime phase split, plus a histogram of the event kinds a wave-step's
+// rows executed: the row kernel runs the union of its four rows' paths under
+// exec masks, so the mix decides how much of the issued work is masked off
 struct RowProf {
-  FKS_LDS uint64_t* c;   // [0, 8): phase cycles, [8]: last timestamp
+  FKS_LDS uint64_t* c;   // [0, 8): phase cycles, [8]: last timestamp, [8 + m]: wave-steps with kind set m
   __device__ void start(FKS_LDS uint64_t* at) {
     c = at;
-    if (lane_id() < 9) c[lane_id()] = lane_id() == 8 ? __builtin_amdgcn_s_memtime() : 0;
+    if (lane_id() < 16) c[lane_id()] = lane_id() == 8 ? __builtin_amdgcn_s_memtime() : 0;
   }
   __device__ void mark(int ph) {
     const uint64_t now = __builtin_amdgcn_s_memtime();
@@ -406,11 +410,18 @@ struct RowProf {
       c[8] = now;
     }
   }
+  // cat: this row's event -- 0 none (no policy), 1 deletion, 2 creation
+  // placed, 3 creation failed; m = the set of kinds present (bit cat - 1)
+  __device__ void kinds(int cat) {
+    const int m = (ballot(cat == 1) != 0 ? 1 : 0) | (ballot(cat == 2) != 0 ? 2 : 0) | (ballot(cat == 3) != 0 ? 4 : 0);
+    if (m != 0 && lane_id() == __builtin_amdgcn_readfirstlane(lane_id())) c[8 + m] += 1;
+  }
   __device__ void flush(uint64_t* o) {
-    if (lane_id() < 8) o[lane_id()] = c[lane_id()];
+    if (lane_id() < 16) o[lane_id()] = lane_id() == 8 ? 0 : c[lane_id()];
   }
 };
 constexpr int kRowProfBytes = 128;
+constexpr int kRowProfWords = 16;   // per wave in the host's profile buffer
 
 // The row kernel body: a persistent work queue of policies.  Every row claims
 // policies with atomicAdd(queue, 1); a row that finishes its replay (or
@@ -587,6 +598,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
     // opaque lane id: keeps the lane-derived subtree predicates out of SGPRs
     asm volatile("" : "+v"(jv));
     heap.j = jv;
+    int ecat = 0;   // (profiled build: the event's kind for the wave-step histogram)
     do {   // one event; `break` = abort the replay (exc set) or end of the event
       // ---------------- pop
       const uint64_t top = heap.ld(0);
@@ -616,6 +628,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
             if ((mask >> g) & 1) nr.g_add(0, g, pod.gmilli);
         }
         if (cold()->trace_hash) rcs[0] = mix_event(rcs[0], ((uint64_t)(uint32_t)rank << 2) | 1, (uint64_t)t);
+        ecat = 1;
         prof.mark(PH_DELETE);
       } else {
         // ---------------- creation: score the row's nodes, first maximum wins
@@ -713,6 +726,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
             bump(1);
           }
           if (cold()->trace_hash) rcs[0] = mix_event(rcs[0], ((uint64_t)(uint32_t)rank << 2) | 2, (uint64_t)t);
+          ecat = 3;
           prof.mark(PH_FAIL);
         } else {
           // ---------------- commit on best_node
@@ -744,6 +758,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
                       ((uint64_t)best_node << 2) | kDelete;
           if (cold()->trace_hash)
             rcs[0] = mix_event(rcs[0], ((uint64_t)(uint32_t)rank << 2), ((uint64_t)t << 8) ^ (uint64_t)best_node);
+          ecat = 2;
           prof.mark(PH_COMMIT);
         }
         // one heappush for both outcomes (re-queued creation or deletion): rows
@@ -792,6 +807,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
       }
       prof.mark(PH_EVAL);
     } while (0);
+    prof.kinds(ecat);
 
     if (n > 0 && exc == EXC_NONE) continue;
     // ---------------- replay done (or aborted): result, then the next policy
@@ -858,7 +874,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
     if (have) begin();
     prof.mark(PH_EVAL + 1);   // result write-back + next policy's prologue
   }
-  if (prof_out) prof.flush(prof_out + (size_t)blockIdx.x * 8);
+  if (prof_out) prof.flush(prof_out + (size_t)blockIdx.x * kRowProfWords);
 }
 
 }  // namespace fksd

@@ -51,7 +51,7 @@ try:
 except ImportError:  # native CPU module not built: the reference's own difflib path
     _similar_at_least = _difflib_at_least
 
-    def _similar_to_any(a: str, bs, threshold: float) -> int:
+    def _similar_to_any(a: str, bs, threshold: float, threads: int = 1) -> int:
         for i, b in enumerate(bs):
             if _difflib_at_least(a, b, threshold):
                 return i
@@ -92,6 +92,8 @@ class SimpleFunSearch:
         self.early_stop_threshold = fs["early_stop_threshold"]
         self.elite_size = fs["elite_size"]
         self.similarity_threshold = fs.get("similarity_threshold", 0.85)
+        #: host threads for one child's similarity scan against the population
+        self.similarity_threads = int(fs.get("similarity_threads", 4))
         self.max_workers = fs.get("max_workers", 8)
         self.policies_per_generation = fs.get("policies_per_generation", 8)
         self.print_lock = threading.Lock()
@@ -161,7 +163,8 @@ class SimpleFunSearch:
         SequenceMatcher (`csrc/cpu/seqmatch.hpp`, ~40x faster) when built."""
         a = new_code.strip()
         others = [code.strip() for code, score in self.population if score >= new_score]
-        return bool(others) and _similar_to_any(a, others, self.similarity_threshold) >= 0
+        return bool(others) and _similar_to_any(a, others, self.similarity_threshold,
+                                                self.similarity_threads if len(others) > 2 else 1) >= 0
 
     def _generate_single_policy(self, idx: int, elites, feedback: str) -> Tuple[int, Optional[str]]:
         with self.print_lock:

@@ -53,6 +53,10 @@ from ..parallel import dist
 from ..utils.trace import roctx_range
 from .search import FEEDBACK
 
+#: device cost of a child scored on the host engines (the JIT declined it):
+#: the selection treats it as the costliest kind of program
+HOST_COST = -1.0
+
 # ---------------------------------------------------------------------------- producer processes
 _W: dict = {}
 
@@ -173,6 +177,51 @@ class _Batch:
     aborted: bool = False            # in flight at a grid rollover's abort: no host fallbacks
 
 
+class _Slots:
+    """Batch slots (a list of `_Batch` or None) that keeps its occupied indices:
+    the program service runs with ~1,000 slots (a straggler holds its batch's
+    slot until its last program is merged), and the dispatcher loop visits
+    only the occupied ones."""
+
+    def __init__(self, n: int):
+        self._b: List[Optional[_Batch]] = [None] * n
+        self._free = collections.deque(range(n))
+        self._active: dict = {}          # slot -> batch (insertion order: launch order)
+
+    def __len__(self) -> int:
+        return len(self._b)
+
+    def __getitem__(self, si: int) -> Optional["_Batch"]:
+        return self._b[si]
+
+    def __setitem__(self, si: int, b: Optional["_Batch"]) -> None:
+        old = self._b[si]
+        self._b[si] = b
+        if b is None and old is not None:
+            del self._active[si]
+            self._free.append(si)
+        elif b is not None and old is None:
+            self._active[si] = b
+            self._free.remove(si) if self._free and self._free[0] != si else self._free.popleft()
+        elif b is not None:
+            self._active[si] = b
+
+    def live(self) -> list:
+        return list(self._active.values())
+
+    def active_ids(self) -> list:
+        return list(self._active)
+
+    def empty(self) -> bool:
+        return not self._active
+
+    def has_free(self) -> bool:
+        return bool(self._free)
+
+    def next_free(self) -> Optional[int]:
+        return self._free[0] if self._free else None
+
+
 @dataclass
 class SteadyStats:
     evaluations: int = 0
@@ -254,7 +303,7 @@ class SteadyStateSearch:
             # slowest program is done; results stream out before that) and the
             # programs kept queued on the grid (`inflight`, default 1.5 x its
             # resident workgroups, set when the service starts)
-            self.slots = max(1, int(svc.get("slots", slots or 64)))
+            self.slots = max(1, int(svc.get("slots", slots or 1024)))
             self.slot_base = dev.SERVICE_SLOT_BASE
         self.service_inflight = 0
         #: device-cost selection (service runs: every child's replay cycles are
@@ -271,11 +320,13 @@ class SteadyStateSearch:
         #: unloads them and starts it again
         self.rollover_deferred = int((svc or {}).get("rollover_modules", 2048)) if isinstance(svc, dict) else 2048
         self.rollover_grace_s = float((svc or {}).get("rollover_grace_s", 3.0)) if isinstance(svc, dict) else 3.0
+        #: programs waiting for (or in) a host-engine fallback at most; more are shed
+        self.fallback_cap = int((svc or {}).get("fallback_cap", 64)) if isinstance(svc, dict) else 1 << 30
         self._cost: dict = {}            # island -> {code: device cycles}
         if dev is not None:
             # the two-wave kernel sizes its LDS heap top so that every slot's batch
             # stays resident at once (csrc/hip/engine_host.hip.h duo_top)
-            dev.set_options(native_inflight=self.batch * self.slots)
+            dev.set_options(native_inflight=min(self.batch * self.slots, 1 << 14))
             if not tierup:
                 # shapes the baseline generator declines (~0.1%) go to the host
                 # engines asynchronously instead of a ~0.2 s LLVM compile on the
@@ -305,11 +356,13 @@ class SteadyStateSearch:
             return None
         cmap = self._cost.get(i) or {}
         costs = [cmap.get(c) for c, _ in elites]
-        known = sorted(x for x in costs if x)
-        if len(known) < 2:
+        known = sorted(x for x in costs if x and x > 0)
+        if not any(x is not None and x < 0 for x in costs) and len(known) < 2:
             return None
-        med = known[len(known) // 2]
-        return [1.0 if not x else min(4.0, max(0.25, med / x)) for x in costs]
+        med = known[len(known) // 2] if known else 1.0
+        # a host-scored elite (HOST_COST: its same-shape children replay on the
+        # CPU VM, seconds of a core each) breeds least
+        return [1.0 if not x else 0.25 if x < 0 else min(4.0, max(0.25, med / x)) for x in costs]
 
     def _merge_one(self, s, code: str, score: float, cost: float = 0.0, island: Optional[int] = None) -> bool:
         if len(s.population) >= s.population_size and score <= min(sc for _, sc in s.population):
@@ -317,14 +370,20 @@ class SteadyStateSearch:
             # ties with): skip the similarity scan, same resulting population
             return False
         cmap = self._cost.setdefault(island, {}) if island is not None else None
-        if cost > 0 and cmap is not None and self.cost_bloat > 0 and score <= s.best_score:
-            known = sorted(cmap[c] for c, _ in s.population if c in cmap)
+        if cost != 0 and cmap is not None and self.cost_bloat > 0 and score <= s.best_score:
+            if cost < 0:
+                # scored on the host (the device JIT declined it): enters only as a
+                # new island best -- its constant-only children would all replay
+                # on the CPU VM
+                self.stats.cost_rejected += 1
+                return False
+            known = sorted(cmap[c] for c, _ in s.population if cmap.get(c, 0) > 0)
             if len(known) >= 3 and cost > self.cost_bloat * known[len(known) // 2]:
                 self.stats.cost_rejected += 1
                 return False
         if s._is_too_similar(code, score):
             return False
-        if cost > 0 and cmap is not None:
+        if cost != 0 and cmap is not None:
             cmap[code] = cost
             if len(cmap) > 4 * s.population_size:   # forget programs that left the population
                 live = {c for c, _ in s.population}
@@ -447,7 +506,7 @@ class SteadyStateSearch:
         self.phase["merge"] += time.perf_counter() - t_ph
         return bool(got) or complete
 
-    def _log_batch(self, log, ctx, si: int, b: _Batch, batches, ready) -> None:
+    def _log_batch(self, log, ctx, si: int, b: _Batch, ready) -> None:
         ev_n = [r.n_events for r in b.results if r is not None and r.engine == "hip-native"]
         cyc = [r.device_cycles for r in b.results if r is not None and r.device_cycles > 0]
         log.write(kind="steady_batch", rank=ctx.rank, slot=si, programs=len(b.items), new_shapes=b.new_shapes,
@@ -538,7 +597,7 @@ class SteadyStateSearch:
         cpl_fut = None
         cpl_next = start_gen
         ready: List[tuple] = []          # produced children waiting for a batch
-        batches: List[Optional[_Batch]] = [None] * self.slots
+        batches = _Slots(self.slots)
         # children requested per island: production stops at the island's target
         requested = [0] * k
         rr = 0
@@ -563,7 +622,7 @@ class SteadyStateSearch:
         try:
             while True:
                 progressed = False
-                self._left = sum(b.left for b in batches if b is not None)   # programs not merged yet
+                self._left = sum(b.left for b in batches.live())   # programs not merged yet
                 # 1) keep producers busy (children from the islands' CURRENT elites)
                 queued = len(ready) + self._left + \
                     sum(len(t) for t, _, pj in staged if pj is None) + self.task_size * len(inflight_tasks)
@@ -611,7 +670,7 @@ class SteadyStateSearch:
                 if self.polish_every and not stop and len(staged) < self.ahead:
                     job = self._polish_job(merged, start_gen, polish_next)
                     if job is None and self.polish_idle and not staged and len(ready) < self.batch \
-                            and any(b is None for b in batches) and (
+                            and batches.has_free() and (
                                 not self.service_inflight
                                 or self._left < self.service_inflight // 2):
                         # a slot would idle until the producers refill a batch
@@ -627,7 +686,7 @@ class SteadyStateSearch:
                 while ready and len(staged) < self.ahead:
                     tail = not inflight_tasks and all(requested[i] >= target_children[i] for i in range(k))
                     if len(ready) < self.batch and not (
-                            tail or stop or (all(b is None for b in batches) and not staged)):
+                            tail or stop or (batches.empty() and not staged)):
                         break
                     take, ready = ready[:self.batch], ready[self.batch:]
                     staged.append((take, stager.submit(ev.prepare_compiled, [c for _, c, _ in take],
@@ -637,10 +696,8 @@ class SteadyStateSearch:
                 # stream slots; on the program service any batch whose staging is
                 # done (a batch of cached shapes does not wait behind one still
                 # generating code), and none while a grid rollover drains it
-                free_si = [si for si in range(self.slots) if batches[si] is None] if staged and not rolling else []
-                for si in free_si:
-                    if not staged:
-                        break
+                while staged and not rolling and batches.has_free():
+                    si = batches.next_free()
                     if self.service_inflight:
                         if self._left >= self.service_inflight:
                             break   # the grid has enough queued: results stream back first
@@ -684,7 +741,10 @@ class SteadyStateSearch:
                         if r.engine == "shed":
                             self.stats.shed += 1
                             continue
-                        self._merge_one(islands[isl], code, r.score)
+                        if self.service_cfg is not None:   # (device-cost selection on)
+                            self._merge_one(islands[isl], code, r.score, HOST_COST, isl)
+                        else:
+                            self._merge_one(islands[isl], code, r.score)
                     self.stats.fallback += len(idx)
                     self.phase["merge"] += time.perf_counter() - t_m
                     progressed = True
@@ -694,10 +754,8 @@ class SteadyStateSearch:
                 # CPU-VM or CPython replay itself).  On the program service one scan
                 # of the done flags names the batches with rows to take
                 news = dev.service_news() if svc_started and dev.service is not None else None
-                for si in range(self.slots):
+                for si in batches.active_ids():
                     b = batches[si]
-                    if b is None:
-                        continue
                     if self.service_cfg is not None:
                         if news is not None and b.pend.native_idx and b.pend.slot not in news:
                             continue
@@ -707,13 +765,20 @@ class SteadyStateSearch:
                             continue
                         # complete: its host fallbacks and the batch record
                         batches[si] = None
-                        if busy_since is not None and all(x is None for x in batches):
+                        if busy_since is not None and batches.empty():
                             self.stats.busy_s += time.time() - busy_since
                             busy_since = None
                         if b.polish is None and b.pend.fallback_idx:
                             nfb = len(b.pend.fallback_idx)
                             if svc_aborted or b.aborted:   # (aborted replays and the rest: not needed)
                                 self.stats.abandoned += nfb
+                            elif sum(x[2] for x in fallbacks) + nfb > self.fallback_cap:
+                                # the host engines are behind (a CPU-VM replay of an evolved
+                                # program takes seconds of a core, and the producers need the
+                                # cores): shed instead of queueing
+                                self.stats.shed += nfb
+                                for i in b.pend.fallback_idx:
+                                    merged[b.items[i][0]] += 1
                             else:             # (merged when their fallback completes)
                                 self.stats.evaluations += nfb
                                 fs.evaluations += nfb
@@ -721,7 +786,7 @@ class SteadyStateSearch:
                                                   nfb))
                         if b.polish is None:
                             self.stats.batches += 1
-                            self._log_batch(log, ctx, si, b, batches, ready)
+                            self._log_batch(log, ctx, si, b, ready)
                         progressed = True
                         continue
                     if not ev.ready(b.pend):
@@ -733,7 +798,7 @@ class SteadyStateSearch:
                         # declined variants are not replayed on the host: the polish
                         # takes the best device-scored setting
                         batches[si] = None
-                        if busy_since is not None and all(x is None for x in batches):
+                        if busy_since is not None and batches.empty():
                             self.stats.busy_s += time.time() - busy_since
                             busy_since = None
                         self._polish_done(b.polish, results, ready)
@@ -747,7 +812,7 @@ class SteadyStateSearch:
                     self.phase["collect"] += t_m - t_ph
                     t_done = time.time()
                     batches[si] = None
-                    if busy_since is not None and all(x is None for x in batches):
+                    if busy_since is not None and batches.empty():
                         self.stats.busy_s += t_done - busy_since
                         busy_since = None
                     for (isl, code, _), res in zip(b.items, results):
@@ -761,7 +826,7 @@ class SteadyStateSearch:
                     self.stats.evaluations += len(b.items)
                     self.stats.batches += 1
                     fs.evaluations += len(b.items)
-                    inflight = sum(len(x.items) for x in batches if x is not None)
+                    inflight = sum(len(x.items) for x in batches.live())
                     ev_n = [r.n_events for r in results if r is not None and r.engine == "hip-native"]
                     log.write(kind="steady_batch", rank=ctx.rank, slot=si, programs=len(b.items),
                               new_shapes=b.new_shapes, jit_s=round(b.jit_s, 4),
@@ -819,7 +884,7 @@ class SteadyStateSearch:
                         fs.log.write(kind="steady_rollover_begin", rank=ctx.rank, deferred=nc.deferred,
                                      inflight=self._left)
                     if rolling:
-                        busy = [b for b in batches if b is not None]
+                        busy = batches.live()
                         if busy and time.time() - rolling > self.rollover_grace_s and not any(b.aborted for b in busy):
                             dev.abort_service()
                             for b in busy:
@@ -839,7 +904,7 @@ class SteadyStateSearch:
                             progressed = True
                 # 6) status (time-weighted programs in flight, for the occupancy figure)
                 now = time.time()
-                self.stats.inflight_sum += sum(b.left for b in batches if b is not None) * (now - t_prev)
+                self.stats.inflight_sum += sum(b.left for b in batches.live()) * (now - t_prev)
                 self.stats.inflight_n += now - t_prev
                 t_prev = now
                 if now - t_status >= self.status_every_s:
@@ -847,7 +912,7 @@ class SteadyStateSearch:
                     self._status(now, t_start, busy_since, batches, ready, inflight_tasks, merged, global_best)
                 # stopping: host fallbacks not started yet are abandoned (a CPU-VM
                 # replay of a large program takes seconds of a core)
-                if stop and fallbacks and all(b is None for b in batches) and not staged:
+                if stop and fallbacks and batches.empty() and not staged:
                     kept = []
                     for items, fut, nfb in fallbacks:
                         if fut.cancel():
@@ -857,7 +922,7 @@ class SteadyStateSearch:
                     fallbacks = kept
                 # 7) done?  (every child merged, or stopping; then every agreed gather finished)
                 all_launched = all(requested[i] >= target_children[i] for i in range(k))
-                idle = (not inflight_tasks and all(b is None for b in batches) and not fallbacks
+                idle = (not inflight_tasks and batches.empty() and not fallbacks
                         and not staged and cpl_fut is None)
                 if idle and (stop or (all_launched and not ready)):
                     ready.clear()
@@ -905,7 +970,7 @@ class SteadyStateSearch:
         wall = max(1e-9, now - t_start)
         busy = st.busy_s + (now - busy_since if busy_since is not None else 0.0)
         fs = self.fs
-        inflight = sum(b.left for b in batches if b is not None)
+        inflight = sum(b.left for b in batches.live())
         self._left = inflight
         # occupancy: programs in flight / programs the device holds resident at the
         # current heap top (device_busy only says that *some* batch was in flight)

@@ -704,9 +704,12 @@ class NativeCompiler:
             declined = self._compile_baseline(items)
             if self.tier == "baseline":
                 with self._lock:
+                    rr = self.stats.setdefault("reject_reasons", {})
                     for k, _, why in declined:
                         self._bad[k] = why
                         self.stats["rejected"] += 1
+                        r = why[:48]
+                        rr[r] = rr.get(r, 0) + 1
                 return
             items = [(k, p) for k, p, _ in declined]
             if not items:

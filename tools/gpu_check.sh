@@ -18,7 +18,8 @@
 #   native=ARGS         tools/native_bench.py ARGS      -> native.jsonl
 #   c5[=ARGS]           config-5 bench (synthetic 65,536 pods / 256 nodes) -> c5.json
 #   pmc=COUNTERS[:ARGS] one rocprofv3 --pmc pass over bench.py ARGS (counters comma-separated)
-#   py=SCRIPT[:ARGS]    python SCRIPT ARGS              -> py_<script>.txt
+#   py=SCRIPT[:ARGS]    python SCRIPT ARGS              -> py_<script>.txt  (ARGS comma-separated)
+#   avail               rocprofv3 --list-avail          -> avail.txt
 set -o pipefail
 export PYTHONPATH=$PWD FKS_NO_AUTOBUILD=1
 ROOT=${GRAFT_REPO_ROOT:-$PWD}
@@ -89,12 +90,17 @@ for step in "$@"; do
       script=${val%%:*}
       args=""
       [ "$script" != "$val" ] && args=${val#*:}
+      args=${args//,/ }   # (commas separate the script's arguments)
       base=$(basename "$script" .py)
       out="$O/py_$base.txt"
       n=2
       while [ -e "$out" ]; do out="$O/py_${base}_$n.txt"; n=$((n + 1)); done   # repeated steps keep their output
       timeout -k 10 900 python -u "$script" $args > "$out" 2>&1 || die "py $script" "$out"
       tail -5 "$out" | cut -c1-400 ;;
+    avail)
+      # the PMC counters this rocprofv3 / gfx950 exposes (names for pmc= passes)
+      timeout -s KILL 60 rocprofv3 --list-avail > "$O/avail.txt" 2>&1 || die avail "$O/avail.txt"
+      grep -c . "$O/avail.txt" ;;
     *)
       die "unknown step $step" ;;
   esac
