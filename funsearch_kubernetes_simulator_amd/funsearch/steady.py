@@ -339,6 +339,8 @@ class SteadyStateSearch:
         self.status_every_s = float(status_every_s)
         self.stats = SteadyStats()
         self.llm_concurrency = 0
+        self._pending_merges: collections.deque = collections.deque()   # deferred similarity scans
+        self._sim_pool = None
         # main-thread wall time by phase (the dispatcher is one thread: its busy
         # fraction bounds the steady-state rate)
         self.phase = {"receive": 0.0, "submit": 0.0, "collect": 0.0, "merge": 0.0}
@@ -364,7 +366,15 @@ class SteadyStateSearch:
         # CPU VM, seconds of a core each) breeds least
         return [1.0 if not x else 0.25 if x < 0 else min(4.0, max(0.25, med / x)) for x in costs]
 
-    def _merge_one(self, s, code: str, score: float, cost: float = 0.0, island: Optional[int] = None) -> bool:
+    def _merge_one(self, s, code: str, score: float, cost: float = 0.0, island: Optional[int] = None,
+                   defer: bool = False) -> bool:
+        """Merge one scored child into island `s` (the reference's rules: dedup by
+        difflib ratio against equal-or-better members, keep the top
+        population_size).  defer: the similarity scan (milliseconds of C++ per
+        evolved child, the dispatcher's largest cost) runs on a worker thread
+        against a snapshot of the population and the child is appended when it
+        returns (`_finish_merges`), after a scan of the members added since;
+        returns True when the child was appended now."""
         if len(s.population) >= s.population_size and score <= min(sc for _, sc in s.population):
             # truncation would drop it anyway (a tie sorts after the members it
             # ties with): skip the similarity scan, same resulting population
@@ -381,8 +391,20 @@ class SteadyStateSearch:
             if len(known) >= 3 and cost > self.cost_bloat * known[len(known) // 2]:
                 self.stats.cost_rejected += 1
                 return False
-        if s._is_too_similar(code, score):
+        if defer:
+            others = [c.strip() for c, sc in s.population if sc >= score]
+            if others:
+                from .search import _similar_to_any
+                fut = self._simpool().submit(_similar_to_any, code.strip(), others, s.similarity_threshold,
+                                             s.similarity_threads if len(others) > 2 else 1)
+                self._pending_merges.append((fut, s, code, score, cost, island, getattr(s, "_pop_version", 0)))
+                return False
+        elif s._is_too_similar(code, score):
             return False
+        self._append(s, code, score, cost, cmap)
+        return True
+
+    def _append(self, s, code: str, score: float, cost: float, cmap) -> None:
         if cost != 0 and cmap is not None:
             cmap[code] = cost
             if len(cmap) > 4 * s.population_size:   # forget programs that left the population
@@ -391,11 +413,43 @@ class SteadyStateSearch:
                 for c in [c for c in cmap if c not in live]:
                     del cmap[c]
         s.population.append((code, score))
+        # (population version + recent appends: a deferred merge scans the members
+        # added after its snapshot)
+        s._pop_version = getattr(s, "_pop_version", 0) + 1
+        added = s.__dict__.setdefault("_added", collections.deque(maxlen=256))
+        added.append((s._pop_version, code, score))
         if score > s.best_score:
             s.best_score, s.best_policy = score, code
         s.population.sort(key=lambda x: x[1], reverse=True)
         del s.population[s.population_size:]
-        return True
+
+    def _simpool(self):
+        if self._sim_pool is None:
+            self._sim_pool = concurrent.futures.ThreadPoolExecutor(max_workers=2, thread_name_prefix="fks-similar")
+        return self._sim_pool
+
+    def _finish_merges(self, block: bool = False) -> bool:
+        """Deferred merges whose similarity scan finished (in submission order):
+        drop the child when the scan found a similar member; else scan the
+        members added since the snapshot (usually none), re-check the
+        truncation rule and append."""
+        done = False
+        pend = self._pending_merges
+        while pend and (block or pend[0][0].done()):
+            fut, s, code, score, cost, island, ver = pend.popleft()
+            done = True
+            if fut.result() >= 0:
+                continue
+            if len(s.population) >= s.population_size and score <= min(sc for _, sc in s.population):
+                continue
+            if getattr(s, "_pop_version", 0) != ver:
+                from .search import _similar_to_any
+                live = {c for c, _ in s.population}
+                newer = [c.strip() for v, c, sc in s.__dict__.get("_added", ()) if v > ver and sc >= score and c in live]
+                if newer and _similar_to_any(code.strip(), newer, s.similarity_threshold, 1) >= 0:
+                    continue
+            self._append(s, code, score, cost, self._cost.setdefault(island, {}) if island is not None else None)
+        return done
 
     def _absorb(self, results) -> bool:
         """Merge finished migrations into the islands (main thread only)."""
@@ -442,6 +496,8 @@ class SteadyStateSearch:
             prog, _ = try_compile(code)
             if prog is None or not prog.device_ok:
                 continue
+            from ..ops.jit import launch_key
+            launch_key(prog)   # (the variants inherit the shape key: one compile, then data)
             tune = tunable_literals(prog)
             if not tune:
                 continue
@@ -492,7 +548,7 @@ class SteadyStateSearch:
                 if r.device_cycles > 0:
                     self.stats.cost_sum += r.device_cycles
                     self.stats.cost_n += 1
-                self._merge_one(islands[isl], code, r.score, r.device_cycles, isl)
+                self._merge_one(islands[isl], code, r.score, r.device_cycles, isl, defer=True)
                 merged[isl] += 1
                 self.stats.native += int(r.engine == "hip-native")
         if b.polish is None:
@@ -669,10 +725,11 @@ class SteadyStateSearch:
                 # of an island champion goes first
                 if self.polish_every and not stop and len(staged) < self.ahead:
                     job = self._polish_job(merged, start_gen, polish_next)
-                    if job is None and self.polish_idle and not staged and len(ready) < self.batch \
-                            and batches.has_free() and (
-                                not self.service_inflight
-                                or self._left < self.service_inflight // 2):
+                    if job is None and self.polish_idle and len(ready) < self.batch and batches.has_free() and (
+                            # stream slots: one would idle; the program service: the grid
+                            # has room the children (not a full batch yet) leave
+                            not staged if not self.service_inflight
+                            else self._left + sum(len(t) for t, _, _ in staged) < (3 * self.service_inflight) // 4):
                         # a slot would idle until the producers refill a batch
                         job = self._polish_job(merged, start_gen, polish_next, idle=True)
                         if job is not None:
@@ -836,6 +893,12 @@ class SteadyStateSearch:
                               events_mean=round(sum(ev_n) / len(ev_n), 1) if ev_n else 0,
                               events_max=max(ev_n) if ev_n else 0)
                     progressed = True
+                # deferred merges whose similarity scans finished
+                if self._pending_merges:
+                    t_m = time.perf_counter()
+                    if self._finish_merges():
+                        progressed = True
+                    self.phase["merge"] += time.perf_counter() - t_m
                 gens = self._gen_of(merged)
                 g_min = start_gen + min(gens)
                 fs.generation = g_min
@@ -922,7 +985,7 @@ class SteadyStateSearch:
                     fallbacks = kept
                 # 7) done?  (every child merged, or stopping; then every agreed gather finished)
                 all_launched = all(requested[i] >= target_children[i] for i in range(k))
-                idle = (not inflight_tasks and batches.empty() and not fallbacks
+                idle = (not inflight_tasks and batches.empty() and not fallbacks and not self._pending_merges
                         and not staged and cpl_fut is None)
                 if idle and (stop or (all_launched and not ready)):
                     ready.clear()
@@ -949,6 +1012,11 @@ class SteadyStateSearch:
                     json.dump(rep, fh, indent=1)
             pool.shutdown(wait=False, cancel_futures=True)
             stager.shutdown(wait=True, cancel_futures=True)
+            if self._pending_merges:
+                self._finish_merges(block=True)
+            if self._sim_pool is not None:
+                self._sim_pool.shutdown(wait=True)
+                self._sim_pool = None
             if cpl_exec is not None:
                 cpl_exec.shutdown(wait=True, cancel_futures=True)
             for _, fut, _pj in staged:   # compiled but never launched: give the modules back

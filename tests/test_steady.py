@@ -1,6 +1,7 @@
 """Steady-state island mode (funsearch/steady.py) on the CPU: children from
 producer processes, batches on evaluator slots, one-by-one merges, async
 migration with a consistent distributed stop."""
+import collections
 import json
 import os
 import subprocess
@@ -271,3 +272,37 @@ def test_steady_with_llm_concurrency(tmp_path):
     assert fs.steady.stats.produced == 2 * 2 * 4
     fin = [r for r in recs if r["kind"] == "steady_final"][-1]
     assert fin["children_per_s"] > 0
+
+
+def test_deferred_merge_rechecks_members_added_since():
+    """The program service's merges: the similarity scan runs on a worker
+    thread against a snapshot; at completion the child is also scanned against
+    members appended after the snapshot, and truncation is re-checked."""
+    from funsearch_kubernetes_simulator_amd.funsearch.steady import SteadyStateSearch
+
+    class Island:
+        population_size, similarity_threshold, similarity_threads = 3, 0.85, 2
+        best_score, best_policy = float("-inf"), None
+
+        def __init__(self):
+            self.population = []
+
+        def _is_too_similar(self, code, score):
+            raise AssertionError("deferred path must not scan synchronously")
+
+    st = object.__new__(SteadyStateSearch)
+    st._pending_merges, st._sim_pool, st._cost = collections.deque(), None, {}
+    st.cost_bloat, st.service_cfg = 3.0, {}
+    st.stats = type("S", (), {"cost_rejected": 0})()
+    s = Island()
+    a = "def f(pod, node):\n    return 1 + node.cpu_milli_left * 0.5\n"
+    b = "def f(pod, node):\n    return 1 + node.cpu_milli_left * 0.6\n"          # similar to a
+    c = "def g(pod, node):\n    x = [q for q in node.gpus]\n    return len(x) * 77 - pod.num_gpu\n"
+    assert st._merge_one(s, a, 0.5, defer=True)        # empty population: appended at once
+    assert not st._merge_one(s, c, 0.4, defer=True)    # scan against a deferred
+    st._append(s, b, 0.45, 0.0, None)                   # a member added after c's snapshot
+    assert not st._merge_one(s, b + "#", 0.44, defer=True)
+    st._finish_merges(block=True)
+    codes = [x for x, _ in s.population]
+    assert a in codes and c in codes and b in codes and (b + "#") not in codes
+    st._sim_pool.shutdown()
