@@ -314,6 +314,15 @@ class SteadyStateSearch:
         cc = dict((svc or {}).get("cost") or {}) if isinstance(svc, dict) else {}
         self.cost_parents = bool(cc.get("parents", True))
         self.cost_bloat = float(cc.get("bloat", 3.0))
+        #: and an absolute anchor: the median cost of the run's first
+        #: `anchor_children` replays; a child costing more than `anchor_cap` x it
+        #: enters only as a new island best (the population median alone drifts
+        #: with the population: every step within `bloat` x, the run 2-3x
+        #: costlier after a few minutes)
+        self.cost_anchor_cap = float(cc.get("anchor_cap", 2.0))
+        self.cost_anchor_children = int(cc.get("anchor_children", 4096))
+        self._anchor_samples: list = []
+        self.cost_anchor = 0.0
         #: grid rollover: retired JIT modules stay loaded while the grid runs
         #: (an unload waits for the device); past this many the loop drains the
         #: grid (launches paused, stragglers aborted after `rollover_grace_s`),
@@ -389,6 +398,9 @@ class SteadyStateSearch:
                 return False
             known = sorted(cmap[c] for c, _ in s.population if cmap.get(c, 0) > 0)
             if len(known) >= 3 and cost > self.cost_bloat * known[len(known) // 2]:
+                self.stats.cost_rejected += 1
+                return False
+            if self.cost_anchor and self.cost_anchor_cap > 0 and cost > self.cost_anchor_cap * self.cost_anchor:
                 self.stats.cost_rejected += 1
                 return False
         if defer:
@@ -548,6 +560,14 @@ class SteadyStateSearch:
                 if r.device_cycles > 0:
                     self.stats.cost_sum += r.device_cycles
                     self.stats.cost_n += 1
+                    if not self.cost_anchor and self.cost_anchor_children > 0:
+                        self._anchor_samples.append(r.device_cycles)
+                        if len(self._anchor_samples) >= self.cost_anchor_children:
+                            xs = sorted(self._anchor_samples)
+                            self.cost_anchor = xs[len(xs) // 2]
+                            self._anchor_samples = []
+                            self.fs.log.write(kind="steady_cost_anchor", rank=self.fs.ctx.rank,
+                                              mcycles=round(self.cost_anchor / 1e6, 3))
                 self._merge_one(islands[isl], code, r.score, r.device_cycles, isl, defer=True)
                 merged[isl] += 1
                 self.stats.native += int(r.engine == "hip-native")
@@ -1040,6 +1060,9 @@ class SteadyStateSearch:
         fs = self.fs
         inflight = sum(b.left for b in batches.live())
         self._left = inflight
+        # programs of batches launched more than 5 s ago that are still replaying:
+        # the grid's workgroups held by long replays (a 15M-event policy takes ~30 s)
+        stragglers = sum(b.left for b in batches.live() if now - b.t_launch > 5.0)
         # occupancy: programs in flight / programs the device holds resident at the
         # current heap top (device_busy only says that *some* batch was in flight)
         capacity = 0
@@ -1069,6 +1092,7 @@ class SteadyStateSearch:
                    # per replay) and what the selection did with it
                    mcycles_per_child=round(st.cost_sum / max(1, st.cost_n) / 1e6, 3), cost_rejected=st.cost_rejected,
                    rollovers=st.rollovers, rollover_s=round(st.rollover_s, 2), mem_used_mb=info.get("mem_used_mb"),
+                   stragglers=stragglers, cost_anchor_mcycles=round(self.cost_anchor / 1e6, 3),
                    producer_tasks=len(tasks), produced=st.produced,
                    children_per_s=round(st.produced / wall, 2),
                    llm_inflight=min(len(tasks), self.producers) * self.task_size if self.llm_concurrency else None,
