@@ -84,12 +84,13 @@ def _produce(task):
     island, elites, n = task[:3]
     weights = task[3] if len(task) > 3 else None
     t0 = time.process_time()
+    w0 = time.perf_counter()
     pool = _W.get("fanout")
     if pool is not None and n > 1:
         out = list(pool.map(lambda _: _produce_one(island, elites, weights), range(n)))
     else:
         out = [_produce_one(island, elites, weights) for _ in range(n)]
-    return out, time.process_time() - t0
+    return out, time.process_time() - t0, time.perf_counter() - w0
 
 
 def _produce_one(island, elites, weights):
@@ -237,6 +238,7 @@ class SteadyStats:
     shed: int = 0                    # children only CPython could score, not evaluated (host_object off)
     abandoned: int = 0               # host fallbacks still queued when the run stopped
     producer_cpu_s: float = 0.0
+    producer_wall_s: float = 0.0     # wall seconds the producers spent on tasks (CPU / wall: their core share)
     polish_batches: int = 0          # constant-polish batches (variants of an island champion)
     polish_evals: int = 0            # their device evaluations (not children)
     polish_improved: int = 0         # polished champions re-entered as children
@@ -319,7 +321,7 @@ class SteadyStateSearch:
         #: enters only as a new island best (the population median alone drifts
         #: with the population: every step within `bloat` x, the run 2-3x
         #: costlier after a few minutes)
-        self.cost_anchor_cap = float(cc.get("anchor_cap", 2.0))
+        self.cost_anchor_cap = float(cc.get("anchor_cap", 3.0))
         self.cost_anchor_children = int(cc.get("anchor_children", 4096))
         self._anchor_samples: list = []
         self.cost_anchor = 0.0
@@ -723,9 +725,10 @@ class SteadyStateSearch:
                 for f in inflight_tasks:
                     if f.done():
                         t_ph = time.perf_counter()
-                        items, cpu_s = f.result()
+                        items, cpu_s, task_wall_s = f.result()
                         self.phase["receive"] += time.perf_counter() - t_ph
                         self.stats.producer_cpu_s += cpu_s
+                        self.stats.producer_wall_s += task_wall_s
                         for isl, code, prog in items:
                             self.stats.produced += 1
                             if prog is None:     # no program: counts toward the island's generation
@@ -1097,6 +1100,10 @@ class SteadyStateSearch:
                    children_per_s=round(st.produced / wall, 2),
                    llm_inflight=min(len(tasks), self.producers) * self.task_size if self.llm_concurrency else None,
                    producer_ms_per_child=round(1e3 * st.producer_cpu_s / max(1, st.produced), 3),
+                   # producers' CPU / wall while on a task (< 1: preempted, the host's
+                   # cores are short) and the fraction of the run they were on tasks
+                   producer_cpu_share=round(st.producer_cpu_s / max(1e-9, st.producer_wall_s), 3),
+                   producer_busy=round(st.producer_wall_s / max(1e-9, wall * self.producers), 3),
                    main_cpu_frac=round((time.process_time() - self._cpu0) / wall, 3), rejected=st.rejected, jit_s=round(st.jit_s, 3),
                    generation=fs.generation, best=round(fs.best[1], 6), best_global=round(best_global, 6),
                    islands=[round(s.best_score, 6) for s in fs.islands], migrations=st.migrations,

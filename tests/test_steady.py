@@ -230,7 +230,7 @@ def test_llm_fanout_overlaps_request_latency():
         steady._producer_init(cfg, 3, 0, fanout=8)
         elites = [(seed_policies()["first_fit"], 0.43), (seed_policies()["best_fit"], 0.45)]
         t0 = time.time()
-        out, _ = steady._produce((1, elites, 8, [1.0, 3.0]))
+        out, _, _ = steady._produce((1, elites, 8, [1.0, 3.0]))
         dt = time.time() - t0
         assert len(out) == 8 and all(isl == 1 and prog is not None for isl, code, prog in out)
         assert dt < 1.6, dt        # sequential: 8 x 0.4 s

@@ -58,8 +58,9 @@ def main() -> None:
     if st:
         print("# 100 s windows: children / s, all program evals / s (children + polish variants)")
         w0, e0, a0 = 0.0, 0, 0
-        for t, e, a in st:
-            if t - w0 >= 99.5:
+        for k, (t, e, a) in enumerate(st):
+            last_rec = k == len(st) - 1
+            if t - w0 >= 99.5 or (last_rec and t - w0 >= 30):
                 print(f"  [{w0:6.0f}, {t:6.0f}) s: {(e - e0) / (t - w0):8.1f} children/s {(a - a0) / (t - w0):8.1f} all/s")
                 w0, e0, a0 = t, e, a
     # steady_batch records by quintile of the run: device seconds per batch
