@@ -326,6 +326,13 @@ class DeviceEngine {
     if (o.contains("gpu_alloc")) W_.first_fit_alloc = o["gpu_alloc"].cast<std::string>() == "first_fit";
     if (o.contains("snapshot_interval")) W_.snapshot_interval = o["snapshot_interval"].cast<double>();
     if (o.contains("budget")) budget_ = o["budget"].cast<int64_t>();
+    // two-wave program replays (batch launches and the service): a replay past
+    // this many events ends with EXC_EVENTS (0: no limit; checked every 1,024)
+    if (o.contains("max_events")) {
+      const int64_t me = o["max_events"].cast<int64_t>();
+      if (me < 0 || me > 0xFFFFFFFFll) throw std::invalid_argument("max_events must be in [0, 2^32)");
+      max_events_ = (uint32_t)me;
+    }
     if (o.contains("heap_top")) heap_top_opt_ = o["heap_top"].cast<int>();   // -1: auto
     if (o.contains("partial_delmap")) partial_delmap_off_ = !o["partial_delmap"].cast<bool>();   // A/B
     if (o.contains("trace_hash")) W_.trace_hash = o["trace_hash"].cast<bool>() ? 1 : 0;
@@ -568,7 +575,7 @@ class DeviceEngine {
     const fksk::BuiltinArgs a{Wl, nullptr, nullptr, nullptr, nullptr, v.res.as<DevResult>(), v.gheap.as<uint64_t>(),
                               nullptr, v.tab.dev<double>()};
     const RowNativeArgs nat{v.fn.dev<const uint64_t>(), v.kc.dev<const int64_t>(), v.koff.dev<const int32_t>(),
-                            v.ctl.dev<const uint32_t>() + 2};
+                            v.ctl.dev<const uint32_t>() + 2, max_events_};
     // `idle_polls` polls with nothing published: the grid drains (a lost host)
     const ServiceCtl c{v.claimed.as<uint32_t>(), v.ctl.dev<const uint32_t>(), v.ctl.dev<const uint32_t>() + 1,
                        v.done.dev<uint32_t>(), v.qslot.dev<const uint32_t>(), v.started.dev<uint32_t>(), v.nq,
@@ -876,6 +883,7 @@ class DeviceEngine {
     d["native_duo_per_cu_last"] = last_duo_per_cu_;   // resident programs per CU at that heap top
     d["native_duo_reg_cap"] = fksk::native_duo_blocks_per_cu(0);   // register-limited programs per CU
     d["native_inflight"] = native_inflight_;
+    d["max_events"] = (int64_t)max_events_;
     d["wave_duo"] = wave_duo_;
     d["wave_duo_heap_top"] = npass_ >= 4 ? heap_top_for(0, false, true) : 0;
     size_t mfree = 0, mtotal = 0;   // (a host-side query: no device synchronisation)
@@ -1269,7 +1277,7 @@ class DeviceEngine {
                                 s.h_tab.dev<double>()};
       s.fused_table = true;
       const RowNativeArgs nat{s.h_in.dev<const uint64_t>(), kc_dev,
-                              reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + fn_bytes)};
+                              reinterpret_cast<const int32_t*>(s.h_in.dev<char>() + fn_bytes), nullptr, max_events_};
       if (std::getenv("FKS_DEBUG_LAUNCH"))
         std::fprintf(stderr, "[fks] native duo: P=%d T=%d lds=%zu per_cu=%d stream=%p\n", P, T, lds,
                      last_duo_per_cu_, (void*)s.stream);
@@ -1375,6 +1383,7 @@ class DeviceEngine {
   std::string arch_;
   std::string heap_mode_ = "auto";
   int64_t budget_ = 0;
+  uint32_t max_events_ = 0;
   int heap_top_opt_ = -1;
   bool partial_delmap_off_ = false;
   bool wave_duo_ = false;   // NPASS-4 builtin launches on the two-wave kernel (`wave_duo`)

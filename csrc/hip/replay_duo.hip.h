@@ -387,11 +387,20 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
   if constexpr (PROF) plast = __builtin_amdgcn_s_memtime();
   for (;;) {
     asm volatile("" : "+v"(jv));
-    if ((k & 1023u) == 1023u && nat.abort != nullptr &&
-        __hip_atomic_load(nat.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
-      exc = EXC_TIMEOUT;   // the host gave up on the replays in flight (a stopping run)
-      if (jv == 0) duo_st(&box->sabort, 1u);
-      break;
+    if ((k & 1023u) == 1023u) {
+      if (nat.abort != nullptr && __hip_atomic_load(nat.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+        exc = EXC_TIMEOUT;   // the host gave up on the replays in flight (a stopping run)
+        if (jv == 0) duo_st(&box->sabort, 1u);
+        break;
+      }
+      if (nat.max_events != 0u && k >= nat.max_events) {
+        // past the caller's event budget (a resource limit: a policy whose failed
+        // placements re-queue for millions of events holds a workgroup for tens
+        // of seconds); the row says so and carries no score
+        exc = EXC_EVENTS;
+        if (jv == 0) duo_st(&box->sabort, 1u);
+        break;
+      }
     }
     // next event, or the end of the replay
     uint32_t spins = 0;

@@ -415,7 +415,7 @@ __device__ __forceinline__ const FKS_CONST fksk::ServiceArgs* service_args(uint6
 __device__ __forceinline__ void service_replay_body(uint64_t kp, int slot) {
   const FKS_CONST fksk::ServiceArgs* A = service_args(kp);
   const fksd::DevWorkload& W = *(const fksd::DevWorkload*)&A->a.W;
-  const RowNativeArgs nat{A->nat.fn, A->nat.kc, A->nat.koff, A->nat.abort};
+  const RowNativeArgs nat{A->nat.fn, A->nat.kc, A->nat.koff, A->nat.abort, A->nat.max_events};
   replay_duo<false>(W, (const fksd::DevWorkload*)uniu64(kp), A->a.gheap, A->a.out, nat, A->a.table, nullptr, slot,
                     (int)blockIdx.x);
 }

@@ -46,6 +46,7 @@ struct RowNativeArgs {
   const int64_t* kc;      // concatenated constant blocks
   const int32_t* koff;    // [P] offset of policy p's block in kc
   const uint32_t* abort = nullptr;   // host flag (two-wave kernel): nonzero ends replays early, EXC_TIMEOUT
+  uint32_t max_events = 0;           // two-wave kernel: a replay past this many events ends, EXC_EVENTS (0: none)
 };
 // Control block of the resident program service (replay_kernels.hip k_native_service)
 struct ServiceCtl {

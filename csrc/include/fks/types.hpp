@@ -28,6 +28,7 @@ enum ExcCode : int32_t {
   EXC_BUDGET = 101,        // instruction budget exhausted (runaway program)
   EXC_INVARIANT = 102,     // resource accounting invariant violated (debug check)
   EXC_TIMEOUT = 103,       // engine-internal timeout (two-wave kernel spin cap): re-run on the next engine
+  EXC_EVENTS = 104,        // the replay passed the caller's event budget (a resource limit): not scored
 };
 
 enum RepushMode : int32_t { REPUSH_FIRST = 0, REPUSH_EARLIEST = 1 };

@@ -158,6 +158,8 @@ def _native_deferred(row, bump) -> bool:
     exc = int(row[COLS["exc"]])
     if exc == Exc.TIMEOUT:
         bump("native_timeout")
+    elif exc == Exc.EVENTS:
+        bump("native_event_cap")   # final: past the caller's replay event budget, not scored
     elif exc == Exc.INVARIANT:
         bump("native_invariant")
         import warnings

@@ -53,6 +53,10 @@ from ..parallel import dist
 from ..utils.trace import roctx_range
 from .search import FEEDBACK
 
+from ..policy.bytecode import Exc as _Exc
+
+_EXC_EVENTS = int(_Exc.EVENTS)
+
 #: device cost of a child scored on the host engines (the JIT declined it):
 #: the selection treats it as the costliest kind of program
 HOST_COST = -1.0
@@ -75,19 +79,45 @@ def _producer_init(llm_cfg: dict, timeout_s: int, seed: int, fanout: int = 0) ->
         # a remote LLM: a task's requests wait concurrently (threads; the wait
         # releases the GIL), so `producers x task_size` requests are in flight
         _W["fanout"] = concurrent.futures.ThreadPoolExecutor(max_workers=fanout, thread_name_prefix="fks-llm")
+        _W["fanout_n"] = fanout
 
 
 def _produce(task):
-    """(island, elites [(code, score)], n[, weights]) -> [(island, code, CompiledPolicy | None)].
+    """(island, elites [(code, score)], n[, weights]) -> ([(island, code, CompiledPolicy | None)], cpu s, wall s).
     weights: per-elite parent weights (the steady search's device-cost
-    weighting, `_parent_weights`), or None for uniform sampling."""
+    weighting, `_parent_weights`), or None for uniform sampling.
+
+    With a request fan-out (a remote LLM, `_producer_init` fanout > 1) a task
+    does not wait for its own requests: it starts its n requests on the
+    process's threads once at most `fanout - n` are still in flight, and
+    returns the children whose requests have completed by then -- so every
+    producer keeps ~fanout requests waiting at all times instead of idling on
+    the slowest of each task's n (16 requests of 2-8 s: a task would last the
+    maximum, ~7.6 s, not the mean).  n = 0 flushes: waits for every request in
+    flight and returns their children (the end of a run)."""
     island, elites, n = task[:3]
     weights = task[3] if len(task) > 3 else None
     t0 = time.process_time()
     w0 = time.perf_counter()
     pool = _W.get("fanout")
-    if pool is not None and n > 1:
-        out = list(pool.map(lambda _: _produce_one(island, elites, weights), range(n)))
+    if pool is not None:
+        pend = _W.setdefault("pending", [])
+        cap = _W["fanout_n"]
+        out = []
+
+        def harvest():
+            done = [f for f in pend if f.done()]
+            if done:
+                pend[:] = [f for f in pend if not f.done()]
+                out.extend(f.result() for f in done)
+
+        if n <= 0:
+            concurrent.futures.wait(pend)
+        while len(pend) + n > cap:
+            concurrent.futures.wait(pend, return_when=concurrent.futures.FIRST_COMPLETED)
+            harvest()
+        harvest()
+        pend.extend(pool.submit(_produce_one, island, elites, weights) for _ in range(max(0, n)))
     else:
         out = [_produce_one(island, elites, weights) for _ in range(n)]
     return out, time.process_time() - t0, time.perf_counter() - w0
@@ -247,6 +277,7 @@ class SteadyStats:
     inflight_sum: float = 0.0        # programs in flight x seconds
     inflight_n: float = 0.0          # seconds observed
     cost_rejected: int = 0           # children not merged by the bloat control (device cost)
+    event_capped: int = 0            # children whose replay passed the event budget (not scored)
     cost_sum: float = 0.0            # device cycles of the children replayed on the service ...
     cost_n: int = 0                  # ... and their number
     rollovers: int = 0               # grid rollovers (module unloads while the service runs)
@@ -331,6 +362,13 @@ class SteadyStateSearch:
         #: unloads them and starts it again
         self.rollover_deferred = int((svc or {}).get("rollover_modules", 2048)) if isinstance(svc, dict) else 2048
         self.rollover_grace_s = float((svc or {}).get("rollover_grace_s", 3.0)) if isinstance(svc, dict) else 3.0
+        #: replay event budget on the device (a resource limit, like the
+        #: reference's per-call timeout but per replay): a child whose replay passes
+        #: it is not scored.  A normal replay of the OpenB trace is 20-45k events;
+        #: some evolved policies re-queue failed placements for 15M events -- tens
+        #: of seconds of a workgroup each, and they exploit the evaluator's
+        #: event-count snapshot schedule (docs/ARCHITECTURE.md).  0: no budget
+        self.max_events = int((svc or {}).get("max_events", 400_000)) if isinstance(svc, dict) else 0
         #: programs waiting for (or in) a host-engine fallback at most; more are shed
         self.fallback_cap = int((svc or {}).get("fallback_cap", 64)) if isinstance(svc, dict) else 1 << 30
         self._cost: dict = {}            # island -> {code: device cycles}
@@ -338,6 +376,8 @@ class SteadyStateSearch:
             # the two-wave kernel sizes its LDS heap top so that every slot's batch
             # stays resident at once (csrc/hip/engine_host.hip.h duo_top)
             dev.set_options(native_inflight=min(self.batch * self.slots, 1 << 14))
+            if self.service_cfg is not None:
+                dev.set_options(max_events=self.max_events)
             if not tierup:
                 # shapes the baseline generator declines (~0.1%) go to the host
                 # engines asynchronously instead of a ~0.2 s LLVM compile on the
@@ -351,6 +391,8 @@ class SteadyStateSearch:
         self.stats = SteadyStats()
         self.llm_concurrency = 0
         self._pending_merges: collections.deque = collections.deque()   # deferred similarity scans
+        self._asked = 0                  # children requested from the producers ...
+        self._got = 0                    # ... and returned (fan-out tasks return what is ready)
         self._sim_pool = None
         # main-thread wall time by phase (the dispatcher is one thread: its busy
         # fraction bounds the steady-state rate)
@@ -559,6 +601,8 @@ class SteadyStateSearch:
             b.left -= 1
             if b.polish is None:
                 isl, code, _ = b.items[i]
+                if r.exc == _EXC_EVENTS:
+                    self.stats.event_capped += 1
                 if r.device_cycles > 0:
                     self.stats.cost_sum += r.device_cycles
                     self.stats.cost_n += 1
@@ -718,6 +762,7 @@ class SteadyStateSearch:
                     n = min(self.task_size, target_children[i] - requested[i])
                     requested[i] += n
                     inflight_tasks.append(pool.submit(_produce, (i, elites, n, self._parent_weights(i, elites))))
+                    self._asked += n
                     queued += n
                     progressed = True
                 # 2) collect produced children
@@ -729,6 +774,7 @@ class SteadyStateSearch:
                         self.phase["receive"] += time.perf_counter() - t_ph
                         self.stats.producer_cpu_s += cpu_s
                         self.stats.producer_wall_s += task_wall_s
+                        self._got += len(items)
                         for isl, code, prog in items:
                             self.stats.produced += 1
                             if prog is None:     # no program: counts toward the island's generation
@@ -1008,6 +1054,11 @@ class SteadyStateSearch:
                     fallbacks = kept
                 # 7) done?  (every child merged, or stopping; then every agreed gather finished)
                 all_launched = all(requested[i] >= target_children[i] for i in range(k))
+                if fanout and all_launched and not stop and not inflight_tasks and self._got < self._asked:
+                    # children still waiting on their requests inside the producers
+                    # (fan-out tasks return what is ready): flush every process
+                    inflight_tasks.extend(pool.submit(_produce, (0, [], 0, None)) for _ in range(self.producers))
+                    progressed = True
                 idle = (not inflight_tasks and batches.empty() and not fallbacks and not self._pending_merges
                         and not staged and cpl_fut is None)
                 if idle and (stop or (all_launched and not ready)):
@@ -1096,6 +1147,7 @@ class SteadyStateSearch:
                    mcycles_per_child=round(st.cost_sum / max(1, st.cost_n) / 1e6, 3), cost_rejected=st.cost_rejected,
                    rollovers=st.rollovers, rollover_s=round(st.rollover_s, 2), mem_used_mb=info.get("mem_used_mb"),
                    stragglers=stragglers, cost_anchor_mcycles=round(self.cost_anchor / 1e6, 3),
+                   event_capped=st.event_capped, max_events=self.max_events,
                    producer_tasks=len(tasks), produced=st.produced,
                    children_per_s=round(st.produced / wall, 2),
                    llm_inflight=min(len(tasks), self.producers) * self.task_size if self.llm_concurrency else None,
@@ -1116,7 +1168,7 @@ class SteadyStateSearch:
                    collective_wait_frac=round(self.channel.wait_s / wall, 5),
                    engines={k: v for k, v in fs.evaluator.stats.items() if k in
                             ("device_native", "device", "cpu_vm", "object", "shed", "compile_errors", "jit_shapes",
-                             "native_timeout", "native_invariant")})
+                             "native_timeout", "native_invariant", "native_event_cap")})
         fs.log.write(**rec)
         st.history.append(rec)
         if fs.verbose and fs.ctx.is_main and not final:

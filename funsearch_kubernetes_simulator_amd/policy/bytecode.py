@@ -105,6 +105,7 @@ class Exc(enum.IntEnum):
     BUDGET = 101
     INVARIANT = 102
     TIMEOUT = 103
+    EVENTS = 104        # the replay passed the caller's event budget (a resource limit): not scored
 
 
 _INSN = struct.Struct("<BBBBi")

@@ -147,3 +147,30 @@ def test_service_idle_drain_and_revive(dev):
     for i in range(len(progs)):
         assert np.array_equal(got[i], want[i]), i
     assert sv["launches"] >= 2 and sv["idle_polls"] == 256, sv
+
+
+def test_service_event_budget(dev):
+    """max_events: a replay past the budget ends with EXC_EVENTS (final, never
+    deferred to the host); with the budget off the same programs replay in full,
+    equal to the batch launch."""
+    from funsearch_kubernetes_simulator_amd.engine import NATIVE_DEFER
+    progs = programs()[:16]
+    want = dev.evaluate_native(progs)
+    native = [i for i in range(len(progs)) if int(want[i, 10]) not in NATIVE_DEFER]
+    assert native
+    dev.set_options(max_events=2048)
+    try:
+        dev.start_service(slots=256, share=0.5)
+        try:
+            capped = dev.evaluate_native(progs)
+        finally:
+            dev.stop_service()
+    finally:
+        dev.set_options(max_events=0)
+    assert int(Exc.EVENTS) not in NATIVE_DEFER
+    for i in native:
+        if want[i, 8] > 2048 + 1024:        # n_events: over the budget -> capped
+            assert int(capped[i, 10]) == Exc.EVENTS, (i, capped[i])
+        else:
+            assert np.array_equal(capped[i], want[i]), i
+    assert dev.info()["max_events"] == 0

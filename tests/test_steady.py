@@ -230,11 +230,19 @@ def test_llm_fanout_overlaps_request_latency():
         steady._producer_init(cfg, 3, 0, fanout=8)
         elites = [(seed_policies()["first_fit"], 0.43), (seed_policies()["best_fit"], 0.45)]
         t0 = time.time()
-        out, _, _ = steady._produce((1, elites, 8, [1.0, 3.0]))
+        out, _, _ = steady._produce((1, elites, 8, [1.0, 3.0]))   # starts 8 requests, returns what is ready
+        assert out == [] and time.time() - t0 < 0.3
+        out2, _, _ = steady._produce((0, [], 0, None))             # flush: waits for the 8 in flight
         dt = time.time() - t0
-        assert len(out) == 8 and all(isl == 1 and prog is not None for isl, code, prog in out)
+        assert len(out2) == 8 and all(isl == 1 and prog is not None for isl, code, prog in out2)
         assert dt < 1.6, dt        # sequential: 8 x 0.4 s
         assert steady._W["gen"].llm_client.calls == 8
+        # a task never leaves more than `fanout` requests in flight: the 9th..16th
+        # wait for earlier ones and return their children
+        steady._produce((1, elites, 8, None))
+        out3, _, _ = steady._produce((1, elites, 8, None))
+        assert len(out3) == 8 and len(steady._W["pending"]) == 8
+        steady._produce((0, [], 0, None))
     finally:
         pool = steady._W.get("fanout")
         if pool is not None:
