@@ -313,7 +313,11 @@ __device__ void replay_duo(const DevWorkload& W, const DevWorkload* Wdev, uint64
   }
 
   // ================= S: nodes, program, evaluator
-  const uint64_t fne = *global_ptr(&nat.fn[p]);
+  // wave-uniform by construction (one program per workgroup): read it into
+  // SGPRs so the call is a single direct s_swappc -- a VGPR-held pointer
+  // (the service path loads `nat` through the ring) makes LLVM wrap the
+  // call in a readfirstlane waterfall loop
+  const uint64_t fne = uniu64(*global_ptr(&nat.fn[p]));
   const ProgFn prog = prog_of(fne);
   const bool feas_pro = prog_feas(fne);   // call only for feasible nodes
   // this lane's node state and accumulators in LDS (kDuoSBytes above)

@@ -109,6 +109,17 @@ inline void expand(const Func& f, std::vector<MI>& out, int& next_label) {
           st.imm = off; off += 4;
           out.push_back(st);
         }
+        // v_writelane writes its lane whatever EXEC holds, and the caller may
+        // keep values in the inactive lanes of any VGPR across the call (the
+        // ABI: a callee preserves them) -- LLVM does, e.g. an `if` result
+        // zeroed before the branch in a caller-saved register.  So the spill
+        // VGPR's own contents are saved first and reloaded after the readlanes.
+        const int orig = off;
+        {
+          MI st = mk(SCRATCH_STORE_DWORD, NONE, NONE, s(32), c.spill_vgpr);
+          st.imm = orig; off += 4;
+          out.push_back(st);
+        }
         int lane = 0;
         for (int sg : c.sgprs) {
           MI wl = mk(V_WRITELANE_B32, c.spill_vgpr, s(sg), ic(lane++));
@@ -167,6 +178,7 @@ inline void expand(const Func& f, std::vector<MI>& out, int& next_label) {
           ldv.imm = off; off += 4;
           out.push_back(ldv);
         }
+        off += 4;   // the spill VGPR's own contents (orig)
         {
           MI ldv = mk(SCRATCH_LOAD_DWORD, c.spill_vgpr, NONE, s(32));
           ldv.imm = off;
@@ -175,6 +187,12 @@ inline void expand(const Func& f, std::vector<MI>& out, int& next_label) {
         out.push_back(mkimm(S_WAITCNT, 0x0F70));   // vmcnt(0)
         lane = 0;
         for (int sg : c.sgprs) out.push_back(mk(V_READLANE_B32, s(sg), c.spill_vgpr, ic(lane++)));
+        {
+          MI ldv = mk(SCRATCH_LOAD_DWORD, c.spill_vgpr, NONE, s(32));
+          ldv.imm = orig;
+          out.push_back(ldv);
+        }
+        out.push_back(mkimm(S_WAITCNT, 0x0F70));   // vmcnt(0)
         out.push_back(mk(S_MOV_B64, EXEC, s(r.sc)));
         out.push_back(mkimm(LABEL, skip));
         break;

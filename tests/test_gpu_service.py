@@ -174,3 +174,31 @@ def test_service_event_budget(dev):
         else:
             assert np.array_equal(capped[i], want[i]), i
     assert dev.info()["max_events"] == 0
+
+
+def test_service_rtcall_population_matches_vm(dev, default_workload):
+    """Regression (round 6): an evolved population whose baseline-JIT code
+    calls the runtime library with its feasibility prologue compiled out.  The
+    RT-call sequence spilled SGPRs with v_writelane into a caller-saved VGPR
+    without restoring that VGPR's inactive lanes; the service's caller keeps
+    the zeroed score of the infeasible nodes there across the call, so 43 of
+    these 80 programs placed pods on infeasible nodes (EXC_ALLOC, or 0.79
+    against the true 0.4467) -- on the service only, the per-batch kernels'
+    register allocation happened not to expose it."""
+    import json
+    from pathlib import Path
+
+    from funsearch_kubernetes_simulator_amd.ops import cpu_engine as ce
+    from funsearch_kubernetes_simulator_amd.policy.compiler import try_compile
+    path = Path(__file__).resolve().parents[1] / "data" / "diag" / "r6i_population.json"
+    progs = [p for p in (try_compile(x["code"])[0] for x in json.load(open(path))["programs"]) if p is not None]
+    assert len(progs) == 80
+    vm = np.asarray(ce.simulate_program_batch(default_workload, progs, threads=8))
+    dev.start_service(slots=1024, share=0.875)
+    try:
+        got = dev.evaluate_native(progs)
+    finally:
+        dev.stop_service()
+    bad = [i for i in range(len(progs)) if not (got[i, 0] == vm[i, 0] and got[i, 8] == vm[i, 8]
+                                                and int(got[i, 10]) == int(vm[i, 10]))]
+    assert not bad, [(i, got[i, [0, 8, 10]].tolist(), vm[i, [0, 8, 10]].tolist()) for i in bad[:8]]

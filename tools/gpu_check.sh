@@ -38,7 +38,8 @@ for step in "$@"; do
   echo "== $step ($(date +%T))"
   case $key in
     tests)
-      timeout -k 10 900 python -u -m pytest ${val:-tests} -m gpu -x -v --timeout 300 --timeout-method thread \
+      [ -z "$val" ] && val=tests
+      timeout -k 10 900 python -u -m pytest ${val//,/ } -m gpu -x -v --timeout 300 --timeout-method thread \
         > "$O/gpu_tests.txt" 2>&1 || die tests "$O/gpu_tests.txt"
       tail -2 "$O/gpu_tests.txt" ;;
     smoke)
