@@ -330,6 +330,11 @@ class SteadyStateSearch:
         svc = service if isinstance(service, dict) else ({} if service else None)
         self.service_cfg = None
         self.slot_base = 0
+        #: host collectives: with the grid resident RCCL collectives cannot
+        #: progress (tools/grid_coexist_probe.py), so a service configuration
+        #: sends the migrations' small host arrays over the gloo group opened
+        #: beside RCCL -- decided from the configuration, the same on every rank
+        self.host_collectives = dist.use_host_collectives(svc is not None)
         if svc is not None and dev is not None and hasattr(dev, "start_service"):
             self.service_cfg = dict(svc)
             # batches in flight at once (a batch holds its entry until its

@@ -94,7 +94,42 @@ def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = No
         else:
             dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
     _ctx = DistContext(rank=rank, world_size=world, local_rank=local, backend=backend, device=device)
+    global _host_pg
+    _host_pg = None
+    hg = os.environ.get("FKS_HOST_GROUP", "1")
+    if (backend == "nccl" and hg != "0") or hg == "force":   # force: a CPU (gloo-on-gloo) rehearsal
+        # a gloo group beside the RCCL one, for host-array collectives that must
+        # progress while the resident program grid holds the device: measured
+        # on MI355X (tools/grid_coexist_probe.py), every RCCL collective --
+        # default or side stream -- waits for the grid to end
+        _host_pg = dist.new_group(backend="gloo")
     return _ctx
+
+
+_host_pg = None            # gloo group beside an RCCL default group (init_distributed)
+_host_transport = False   # route the host-array collectives through it
+
+
+def use_host_collectives(on: bool = True) -> bool:
+    """Send the host-array collectives (all_gather_array[_async],
+    all_reduce_max/sum, all_gather_bytes, barrier) over the gloo group that
+    init_distributed opens beside RCCL.  Every rank must make the same call at
+    the same point (it changes which group the next collective uses): the
+    island search does it at construction when its configuration runs the
+    resident program service.  Returns whether host collectives are now in use
+    (False without an RCCL group: gloo-only and local runs are host already)."""
+    global _host_transport
+    _host_transport = bool(on) and _host_pg is not None
+    return _host_transport
+
+
+def _host_group():
+    """(group, device) of the next host-array collective."""
+    ctx = context()
+    if _host_transport and _host_pg is not None:
+        import torch
+        return _host_pg, torch.device("cpu")
+    return None, ctx.device
 
 
 def context() -> DistContext:
@@ -105,7 +140,10 @@ def barrier() -> None:
     ctx = context()
     if ctx.group:
         import torch.distributed as dist
-        if ctx.backend == "nccl":
+        grp, _ = _host_group()
+        if grp is not None:
+            dist.barrier(group=grp)
+        elif ctx.backend == "nccl":
             import torch
             dist.barrier(device_ids=[ctx.local_rank])
             torch.cuda.synchronize()
@@ -120,9 +158,10 @@ def all_gather_array(x: np.ndarray) -> np.ndarray:
         return x[None].copy()
     import torch
     import torch.distributed as dist
-    t = torch.from_numpy(np.ascontiguousarray(x)).to(ctx.device)
+    grp, d = _host_group()
+    t = torch.from_numpy(np.ascontiguousarray(x)).to(d)
     out = [torch.empty_like(t) for _ in range(ctx.world_size)]
-    dist.all_gather(out, t)
+    dist.all_gather(out, t, group=grp)
     return np.stack([o.cpu().numpy() for o in out])
 
 
@@ -150,9 +189,10 @@ def all_gather_array_async(x: np.ndarray) -> PendingGather:
         return PendingGather(ready=x[None].copy())
     import torch
     import torch.distributed as dist
-    t = torch.from_numpy(np.ascontiguousarray(x)).to(ctx.device)
+    grp, d = _host_group()
+    t = torch.from_numpy(np.ascontiguousarray(x)).to(d)
     out = [torch.empty_like(t) for _ in range(ctx.world_size)]
-    work = dist.all_gather(out, t, async_op=True)
+    work = dist.all_gather(out, t, async_op=True, group=grp)
     return PendingGather(work, out)
 
 
@@ -162,8 +202,9 @@ def all_reduce_max(v: float) -> float:
         return float(v)
     import torch
     import torch.distributed as dist
-    t = torch.tensor([float(v)], dtype=torch.float64, device=ctx.device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    grp, d = _host_group()
+    t = torch.tensor([float(v)], dtype=torch.float64, device=d)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=grp)
     return float(t.item())
 
 
@@ -173,8 +214,9 @@ def all_reduce_sum(v: float) -> float:
         return float(v)
     import torch
     import torch.distributed as dist
-    t = torch.tensor([float(v)], dtype=torch.float64, device=ctx.device)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    grp, d = _host_group()
+    t = torch.tensor([float(v)], dtype=torch.float64, device=d)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=grp)
     return float(t.item())
 
 
@@ -185,7 +227,7 @@ def degrade_to_local(reason: str = "") -> DistContext:
     the island search so that losing one rank does not end the run (SURVEY
     §5.3); the lost islands come back through `--resume` (see
     `IslandFunSearch.load_elastic`)."""
-    global _ctx
+    global _ctx, _host_pg, _host_transport
     ctx = context()
     if ctx.group:
         import torch.distributed as dist
@@ -194,13 +236,15 @@ def degrade_to_local(reason: str = "") -> DistContext:
                 dist.destroy_process_group()
         except Exception:       # the group may already be broken; nothing left to release
             pass
+    _host_pg, _host_transport = None, False
     _ctx = DistContext(rank=ctx.rank, world_size=1, local_rank=ctx.local_rank, backend="none",
                        device=ctx.device)
     return _ctx
 
 
 def shutdown() -> None:
-    global _ctx
+    global _ctx, _host_pg, _host_transport
+    _host_pg, _host_transport = None, False
     if _ctx is not None and _ctx.group:
         import torch.distributed as dist
         if dist.is_initialized():

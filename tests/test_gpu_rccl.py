@@ -31,3 +31,5 @@ def test_rccl_group_beside_replay_slots():
     assert out["replays_equal_after_collectives"]
     assert out["steady_migrations"] >= 1 and out["steady_best"] > 0.4
     assert out["service"] and out["service_blocks"] > 0 and out["max_stall_s"] <= 1.0
+    # beside the resident grid the migrations go over the gloo group next to RCCL
+    assert out["host_collectives"]

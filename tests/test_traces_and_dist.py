@@ -95,6 +95,35 @@ def test_gloo_collectives_and_migration(tmp_path):
     assert out["ok"] and out["best_island0"] >= 100
 
 
+def test_host_group_collectives_two_ranks(tmp_path):
+    """The gloo group opened beside the default one (RCCL on a GPU node; a
+    second gloo group here, FKS_HOST_GROUP=force): with use_host_collectives
+    every host-array collective goes through it and returns what the default
+    group returns."""
+    script = tmp_path / "h.py"
+    script.write_text(
+        "import json, os, numpy as np\n"
+        "os.environ['FKS_HOST_GROUP'] = 'force'\n"
+        "from funsearch_kubernetes_simulator_amd.parallel import dist\n"
+        "ctx = dist.init_distributed(use_gpu=False)\n"
+        "x = np.full((2, 3), ctx.rank, dtype=np.float64)\n"
+        "ref = dist.all_gather_array(x)\n"
+        "assert dist.use_host_collectives(True)\n"
+        "assert dist._host_group()[0] is not None\n"
+        "g = dist.all_gather_array(x)\n"
+        "assert np.array_equal(g, ref)\n"
+        "assert np.array_equal(dist.all_gather_array_async(x + 1).wait(), ref + 1)\n"
+        "assert dist.all_reduce_max(ctx.rank * 10.0) == 10.0 and dist.all_reduce_sum(1.0) == 2.0\n"
+        "assert dist.all_gather_bytes(b'r%d' % ctx.rank) == [b'r0', b'r1']\n"
+        "dist.barrier()\n"
+        "assert not dist.use_host_collectives(False)\n"
+        "if ctx.rank == 0: print(json.dumps({'ok': True}))\n"
+        "dist.shutdown()\n")
+    r = _run_torchrun(str(script))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])["ok"]
+
+
 def test_global_best_carries_long_program_across_ranks(tmp_path):
     """The cross-rank champion travels whatever its length: rank 1 holds a
     >8 KB best program, both ranks return it (no fixed-width record)."""
@@ -336,8 +365,11 @@ def test_scaling_harness_cpu():
 def test_config4_launcher_two_gloo_ranks(tmp_path):
     """tools/run_config4.sh (BASELINE config 4: one island per rank, RCCL elite
     migration, torchrun --max-restarts + --resume) rehearsed with 2 gloo ranks."""
+    # (the CPU rehearsal config: config 4's structure -- steady loop, polish,
+    # family coupler -- with per-generation work a CPU evaluator finishes)
     env = dict(os.environ, NPROC="2", GENS="2", RUN_DIR=str(tmp_path / "c4"), FKS_DIST_BACKEND="gloo",
-               PORT=str(34000 + os.getpid() % 1000), OMP_NUM_THREADS="1", GLOO_SOCKET_IFNAME="lo")
+               PORT=str(34000 + os.getpid() % 1000), OMP_NUM_THREADS="1", GLOO_SOCKET_IFNAME="lo",
+               CONFIG="configs/config4_rehearsal.json", DEVICE_ARGS="--device cpu")
     r = subprocess.run(["bash", os.path.join(REPO, "tools", "run_config4.sh")], env=env, capture_output=True,
                        text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]

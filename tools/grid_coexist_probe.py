@@ -71,6 +71,11 @@ def main() -> None:
         ("all_gather_default_stream", gather_default),
         ("all_gather_side_stream", gather_side),
         ("dist_all_gather_array_async", lambda: dist.all_gather_array_async(x).wait()),
+        ("host_group_all_gather_async", lambda: (dist.use_host_collectives(True),
+                                                 dist.all_gather_array_async(x).wait(),
+                                                 dist.use_host_collectives(False))),
+        ("host_group_all_reduce_max", lambda: (dist.use_host_collectives(True), dist.all_reduce_max(1.5),
+                                               dist.use_host_collectives(False))),
         ("cuda_synchronize", torch.cuda.synchronize),
     ]
     for name, fn in probes:

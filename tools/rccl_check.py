@@ -13,9 +13,12 @@ exercises, on the one-GPU box, everything a rank does with RCCL:
 * `MigrationChannel.post / poll` round trips with the search's own payloads;
 * a short steady-state run of the shipped config 4 (``--config``: steady loop,
   resident program service, family coupler; ``migrate_every`` 5 here, so every
-  few seconds an RCCL all-gather runs beside the persistent grid), ending with
-  the service's abort + stop: every gather must complete, none may block the
-  dispatcher for more than ``--max-stall-s``, and the run must end promptly.
+  few seconds a migration all-gather runs beside the persistent grid), ending
+  with the service's abort + stop: every gather must complete, none may block
+  the dispatcher for more than ``--max-stall-s``, and the run must end
+  promptly.  RCCL collectives cannot progress while the grid is resident
+  (tools/grid_coexist_probe.py), so those gathers go over the gloo group
+  `dist.init_distributed` opens beside RCCL (`host_collectives` in the output).
 
 Prints one JSON line.  Run it under ``rocprofv3 --kernel-trace --stats`` to
 see the RCCL all-gather kernels beside ``k_replay_native_duo``.
@@ -110,6 +113,7 @@ def main() -> None:
     out["steady_best"] = round(float(score), 6)
     out["steady_evaluations"] = int(run.evaluations)
     out["collective_wait_s"] = mig[-1]["collective_wait_s"] if mig else None
+    out["host_collectives"] = bool(getattr(run.steady, "host_collectives", False))
     out["max_stall_s"] = round(run.steady.channel.max_stall_s, 4)
     out["max_gather_s"] = round(run.steady.channel.max_gather_s, 4)
     out["posted"] = (run.steady.channel.next - run.steady.channel.every) // max(1, run.steady.channel.every) \
