@@ -83,7 +83,8 @@ def _producer_init(llm_cfg: dict, timeout_s: int, seed: int, fanout: int = 0) ->
 
 
 def _produce(task):
-    """(island, elites [(code, score)], n[, weights]) -> ([(island, code, CompiledPolicy | None)], cpu s, wall s).
+    """(island, elites [(code, score)], n[, weights]) -> ([(island, code, CompiledPolicy | None)], cpu s, wall s,
+    gap s).
     weights: per-elite parent weights (the steady search's device-cost
     weighting, `_parent_weights`), or None for uniform sampling.
 
@@ -99,6 +100,11 @@ def _produce(task):
     weights = task[3] if len(task) > 3 else None
     t0 = time.process_time()
     w0 = time.perf_counter()
+    # the producer's gap since its previous task ended: its last result's
+    # trip to the dispatcher plus this task's trip to the process (idle time
+    # the pool's hand-offs cost; reported with the task)
+    last = _W.get("t_end")
+    gap = w0 - last if last is not None else 0.0
     pool = _W.get("fanout")
     if pool is not None:
         pend = _W.setdefault("pending", [])
@@ -120,7 +126,14 @@ def _produce(task):
         pend.extend(pool.submit(_produce_one, island, elites, weights) for _ in range(max(0, n)))
     else:
         out = [_produce_one(island, elites, weights) for _ in range(n)]
-    return out, time.process_time() - t0, time.perf_counter() - w0
+    for _, code, prog in out:
+        # the program's source is the child's text: sent once (results travel
+        # through one pipe read by the pool's result thread in the GIL-bound
+        # dispatcher; the duplicate text was ~half of the ~6.6 KB per child)
+        if prog is not None and prog.source == code:
+            prog.source = None
+    _W["t_end"] = time.perf_counter()
+    return out, time.process_time() - t0, _W["t_end"] - w0, gap
 
 
 def _produce_one(island, elites, weights):
@@ -268,6 +281,9 @@ class SteadyStats:
     shed: int = 0                    # children only CPython could score, not evaluated (host_object off)
     abandoned: int = 0               # host fallbacks still queued when the run stopped
     producer_cpu_s: float = 0.0
+    task_turnaround_s: float = 0.0   # producer tasks: submit -> result collected (wall), summed
+    task_n: int = 0
+    producer_gap_s: float = 0.0      # producers idle between tasks (result out + next task in), summed
     producer_wall_s: float = 0.0     # wall seconds the producers spent on tasks (CPU / wall: their core share)
     polish_batches: int = 0          # constant-polish batches (variants of an island champion)
     polish_evals: int = 0            # their device evaluations (not children)
@@ -592,7 +608,10 @@ class SteadyStateSearch:
                 ready.insert(0, (job.island, text, prog))
                 st.polish_improved += 1
                 rec["improved"] = True
-        self.fs.log.write(**rec)
+                # (only the improving batches: ~15 polish batches/s would put a
+                # JSON record per batch on the dispatcher thread; the status
+                # records carry polish_batches / polish_improved)
+                self.fs.log.write(**rec)
 
     def _stream(self, b: _Batch, merged: List[int], islands, ready: list) -> bool:
         """Program service: merge the batch's programs that finished since the
@@ -699,8 +718,12 @@ class SteadyStateSearch:
         conc = int(llm_cfg.get("concurrency", 0) or 0)
         fanout = 0
         if conc > 0 and remote_like(llm_cfg):
-            self.task_size = max(1, -(-conc // self.producers))
-            fanout = self.task_size
+            # each producer keeps `fanout` requests in flight; a task tops them
+            # up by a quarter of that and returns what completed meanwhile (a
+            # task of the full fanout would wait for every request in flight --
+            # the slowest of 16 at 2-8 s: 7.5 s per task, 33 children/s of 51)
+            fanout = max(1, -(-conc // self.producers))
+            self.task_size = max(1, fanout // 4)
         self.llm_concurrency = fanout * self.producers
         if fanout:
             fs.log.write(kind="steady_llm", rank=ctx.rank, concurrency=self.llm_concurrency, producers=self.producers,
@@ -736,6 +759,14 @@ class SteadyStateSearch:
         if os.environ.get("FKS_THREAD_PROFILE"):
             from ..utils.trace import ThreadSampler
             sampler = ThreadSampler().start()
+        # the dispatcher process runs several Python threads (this loop, the
+        # stagers, the similarity scans, the process pool's result thread); at
+        # CPython's default 5 ms GIL switch interval a thread that only needs
+        # the GIL for a moment (the pool thread handing a finished task back)
+        # waits up to 5 ms per hand-off behind the busy ones
+        import sys as _sys
+        gil_prev = _sys.getswitchinterval()
+        _sys.setswitchinterval(float(os.environ.get("FKS_GIL_SWITCH_S", "0.0005")))
         t_status = t_start
         t_prev = t_start
         busy_since = None
@@ -749,9 +780,15 @@ class SteadyStateSearch:
         try:
             while True:
                 progressed = False
-                self._left = sum(b.left for b in batches.live())   # programs not merged yet
-                # 1) keep producers busy (children from the islands' CURRENT elites)
-                queued = len(ready) + self._left + \
+                live = batches.live()
+                self._left = sum(b.left for b in live)   # programs not merged yet
+                # 1) keep producers busy (children from the islands' CURRENT elites);
+                # children only: polish variants filling the grid's spare room must
+                # not hold the producers back (they did: polish kept ~2/3 of the
+                # in-flight count, the producers idled at ~40 % busy, and the
+                # emptier child queue then let in more polish)
+                left_children = sum(b.left for b in live if b.polish is None)
+                queued = len(ready) + left_children + \
                     sum(len(t) for t, _, pj in staged if pj is None) + self.task_size * len(inflight_tasks)
                 while (not stop and queued < want_buffer + self.task_size * self.producers
                        and len(inflight_tasks) < 2 * self.producers):
@@ -766,7 +803,9 @@ class SteadyStateSearch:
                         continue
                     n = min(self.task_size, target_children[i] - requested[i])
                     requested[i] += n
-                    inflight_tasks.append(pool.submit(_produce, (i, elites, n, self._parent_weights(i, elites))))
+                    fut = pool.submit(_produce, (i, elites, n, self._parent_weights(i, elites)))
+                    fut.t_sub = time.perf_counter()
+                    inflight_tasks.append(fut)
                     self._asked += n
                     queued += n
                     progressed = True
@@ -775,13 +814,20 @@ class SteadyStateSearch:
                 for f in inflight_tasks:
                     if f.done():
                         t_ph = time.perf_counter()
-                        items, cpu_s, task_wall_s = f.result()
+                        items, cpu_s, task_wall_s, gap_s = f.result()
+                        self.stats.producer_gap_s += gap_s
                         self.phase["receive"] += time.perf_counter() - t_ph
                         self.stats.producer_cpu_s += cpu_s
                         self.stats.producer_wall_s += task_wall_s
+                        t_sub = getattr(f, "t_sub", None)
+                        if t_sub is not None:   # submit -> collected, beyond the task itself
+                            self.stats.task_turnaround_s += t_ph - t_sub
+                            self.stats.task_n += 1
                         self._got += len(items)
                         for isl, code, prog in items:
                             self.stats.produced += 1
+                            if prog is not None and prog.source is None:
+                                prog.source = code       # (stripped for the trip: _produce)
                             if prog is None:     # no program: counts toward the island's generation
                                 self.stats.rejected += 1
                                 if code is not None:
@@ -1078,6 +1124,7 @@ class SteadyStateSearch:
                 if not progressed:
                     time.sleep(0.0005)
         finally:
+            _sys.setswitchinterval(gil_prev)
             if sampler is not None:
                 sampler.stop()
                 rep = sampler.report()
@@ -1161,6 +1208,11 @@ class SteadyStateSearch:
                    # cores are short) and the fraction of the run they were on tasks
                    producer_cpu_share=round(st.producer_cpu_s / max(1e-9, st.producer_wall_s), 3),
                    producer_busy=round(st.producer_wall_s / max(1e-9, wall * self.producers), 3),
+                   # mean producer task: submit -> collected, and its own wall time (the
+                   # difference: queueing in the pool + hand-off to / from the worker)
+                   task_turnaround_ms=round(1e3 * st.task_turnaround_s / max(1, st.task_n), 2),
+                   task_wall_ms=round(1e3 * st.producer_wall_s / max(1, st.task_n), 2),
+                   task_gap_ms=round(1e3 * st.producer_gap_s / max(1, st.task_n), 2),
                    main_cpu_frac=round((time.process_time() - self._cpu0) / wall, 3), rejected=st.rejected, jit_s=round(st.jit_s, 3),
                    generation=fs.generation, best=round(fs.best[1], 6), best_global=round(best_global, 6),
                    islands=[round(s.best_score, 6) for s in fs.islands], migrations=st.migrations,

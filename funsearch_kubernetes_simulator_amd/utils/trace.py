@@ -121,7 +121,9 @@ class ThreadSampler:
                 f = frame
                 while f is not None and len(parts) < self.depth:
                     co = f.f_code
-                    parts.append(f"{os.path.basename(co.co_filename)}:{co.co_name}")
+                    # the innermost frame with its line: where in a long loop body
+                    ln = f":{f.f_lineno}" if not parts else ""
+                    parts.append(f"{os.path.basename(co.co_filename)}:{co.co_name}{ln}")
                     f = f.f_back
                 key = " < ".join(parts)
                 d = self.samples.setdefault(name, {})
