@@ -54,6 +54,10 @@ def main() -> None:
             except ValueError:
                 continue
             if r.get("kind") in ("steady_status", "steady_final"):
+                # (the drain after the wall limit -- no producer task, nothing
+                # queued, the last replays finishing -- is not part of a window)
+                if st and r.get("producer_tasks", 1) == 0 and r.get("queued", 1) == 0:
+                    continue
                 st.append((r["wall_s"], r["evaluations"], r.get("evaluations", 0) + r.get("polish_evals", 0)))
     if st:
         print("# 100 s windows: children / s, all program evals / s (children + polish variants)")
