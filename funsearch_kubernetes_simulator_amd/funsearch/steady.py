@@ -60,6 +60,7 @@ _EXC_EVENTS = int(_Exc.EVENTS)
 #: device cost of a child scored on the host engines (the JIT declined it):
 #: the selection treats it as the costliest kind of program
 HOST_COST = -1.0
+_POLISH_SIGMAS = (0.6, 0.35, 0.15, 0.06, 0.02)   # constant-polish step sizes (log-normal sigma)
 
 # ---------------------------------------------------------------------------- producer processes
 _W: dict = {}
@@ -566,7 +567,14 @@ class SteadyStateSearch:
             s = fs.islands[i]
             if not s.population:
                 continue
-            code, score = max(s.population, key=lambda x: x[1])
+            n_done = self._polish_count.get(i, 0)
+            # every third polish of an island takes its second or third best
+            # member instead of the champion: a champion polished over and over
+            # sits on a plateau its literals no longer leave, while a runner-up's
+            # basin may hold a better setting
+            ranked = sorted(s.population, key=lambda x: -x[1])
+            pick = 0 if n_done % 3 != 2 or len(ranked) < 2 else 1 + (n_done // 3) % min(2, len(ranked) - 1)
+            code, score = ranked[pick]
             if not fs.polish_repeat and code in fs._polished:
                 continue
             fs._polished.add(code)
@@ -580,9 +588,9 @@ class SteadyStateSearch:
                 continue
             base = {prog.literals[j][0]: (prog.fconst[prog.literals[j][0]] if prog.ctag[prog.literals[j][0]] == TAG_FLOAT
                                           else prog.iconst[prog.literals[j][0]]) for j in range(len(prog.literals))}
-            n_done = self._polish_count.get(i, 0)
             self._polish_count[i] = n_done + 1
-            sigma = 0.35 * (0.6 ** (n_done % 3))
+            # step sizes cycle from coarse (a new basin) to fine (the last digits)
+            sigma = _POLISH_SIGMAS[n_done % len(_POLISH_SIGMAS)]
             rng = random.Random(hash((fs.ctx.rank, i, g)) & 0xFFFFFFFF)
             cands = [_perturb(prog, base, tune, sigma, rng) for _ in range(self.polish_variants)]
             return _Polish(i, code, prog, score, cands, [with_values(prog, v) for v in cands])
