@@ -47,7 +47,7 @@ for step in "$@"; do
         || die smoke "$O/smoke.txt"
       tail -1 "$O/smoke.txt" ;;
     bench)
-      timeout -k 10 600 python -u bench.py $val > "$O/bench.json" 2> "$O/bench.err" || die bench "$O/bench.err"
+      timeout -k 10 600 python -u bench.py ${val//,/ } > "$O/bench.json" 2> "$O/bench.err" || die bench "$O/bench.err"
       cut -c1-400 "$O/bench.json" ;;
     prof)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py ${val:---steps 3 --warmup 1 --programs 0 --novel 0 --novel-large 0 --evolved 0} \
