@@ -94,31 +94,33 @@ def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = No
         else:
             dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
     _ctx = DistContext(rank=rank, world_size=world, local_rank=local, backend=backend, device=device)
-    global _host_pg
-    _host_pg = None
-    hg = os.environ.get("FKS_HOST_GROUP", "1")
-    if (backend == "nccl" and hg != "0") or hg == "force":   # force: a CPU (gloo-on-gloo) rehearsal
-        # a gloo group beside the RCCL one, for host-array collectives that must
-        # progress while the resident program grid holds the device: measured
-        # on MI355X (tools/grid_coexist_probe.py), every RCCL collective --
-        # default or side stream -- waits for the grid to end
-        _host_pg = dist.new_group(backend="gloo")
     return _ctx
 
 
-_host_pg = None            # gloo group beside an RCCL default group (init_distributed)
+_host_pg = None            # gloo group beside an RCCL default group (use_host_collectives)
 _host_transport = False   # route the host-array collectives through it
 
 
 def use_host_collectives(on: bool = True) -> bool:
     """Send the host-array collectives (all_gather_array[_async],
-    all_reduce_max/sum, all_gather_bytes, barrier) over the gloo group that
-    init_distributed opens beside RCCL.  Every rank must make the same call at
+    all_reduce_max/sum, all_gather_bytes, barrier) over a gloo group beside
+    RCCL (opened by the first such call: with the resident program grid on the
+    device, RCCL collectives -- default or side stream -- wait for the grid to
+    end, measured by tools/grid_coexist_probe.py).  Every rank must make the same call at
     the same point (it changes which group the next collective uses): the
     island search does it at construction when its configuration runs the
     resident program service.  Returns whether host collectives are now in use
     (False without an RCCL group: gloo-only and local runs are host already)."""
-    global _host_transport
+    global _host_transport, _host_pg
+    ctx = context()
+    hg = os.environ.get("FKS_HOST_GROUP", "1")
+    if on and _host_pg is None and ctx.group and (
+            (ctx.backend == "nccl" and hg != "0") or hg == "force"):   # force: a CPU (gloo-on-gloo) rehearsal
+        # opened here, not in init_distributed: only runs that need it (the
+        # service configurations) pay for a second group -- every rank reaches
+        # this call at the same point, as new_group requires
+        import torch.distributed as dist
+        _host_pg = dist.new_group(backend="gloo")
     _host_transport = bool(on) and _host_pg is not None
     return _host_transport
 
