@@ -316,3 +316,38 @@ def test_deferred_merge_rechecks_members_added_since():
     codes = [x for x, _ in s.population]
     assert a in codes and c in codes and b in codes and (b + "#") not in codes
     st._sim_pool.shutdown()
+
+
+def test_device_cost_steers_selection_never_scores():
+    """Per-program device cycles (service row column 13) decide only whether a
+    non-best child is merged (bloat vs the island median and the run's anchor)
+    and how parents are weighted: a merged child keeps its exact score, a new
+    island best is merged whatever it costs, host-scored children (cost < 0)
+    enter only as a new best."""
+    from funsearch_kubernetes_simulator_amd.funsearch.steady import HOST_COST, SteadyStateSearch
+
+    class Island:
+        population_size, similarity_threshold, similarity_threads = 8, 0.85, 1
+        best_score, best_policy = 0.6, None
+
+        def __init__(self):
+            self.population = []
+
+        def _is_too_similar(self, code, score):
+            return False
+
+    st = object.__new__(SteadyStateSearch)
+    st._pending_merges, st._sim_pool, st._cost = collections.deque(), None, {}
+    st.cost_bloat, st.service_cfg = 3.0, {}
+    st.cost_anchor, st.cost_anchor_cap = 100.0, 3.0
+    st.stats = type("S", (), {"cost_rejected": 0})()
+    s = Island()
+    progs = [f"def f(pod, node):\n    return {k} + node.cpu_milli_left\n" for k in range(8)]
+    for k in range(3):
+        assert st._merge_one(s, progs[k], 0.5 + 0.01 * k, cost=100.0, island=0)
+    assert not st._merge_one(s, progs[3], 0.55, cost=1000.0, island=0)     # 10x the median, not a best
+    assert not st._merge_one(s, progs[4], 0.55, cost=HOST_COST, island=0)  # host-scored, not a best
+    assert st._merge_one(s, progs[5], 0.7, cost=1e6, island=0)             # new best: merged regardless
+    assert st._merge_one(s, progs[6], 0.55, cost=250.0, island=0)          # within 3x median and anchor
+    assert st.stats.cost_rejected == 2
+    assert dict(s.population) == {progs[0]: 0.5, progs[1]: 0.51, progs[2]: 0.52, progs[5]: 0.7, progs[6]: 0.55}
