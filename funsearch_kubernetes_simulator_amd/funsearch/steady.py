@@ -361,6 +361,9 @@ class SteadyStateSearch:
             self.slots = max(1, int(svc.get("slots", slots or 1024)))
             self.slot_base = dev.SERVICE_SLOT_BASE
         self.service_inflight = 0
+        #: producer tasks kept submitted per producer process (FKS_TASKS_PER_PRODUCER;
+        #: the pool hands a finished producer its next task from this backlog)
+        self.tasks_per_producer = max(1, int(os.environ.get("FKS_TASKS_PER_PRODUCER", "2")))
         #: device-cost selection (service runs: every child's replay cycles are
         #: measured on the grid): parents are sampled with weight median / cost
         #: (clipped to [1/4, 4]) among an island's elites, and a child costing more
@@ -799,7 +802,7 @@ class SteadyStateSearch:
                 queued = len(ready) + left_children + \
                     sum(len(t) for t, _, pj in staged if pj is None) + self.task_size * len(inflight_tasks)
                 while (not stop and queued < want_buffer + self.task_size * self.producers
-                       and len(inflight_tasks) < 2 * self.producers):
+                       and len(inflight_tasks) < self.tasks_per_producer * self.producers):
                     cands = [i for i in range(k) if requested[i] < target_children[i]]
                     if not cands:
                         break
