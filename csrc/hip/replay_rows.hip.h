@@ -374,7 +374,7 @@ __device__ __forceinline__ void fill_node_tables(const DevWorkload& W, FKS_LDS i
 // per row: deletion bitmap | heap top (T + 1 slots) | cold state (trace hash,
 // snapshot threshold beyond the host's schedule: read rarely, so kept out of
 // the registers the 4- and 5-waves-per-SIMD register budgets are tight on)
-constexpr int kRowColdBytes = 32;   // hash, threshold, repush / dropped / snapshot counters, stranded cache
+constexpr int kRowColdBytes = 32;   // hash, threshold, repush / dropped / snapshot counters
 __host__ __device__ inline size_t rows_row_bytes(int n_pods, int T) {
   return (size_t)lds_delmap_words(n_pods) * 4 + (size_t)(T + 1) * 8 + kRowColdBytes;
 }
@@ -522,10 +522,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
   int32_t processed = 0, next_fire = INT32_MAX;
   int n = 0;
   FKS_LDS uint64_t* rcs = heap.top + (T + 1);   // [0] trace hash, [1] threshold bits
-  // [0] repushes, [1] dropped pods, [2] snapshots taken (per-row counters),
-  // [3] the failed-placement fragmentation cache: 1 << 31 | class << 24 |
-  // stranded GPU milli of the cluster for that waiting class, valid until a
-  // deletion or placement changes the nodes (0: empty)
+  // [0] repushes, [1] dropped pods, [2] snapshots taken (per-row counters)
   FKS_LDS uint32_t* rcn = reinterpret_cast<FKS_LDS uint32_t*>(rcs + 2);
   auto bump = [&](int k) {   // one lane of the row adds 1
     if (jv == 0) __hip_atomic_fetch_add(&rcn[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -576,7 +573,7 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
     for (int k = 0; k < kRowClassSlots / 2; ++k) wcp[k] = 0u;
     acc.init();
     processed = 0;
-    rcn[0] = 0u; rcn[1] = 0u; rcn[2] = 0u; rcn[3] = 0u;
+    rcn[0] = 0u; rcn[1] = 0u; rcn[2] = 0u;
     const double thr = Wb->thr_after_fire;
     rcs[1] = (uint64_t)__double_as_longlong(thr);
     if (Wb->n_fire > 0) {
@@ -631,7 +628,6 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
           for (int g = 0; g < kGmax; ++g)
             if ((mask >> g) & 1) nr.g_add(0, g, pod.gmilli);
         }
-        if constexpr (FAM != -1) rcn[3] = 0u;   // the nodes changed: no cached stranded sum
         if (cold()->trace_hash) rcs[0] = mix_event(rcs[0], ((uint64_t)(uint32_t)rank << 2) | 1, (uint64_t)t);
         ecat = 1;
         prof.mark(PH_DELETE);
@@ -707,28 +703,14 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
           for (int k = 0; k < kRowClassSlots / 2; ++k) any = any || wcp[k] != 0u;
           const int mcls = (int)row_min_u32(any ? nzs * kRow + (uint32_t)jv : 64u);
           if (mcls < 64) {
-            // consecutive failures with no deletion or placement between them
-            // (a saturated cluster) see the same nodes: the stranded sum for the
-            // same waiting class is reused (row-uniform: one LDS word per row)
-            // (not in the mixed-family instance, FAM -1: there the extra
-            // registers cross 128 VGPRs, 3 waves per SIMD instead of 4)
-            constexpr bool kCache = FAM != -1;
-            const uint32_t key = 0x80000000u | ((uint32_t)mcls << 24);
-            const uint32_t cw = kCache ? rcn[3] : 0u;
-            int32_t stranded;
-            if (kCache && (cw & 0xFF000000u) == key) {
-              stranded = (int32_t)(cw & 0xFFFFFFu);
-            } else {
-              const int mv = cls_lds[mcls];
-              stranded = 0;   // the cluster's GPU milli total < 2^31 (host-checked)
+            const int mv = cls_lds[mcls];
+            int32_t stranded = 0;   // the cluster's GPU milli total < 2^31 (host-checked)
 #pragma unroll
-              for (int g = 0; g < kGmax; ++g) {
-                const int l = nr.g(0, g);
-                if (0 < l && l < mv) stranded += l;   // GPUs past ngpus hold 0 milli (host padding)
-              }
-              stranded = row_sum_i32(node_valid ? stranded : 0);
-              if (kCache && stranded < (1 << 24)) rcn[3] = key | (uint32_t)stranded;
+            for (int g = 0; g < kGmax; ++g) {
+              const int l = nr.g(0, g);
+              if (0 < l && l < mv) stranded += l;   // GPUs past ngpus hold 0 milli (host padding)
             }
+            stranded = row_sum_i32(node_valid ? stranded : 0);
             const int64_t tg = cold()->tot_gmilli;
             // stranded in [0, tg]: W.z_tg is verified there
             frag = tg <= 0 ? 0.0 : W.z_tg != 0.0 ? div_by_recip((double)stranded, W.tot_gmilli_d, W.z_tg)
@@ -771,7 +753,6 @@ __device__ void replay_rows(const DevWorkload& W, const DevWorkload* Wdev, const
             for (int sl = 0; sl < kRowClassSlots; ++sl)
               if (sl == (pod.cls >> 4) && jv == (pod.cls & 15)) wcp[sl >> 1] -= 1u << (16 * (sl & 1));
           }
-          if constexpr (FAM != -1) rcn[3] = 0u;   // the nodes changed: no cached stranded sum
           const uint64_t dt = (uint64_t)(t + pod.dur);
           if (t + pod.dur < 0 || dt > time_max) { exc = EXC_UNSUPPORTED; break; }
           push_item = (dt << tshift) | ((uint64_t)rank << lb) | ((uint64_t)gmask << (2 + nb)) |
