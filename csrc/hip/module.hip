@@ -30,6 +30,7 @@
 #include "scorers.hip.h"
 #include "vm_dev.hip.h"
 #include "jit_abi.h"
+#include "screen_mfma.hip.h"
 
 namespace py = pybind11;
 using namespace fksd;
@@ -158,6 +159,57 @@ py::array_t<uint64_t> test_wave_ops(py::array_t<uint64_t, py::array::c_style | p
   (void)hipFree(din);
   (void)hipFree(dout);
   return out;
+}
+
+// k_score_linear_mfma (screen_mfma.hip.h): signatures (and optionally the
+// per-state decisions) of P linear-family candidates on S recorded states.
+// X: float32 [S * 4 * 64], W: float32 [tiles * 4 * 64] in the kernel's layout
+// (ops/screen.py arranges them).  Returns (sig uint64 [P], dec uint8 [P, S] or None, kernel ms).
+py::tuple screen_linear(py::array_t<float, py::array::c_style | py::array::forcecast> X,
+                        py::array_t<float, py::array::c_style | py::array::forcecast> W, int S, int P, bool want_dec,
+                        int device) {
+  using namespace fks_screen;
+  const int tiles = (P + kScreenCands - 1) / kScreenCands;
+  if (S < 1 || P < 1) throw std::invalid_argument("screen: empty");
+  if ((size_t)X.size() != (size_t)S * 256) throw std::invalid_argument("screen: X must be S * 4 * 64 floats");
+  if ((size_t)W.size() != (size_t)tiles * 256) throw std::invalid_argument("screen: W must be tiles * 4 * 64 floats");
+  HIP_OK(hipSetDevice(device));
+  float *dx = nullptr, *dw = nullptr;
+  uint8_t* dd = nullptr;
+  uint64_t* ds = nullptr;
+  hipEvent_t e0, e1;
+  HIP_OK(hipMalloc(&dx, (size_t)S * 256 * 4));
+  HIP_OK(hipMalloc(&dw, (size_t)tiles * 256 * 4));
+  HIP_OK(hipMalloc(&ds, (size_t)P * 8));
+  if (want_dec) HIP_OK(hipMalloc(&dd, (size_t)P * S));
+  HIP_OK(hipMemcpy(dx, X.data(), (size_t)S * 256 * 4, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(dw, W.data(), (size_t)tiles * 256 * 4, hipMemcpyHostToDevice));
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  float ms = 0.f;
+  {
+    py::gil_scoped_release rel;
+    const int blocks = (tiles + kScreenWaves - 1) / kScreenWaves;
+    HIP_OK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL(k_score_linear_mfma, dim3(blocks), dim3(64 * kScreenWaves), 0, 0, dx, dw, S, tiles, dd, ds, P);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(e1, 0));
+    HIP_OK(hipEventSynchronize(e1));
+    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+  }
+  py::array_t<uint64_t> sig(P);
+  HIP_OK(hipMemcpy(sig.mutable_data(), ds, (size_t)P * 8, hipMemcpyDeviceToHost));
+  py::object dec = py::none();
+  if (want_dec) {
+    py::array_t<uint8_t> d({(py::ssize_t)P, (py::ssize_t)S});
+    HIP_OK(hipMemcpy(d.mutable_data(), dd, (size_t)P * S, hipMemcpyDeviceToHost));
+    dec = d;
+  }
+  for (void* q : {(void*)dx, (void*)dw, (void*)ds, (void*)dd})
+    if (q) (void)hipFree(q);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return py::make_tuple(sig, dec, (double)ms);
 }
 
 py::tuple test_heap(py::array_t<uint64_t, py::array::c_style | py::array::forcecast> init,
@@ -450,6 +502,8 @@ PYBIND11_MODULE(_fks_hip, m) {
   m.def("device_count", &device_count);
   m.def("test_wave_ops", &test_wave_ops);
   m.def("test_heap", &test_heap);
+  m.def("screen_linear", &screen_linear, py::arg("X"), py::arg("W"), py::arg("S"), py::arg("P"),
+        py::arg("want_dec") = false, py::arg("device") = 0);
   py::class_<DeviceEngine>(m, "DeviceEngine")
       .def(py::init<py::dict, int, int>(), py::arg("workload"), py::arg("device") = 0, py::arg("n_slots") = 4)
       .def("set_options", &DeviceEngine::set_options)

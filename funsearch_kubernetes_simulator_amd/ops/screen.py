@@ -1,0 +1,179 @@
+"""Behavioural screening of `feature_linear` candidates on the matrix cores.
+
+A linear-family candidate is a weight vector over the family's 12 node
+features (`models.families.FEATURES`).  Replays diverge after the first
+placement, so the per-event products are per-policy (VALU work, see
+docs/ARCHITECTURE.md "Considered and not built"); but scored on one common set
+of *recorded* cluster states, every candidate shares the same feature blocks
+and the scoring is a real GEMM -- `k_score_linear_mfma`
+(`csrc/hip/screen_mfma.hip.h`, v_mfma_f32_16x16x4_f32), SURVEY section 7.4
+item 3's shared-operand case.
+
+What it is for: a candidate's *decisions* on the recorded states (which node
+each recorded pod would go to) give a behavioural signature; candidates with
+equal signatures place every recorded pod alike and mostly replay alike, so a
+search can replay one of each (`unique_by_signature`).  It is a screen, not a
+score: f32 products may differ from the replay's f64 arithmetic at near-ties,
+and the exact replay stays the only fitness.
+
+    states = record_states(workload, seed_weights)     # object-engine replay, every k-th creation
+    sig, dec, ms = screen(states, W)                    # MFMA on the device
+    keep = unique_by_signature(sig)
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+from ..models.families import FEATURES, N_FEATURES
+
+K = 16           # feature slots: 12 family features, 3 zero pads, the feasibility bias
+NODES = 16       # nodes per state (the row-kernel cluster size)
+MASK = -1e30     # bias of an infeasible (or padding) node
+
+
+@dataclass
+class States:
+    """Recorded states: node features [S, 16, 12] (float64), feasibility
+    [S, 16] and the node the recording policy chose (-1: none)."""
+    feats: np.ndarray
+    feasible: np.ndarray
+    chosen: np.ndarray
+
+    @property
+    def S(self) -> int:
+        return int(self.feats.shape[0])
+
+
+def _feature_fn():
+    # the family's own expressions (models/families.py), evaluated per (pod, node)
+    src = "lambda pod, node: (" + ", ".join(e for _, e in FEATURES) + ",)"
+    return eval(src, {"min": min, "max": max, "sum": sum, "abs": abs, "len": len})   # our constants only
+
+
+def _feasible(pod, node) -> bool:
+    # the template's feasibility prologue (policy/template.py)
+    if pod.cpu_milli > node.cpu_milli_left or pod.memory_mib > node.memory_mib_left or pod.num_gpu > node.gpu_left:
+        return False
+    if pod.num_gpu > 0:
+        return sum(1 for g in node.gpus if g.gpu_milli_left >= pod.gpu_milli) >= pod.num_gpu
+    return True
+
+
+def record_states(workload, weights: Sequence[float], every: int = 16, max_states: int = 512) -> States:
+    """Replay the `feature_linear` policy `weights` on the object engine and
+    record the node features, feasibility and the chosen node at every
+    `every`-th creation event (up to `max_states`)."""
+    from ..models.families import feature_linear_program
+    from ..funsearch.scheduler import FunSearchScheduler
+    from ..simulator import DiscreteEventSimulator, KubernetesSimulator
+    if workload.cluster.n_nodes > NODES:
+        raise ValueError(f"screening records clusters of <= {NODES} nodes")
+    feat = _feature_fn()
+    sched = FunSearchScheduler(feature_linear_program(weights))
+    cluster, pods = workload.to_objects()
+    F, M, C = [], [], []
+    count = [0]
+
+    class Recorder(KubernetesSimulator):
+        def _select_node(self, pod):
+            best = super()._select_node(pod)
+            count[0] += 1
+            if count[0] % every == 0 and len(F) < max_states:
+                f = np.zeros((NODES, N_FEATURES))
+                m = np.zeros(NODES, dtype=bool)
+                ch = -1
+                for j, node in enumerate(self.cluster.nodes_dict.values()):
+                    if _feasible(pod, node):
+                        m[j] = True
+                        f[j] = feat(pod, node)
+                    if node is best:
+                        ch = j
+                F.append(f)
+                M.append(m)
+                C.append(ch)
+            return best
+
+    Recorder(cluster, pods, DiscreteEventSimulator(pods), sched).run_schedule()
+    return States(np.asarray(F), np.asarray(M), np.asarray(C, dtype=np.int64))
+
+
+def arrange_states(st: States) -> np.ndarray:
+    """X in the kernel's A-fragment layout: float32 [S, 4, 64], element
+    (s, t, l) = feature 4t + (l >> 4) of node l & 15 (slot 15: the bias)."""
+    S = st.S
+    full = np.zeros((S, NODES, K), dtype=np.float64)
+    full[:, :, :N_FEATURES] = st.feats
+    full[:, :, K - 1] = np.where(st.feasible, 0.0, MASK)
+    lanes = np.arange(64)
+    out = np.empty((S, 4, 64), dtype=np.float32)
+    for t in range(4):
+        out[:, t, :] = full[:, lanes & 15, 4 * t + (lanes >> 4)]
+    return out
+
+
+def arrange_weights(W: np.ndarray) -> Tuple[np.ndarray, int]:
+    """W [P, 12] in the B-fragment layout: float32 [tiles, 4, 64], element
+    (tile, t, l) = weight 4t + (l >> 4) of candidate 16 tile + (l & 15);
+    slot 15 = 1 (the feasibility bias), padding candidates all zero."""
+    W = np.asarray(W, dtype=np.float64)
+    P = W.shape[0]
+    tiles = (P + 15) // 16
+    full = np.zeros((tiles * 16, K), dtype=np.float64)
+    full[:P, :N_FEATURES] = W[:, :N_FEATURES]
+    full[:P, K - 1] = 1.0
+    lanes = np.arange(64)
+    out = np.empty((tiles, 4, 64), dtype=np.float32)
+    for t in range(4):
+        out[:, t, :] = full.reshape(tiles, 16, K)[:, lanes & 15, 4 * t + (lanes >> 4)]
+    return out, P
+
+
+def decisions_reference(st: States, W: np.ndarray, dtype=np.float64) -> np.ndarray:
+    """[P, S] node the family's rule picks on each recorded state (255: none
+    feasible): score = max(1, int(w . f)) on feasible nodes, the first maximum
+    wins.  float64: the replay's arithmetic; float32: the kernel's."""
+    W = np.asarray(W, dtype=dtype)[:, :N_FEATURES]
+    f = st.feats.astype(dtype)
+    v = np.einsum("snf,pf->psn", f, W)                         # [P, S, 16]
+    sc = np.maximum(1.0, np.trunc(v))
+    sc = np.where(st.feasible[None, :, :], sc, -2.0)
+    best = sc.argmax(axis=2)                                   # first maximum
+    none = ~st.feasible.any(axis=1)
+    best = np.where(none[None, :], 255, best)
+    return best.astype(np.uint8)
+
+
+def signature(dec: np.ndarray) -> np.ndarray:
+    """The kernel's FNV-1a fold of a [P, S] decision matrix (host twin)."""
+    h = np.full(dec.shape[0], 0xcbf29ce484222325, dtype=np.uint64)
+    prime = np.uint64(0x100000001b3)
+    d = dec.astype(np.uint64)
+    # 255 (none) folds as 256, like the kernel's (d + 1) with d = 255
+    for s in range(dec.shape[1]):
+        h = (h ^ (d[:, s] + np.uint64(1))) * prime
+    return h
+
+
+def screen(st: States, W: np.ndarray, want_dec: bool = False, device: int = 0):
+    """(sig [P] uint64, dec [P, S] uint8 or None, kernel ms) on the MI355X."""
+    from . import hip_engine
+    mod = hip_engine.native()
+    X = arrange_states(st)
+    Wt, P = arrange_weights(W)
+    sig, dec, ms = mod.screen_linear(X.reshape(-1), Wt.reshape(-1), st.S, P, want_dec, device)
+    return np.asarray(sig), (None if dec is None else np.asarray(dec)), float(ms)
+
+
+def unique_by_signature(sig: np.ndarray, exclude: Optional[Sequence[int]] = None) -> np.ndarray:
+    """Indices of the first candidate of every distinct signature (in order),
+    without the signatures in `exclude` (e.g. the parents already scored)."""
+    seen = set(int(x) for x in (exclude or ()))
+    keep = []
+    for i, x in enumerate(np.asarray(sig, dtype=np.uint64).tolist()):
+        if x not in seen:
+            seen.add(x)
+            keep.append(i)
+    return np.asarray(keep, dtype=np.int64)
