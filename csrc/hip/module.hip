@@ -163,52 +163,72 @@ py::array_t<uint64_t> test_wave_ops(py::array_t<uint64_t, py::array::c_style | p
 
 // k_score_linear_mfma (screen_mfma.hip.h): signatures (and optionally the
 // per-state decisions) of P linear-family candidates on S recorded states.
-// X: float32 [S * 4 * 64], W: float32 [tiles * 4 * 64] in the kernel's layout
+// X: float32 [S * 5 * 64], W: float32 [tiles * 5 * 64] in the kernel's layout
 // (ops/screen.py arranges them).  Returns (sig uint64 [P], dec uint8 [P, S] or None, kernel ms).
+// It runs beside the resident program grid (the family coupler calls it), so
+// nothing here may wait for the whole device: a private non-blocking stream,
+// buffers that only grow (a replaced one is parked by the FreeQueue while a
+// grid runs), and a wait on that stream alone.
+struct ScreenCtx {
+  std::mutex mu;
+  int device = -1;
+  hipStream_t stream = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  fks_host::DevBuf x, w, sig, dec;
+};
+ScreenCtx& screen_ctx() {
+  static ScreenCtx c;
+  return c;
+}
+
 py::tuple screen_linear(py::array_t<float, py::array::c_style | py::array::forcecast> X,
                         py::array_t<float, py::array::c_style | py::array::forcecast> W, int S, int P, bool want_dec,
                         int device) {
   using namespace fks_screen;
   const int tiles = (P + kScreenCands - 1) / kScreenCands;
   if (S < 1 || P < 1) throw std::invalid_argument("screen: empty");
-  if ((size_t)X.size() != (size_t)S * 256) throw std::invalid_argument("screen: X must be S * 4 * 64 floats");
-  if ((size_t)W.size() != (size_t)tiles * 256) throw std::invalid_argument("screen: W must be tiles * 4 * 64 floats");
+  const size_t per = (size_t)kScreenSteps * 64;
+  if ((size_t)X.size() != (size_t)S * per) throw std::invalid_argument("screen: X must be S * 5 * 64 floats");
+  if ((size_t)W.size() != (size_t)tiles * per) throw std::invalid_argument("screen: W must be tiles * 5 * 64 floats");
+  ScreenCtx& c = screen_ctx();
+  std::lock_guard<std::mutex> g(c.mu);
   HIP_OK(hipSetDevice(device));
-  float *dx = nullptr, *dw = nullptr;
-  uint8_t* dd = nullptr;
-  uint64_t* ds = nullptr;
-  hipEvent_t e0, e1;
-  HIP_OK(hipMalloc(&dx, (size_t)S * 256 * 4));
-  HIP_OK(hipMalloc(&dw, (size_t)tiles * 256 * 4));
-  HIP_OK(hipMalloc(&ds, (size_t)P * 8));
-  if (want_dec) HIP_OK(hipMalloc(&dd, (size_t)P * S));
-  HIP_OK(hipMemcpy(dx, X.data(), (size_t)S * 256 * 4, hipMemcpyHostToDevice));
-  HIP_OK(hipMemcpy(dw, W.data(), (size_t)tiles * 256 * 4, hipMemcpyHostToDevice));
-  HIP_OK(hipEventCreate(&e0));
-  HIP_OK(hipEventCreate(&e1));
+  if (c.device != device) {
+    if (c.stream) throw std::runtime_error("screen: one device per process");
+    HIP_OK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    HIP_OK(hipEventCreate(&c.e0));
+    HIP_OK(hipEventCreate(&c.e1));
+    c.device = device;
+  }
+  c.x.reserve((size_t)S * per * 4);
+  c.w.reserve((size_t)tiles * per * 4);
+  c.sig.reserve((size_t)P * 8);
+  if (want_dec) c.dec.reserve((size_t)P * S);
   float ms = 0.f;
+  py::array_t<uint64_t> sig(P);
+  py::array_t<uint8_t> decv;
+  if (want_dec) decv = py::array_t<uint8_t>({(py::ssize_t)P, (py::ssize_t)S});
+  uint8_t* dec_host = want_dec ? decv.mutable_data() : nullptr;
+  uint64_t* sig_host = sig.mutable_data();
+  const float* xh = X.data();
+  const float* wh = W.data();
   {
     py::gil_scoped_release rel;
+    HIP_OK(hipMemcpyAsync(c.x.p, xh, (size_t)S * per * 4, hipMemcpyHostToDevice, c.stream));
+    HIP_OK(hipMemcpyAsync(c.w.p, wh, (size_t)tiles * per * 4, hipMemcpyHostToDevice, c.stream));
     const int blocks = (tiles + kScreenWaves - 1) / kScreenWaves;
-    HIP_OK(hipEventRecord(e0, 0));
-    hipLaunchKernelGGL(k_score_linear_mfma, dim3(blocks), dim3(64 * kScreenWaves), 0, 0, dx, dw, S, tiles, dd, ds, P);
+    HIP_OK(hipEventRecord(c.e0, c.stream));
+    hipLaunchKernelGGL(k_score_linear_mfma, dim3(blocks), dim3(64 * kScreenWaves), 0, c.stream, c.x.as<float>(),
+                       c.w.as<float>(), S, tiles, want_dec ? c.dec.as<uint8_t>() : nullptr, c.sig.as<uint64_t>(), P);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(e1, 0));
-    HIP_OK(hipEventSynchronize(e1));
-    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+    HIP_OK(hipEventRecord(c.e1, c.stream));
+    HIP_OK(hipMemcpyAsync(sig_host, c.sig.p, (size_t)P * 8, hipMemcpyDeviceToHost, c.stream));
+    if (want_dec) HIP_OK(hipMemcpyAsync(dec_host, c.dec.p, (size_t)P * S, hipMemcpyDeviceToHost, c.stream));
+    HIP_OK(hipStreamSynchronize(c.stream));
+    HIP_OK(hipEventElapsedTime(&ms, c.e0, c.e1));
   }
-  py::array_t<uint64_t> sig(P);
-  HIP_OK(hipMemcpy(sig.mutable_data(), ds, (size_t)P * 8, hipMemcpyDeviceToHost));
   py::object dec = py::none();
-  if (want_dec) {
-    py::array_t<uint8_t> d({(py::ssize_t)P, (py::ssize_t)S});
-    HIP_OK(hipMemcpy(d.mutable_data(), dd, (size_t)P * S, hipMemcpyDeviceToHost));
-    dec = d;
-  }
-  for (void* q : {(void*)dx, (void*)dw, (void*)ds, (void*)dd})
-    if (q) (void)hipFree(q);
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
+  if (want_dec) dec = decv;
   return py::make_tuple(sig, dec, (double)ms);
 }
 

@@ -3,16 +3,16 @@
 // shared-operand case: every candidate is scored on the SAME recorded states,
 // so the per-state node-feature block is a real GEMM operand).
 //
-//   scores[s] = X[s] (16 nodes x 16 features) . W^T (16 features x P candidates)
+//   scores[s] = X[s] (16 nodes x 20 feature slots) . W^T (20 x P candidates)
 //
 // One v_mfma_f32_16x16x4_f32 tile is one state's 16 nodes x 16 candidates;
-// K = 16 features = four k-steps.  Each wave owns 16 candidates: their weight
+// K = 20 feature slots = five k-steps.  Each wave owns 16 candidates: their weight
 // fragments (the B operand, one f32 per lane per k-step) stay in registers for
 // the whole launch while the wave streams every recorded state's A fragments
-// (1 KB per state, coalesced: the host lays X out as [state][k-step][lane]).
+// (1.25 KB per state, coalesced: the host lays X out as [state][k-step][lane]).
 // Per state the wave turns the tile into each candidate's decision: the
 // family's own rule in f32 -- score max(1, trunc(v)) for feasible nodes, first
-// maximum wins, -1 when no node is feasible (feature 15 carries 0 for a
+// maximum wins, 255 when no node is feasible (slot 19 carries 0 for a
 // feasible node and -1e30 otherwise, with weight 1) -- and folds it into a
 // 64-bit FNV-1a signature per candidate.  Candidates with equal signatures
 // place every recorded pod alike: the search replays one of them exactly.
@@ -28,15 +28,15 @@
 
 namespace fks_screen {
 
-constexpr int kScreenFeatures = 16;   // K: 12 family features, 3 zero pads, the feasibility bias
+constexpr int kScreenSteps = 5;       // k-steps of 4: K = 20 slots (<= 19 family features + the feasibility bias)
 constexpr int kScreenNodes = 16;      // M: nodes per state (clusters of <= 16 nodes)
 constexpr int kScreenCands = 16;      // N: candidates per wave tile
 constexpr int kScreenWaves = 4;       // waves per workgroup
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// X: [S][4][64] (k-step t, lane l: X[s][node l&15][feature 4t + (l>>4)])
-// W: [tiles][4][64] (k-step t, lane l: W[16 tile + (l&15)][feature 4t + (l>>4)])
+// X: [S][5][64] (k-step t, lane l: X[s][node l&15][feature 4t + (l>>4)])
+// W: [tiles][5][64] (k-step t, lane l: W[16 tile + (l&15)][feature 4t + (l>>4)])
 // dec: [P][S] uint8 node index or 255 (none feasible), may be null; sig: [P]
 __global__ __launch_bounds__(64 * kScreenWaves) void k_score_linear_mfma(const float* __restrict__ X,
                                                                       const float* __restrict__ W, int S, int tiles,
@@ -45,19 +45,19 @@ __global__ __launch_bounds__(64 * kScreenWaves) void k_score_linear_mfma(const f
   const int lane = threadIdx.x & 63;
   const int tile = blockIdx.x * kScreenWaves + (threadIdx.x >> 6);
   if (tile >= tiles) return;   // whole waves only: no MFMA runs with a partial wave
-  const float* wt = W + (size_t)tile * 4 * 64;
-  const float b0 = wt[lane], b1 = wt[64 + lane], b2 = wt[128 + lane], b3 = wt[192 + lane];
+  const float* wt = W + (size_t)tile * kScreenSteps * 64;
+  float b[kScreenSteps];
+#pragma unroll
+  for (int t = 0; t < kScreenSteps; ++t) b[t] = wt[64 * t + lane];
   const int col = lane & 15;
   const int rbase = (lane >> 4) * 4;
   const int cand = tile * kScreenCands + col;
   uint64_t h = 0xcbf29ce484222325ull;
   for (int s = 0; s < S; ++s) {
-    const float* xs = X + (size_t)s * 4 * 64;
+    const float* xs = X + (size_t)s * kScreenSteps * 64;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xs[lane], b0, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xs[64 + lane], b1, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xs[128 + lane], b2, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xs[192 + lane], b3, acc, 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < kScreenSteps; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xs[64 * t + lane], b[t], acc, 0, 0, 0);
     // this lane's four nodes (rows rbase..rbase+3) for candidate `col`
     float best = -1.f;   // below every feasible score (>= 1)
     int brow = 255;

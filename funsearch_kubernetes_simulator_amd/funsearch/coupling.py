@@ -52,6 +52,12 @@ class FamilyCoupler:
             f: make_islands(1, f, self.candidates, self.elite, seed=seed + 31 * k)[0]
             for k, f in enumerate(self.families)}
         self.exported: Dict[str, float] = {f: float("-inf") for f in self.families}   # best score handed out
+        #: behavioural screen on the matrix cores (``coupling.screen``: {"factor",
+        #: "states", "every"}): linear families draw factor x the candidates and
+        #: replay only those that place the recorded pods differently from the
+        #: elites and each other (ops/screen.py)
+        self.screen_cfg = cfg.get("screen")
+        self._screen_ready = False
         self.rounds = 0
         self.evaluated = 0
         self.seconds = 0.0
@@ -70,6 +76,27 @@ class FamilyCoupler:
             return ev.wait(self.slot)
         return ev.evaluate_family(family, weights)
 
+    def _setup_screen(self) -> None:
+        self._screen_ready = True
+        sc = self.screen_cfg
+        ev = self.evaluator
+        if not sc or getattr(ev, "device", None) is None:
+            return
+        from ..ops import screen
+        w = ev.workload
+        if w.cluster.n_nodes > screen.NODES:
+            return
+        sc = sc if isinstance(sc, dict) else {}
+        dev_index = int(getattr(ev.device, "device", 0) or 0)
+        for f, isl in self.islands.items():
+            if f not in screen.FAMILIES:
+                continue
+            seed = fam.CHAMPION_COMPOSITE if f == "composite_linear" else fam.SAMPLERS[f](1, np.random.default_rng(0))[0]
+            st = screen.record_states(w, seed, family=f, every=int(sc.get("every", 8)),
+                                      max_states=int(sc.get("states", 512)))
+            isl.screener = (lambda W, st=st: screen.screen(st, W, device=dev_index)[0])
+            isl.screen_factor = int(sc.get("factor", 4))
+
     def round(self) -> List[dict]:
         """Advance every family island by ``generations``; return one record
         per family whose champion beat what was exported before:
@@ -77,6 +104,8 @@ class FamilyCoupler:
         ``score`` is the exact re-score of the rendered program text."""
         from ..engine import COLS
         t0 = time.time()
+        if not self._screen_ready:
+            self._setup_screen()
         out = []
         for f, isl in self.islands.items():
             for _ in range(self.generations):

@@ -36,6 +36,14 @@ class ParamIsland:
     elite_scores: np.ndarray = field(default=None)  # [E]
     elite_events: np.ndarray = field(default=None)  # [E] replay events of each elite (NaN: unknown)
     generation: int = 0
+    #: behavioural screen (ops/screen.py, k_score_linear_mfma): weights [P, K] ->
+    #: signatures [P]; with it a generation draws `screen_factor` x the
+    #: candidates and keeps those whose decisions on the recorded states differ
+    #: from every elite's and from each other's (None: no screen)
+    screener: Optional[Callable[[np.ndarray], np.ndarray]] = None
+    screen_factor: int = 4
+    screened: int = 0          # candidates drawn for the screen
+    screen_kept: int = 0       # of those, behaviourally new (replayed)
 
     def __post_init__(self):
         k = self.sampler(1, self.rng).shape[1]
@@ -59,6 +67,19 @@ class ParamIsland:
         mutant is predicted to replay as many events as its parent, a
         crossover as its longer parent; fresh samples (unknown) go first."""
         n = self.n_candidates if n is None else int(n)
+        if self.screener is not None and len(self.elites):
+            from ..ops.screen import unique_by_signature
+            draw = self._propose(n * max(1, int(self.screen_factor)))
+            sig = np.asarray(self.screener(draw))
+            known = np.asarray(self.screener(self.elites))
+            keep = unique_by_signature(sig, exclude=known.tolist())[:n]   # LPT order kept
+            self.screened += len(draw)
+            self.screen_kept += len(keep)
+            if len(keep):
+                return draw[keep]
+        return self._propose(n)
+
+    def _propose(self, n: int) -> np.ndarray:
         if len(self.elites) == 0:
             return self.sampler(n, self.rng)
         n_fresh = max(1, int(n * self.fresh_fraction))

@@ -1199,6 +1199,9 @@ class SteadyStateSearch:
                    polish_evals=st.polish_evals, polish_improved=st.polish_improved, polish_idle=st.polish_idle,
                    coupled=st.coupled,
                    coupler_evals=(fs.coupler.evaluated if fs.coupler is not None else 0),
+                   # MFMA behavioural screen of the coupler's linear families: drawn / replayed
+                   coupler_screened=(sum(i.screened for i in fs.coupler.islands.values()) if fs.coupler else 0),
+                   coupler_screen_kept=(sum(i.screen_kept for i in fs.coupler.islands.values()) if fs.coupler else 0),
                    all_evals_per_s=round((st.evaluations + st.polish_evals) / wall, 2),
                    inflight=inflight, inflight_mean=round(st.inflight_sum / max(1e-9, st.inflight_n), 1),
                    resident_capacity=capacity,

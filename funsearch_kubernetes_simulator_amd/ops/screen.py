@@ -1,7 +1,7 @@
-"""Behavioural screening of `feature_linear` candidates on the matrix cores.
+"""Behavioural screening of linear-family candidates on the matrix cores.
 
-A linear-family candidate is a weight vector over the family's 12 node
-features (`models.families.FEATURES`).  Replays diverge after the first
+A `feature_linear` / `composite_linear` candidate is a weight vector over the
+family's node features (`models.families.FEATURES`, `COMPOSITE_FEATURES`).  Replays diverge after the first
 placement, so the per-event products are per-policy (VALU work, see
 docs/ARCHITECTURE.md "Considered and not built"); but scored on one common set
 of *recorded* cluster states, every candidate shares the same feature blocks
@@ -16,7 +16,7 @@ search can replay one of each (`unique_by_signature`).  It is a screen, not a
 score: f32 products may differ from the replay's f64 arithmetic at near-ties,
 and the exact replay stays the only fitness.
 
-    states = record_states(workload, seed_weights)     # object-engine replay, every k-th creation
+    states = record_states(workload, seed_weights, family)   # object-engine replay, every k-th creation
     sig, dec, ms = screen(states, W)                    # MFMA on the device
     keep = unique_by_signature(sig)
 """
@@ -27,16 +27,17 @@ from typing import Optional, Sequence, Tuple
 
 import numpy as np
 
-from ..models.families import FEATURES, N_FEATURES
+from ..models import families as fam
 
-K = 16           # feature slots: 12 family features, 3 zero pads, the feasibility bias
+STEPS = 5        # MFMA k-steps of 4 (csrc/hip/screen_mfma.hip.h kScreenSteps)
+K = 4 * STEPS    # feature slots: the family's features, zero pads, the feasibility bias (last)
 NODES = 16       # nodes per state (the row-kernel cluster size)
 MASK = -1e30     # bias of an infeasible (or padding) node
 
 
 @dataclass
 class States:
-    """Recorded states: node features [S, 16, 12] (float64), feasibility
+    """Recorded states: node features [S, 16, F] (float64), feasibility
     [S, 16] and the node the recording policy chose (-1: none)."""
     feats: np.ndarray
     feasible: np.ndarray
@@ -47,10 +48,29 @@ class States:
         return int(self.feats.shape[0])
 
 
-def _feature_fn():
-    # the family's own expressions (models/families.py), evaluated per (pod, node)
-    src = "lambda pod, node: (" + ", ".join(e for _, e in FEATURES) + ",)"
-    return eval(src, {"min": min, "max": max, "sum": sum, "abs": abs, "len": len})   # our constants only
+FAMILIES = ("feature_linear", "composite_linear")
+
+
+def _features(family: str):
+    if family == "feature_linear":
+        return fam.FEATURES, ""
+    if family == "composite_linear":
+        return fam.COMPOSITE_FEATURES, fam.COMPOSITE_PREAMBLE
+    raise ValueError(f"screening covers {FAMILIES}, not {family!r}")
+
+
+def n_features(family: str) -> int:
+    return len(_features(family)[0])
+
+
+def _feature_fn(family: str):
+    # the family's own expressions (models/families.py, our constants only),
+    # evaluated per (pod, node) after the family's preamble
+    feats, pre = _features(family)
+    src = "def _f(pod, node):\n" + pre + "    return (" + ", ".join(e for _, e in feats) + ",)\n"
+    env = {"min": min, "max": max, "sum": sum, "abs": abs, "len": len}
+    exec(compile(src, "<screen-features>", "exec"), env)
+    return env["_f"]
 
 
 def _feasible(pod, node) -> bool:
@@ -62,17 +82,20 @@ def _feasible(pod, node) -> bool:
     return True
 
 
-def record_states(workload, weights: Sequence[float], every: int = 16, max_states: int = 512) -> States:
-    """Replay the `feature_linear` policy `weights` on the object engine and
-    record the node features, feasibility and the chosen node at every
-    `every`-th creation event (up to `max_states`)."""
-    from ..models.families import feature_linear_program
+def record_states(workload, weights: Sequence[float], family: str = "feature_linear", every: int = 16,
+                  max_states: int = 512) -> States:
+    """Replay the `family` policy `weights` on the object engine and record
+    the node features, feasibility and the chosen node at every `every`-th
+    creation event (up to `max_states`; the replay stops there)."""
     from ..funsearch.scheduler import FunSearchScheduler
     from ..simulator import DiscreteEventSimulator, KubernetesSimulator
     if workload.cluster.n_nodes > NODES:
         raise ValueError(f"screening records clusters of <= {NODES} nodes")
-    feat = _feature_fn()
-    sched = FunSearchScheduler(feature_linear_program(weights))
+    feat = _feature_fn(family)
+    F_n = n_features(family)
+    if F_n > K - 1:
+        raise ValueError(f"{family}: {F_n} features do not fit {K - 1} slots")
+    sched = FunSearchScheduler(fam.to_program(family, weights))
     cluster, pods = workload.to_objects()
     F, M, C = [], [], []
     count = [0]
@@ -82,7 +105,7 @@ def record_states(workload, weights: Sequence[float], every: int = 16, max_state
             best = super()._select_node(pod)
             count[0] += 1
             if count[0] % every == 0 and len(F) < max_states:
-                f = np.zeros((NODES, N_FEATURES))
+                f = np.zeros((NODES, F_n))
                 m = np.zeros(NODES, dtype=bool)
                 ch = -1
                 for j, node in enumerate(self.cluster.nodes_dict.values()):
@@ -94,39 +117,48 @@ def record_states(workload, weights: Sequence[float], every: int = 16, max_state
                 F.append(f)
                 M.append(m)
                 C.append(ch)
+                if len(F) >= max_states:
+                    raise _Done
             return best
 
-    Recorder(cluster, pods, DiscreteEventSimulator(pods), sched).run_schedule()
+    try:
+        Recorder(cluster, pods, DiscreteEventSimulator(pods), sched).run_schedule()
+    except _Done:
+        pass
     return States(np.asarray(F), np.asarray(M), np.asarray(C, dtype=np.int64))
 
 
+class _Done(Exception):
+    """Enough states recorded: the replay stops."""
+
+
 def arrange_states(st: States) -> np.ndarray:
-    """X in the kernel's A-fragment layout: float32 [S, 4, 64], element
-    (s, t, l) = feature 4t + (l >> 4) of node l & 15 (slot 15: the bias)."""
-    S = st.S
+    """X in the kernel's A-fragment layout: float32 [S, STEPS, 64], element
+    (s, t, l) = feature 4t + (l >> 4) of node l & 15 (slot K - 1: the bias)."""
+    S, F_n = st.S, st.feats.shape[2]
     full = np.zeros((S, NODES, K), dtype=np.float64)
-    full[:, :, :N_FEATURES] = st.feats
+    full[:, :, :F_n] = st.feats
     full[:, :, K - 1] = np.where(st.feasible, 0.0, MASK)
     lanes = np.arange(64)
-    out = np.empty((S, 4, 64), dtype=np.float32)
-    for t in range(4):
+    out = np.empty((S, STEPS, 64), dtype=np.float32)
+    for t in range(STEPS):
         out[:, t, :] = full[:, lanes & 15, 4 * t + (lanes >> 4)]
     return out
 
 
-def arrange_weights(W: np.ndarray) -> Tuple[np.ndarray, int]:
-    """W [P, 12] in the B-fragment layout: float32 [tiles, 4, 64], element
-    (tile, t, l) = weight 4t + (l >> 4) of candidate 16 tile + (l & 15);
-    slot 15 = 1 (the feasibility bias), padding candidates all zero."""
+def arrange_weights(W: np.ndarray, F_n: int) -> Tuple[np.ndarray, int]:
+    """W [P, >= F_n] in the B-fragment layout: float32 [tiles, STEPS, 64],
+    element (tile, t, l) = weight 4t + (l >> 4) of candidate 16 tile + (l & 15);
+    slot K - 1 = 1 (the feasibility bias), padding candidates all zero."""
     W = np.asarray(W, dtype=np.float64)
     P = W.shape[0]
     tiles = (P + 15) // 16
     full = np.zeros((tiles * 16, K), dtype=np.float64)
-    full[:P, :N_FEATURES] = W[:, :N_FEATURES]
+    full[:P, :F_n] = W[:, :F_n]
     full[:P, K - 1] = 1.0
     lanes = np.arange(64)
-    out = np.empty((tiles, 4, 64), dtype=np.float32)
-    for t in range(4):
+    out = np.empty((tiles, STEPS, 64), dtype=np.float32)
+    for t in range(STEPS):
         out[:, t, :] = full.reshape(tiles, 16, K)[:, lanes & 15, 4 * t + (lanes >> 4)]
     return out, P
 
@@ -135,8 +167,8 @@ def decisions_reference(st: States, W: np.ndarray, dtype=np.float64) -> np.ndarr
     """[P, S] node the family's rule picks on each recorded state (255: none
     feasible): score = max(1, int(w . f)) on feasible nodes, the first maximum
     wins.  float64: the replay's arithmetic; float32: the kernel's."""
-    W = np.asarray(W, dtype=dtype)[:, :N_FEATURES]
     f = st.feats.astype(dtype)
+    W = np.asarray(W, dtype=dtype)[:, :f.shape[2]]
     v = np.einsum("snf,pf->psn", f, W)                         # [P, S, 16]
     sc = np.maximum(1.0, np.trunc(v))
     sc = np.where(st.feasible[None, :, :], sc, -2.0)
@@ -162,7 +194,7 @@ def screen(st: States, W: np.ndarray, want_dec: bool = False, device: int = 0):
     from . import hip_engine
     mod = hip_engine.native()
     X = arrange_states(st)
-    Wt, P = arrange_weights(W)
+    Wt, P = arrange_weights(W, st.feats.shape[2])
     sig, dec, ms = mod.screen_linear(X.reshape(-1), Wt.reshape(-1), st.S, P, want_dec, device)
     return np.asarray(sig), (None if dec is None else np.asarray(dec)), float(ms)
 
