@@ -183,13 +183,16 @@ ScreenCtx& screen_ctx() {
 
 py::tuple screen_linear(py::array_t<float, py::array::c_style | py::array::forcecast> X,
                         py::array_t<float, py::array::c_style | py::array::forcecast> W, int S, int P, bool want_dec,
-                        int device) {
+                        int device, int chunks) {
   using namespace fks_screen;
   const int tiles = (P + kScreenCands - 1) / kScreenCands;
   if (S < 1 || P < 1) throw std::invalid_argument("screen: empty");
   const size_t per = (size_t)kScreenSteps * 64;
   if ((size_t)X.size() != (size_t)S * per) throw std::invalid_argument("screen: X must be S * 5 * 64 floats");
   if ((size_t)W.size() != (size_t)tiles * per) throw std::invalid_argument("screen: W must be tiles * 5 * 64 floats");
+  if (chunks < 1 || chunks > S) throw std::invalid_argument("screen: chunks must be in [1, S]");
+  const int spc = (S + chunks - 1) / chunks;
+  const int C = (S + spc - 1) / spc;   // chunks actually holding states
   ScreenCtx& c = screen_ctx();
   std::lock_guard<std::mutex> g(c.mu);
   HIP_OK(hipSetDevice(device));
@@ -202,14 +205,15 @@ py::tuple screen_linear(py::array_t<float, py::array::c_style | py::array::force
   }
   c.x.reserve((size_t)S * per * 4);
   c.w.reserve((size_t)tiles * per * 4);
-  c.sig.reserve((size_t)P * 8);
+  c.sig.reserve((size_t)P * C * 8);
   if (want_dec) c.dec.reserve((size_t)P * S);
   float ms = 0.f;
   py::array_t<uint64_t> sig(P);
+  std::vector<uint64_t> sigc((size_t)P * C);
   py::array_t<uint8_t> decv;
   if (want_dec) decv = py::array_t<uint8_t>({(py::ssize_t)P, (py::ssize_t)S});
   uint8_t* dec_host = want_dec ? decv.mutable_data() : nullptr;
-  uint64_t* sig_host = sig.mutable_data();
+  uint64_t* sig_host = sigc.data();
   const float* xh = X.data();
   const float* wh = W.data();
   {
@@ -218,14 +222,22 @@ py::tuple screen_linear(py::array_t<float, py::array::c_style | py::array::force
     HIP_OK(hipMemcpyAsync(c.w.p, wh, (size_t)tiles * per * 4, hipMemcpyHostToDevice, c.stream));
     const int blocks = (tiles + kScreenWaves - 1) / kScreenWaves;
     HIP_OK(hipEventRecord(c.e0, c.stream));
-    hipLaunchKernelGGL(k_score_linear_mfma, dim3(blocks), dim3(64 * kScreenWaves), 0, c.stream, c.x.as<float>(),
-                       c.w.as<float>(), S, tiles, want_dec ? c.dec.as<uint8_t>() : nullptr, c.sig.as<uint64_t>(), P);
+    hipLaunchKernelGGL(k_score_linear_mfma, dim3(blocks, C), dim3(64 * kScreenWaves), 0, c.stream, c.x.as<float>(),
+                       c.w.as<float>(), S, tiles, want_dec ? c.dec.as<uint8_t>() : nullptr, c.sig.as<uint64_t>(), P,
+                       spc);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(c.e1, c.stream));
-    HIP_OK(hipMemcpyAsync(sig_host, c.sig.p, (size_t)P * 8, hipMemcpyDeviceToHost, c.stream));
+    HIP_OK(hipMemcpyAsync(sig_host, c.sig.p, (size_t)P * C * 8, hipMemcpyDeviceToHost, c.stream));
     if (want_dec) HIP_OK(hipMemcpyAsync(dec_host, c.dec.p, (size_t)P * S, hipMemcpyDeviceToHost, c.stream));
     HIP_OK(hipStreamSynchronize(c.stream));
     HIP_OK(hipEventElapsedTime(&ms, c.e0, c.e1));
+  }
+  // fold the chunk signatures in chunk order (ops/screen.py signature())
+  uint64_t* out = sig.mutable_data();
+  for (int p = 0; p < P; ++p) {
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (int k = 0; k < C; ++k) h = (h ^ sigc[(size_t)p * C + k]) * 0x100000001b3ull;
+    out[p] = h;
   }
   py::object dec = py::none();
   if (want_dec) dec = decv;
@@ -523,7 +535,7 @@ PYBIND11_MODULE(_fks_hip, m) {
   m.def("test_wave_ops", &test_wave_ops);
   m.def("test_heap", &test_heap);
   m.def("screen_linear", &screen_linear, py::arg("X"), py::arg("W"), py::arg("S"), py::arg("P"),
-        py::arg("want_dec") = false, py::arg("device") = 0);
+        py::arg("want_dec") = false, py::arg("device") = 0, py::arg("chunks") = 1);
   py::class_<DeviceEngine>(m, "DeviceEngine")
       .def(py::init<py::dict, int, int>(), py::arg("workload"), py::arg("device") = 0, py::arg("n_slots") = 4)
       .def("set_options", &DeviceEngine::set_options)

@@ -37,13 +37,19 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // X: [S][5][64] (k-step t, lane l: X[s][node l&15][feature 4t + (l>>4)])
 // W: [tiles][5][64] (k-step t, lane l: W[16 tile + (l&15)][feature 4t + (l>>4)])
-// dec: [P][S] uint8 node index or 255 (none feasible), may be null; sig: [P]
+// dec: [P][S] uint8 node index or 255 (none feasible), may be null;
+// sig: [P][C] the signature of each chunk of `spc` states (blockIdx.y = chunk):
+// a launch of few candidate tiles splits the states over more waves, so the
+// SIMDs hold enough waves to cover the MFMA chain's latency (the host folds
+// the chunk signatures in order)
 __global__ __launch_bounds__(64 * kScreenWaves) void k_score_linear_mfma(const float* __restrict__ X,
                                                                       const float* __restrict__ W, int S, int tiles,
                                                                       uint8_t* __restrict__ dec,
-                                                                      uint64_t* __restrict__ sig, int P) {
+                                                                      uint64_t* __restrict__ sig, int P, int spc) {
   const int lane = threadIdx.x & 63;
   const int tile = blockIdx.x * kScreenWaves + (threadIdx.x >> 6);
+  const int C = gridDim.y, chunk = blockIdx.y;
+  const int s0 = chunk * spc, s1 = min(S, s0 + spc);
   if (tile >= tiles) return;   // whole waves only: no MFMA runs with a partial wave
   const float* wt = W + (size_t)tile * kScreenSteps * 64;
   float b[kScreenSteps];
@@ -53,7 +59,7 @@ __global__ __launch_bounds__(64 * kScreenWaves) void k_score_linear_mfma(const f
   const int rbase = (lane >> 4) * 4;
   const int cand = tile * kScreenCands + col;
   uint64_t h = 0xcbf29ce484222325ull;
-  for (int s = 0; s < S; ++s) {
+  for (int s = s0; s < s1; ++s) {
     const float* xs = X + (size_t)s * kScreenSteps * 64;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -78,7 +84,7 @@ __global__ __launch_bounds__(64 * kScreenWaves) void k_score_linear_mfma(const f
     if (dec != nullptr && lane < 16 && cand < P) dec[(size_t)cand * S + s] = (uint8_t)d;
     h = (h ^ (uint64_t)(d + 1)) * 0x100000001b3ull;
   }
-  if (lane < 16 && cand < P) sig[cand] = h;
+  if (lane < 16 && cand < P) sig[(size_t)cand * C + chunk] = h;
 }
 
 }  // namespace fks_screen

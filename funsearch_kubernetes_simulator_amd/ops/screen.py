@@ -178,24 +178,45 @@ def decisions_reference(st: States, W: np.ndarray, dtype=np.float64) -> np.ndarr
     return best.astype(np.uint8)
 
 
-def signature(dec: np.ndarray) -> np.ndarray:
-    """The kernel's FNV-1a fold of a [P, S] decision matrix (host twin)."""
-    h = np.full(dec.shape[0], 0xcbf29ce484222325, dtype=np.uint64)
+#: states per signature chunk: fixed, so a signature does not depend on the
+#: batch it was computed in (an elite screened alone must match its copy in a
+#: batch of 65,536); the launch runs one wave per (16 candidates, chunk), which
+#: also gives small batches enough waves to cover the MFMA chain's latency
+CHUNK = 16
+
+
+def chunks_for(P: int, S: int) -> int:
+    """State chunks of a launch (grid y): ceil(S / CHUNK), whatever P."""
+    return int(-(-S // CHUNK))
+
+
+def signature(dec: np.ndarray, chunks: int = 1) -> np.ndarray:
+    """The kernel's signature of a [P, S] decision matrix (host twin): an
+    FNV-1a fold of the decisions within each chunk of states, then of the
+    chunk signatures in order."""
+    P, S = dec.shape
+    spc = -(-S // max(1, chunks))
     prime = np.uint64(0x100000001b3)
+    basis = np.uint64(0xcbf29ce484222325)
     d = dec.astype(np.uint64)
-    # 255 (none) folds as 256, like the kernel's (d + 1) with d = 255
-    for s in range(dec.shape[1]):
-        h = (h ^ (d[:, s] + np.uint64(1))) * prime
-    return h
+    out = np.full(P, basis, dtype=np.uint64)
+    for s0 in range(0, S, spc):
+        h = np.full(P, basis, dtype=np.uint64)
+        # 255 (none) folds as 256, like the kernel's (d + 1) with d = 255
+        for s in range(s0, min(S, s0 + spc)):
+            h = (h ^ (d[:, s] + np.uint64(1))) * prime
+        out = (out ^ h) * prime
+    return out
 
 
 def screen(st: States, W: np.ndarray, want_dec: bool = False, device: int = 0):
-    """(sig [P] uint64, dec [P, S] uint8 or None, kernel ms) on the MI355X."""
+    """(sig [P] uint64, dec [P, S] uint8 or None, kernel ms) on the MI355X
+    (signature(dec, chunks_for(P, S)) is the signature's host twin)."""
     from . import hip_engine
     mod = hip_engine.native()
     X = arrange_states(st)
     Wt, P = arrange_weights(W, st.feats.shape[2])
-    sig, dec, ms = mod.screen_linear(X.reshape(-1), Wt.reshape(-1), st.S, P, want_dec, device)
+    sig, dec, ms = mod.screen_linear(X.reshape(-1), Wt.reshape(-1), st.S, P, want_dec, device, chunks_for(P, st.S))
     return np.asarray(sig), (None if dec is None else np.asarray(dec)), float(ms)
 
 

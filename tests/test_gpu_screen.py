@@ -32,7 +32,10 @@ def test_mfma_decisions_match_reference(states):
     # f32 accumulation order differs from numpy's only at near-ties
     assert (dec == ref32).mean() > 0.999, (dec == ref32).mean()
     assert (dec == ref64).mean() > 0.995, (dec == ref64).mean()
-    assert np.array_equal(sig, screen.signature(dec))
+    assert np.array_equal(sig, screen.signature(dec, screen.chunks_for(1000, st.S)))
+    # a signature does not depend on the batch it was computed in
+    one, _, _ = screen.screen(st, W[7:8])
+    assert one[0] == sig[7]
 
 
 def test_mfma_exact_on_integer_data(states):

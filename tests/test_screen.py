@@ -67,7 +67,7 @@ def test_signatures_and_unique(states):
     W = sample_feature_linear(8, np.random.default_rng(2))
     W = np.concatenate([W, W[:3]])                  # three exact duplicates
     dec = screen.decisions_reference(st, W)
-    sig = screen.signature(dec)
+    sig = screen.signature(dec, screen.chunks_for(len(W), st.S))
     assert len(set(sig.tolist())) <= 8
     keep = screen.unique_by_signature(sig)
     assert list(keep[:len(keep)]) == sorted(keep) and all(k < 8 for k in keep)
@@ -90,3 +90,14 @@ def test_param_island_screen_keeps_new_behaviours(composite_states):
     sig = isl.screener(out)
     assert len(set(sig.tolist())) == len(out)
     assert not set(sig.tolist()) & set(isl.screener(isl.elites).tolist())
+
+
+def test_signature_independent_of_batch(states):
+    """A candidate's signature is the same alone or inside a larger batch (the
+    island compares its elites' signatures with a batch's)."""
+    _, st = states
+    W = sample_feature_linear(40, np.random.default_rng(9))
+    dec = screen.decisions_reference(st, W)
+    full = screen.signature(dec, screen.chunks_for(40, st.S))
+    one = screen.signature(dec[3:4], screen.chunks_for(1, st.S))
+    assert one[0] == full[3]
